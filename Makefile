@@ -1,0 +1,49 @@
+# Native build of the seed-extension engine (gfx950 only) and its test infrastructure.
+#   make            -> product library + tools + oracle
+#   make product    -> bwa-mem2-arm_amd/lib/libbsw_hip.so   (HIP kernels + C ABI)
+#   make oracle     -> oracle/liboracle.so                  (CPU oracle + SSE4.1 baseline; tests only)
+PKG      := bwa-mem2-arm_amd
+CSRC     := $(PKG)/csrc
+LIBDIR   := $(PKG)/lib
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function \
+            -munsafe-fp-atomics -Iinclude
+CFLAGS   ?= -O3 -fPIC -Wall -Iinclude
+
+PRODUCT  := $(LIBDIR)/libbsw_hip.so
+SYNTH    := $(LIBDIR)/libbsw_synth.so
+SHIMTEST := $(LIBDIR)/bsw_shim_example
+ORACLE   := oracle/liboracle.so
+
+HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_host.cpp
+HIP_HDRS := $(CSRC)/bsw_kernels.h include/bsw.h include/bsw_seqpair.h
+
+all: product synth oracle
+
+product: $(PRODUCT)
+synth: $(SYNTH)
+oracle: $(ORACLE)
+
+$(LIBDIR):
+	mkdir -p $(LIBDIR)
+
+$(LIBDIR)/bsw_kernels.o: $(CSRC)/bsw_kernels.hip $(HIP_HDRS) | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/bsw_host.o: $(CSRC)/bsw_host.cpp $(HIP_HDRS) | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_host.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+
+$(SYNTH): $(CSRC)/bsw_synth.c include/bsw_seqpair.h | $(LIBDIR)
+	gcc $(CFLAGS) -shared -o $@ $<
+
+$(ORACLE): oracle/ksw_ext_ref.c oracle/bsw_sse41.c include/bsw_seqpair.h
+	gcc $(CFLAGS) -msse4.1 -shared -o $@ oracle/ksw_ext_ref.c oracle/bsw_sse41.c -lpthread
+
+clean:
+	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so $(ORACLE)
+
+.PHONY: all product synth oracle clean

@@ -1,0 +1,441 @@
+// bsw_host.cpp -- host engine behind the C ABI (include/bsw.h).
+//
+// Replaces upstream BandedPairWiseSW's batch wrapper (smithWatermanBatchWrapper16/8:
+// sort -> pad -> AoS->SoA -> kernel -> write back; SURVEY.md §3.2,
+// docs-archive/WEEK1_WRAPPER_COMPLETE.md:27-118) with an MI355X pipeline that keeps the
+// upstream AoS layout in HBM and does the "transpose" implicitly (one lane per pair):
+//
+//   plan_kernel   : per pair -> kernel class (lane QMAX bucket 32..160 | wide) + sort key
+//                   (class, qlen desc, tlen desc) so every wavefront gets 64 like-shaped pairs
+//   radix sort    : hipCUB DeviceRadixSort on the 27-bit key -> order[] (= sortPairsLen)
+//   DP kernels    : one launch per non-empty class over its slice of order[]
+//   results       : written by the kernels straight into the SeqPair records
+//
+// Concurrency: upstream calls getScores* from kt_for workers; every call here takes a Slot
+// (own HIP stream + device buffers) from a per-device pool, so calls are reentrant.
+// Host-buffer calls on an n_gpus context shard the batch by contiguous pair ranges across
+// devices (one host thread per device) -- pairs are independent.
+// Errors are returned as BSW_E* codes; there is no CPU path in this library.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <type_traits>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include "../../include/bsw.h"
+#include "bsw_kernels.h"
+
+namespace bsw {
+
+constexpr int kNumLaneClasses = 5;          // QMAX 32, 64, 96, 128, 160
+constexpr int kWideClass = kNumLaneClasses; // index of the wide-kernel class
+constexpr int kNumClasses = kNumLaneClasses + 1;
+constexpr int kKeyBits = 27;                // 3 class bits + 8 qlen bits + 16 tlen bits
+
+// Per pair: class + sort key.  Lane classes need qlen <= QMAX and int16-safe scores.
+__global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_t maxsc,
+                            uint32_t *__restrict__ keys, int32_t *__restrict__ vals,
+                            int32_t *__restrict__ counts, int32_t *__restrict__ maxq_wide)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SeqPair p = pairs[i];
+    const int qlen = max(p.len2, 0), tlen = max(p.len1, 0);
+    const int64_t hi = (int64_t)max(p.h0, 0) + (int64_t)max(maxsc, 0) * min(qlen, tlen);
+    int c = kWideClass;
+    if (hi < 32768 && p.h0 >= 0) {
+        if (qlen <= 32) c = 0;
+        else if (qlen <= 64) c = 1;
+        else if (qlen <= 96) c = 2;
+        else if (qlen <= 128) c = 3;
+        else if (qlen <= 160) c = 4;
+    }
+    if (c == kWideClass) atomicMax(maxq_wide, qlen);
+    keys[i] = ((uint32_t)c << 24) | ((uint32_t)(255 - min(qlen, 255)) << 16) |
+              (uint32_t)(65535 - min(tlen, 65535));
+    vals[i] = i;
+    atomicAdd(&counts[c], 1);
+}
+
+struct Slot {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // device buffers (grown on demand)
+    SeqPair *d_pairs = nullptr; size_t cap_pairs = 0;
+    uint8_t *d_ref = nullptr; size_t cap_ref = 0;
+    uint8_t *d_qer = nullptr; size_t cap_qer = 0;
+    uint32_t *d_keys = nullptr, *d_keys2 = nullptr;
+    int32_t *d_vals = nullptr, *d_order = nullptr; size_t cap_sort = 0;
+    void *d_tmp = nullptr; size_t cap_tmp = 0;
+    int32_t *d_meta = nullptr;          // counts[8], maxq_wide, err
+    int32_t *h_meta = nullptr;          // pinned mirror
+    int2 *d_scratch = nullptr; size_t cap_scratch = 0;
+    bool timed = false;
+    bsw_stats_t stats{};
+};
+
+static int hip_rc(hipError_t e)
+{
+    if (e == hipSuccess) return BSW_OK;
+    if (e == hipErrorOutOfMemory) return BSW_E_NOMEM;
+    return BSW_E_HIP;
+}
+#define BSW_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return ::bsw::hip_rc(_e); } while (0)
+
+template <class T>
+static hipError_t grow(T *&p, size_t &cap, size_t need)   // cap counts elements (bytes for void)
+{
+    if (need <= cap) return hipSuccess;
+    const size_t n = std::max(need, cap * 3 / 2);
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    constexpr size_t esz = std::is_void<T>::value ? 1 : sizeof(typename std::conditional<std::is_void<T>::value, char, T>::type);
+    hipError_t e = hipMalloc((void **)&p, n * esz);
+    if (e == hipSuccess) cap = n;
+    return e;
+}
+
+struct DeviceCtx {
+    int device = 0;
+    std::mutex mu;
+    std::vector<std::unique_ptr<Slot>> free_slots;
+
+    ~DeviceCtx()
+    {
+        for (auto &s : free_slots) release_slot(s.get());
+    }
+    static void release_slot(Slot *s)
+    {
+        (void)hipSetDevice(s->device);
+        (void)hipFree(s->d_pairs); (void)hipFree(s->d_ref); (void)hipFree(s->d_qer);
+        (void)hipFree(s->d_keys); (void)hipFree(s->d_keys2); (void)hipFree(s->d_vals); (void)hipFree(s->d_order);
+        (void)hipFree(s->d_tmp); (void)hipFree(s->d_meta); (void)hipFree(s->d_scratch);
+        if (s->h_meta) (void)hipHostFree(s->h_meta);
+        if (s->ev0) (void)hipEventDestroy(s->ev0);
+        if (s->ev1) (void)hipEventDestroy(s->ev1);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+    }
+    std::unique_ptr<Slot> acquire(int &rc)
+    {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free_slots.empty()) {
+                auto s = std::move(free_slots.back());
+                free_slots.pop_back();
+                rc = BSW_OK;
+                return s;
+            }
+        }
+        auto s = std::make_unique<Slot>();
+        s->device = device;
+        rc = hip_rc(hipSetDevice(device));
+        if (rc) return nullptr;
+        if ((rc = hip_rc(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)))) return nullptr;
+        if ((rc = hip_rc(hipEventCreate(&s->ev0)))) return nullptr;
+        if ((rc = hip_rc(hipEventCreate(&s->ev1)))) return nullptr;
+        if ((rc = hip_rc(hipMalloc((void **)&s->d_meta, 16 * sizeof(int32_t))))) return nullptr;
+        if ((rc = hip_rc(hipHostMalloc((void **)&s->h_meta, 16 * sizeof(int32_t), 0)))) return nullptr;
+        return s;
+    }
+    void give_back(std::unique_ptr<Slot> s)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        free_slots.push_back(std::move(s));
+    }
+};
+
+}  // namespace bsw
+
+struct bsw_ctx {
+    bsw_params_t params;
+    bsw::KParams kp;
+    std::vector<std::unique_ptr<bsw::DeviceCtx>> devs;
+    std::mutex stats_mu;
+    bsw_stats_t last{};
+};
+
+namespace bsw {
+
+static void make_kparams(const bsw_params_t &p, KParams &kp)
+{
+    memset(&kp, 0, sizeof(kp));
+    kp.o_del = p.o_del; kp.e_del = p.e_del; kp.o_ins = p.o_ins; kp.e_ins = p.e_ins;
+    kp.zdrop = p.zdrop; kp.end_bonus = p.end_bonus;
+    int mx = 0;
+    for (int i = 0; i < 25; ++i) mx = std::max(mx, (int)p.mat[i]);
+    kp.maxsc = mx;
+    memcpy(kp.mat, p.mat, 25);
+    // prof[t] byte q = mat[t][q] for q < 5; q = 5..7 (invalid codes) score as N
+    for (int t = 0; t < 8; ++t) {
+        const int tt = std::min(t, 4);
+        uint8_t b[8];
+        for (int q = 0; q < 8; ++q) b[q] = (uint8_t)p.mat[tt * 5 + std::min(q, 4)];
+        kp.prof[t][0] = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+        kp.prof[t][1] = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+    }
+}
+
+// The device pipeline on one slot's device; d_* are device pointers valid on `stream`.
+static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_t *d_ref,
+                      const uint8_t *d_qer, int32_t n, int32_t w, hipStream_t stream)
+{
+    s.stats = bsw_stats_t{};
+    if (n == 0) return BSW_OK;
+    if ((size_t)n > s.cap_sort) {           // keys / keys2 / vals / order grow together
+        (void)hipFree(s.d_keys); (void)hipFree(s.d_keys2); (void)hipFree(s.d_vals); (void)hipFree(s.d_order);
+        s.d_keys = s.d_keys2 = nullptr; s.d_vals = s.d_order = nullptr; s.cap_sort = 0;
+        const size_t cap = std::max((size_t)n, (size_t)1024);
+        BSW_TRY(hipMalloc((void **)&s.d_keys, cap * sizeof(uint32_t)));
+        BSW_TRY(hipMalloc((void **)&s.d_keys2, cap * sizeof(uint32_t)));
+        BSW_TRY(hipMalloc((void **)&s.d_vals, cap * sizeof(int32_t)));
+        BSW_TRY(hipMalloc((void **)&s.d_order, cap * sizeof(int32_t)));
+        s.cap_sort = cap;
+    }
+    BSW_TRY(hipMemsetAsync(s.d_meta, 0, 16 * sizeof(int32_t), stream));
+    int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + 8, *d_err = s.d_meta + 9;
+    hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                       d_pairs, n, kp.maxsc, s.d_keys, s.d_vals, d_counts, d_maxq);
+    BSW_TRY(hipGetLastError());
+    size_t tmp_bytes = 0;
+    BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals,
+                                               s.d_order, n, 0, kKeyBits, stream));
+    BSW_TRY(grow(s.d_tmp, s.cap_tmp, tmp_bytes));
+    BSW_TRY(hipcub::DeviceRadixSort::SortPairs(s.d_tmp, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals,
+                                               s.d_order, n, 0, kKeyBits, stream));
+    BSW_TRY(hipMemcpyAsync(s.h_meta, s.d_meta, 16 * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    BSW_TRY(hipStreamSynchronize(stream));
+    int32_t counts[kNumClasses];
+    memcpy(counts, s.h_meta, sizeof(counts));
+    const int32_t maxq_wide = s.h_meta[8];
+    // DP kernels, one launch per non-empty class; event-timed as the hot region
+    BSW_TRY(hipEventRecord(s.ev0, stream));
+    int32_t off = 0;
+    for (int c = 0; c < kNumLaneClasses; ++c) {
+        if (counts[c] > 0) {
+            BSW_TRY(launch_lane_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, counts[c],
+                                       d_ref, d_qer, d_err, stream));
+            s.stats.n_launches++;
+            s.stats.n_i16 += counts[c];
+        }
+        off += counts[c];
+    }
+    if (counts[kWideClass] > 0) {
+        const int32_t nw = counts[kWideClass];
+        const size_t need = (size_t)(maxq_wide + 2) * (size_t)nw;
+        BSW_TRY(grow(s.d_scratch, s.cap_scratch, need));
+        BSW_TRY(launch_wide_kernel(kp, w, d_pairs, s.d_order + off, nw, d_ref, d_qer, s.d_scratch,
+                                   nw, stream));
+        s.stats.n_launches++;
+        s.stats.n_wide += nw;
+    }
+    BSW_TRY(hipEventRecord(s.ev1, stream));
+    s.timed = true;
+    return BSW_OK;
+}
+
+static int finish_stats(Slot &s)
+{
+    if (s.timed) {
+        float ms = 0.f;
+        BSW_TRY(hipEventSynchronize(s.ev1));
+        BSW_TRY(hipEventElapsedTime(&ms, s.ev0, s.ev1));
+        s.stats.kernel_ms = ms;
+        s.timed = false;
+    }
+    return BSW_OK;
+}
+
+// One device's share of a host-buffer call.
+static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref,
+                      const uint8_t *qer, int32_t n, int32_t w, bsw_stats_t *st)
+{
+    if (n == 0) return BSW_OK;
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    Slot &s = *slot;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        // extents of the byte buffers this shard touches
+        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            const SeqPair &p = pairs[i];
+            if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
+            if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
+        }
+        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+        const size_t rbytes = (size_t)(r_hi - r_lo) + 1, qbytes = (size_t)(q_hi - q_lo) + 1;
+        BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)n));
+        BSW_TRY(grow(s.d_ref, s.cap_ref, rbytes));
+        BSW_TRY(grow(s.d_qer, s.cap_qer, qbytes));
+        BSW_TRY(hipMemcpyAsync(s.d_pairs, pairs, (size_t)n * sizeof(SeqPair), hipMemcpyHostToDevice, s.stream));
+        if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, ref + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
+        if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, qer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
+        // kernels index ref/qer by idr/idq: shift the base so d_ref[idr - r_lo] is byte idr
+        int r = run_device(kp, s, s.d_pairs, s.d_ref - r_lo, s.d_qer - q_lo, n, w, s.stream);
+        if (r) return r;
+        BSW_TRY(hipMemcpyAsync(pairs, s.d_pairs, (size_t)n * sizeof(SeqPair), hipMemcpyDeviceToHost, s.stream));
+        BSW_TRY(hipStreamSynchronize(s.stream));
+        if ((r = finish_stats(s))) return r;
+        if (s.h_meta[9] != 0) return BSW_E_RANGE;   // kernel guard tripped (routing bug)
+        if (st) *st = s.stats;
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+
+}  // namespace bsw
+
+// ====================================================================== C ABI
+extern "C" {
+
+void bsw_params_default(bsw_params_t *p)
+{
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->o_del = p->o_ins = 6;
+    p->e_del = p->e_ins = 1;
+    p->zdrop = 100;
+    p->end_bonus = 5;
+    p->w_match = 1;
+    p->w_mismatch = -4;
+    p->w_ambig = -1;
+    for (int t = 0; t < 5; ++t)
+        for (int q = 0; q < 5; ++q)
+            p->mat[t * 5 + q] = (t == 4 || q == 4) ? -1 : (t == q ? 1 : -4);
+}
+
+static bool params_ok(const bsw_params_t *p)
+{
+    if (p->e_del < 1 || p->e_ins < 1 || p->o_del < 0 || p->o_ins < 0) return false;
+    if (p->o_del + p->e_del > 32767 || p->o_ins + p->e_ins > 32767) return false;
+    return true;
+}
+
+int bsw_create(const bsw_params_t *params, int device0, int n_gpus, bsw_ctx_t **out)
+{
+    if (!params || !out || n_gpus < 1 || device0 < 0 || !params_ok(params)) return BSW_E_INVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return BSW_E_NODEV;
+    if (device0 + n_gpus > ndev) return BSW_E_NODEV;
+    auto *c = new bsw_ctx();
+    c->params = *params;
+    bsw::make_kparams(*params, c->kp);
+    for (int d = 0; d < n_gpus; ++d) {
+        auto dc = std::make_unique<bsw::DeviceCtx>();
+        dc->device = device0 + d;
+        c->devs.push_back(std::move(dc));
+    }
+    *out = c;
+    return BSW_OK;
+}
+
+void bsw_destroy(bsw_ctx_t *ctx) { delete ctx; }
+
+static int validate(const SeqPair *pairs, int32_t n, int32_t w, int cell_bits)
+{
+    if (n < 0 || w < 0 || (cell_bits != 8 && cell_bits != 16)) return BSW_E_INVAL;
+    if (n > 0 && !pairs) return BSW_E_INVAL;
+    return BSW_OK;
+}
+
+int bsw_get_scores(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef,
+                   const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits)
+{
+    if (!ctx) return BSW_E_INVAL;
+    int rc = validate(pairs, n, w, cell_bits);
+    if (rc) return rc;
+    if (n == 0) return BSW_OK;
+    if (!seqBufRef || !seqBufQer) return BSW_E_INVAL;
+    for (int32_t i = 0; i < n; ++i)
+        if (pairs[i].len1 < 0 || pairs[i].len2 < 0 || pairs[i].len1 > BSW_MAX_LEN ||
+            pairs[i].len2 > BSW_MAX_LEN || pairs[i].idr < 0 || pairs[i].idq < 0)
+            return BSW_E_RANGE;
+    const int nd = (int)ctx->devs.size();
+    std::vector<int> rcs(nd, BSW_OK);
+    std::vector<bsw_stats_t> st(nd);
+    if (nd == 1) {
+        rcs[0] = bsw::host_shard(ctx->kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, &st[0]);
+    } else {
+        std::vector<std::thread> th;
+        for (int d = 0; d < nd; ++d) {
+            const int32_t a = (int32_t)((int64_t)n * d / nd), b = (int32_t)((int64_t)n * (d + 1) / nd);
+            th.emplace_back([&, d, a, b] {
+                rcs[d] = bsw::host_shard(ctx->kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer,
+                                         b - a, w, &st[d]);
+            });
+        }
+        for (auto &t : th) t.join();
+    }
+    bsw_stats_t agg{};
+    for (int d = 0; d < nd; ++d) {
+        if (rcs[d]) return rcs[d];
+        agg.kernel_ms = std::max(agg.kernel_ms, st[d].kernel_ms);
+        agg.n_i16 += st[d].n_i16; agg.n_u8 += st[d].n_u8; agg.n_wide += st[d].n_wide;
+        agg.n_launches += st[d].n_launches;
+    }
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    ctx->last = agg;
+    return BSW_OK;
+}
+
+int bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref,
+                          const uint8_t *d_qer, int32_t n, int32_t w, int cell_bits, void *stream)
+{
+    if (!ctx) return BSW_E_INVAL;
+    int rc = validate(d_pairs, n, w, cell_bits);
+    if (rc) return rc;
+    if (n == 0) return BSW_OK;
+    if (!d_ref || !d_qer) return BSW_E_INVAL;
+    bsw::DeviceCtx &dc = *ctx->devs[0];
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        hipStream_t st = stream ? (hipStream_t)stream : slot->stream;
+        int r = bsw::run_device(ctx->kp, *slot, d_pairs, d_ref, d_qer, n, w, st);
+        if (r) return r;
+        if ((r = bsw::finish_stats(*slot))) return r;
+        if (slot->h_meta[9] != 0) return BSW_E_RANGE;
+        std::lock_guard<std::mutex> g(ctx->stats_mu);
+        ctx->last = slot->stats;
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+
+int bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out)
+{
+    if (!ctx || !out) return BSW_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    *out = ctx->last;
+    return BSW_OK;
+}
+
+const char *bsw_strerror(int code)
+{
+    switch (code) {
+    case BSW_OK: return "ok";
+    case BSW_E_INVAL: return "invalid argument";
+    case BSW_E_NOMEM: return "out of device or pinned host memory";
+    case BSW_E_NODEV: return "no such HIP device";
+    case BSW_E_HIP: return "HIP runtime error";
+    case BSW_E_RANGE: return "pair exceeds supported lengths";
+    default: return "unknown error";
+    }
+}
+
+int bsw_abi_version(void) { return BSW_ABI_VERSION; }
+
+}  // extern "C"

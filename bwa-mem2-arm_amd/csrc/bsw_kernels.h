@@ -1,0 +1,42 @@
+// bsw_kernels.h -- host-visible launch interface of the seed-extension DP kernels (gfx950).
+//
+// Kernel families:
+//   lane kernel  : one LANE per SeqPair, the whole DP row of the pair (eh[0..qlen], packed
+//                  {h:16, e:16} per column) held in VGPRs; 64 pairs per wavefront advance
+//                  through their target rows in lock-step.  qlen <= QMAX (template), int16 cells.
+//   wide kernel  : one lane per pair, eh row in HBM scratch, int32 cells; any length.
+//                  Used for qlen > QMAX or scores that could overflow int16.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+#include "../../include/bsw_seqpair.h"
+
+namespace bsw {
+
+// Scoring constants as the kernels consume them.
+struct KParams {
+    int32_t o_del, e_del, o_ins, e_ins;
+    int32_t zdrop, end_bonus;
+    int32_t maxsc;              // max(0, max(mat)) -- A.2 band cap and the M-gate bound
+    int32_t pad;
+    uint32_t prof[8][2];        // prof[t] = 8 score bytes mat[t][q], q = 0..7 (q>4 -> ambig)
+    int8_t mat[25];
+};
+
+// qlen limit of the register-resident kernel instantiations.
+constexpr int kLaneQmax[] = {32, 64, 96, 128, 160};
+constexpr int kLaneQmaxMax = 160;
+
+// Launch the lane kernel for pairs order[0..n) (indices into pairs).  qlen of every pair
+// must be <= qmax (one of kLaneQmax) and h0 + maxsc*min(len1,len2) < 32768.
+hipError_t launch_lane_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
+                              const int32_t *order, int32_t n, const uint8_t *ref,
+                              const uint8_t *qer, int32_t *err, hipStream_t s);
+
+// Wide kernel: any qlen/tlen, int32 cells, eh scratch of n * (max_qlen + 2) int2 in HBM.
+hipError_t launch_wide_kernel(const KParams &kp, int32_t w, SeqPair *pairs,
+                              const int32_t *order, int32_t n, const uint8_t *ref,
+                              const uint8_t *qer, int2 *scratch, int32_t scratch_stride,
+                              hipStream_t s);
+
+}  // namespace bsw

@@ -1,0 +1,184 @@
+"""ctypes binding of the product C ABI (include/bsw.h -> lib/libbsw_hip.so) and of the
+synthetic-batch tool (lib/libbsw_synth.so).
+
+This is plumbing for tests and bench.py: the product is the C ABI / C++ shim; PyTorch
+is used only for device memory, streams and torch.distributed.  Loading fails loudly
+when the HIP library is missing -- there is no CPU fallback anywhere in this module.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(PKG, "lib")
+HIP_LIB = os.path.join(LIBDIR, "libbsw_hip.so")
+SYNTH_LIB = os.path.join(LIBDIR, "libbsw_synth.so")
+
+SEQPAIR_DTYPE = np.dtype(
+    [(n, "<i4") for n in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid",
+                          "score", "tle", "gtle", "qle", "gscore", "max_off")]
+)
+OUT_FIELDS = ("score", "tle", "gtle", "qle", "gscore", "max_off")
+assert SEQPAIR_DTYPE.itemsize == 56
+
+# Every symbol include/bsw.h declares (tests check the library exports all of them).
+ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_scores",
+               "bsw_get_scores_device", "bsw_last_stats", "bsw_strerror", "bsw_abi_version")
+
+
+class Params(ctypes.Structure):
+    """Mirror of bsw_params_t (include/bsw.h)."""
+    _fields_ = [("o_del", ctypes.c_int32), ("e_del", ctypes.c_int32),
+                ("o_ins", ctypes.c_int32), ("e_ins", ctypes.c_int32),
+                ("zdrop", ctypes.c_int32), ("end_bonus", ctypes.c_int32),
+                ("mat", ctypes.c_int8 * 25), ("w_match", ctypes.c_int8),
+                ("w_mismatch", ctypes.c_int8), ("w_ambig", ctypes.c_int8)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_float), ("n_i16", ctypes.c_int32),
+                ("n_u8", ctypes.c_int32), ("n_wide", ctypes.c_int32),
+                ("n_launches", ctypes.c_int32)]
+
+
+def default_params(a=1, b=4, o_del=6, e_del=1, o_ins=6, e_ins=1, zdrop=100, end_bonus=5,
+                   ambig=-1, mat=None) -> Params:
+    p = Params()
+    p.o_del, p.e_del, p.o_ins, p.e_ins = o_del, e_del, o_ins, e_ins
+    p.zdrop, p.end_bonus = zdrop, end_bonus
+    if mat is None:
+        mat = [ambig if (t == 4 or q == 4) else (a if t == q else -b)
+               for t in range(5) for q in range(5)]
+    for i, v in enumerate(mat):
+        p.mat[i] = int(v)
+    p.w_match, p.w_mismatch, p.w_ambig = a, -b, ambig
+    return p
+
+
+class BswError(RuntimeError):
+    pass
+
+
+_hip = None
+
+
+def hip_lib():
+    """Load libbsw_hip.so (raises if it was not built: no silent fallback)."""
+    global _hip
+    if _hip is None:
+        if not os.path.exists(HIP_LIB):
+            raise BswError(f"{HIP_LIB} not built: run `make` or __graft_entry__.build()")
+        L = ctypes.CDLL(HIP_LIB)
+        P = ctypes.c_void_p
+        L.bsw_params_default.argtypes = [P]
+        L.bsw_create.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
+        L.bsw_destroy.argtypes = [P]
+        L.bsw_get_scores.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
+        L.bsw_get_scores_device.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int, P]
+        L.bsw_last_stats.argtypes = [P, P]
+        L.bsw_strerror.restype = ctypes.c_char_p
+        L.bsw_strerror.argtypes = [ctypes.c_int]
+        for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
+                  "bsw_abi_version"):
+            getattr(L, f).restype = ctypes.c_int
+        _hip = L
+    return _hip
+
+
+def _check(rc):
+    if rc != 0:
+        raise BswError(f"bsw error {rc}: {hip_lib().bsw_strerror(rc).decode()}")
+
+
+def _ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Engine:
+    """Python mirror of the C++ shim: one engine = one bsw_ctx_t."""
+
+    def __init__(self, params: Params | None = None, device: int = 0, n_gpus: int = 1):
+        self.params = params if params is not None else default_params()
+        self._ctx = ctypes.c_void_p()
+        _check(hip_lib().bsw_create(ctypes.byref(self.params), device, n_gpus,
+                                    ctypes.byref(self._ctx)))
+
+    def close(self):
+        if self._ctx:
+            hip_lib().bsw_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def get_scores(self, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray, w: int,
+                   cell_bits: int = 16):
+        """getScores16 / getScores8 on host buffers; results in place in `pairs`."""
+        assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+        ref = np.ascontiguousarray(ref, dtype=np.uint8)
+        qer = np.ascontiguousarray(qer, dtype=np.uint8)
+        _check(hip_lib().bsw_get_scores(self._ctx, _ptr(pairs), _ptr(ref), _ptr(qer),
+                                        len(pairs), w, cell_bits))
+
+    def get_scores_device(self, d_pairs: int, d_ref: int, d_qer: int, n: int, w: int,
+                          cell_bits: int = 16, stream: int = 0):
+        """Device-resident call: raw device pointers (e.g. torch tensor .data_ptr())."""
+        _check(hip_lib().bsw_get_scores_device(self._ctx, ctypes.c_void_p(d_pairs),
+                                               ctypes.c_void_p(d_ref), ctypes.c_void_p(d_qer),
+                                               n, w, cell_bits, ctypes.c_void_p(stream)))
+
+    def last_stats(self) -> Stats:
+        s = Stats()
+        _check(hip_lib().bsw_last_stats(self._ctx, ctypes.byref(s)))
+        return s
+
+
+# ---------------------------------------------------------------- synthetic batches
+class SynthCfg(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("tlen", ctypes.c_int32), ("qlen", ctypes.c_int32),
+                ("h0_lo", ctypes.c_int32), ("h0_hi", ctypes.c_int32),
+                ("p_sub", ctypes.c_double), ("p_indel", ctypes.c_double),
+                ("p_unrelated", ctypes.c_double), ("p_n", ctypes.c_double)]
+
+
+_synth = None
+
+
+def synth_lib():
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_LIB):
+            raise BswError(f"{SYNTH_LIB} not built: run `make synth`")
+        L = ctypes.CDLL(SYNTH_LIB)
+        L.bsw_synth_default.argtypes = [ctypes.c_void_p]
+        L.bsw_synth_batch.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _synth = L
+    return _synth
+
+
+def synth_cfg(**kw) -> SynthCfg:
+    c = SynthCfg()
+    synth_lib().bsw_synth_default(ctypes.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def synth_batch(n: int, pair_base: int = 0, cfg: SynthCfg | None = None):
+    """C2 workload batch: (pairs, ref, qer) numpy arrays in the upstream layout."""
+    cfg = cfg if cfg is not None else synth_cfg()
+    pairs = np.zeros(n, dtype=SEQPAIR_DTYPE)
+    ref = np.zeros(max(1, n * cfg.tlen), dtype=np.uint8)
+    qer = np.zeros(max(1, n * cfg.qlen), dtype=np.uint8)
+    synth_lib().bsw_synth_batch(ctypes.byref(cfg), pair_base, n, _ptr(pairs), _ptr(ref),
+                                _ptr(qer))
+    return pairs, ref, qer

@@ -1,0 +1,105 @@
+/*
+ * bsw.h -- C ABI of the MI355X-native seed-extension engine (banded Smith-Waterman,
+ * BWA-MEM2 `BandedPairWiseSW::getScores16/getScores8` semantics = `ksw_extend2`).
+ *
+ * Plain pointers and sizes only (no torch, no HIP types in the signatures), so an
+ * upstream bwa-mem2 build, a ctypes loader or any FFI can bind it.  Every entry point
+ * below names the reference interface it replaces:
+ *
+ *   bsw_create        <- BandedPairWiseSW::BandedPairWiseSW(o_del, e_del, o_ins, e_ins,
+ *                        zdrop, end_bonus, mat, w_match, w_mismatch, numThreads)
+ *                        (call site: docs-archive/INTEGRATION_COMPLETE.md:61-63)
+ *   bsw_destroy       <- BandedPairWiseSW::~BandedPairWiseSW (frees the F8_/H8_ scratch,
+ *                        PHASE2_WEEK1_WEEK2_COMPLETE.md:83-98)
+ *   bsw_get_scores    <- getScores16 / getScores8 (SeqPair*, uint8_t *seqBufRef,
+ *                        uint8_t *seqBufQer, int32_t numPairs, uint16_t numThreads,
+ *                        int32_t w)   (docs-archive/WEEK1_WRAPPER_COMPLETE.md:259-269)
+ *                        with cell_bits = 16 or 8 selecting the entry point.
+ *   bsw_get_scores_device   device-resident form of the same call (inputs already in
+ *                        HBM; what bench.py times).  No upstream counterpart.
+ *
+ * Semantics: for every pair p in [0, n) the outputs p.score, p.tle, p.gtle, p.qle,
+ * p.gscore, p.max_off are bit-identical to scalar `ksw_extend2(qlen=len2,
+ * query=seqBufQer+idq, tlen=len1, target=seqBufRef+idr, m=5, mat, o_del, e_del, o_ins,
+ * e_ins, w, end_bonus, zdrop, h0, ...)`.  Inputs are base codes 0..4 (4 = N).
+ * Unlike upstream, nothing is written to pairs[n .. roundUp(n, SIMD_WIDTH)).
+ *
+ * Errors: every call returns 0 or a negative BSW_E* code; nothing throws; nothing
+ * falls back to the CPU (there is no CPU path in the product).  The C++ shim
+ * (bandedSWA_gpu.h) keeps upstream's `void` + fprintf/exit convention on top.
+ * Thread safety: bsw_get_scores may be called concurrently on one context (upstream
+ * calls getScores* from kt_for workers); each call takes its own stream + buffers.
+ */
+#ifndef BSW_H
+#define BSW_H
+
+#include <stdint.h>
+#include "bsw_seqpair.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSW_ABI_VERSION 1
+
+enum {
+    BSW_OK = 0,
+    BSW_E_INVAL = -22,      /* bad argument (null pointer, n < 0, bad cell_bits, bad params) */
+    BSW_E_NOMEM = -12,      /* device or pinned host allocation failed                      */
+    BSW_E_NODEV = -19,      /* no HIP device / device index out of range                    */
+    BSW_E_HIP = -5,         /* a HIP runtime call or kernel launch failed                   */
+    BSW_E_RANGE = -34       /* a pair exceeds a supported size (len > BSW_MAX_LEN)          */
+};
+
+#define BSW_MAX_LEN 32767     /* per-sequence length limit (int16 cell range, upstream MAX_SEQ_LEN16) */
+
+/* Scoring parameters: the upstream BandedPairWiseSW constructor arguments. */
+typedef struct bsw_params_t {
+    int32_t o_del, e_del, o_ins, e_ins;   /* gap open / extend (positive penalties)   */
+    int32_t zdrop;                        /* z-drop; <= 0 disables                      */
+    int32_t end_bonus;                    /* opt->pen_clip5 at the call site            */
+    int8_t  mat[25];                      /* 5x5 score matrix [target*5 + query]       */
+    int8_t  w_match, w_mismatch;          /* opt->a, -opt->b (kept for the shim)       */
+    int8_t  w_ambig;                      /* score vs N; upstream DEFAULT_AMBIG = -1   */
+} bsw_params_t;
+
+typedef struct bsw_ctx bsw_ctx_t;
+
+/* Fill *p with bwa-mem defaults: -A1 -B4 -O6,6 -E1,1 -d100 -L5 (mat = bwa_fill_scmat). */
+void bsw_params_default(bsw_params_t *p);
+
+/* Create an engine on HIP devices [device0, device0 + n_gpus).  n_gpus >= 1.
+ * Host-buffer calls shard each batch across those devices by contiguous pair range. */
+int  bsw_create(const bsw_params_t *params, int device0, int n_gpus, bsw_ctx_t **out);
+void bsw_destroy(bsw_ctx_t *ctx);
+
+/* Blocking host-buffer call (drop-in for getScores16 / getScores8).
+ * cell_bits: 16 -> int16 cells; 8 -> uint8 cells for pairs whose scores provably fit
+ * (h0 + max(mat) * min(len1, len2) <= 255), int16 for the rest (overflow fallback). */
+int  bsw_get_scores(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef,
+                    const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits);
+
+/* Device-resident call on the context's first device: d_pairs, d_ref and d_qer are
+ * device pointers (idr / idq index d_ref / d_qer); results are written into d_pairs.
+ * Runs on `stream` (a hipStream_t, or NULL for a stream of the context's own) and
+ * returns when the results are in d_pairs (blocking, like getScores*). */
+int  bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref,
+                           const uint8_t *d_qer, int32_t n, int32_t w, int cell_bits,
+                           void *stream);
+
+/* Per-call statistics of the last bsw_get_scores_device / bsw_get_scores on this
+ * thread: the hot kernel's event-timed duration (ms) and the pairs routed per kernel. */
+typedef struct bsw_stats_t {
+    float   kernel_ms;          /* sum of DP-kernel durations (HIP events, same stream) */
+    int32_t n_i16, n_u8, n_wide; /* pairs per kernel class                               */
+    int32_t n_launches;         /* DP-kernel launches                                    */
+} bsw_stats_t;
+int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
+
+const char *bsw_strerror(int code);
+int  bsw_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSW_H */

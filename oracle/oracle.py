@@ -1,0 +1,97 @@
+"""ctypes binding of the CPU oracle library (oracle/liboracle.so) -- TEST INFRASTRUCTURE.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+Exposes the scalar `ksw_extend2` restatement (oracle/ksw_ext_ref.c) and the SSE4.1
+inter-pair restatement of upstream's getScores16 (oracle/bsw_sse41.c), both over numpy
+arrays in the upstream SeqPair layout.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+SEQPAIR_DTYPE = np.dtype(
+    [(n, "<i4") for n in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid",
+                          "score", "tle", "gtle", "qle", "gscore", "max_off")]
+)
+OUT_FIELDS = ("score", "tle", "gtle", "qle", "gscore", "max_off")
+assert SEQPAIR_DTYPE.itemsize == 56
+
+
+class OracleParams(ctypes.Structure):
+    _fields_ = [("o_del", ctypes.c_int32), ("e_del", ctypes.c_int32),
+                ("o_ins", ctypes.c_int32), ("e_ins", ctypes.c_int32),
+                ("zdrop", ctypes.c_int32), ("end_bonus", ctypes.c_int32),
+                ("mat", ctypes.c_int8 * 25)]
+
+
+def make_params(o_del=6, e_del=1, o_ins=6, e_ins=1, zdrop=100, end_bonus=5, mat=None):
+    from ksw_ext_ref import bwa_fill_scmat  # noqa: E402  (sibling module)
+    p = OracleParams()
+    p.o_del, p.e_del, p.o_ins, p.e_ins = o_del, e_del, o_ins, e_ins
+    p.zdrop, p.end_bonus = zdrop, end_bonus
+    for i, v in enumerate(mat if mat is not None else bwa_fill_scmat()):
+        p.mat[i] = v
+    return p
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `make oracle` (or __graft_entry__.build())")
+        _lib = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        _lib.oracle_ksw_extend2.restype = ctypes.c_int
+        _lib.oracle_ksw_extend2.argtypes = [ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P] + \
+            [ctypes.c_int] * 8 + [P] * 5
+        _lib.oracle_get_scores.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32]
+        _lib.oracle_get_scores_mt.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
+        _lib.sse41_get_scores16.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
+        _lib.sse41_get_scores16.restype = ctypes.c_int
+    return _lib
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def ksw_extend2(query, target, params: OracleParams, w, h0):
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    t = np.ascontiguousarray(target, dtype=np.uint8)
+    outs = [ctypes.c_int() for _ in range(5)]
+    mat = np.frombuffer(bytes(params.mat), dtype=np.int8).copy()
+    sc = lib().oracle_ksw_extend2(len(q), _ptr(q), len(t), _ptr(t), 5, _ptr(mat),
+                                  params.o_del, params.e_del, params.o_ins, params.e_ins,
+                                  w, params.end_bonus, params.zdrop, h0,
+                                  *[ctypes.byref(o) for o in outs])
+    qle, tle, gtle, gscore, max_off = (o.value for o in outs)
+    return sc, qle, tle, gtle, gscore, max_off
+
+
+def get_scores(params: OracleParams, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray, w: int,
+               nthreads: int = 1):
+    """In place on `pairs` (structured SEQPAIR_DTYPE array)."""
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    if nthreads > 1:
+        lib().oracle_get_scores_mt(ctypes.byref(params), _ptr(pairs), _ptr(ref), _ptr(qer),
+                                   len(pairs), w, nthreads)
+    else:
+        lib().oracle_get_scores(ctypes.byref(params), _ptr(pairs), _ptr(ref), _ptr(qer),
+                                len(pairs), w)
+
+
+def sse41_get_scores16(params: OracleParams, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray,
+                       w: int, nthreads: int = 1) -> int:
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    return lib().sse41_get_scores16(ctypes.byref(params), _ptr(pairs), _ptr(ref), _ptr(qer),
+                                    len(pairs), w, nthreads)
