@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""bench.py -- M seed-extensions/s of the MI355X banded-SW engine (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "C2"): per GPU a resident synthetic SeqPair batch of
+1,000,000 pairs, 150 bp query / 300 bp ref window, band w = 100, int16 cells, bwa-mem
+default scoring (-A1 -B4 -O6 -E1 -d100 -L5); generator bwa-mem2-arm_amd/csrc/bsw_synth.c
+(splitmix64 seed 42; 2% subs, 0.2% indels, 10% unrelated queries, 0.1% N, h0 U[19,100]).
+
+One step = one bsw_get_scores_device() call over the whole resident batch (plan + sort +
+DP kernel + results written back into the SeqPair records in HBM).  Inputs are resident in
+HBM before timing starts.  N GPUs: one process per GPU (torchrun), each with its own
+1M-pair shard (weak scaling, pairs are independent -> no data-path collective); the
+control plane (barriers, max-over-ranks timing) is torch.distributed/gloo.
+
+Reported beside the metric:
+  roofline     -- dominant kernel (lane_kernel<160>), integer-VALU bound: algorithmic ops
+                  = 14 int ops x 25,100 static band cells per pair per
+                  launch / HIP-event-timed launch duration, vs the gfx950 packed-int16 VALU
+                  peak; traffic = HBM bytes per launch from rocprofv3 PMC (profiles/).
+  cpu_baseline -- oracle/bsw_sse41.c (restated upstream SSE4.1 getScores16 design, "port")
+                  on a bounded sample of the same batch, rank 0, N = 1 only.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bwa-mem2-arm_amd", "py"))
+
+import numpy as np  # noqa: E402
+
+import hiprt  # noqa: E402  (loads the HIP runtime before anything imports torch)
+import bsw  # noqa: E402
+
+METRIC = "M seed-extensions/sec (150 bp, band=100) at 1/2/4/8 MI355X vs CPU"
+UNIT = "M seed-extensions/s"
+STATIC_CELLS_C2 = 25_100          # band cells per pair at 150/300, w=100
+OPS_PER_CELL = 14                 # algorithmic int ops per cell
+# gfx950 integer VALU peak, packed int16: 256 CU x 4 SIMD x 32 lanes x 2 (v_pk) x 2.4 GHz
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2 * 2.4e9 / 1e12
+
+
+def static_band_cells(qlen: int, tlen: int, w: int, maxsc=1, end_bonus=5, o=6, e=1) -> int:
+    wl = min(w, max((qlen * maxsc + end_bonus - o + e) // e, 1))
+    return sum(max(0, min(qlen, i + wl + 1) - max(0, i - wl)) for i in range(tlen))
+
+
+def dist_init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    return rank, local, world
+
+
+def allreduce_max(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world: int):
+    hiprt.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def traffic_per_launch(kernel_name: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
+    (profiles/pmc_latest.json, written by tools/profile.sh); None if absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        return d.get(kernel_name, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
+    """oracle/bsw_sse41.c on a bounded sample (first S pairs), median of 3 after warm-up."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # CPU baseline leg only (test infrastructure)
+    P = oracle.make_params()
+    S = min(len(pairs), 200_000)
+    sample = pairs[:S]
+    times = []
+    out = None
+    for k in range(4):
+        a = sample.copy()
+        t = time.perf_counter()
+        oracle.sse41_get_scores16(P, a, ref, qer, w, cores)
+        dt = time.perf_counter() - t
+        if k:
+            times.append(dt)
+        out = a
+    sse_mt = S / statistics.median(times) / 1e6
+    S1 = min(len(pairs), 20_000)
+    a = pairs[:S1].copy()
+    t = time.perf_counter()
+    oracle.sse41_get_scores16(P, a, ref, qer, w, 1)
+    sse_1t = S1 / (time.perf_counter() - t) / 1e6
+    S2 = min(len(pairs), 10_000)
+    a = pairs[:S2].copy()
+    t = time.perf_counter()
+    oracle.get_scores(P, a, ref, qer, w, 1)
+    scalar_1t = S2 / (time.perf_counter() - t) / 1e6
+    agree = all(np.array_equal(out[f], gpu_pairs[:S][f]) for f in bsw.OUT_FIELDS)
+    return {
+        "value": round(sse_mt, 4), "unit": UNIT, "cores": cores, "kind": "port",
+        "sample": f"first {S} pairs of the rank-0 C2 batch; oracle/bsw_sse41.c (SSE4.1, 8 x int16 "
+                  f"lanes, restated upstream getScores16 design), {cores} threads, median of 3 after 1 warm-up",
+        "sse41_1thread": round(sse_1t, 4), "scalar_ksw_extend2_1thread": round(scalar_1t, 4),
+        "outputs_identical_to_gpu": bool(agree),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=1_000_000, help="pairs per GPU")
+    ap.add_argument("--w", type=int, default=100)
+    ap.add_argument("--cell-bits", type=int, default=16, choices=(8, 16))
+    ap.add_argument("--h0-hi", type=int, default=100, help="h0 upper bound (C3 uses 105)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    rank, local, world = dist_init()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    hiprt.set_device(local)
+
+    cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
+    t0 = time.perf_counter()
+    pairs, ref, qer = bsw.synth_batch(args.pairs, pair_base=rank * args.pairs, cfg=cfg)
+    gen_s = time.perf_counter() - t0
+    d_pairs = hiprt.DeviceBuffer.from_array(pairs)
+    d_ref = hiprt.DeviceBuffer.from_array(ref)
+    d_qer = hiprt.DeviceBuffer.from_array(qer)
+    eng = bsw.Engine(device=local)
+
+    def step():
+        eng.get_scores_device(d_pairs.ptr, d_ref.ptr, d_qer.ptr, args.pairs, args.w, args.cell_bits)
+
+    for _ in range(args.warmup):
+        step()
+    kms = []
+    barrier(world)
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kms.append(eng.last_stats().kernel_ms)
+    barrier(world)
+    dt = time.perf_counter() - t
+    dt_max = allreduce_max(dt, world)
+    st = eng.last_stats()
+
+    res = np.empty_like(pairs)
+    d_pairs.download(res)
+    if rank != 0:
+        return
+    total_pairs = args.pairs * world * args.steps
+    value = total_pairs / dt_max / 1e6
+    kms_mean = float(np.mean(kms))
+    per_launch_pairs = args.pairs if st.n_launches == 1 else None
+    cells = STATIC_CELLS_C2 if (cfg.qlen, cfg.tlen, args.w) == (150, 300, 100) else \
+        static_band_cells(cfg.qlen, cfg.tlen, args.w)
+    achieved = (args.pairs * cells * OPS_PER_CELL) / (kms_mean * 1e-3) / 1e12
+    kname = "lane_kernel<160>"
+    roof = {
+        "bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
+        "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
+        "traffic": traffic_per_launch(kname),
+        "kernel": kname, "launch_ms": round(kms_mean, 4),
+        "cells_per_s": round(args.pairs * cells / (kms_mean * 1e-3) / 1e12, 4),
+        "cells_unit": "T band cells/s (25,100 static cells/pair)",
+        "algorithmic": f"{OPS_PER_CELL} int ops x {cells} band cells x {args.pairs} pairs per launch",
+        "pairs_per_launch": per_launch_pairs,
+    }
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": UNIT, "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int16" if args.cell_bits == 16 else "u8+int16",
+        "data": "synthetic (bsw_synth.c, seed 42)",
+        "config": {"workload": f"C2: {args.pairs} SeqPairs/GPU resident in HBM, {cfg.qlen} bp query / "
+                               f"{cfg.tlen} bp ref, band w={args.w}, cell_bits={args.cell_bits}, "
+                               f"h0 U[{cfg.h0_lo},{cfg.h0_hi}]",
+                   "pairs_per_gpu": args.pairs, "parallelism": f"shard{world} (independent pairs)"},
+        "roofline": roof,
+        "kernel_only_value": round(args.pairs * world / (kms_mean * 1e-3) / 1e6, 3),
+    }
+    if world == 1 and not args.no_cpu:
+        cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        out["cpu_baseline"] = cpu_baseline(pairs, ref, qer, args.w, res, cores)
+        out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
+    out["synth_gen_s"] = round(gen_s, 2)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -35,7 +35,7 @@ namespace bsw {
 constexpr int kNumLaneClasses = 5;          // QMAX 32, 64, 96, 128, 160
 constexpr int kWideClass = kNumLaneClasses; // index of the wide-kernel class
 constexpr int kNumClasses = kNumLaneClasses + 1;
-constexpr int kKeyBits = 27;                // 3 class bits + 8 qlen bits + 16 tlen bits
+constexpr int kKeyBits = 31;                // 3 class + 8 qlen + 12 tlen + 8 h0 bits
 
 // Per pair: class + sort key.  Lane classes need qlen <= QMAX and int16-safe scores.
 __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_t maxsc,
@@ -43,8 +43,9 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
                             int32_t *__restrict__ counts, int32_t *__restrict__ maxq_wide)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const SeqPair p = pairs[i];
+    const bool valid = i < n;
+    SeqPair p{};
+    if (valid) p = pairs[i];
     const int qlen = max(p.len2, 0), tlen = max(p.len1, 0);
     const int64_t hi = (int64_t)max(p.h0, 0) + (int64_t)max(maxsc, 0) * min(qlen, tlen);
     int c = kWideClass;
@@ -55,11 +56,21 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
         else if (qlen <= 128) c = 3;
         else if (qlen <= 160) c = 4;
     }
-    if (c == kWideClass) atomicMax(maxq_wide, qlen);
-    keys[i] = ((uint32_t)c << 24) | ((uint32_t)(255 - min(qlen, 255)) << 16) |
-              (uint32_t)(65535 - min(tlen, 65535));
-    vals[i] = i;
-    atomicAdd(&counts[c], 1);
+    if (valid) {
+        if (c == kWideClass) atomicMax(maxq_wide, qlen);
+        // (class, qlen desc, tlen desc, h0 desc): like-shaped pairs share a wavefront, and
+        // equal h0 gives lanes similar band-end trajectories (fewer masked edge groups)
+        keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
+                  ((uint32_t)(4095 - min(tlen, 4095)) << 8) | (uint32_t)(255 - min(max(p.h0, 0), 255));
+        vals[i] = i;
+    }
+    // one atomic per wave and class (1M same-address atomics cost ~11 ms)
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < kNumClasses; ++k) {
+        const unsigned long long m = __ballot(valid && c == k);
+        if (m && lane == __ffsll((long long)m) - 1) atomicAdd(&counts[k], __popcll(m));
+    }
 }
 
 struct Slot {

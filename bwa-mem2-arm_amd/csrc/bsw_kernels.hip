@@ -23,6 +23,23 @@
 #include <utility>
 #include "bsw_kernels.h"
 
+// Timing-only experiment hooks (never defined in product builds): extra dummy instructions
+// injected into the fast group, writing temps that are dead at that point.
+#if defined(BSW_EXP_SDWA)
+#define BSW_EXP_EXTRA BSW_X4("v_min_i32_sdwa %[k0], sext(%[pw]), %[v0] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:WORD_0\n\t")
+#elif defined(BSW_EXP_PLAIN)
+#define BSW_EXP_EXTRA BSW_X4("v_min_i32_e32 %[k0], %[pw], %[v0]\n\t")
+#elif defined(BSW_EXP_VOP3)
+#define BSW_EXP_EXTRA BSW_X4("v_max3_i32 %[k0], %[pw], %[v0], 0\n\t")
+#elif defined(BSW_EXP_BRANCH)
+#define BSW_EXP_EXTRA "s_branch 7f\n7:\n\t"
+#elif defined(BSW_EXP_SALU)
+#define BSW_EXP_EXTRA BSW_X4("s_add_u32 %[st], %[st], 1\n\t")
+#else
+#define BSW_EXP_EXTRA
+#endif
+#define BSW_X4(x) x x x x x x x x x x x x x x x x
+
 #ifndef BSW_CELL_FENCE
 #define BSW_CELL_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
@@ -42,7 +59,16 @@ __device__ __forceinline__ int wave_max(int x)
     int c = __builtin_amdgcn_readlane(x, 47), d = __builtin_amdgcn_readlane(x, 63);
     return max(max(a, b), max(c, d));
 }
-__device__ __forceinline__ int wave_min(int x) { return -wave_max(-x); }
+__device__ __forceinline__ int wave_min(int x)
+{
+    x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x111, 0xf, 0xf, false));
+    x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x112, 0xf, 0xf, false));
+    x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x114, 0xf, 0xf, false));
+    x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x118, 0xf, 0xf, false));
+    int a = __builtin_amdgcn_readlane(x, 15), b = __builtin_amdgcn_readlane(x, 31);
+    int c = __builtin_amdgcn_readlane(x, 47), d = __builtin_amdgcn_readlane(x, 63);
+    return min(min(a, b), min(c, d));
+}
 
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
@@ -50,6 +76,8 @@ __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b)
 struct LaneRow {          // per-row uniform (SGPR) bounds
     int ulo, uhi;         // min beg / max end over live lanes (columns outside: skipped)
     int fast_lo, fast_hi; // max beg / min end over live lanes (columns inside: unmasked)
+    int glo, gsp;         // groups touching [ulo, uhi]: glo <= G <= glo + gsp
+    int gfa, gfn;         // groups fully inside [fast_lo, fast_hi): gfa <= G < gfa + gfn
 };
 
 struct LaneCx {           // per-kernel constants
@@ -88,79 +116,238 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[NE], int s, int &f, int
     h1 = h;
 }
 
-// Row pass structure.  Per row the wave knows, over its live lanes,
-//   [flo, fhi)  : columns where EVERY live lane is in band  -> fast pass, no lane masks
-//   [elo, ehi]  : remaining columns up to the largest end   -> edge pass, per-lane masks
-// Both passes are straight-line unrolled sequences whose columns are guarded only by
-// uniform (SGPR) range tests -- no if/else pair ever writes the same eh[] register, so the
-// row stays in place in its VGPRs (no merge copies).
+// Row structure.  The row's columns are visited as 4-column groups in a
+// straight unrolled sequence.  Per group one uniform (SGPR) test decides:
+//   skip   : group outside [min beg, max end] of the live lanes;
+//   fast   : every live lane is in band for all four columns -> one inline-asm block,
+//            no lane masks, eh[]/f/h1/key/lp1 updated IN PLACE (tied "+v" operands);
+//   masked : otherwise each column runs under its per-lane EXEC mask (band edges).
+// Only the masked path (a few columns per row) pays merge copies.
 
-// Fast-pass column J.
-template <int J, int QMAX, int SM, bool SYM>
-__device__ __forceinline__ void lane_col_fast(uint32_t (&eh)[QMAX + 1], uint32_t pw, int &f, int &h1,
-                                              int &key, int &lp1, const LaneRow &r, const LaneCx &c)
-{
-    if constexpr (J < QMAX) {
-        if (J >= r.fast_lo && J < r.fast_hi)
-            lane_cell<J, SM, SYM, QMAX + 1>(eh, (int)(int8_t)(pw >> (8 * (J & 3))), f, h1, key, lp1, c);
-    }
-}
-
-// Edge-pass column J: per-lane band membership under EXEC; at j == end write
+// Masked column J: per-lane band membership under EXEC; at j == end write
 // { H(i,end-1), 0 } (A.4 end of row); beyond end leave eh untouched (A.7 stale columns).
 template <int J, int QMAX, int SM, bool SYM>
-__device__ __forceinline__ void lane_col_edge(uint32_t (&eh)[QMAX + 1], const uint32_t (&q4)[QMAX / 4],
-                                              uint2 pr, int beg, int end, int &f, int &h1, int &key,
-                                              int &lp1, const LaneRow &r, const LaneCx &c)
+__device__ __forceinline__ void lane_col_masked(uint32_t (&eh)[QMAX + 1], int s, int beg, int end,
+                                                int &f, int &h1, int &key, int &lp1,
+                                                const LaneRow &r, const LaneCx &c)
 {
     if (J < r.ulo || J > r.uhi) return;                   // uniform
     if constexpr (J < QMAX) {
         if (J >= beg && J < end) {
-            const uint32_t pw = __builtin_amdgcn_perm(pr.y, pr.x, q4[J / 4]);
-            lane_cell<J, SM, SYM, QMAX + 1>(eh, (int)(int8_t)(pw >> (8 * (J & 3))), f, h1, key,
-                                            lp1, c);
+            lane_cell<J, SM, SYM, QMAX + 1>(eh, s, f, h1, key, lp1, c);
             return;
         }
     }
     if (J == end) eh[J] = (uint32_t)h1;
 }
 
-template <int G, int QMAX, int SM, bool SYM>
-__device__ __forceinline__ void lane_group_fast(uint32_t (&eh)[QMAX + 1], const uint32_t (&q4)[QMAX / 4],
-                                                uint2 pr, int &f, int &h1, int &key, int &lp1,
-                                                const LaneRow &r, const LaneCx &c)
+// One 4-column group, default scoring (max(mat) == 1, symmetric gaps), as ONE asm
+// statement, so the compiler sees a single in-place update of eh[4G..4G+3], f, h1, key,
+// lp1 (no control-flow merge of the DP row, hence no register copies):
+//   skip    : group outside [min beg, max end] of the live lanes (scalar test);
+//   phase 1 : the four cells' independent work -- M (gated), E' = max(E-e, M-oe, 0),
+//             max(M, E), M - oe -- shared by both bodies;
+//   fast    : every live lane in band (scalar test): the F chain (2 dependent ops per
+//             cell) with H / pack / key / last-positive interleaved -- 56 VALU per 4 cells;
+//   masked  : band edges by per-lane SELECTS (no EXEC changes): d = j - beg, in = d < span,
+//             inat = d <= span (j == end stores {H(i,end-1), 0}: E' forced to 0), j < beg
+//             resets F; out-of-band lanes pass H(i,j-1) along the chain but feed 0 to
+//             key / last-positive -- 92 VALU.
+template <int G>
+__device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint32_t &v2, uint32_t &v3,
+                                               uint32_t q, uint32_t plo, uint32_t phi, int &f,
+                                               int &h1, int &key, int &lp1, int oe, int ed,
+                                               int glo, int gsp, int gfa, int gfn, int beg, int span)
 {
-    constexpr int J0 = 4 * G;
-    if constexpr (J0 >= QMAX) return;
-    if (J0 + 3 < r.fast_lo || J0 >= r.fast_hi) return;   // uniform skip
-    const uint32_t pw = __builtin_amdgcn_perm(pr.y, pr.x, q4[G]);
-    lane_col_fast<J0 + 0, QMAX, SM, SYM>(eh, pw, f, h1, key, lp1, r, c);
-    lane_col_fast<J0 + 1, QMAX, SM, SYM>(eh, pw, f, h1, key, lp1, r, c);
-    lane_col_fast<J0 + 2, QMAX, SM, SYM>(eh, pw, f, h1, key, lp1, r, c);
-    lane_col_fast<J0 + 3, QMAX, SM, SYM>(eh, pw, f, h1, key, lp1, r, c);
+    int m0, m1, m2, m3, t0, t1, t2, t3, x0, x1, x2, x3, ha, hb, k0, k1, l0, l1, pw, st, d, tp;
+    uint64_t sat, slt;
+    asm volatile(
+        "s_sub_u32 %[st], %[g], %[glo]\n\t"     // group outside [min beg, max end]: skip
+        "s_cmp_le_u32 %[st], %[gsp]\n\t"
+        "s_cbranch_scc0 3f\n\t"
+        "v_perm_b32 %[pw], %[phi], %[plo], %[q]\n\t"
+        BSW_EXP_EXTRA
+        "v_sub_u32_sdwa %[x0], %[v0], %[ed] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_sub_u32_sdwa %[x1], %[v1], %[ed] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_sub_u32_sdwa %[x2], %[v2], %[ed] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_sub_u32_sdwa %[x3], %[v3], %[ed] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_min_i32_sdwa %[m0], sext(%[pw]), %[v0] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:WORD_0\n\t"
+        "v_min_i32_sdwa %[m1], sext(%[pw]), %[v1] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:WORD_0\n\t"
+        "v_min_i32_sdwa %[m2], sext(%[pw]), %[v2] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:WORD_0\n\t"
+        "v_min_i32_sdwa %[m3], sext(%[pw]), %[v3] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %[m0], %[m0], %[v0] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %[m1], %[m1], %[v1] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %[m2], %[m2], %[v2] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %[m3], %[m3], %[v3] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_subrev_u32_e32 %[t0], %[oe], %[m0]\n\t"
+        "v_subrev_u32_e32 %[t1], %[oe], %[m1]\n\t"
+        "v_subrev_u32_e32 %[t2], %[oe], %[m2]\n\t"
+        "v_subrev_u32_e32 %[t3], %[oe], %[m3]\n\t"
+        "v_max_i32_sdwa %[m0], %[m0], %[v0] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_max_i32_sdwa %[m1], %[m1], %[v1] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_max_i32_sdwa %[m2], %[m2], %[v2] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_max_i32_sdwa %[m3], %[m3], %[v3] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_max3_i32 %[x0], %[x0], %[t0], 0\n\t"
+        "v_max3_i32 %[x1], %[x1], %[t1], 0\n\t"
+        "v_max3_i32 %[x2], %[x2], %[t2], 0\n\t"
+        "v_max3_i32 %[x3], %[x3], %[t3], 0\n\t"
+        "s_sub_u32 %[st], %[g], %[gfa]\n\t"     // gfa <= G < gfa + gfn: all lanes in band
+        "s_cmp_lt_u32 %[st], %[gfn]\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "v_max_i32_e32 %[ha], %[f], %[m0]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_lshl_or_b32 %[v0], %[x0], 16, %[h1]\n\t"
+        "v_max3_i32 %[f], %[f], %[t0], 0\n\t"
+        "v_lshlrev_b32_e32 %[m0], 16, %[ha]\n\t"
+        "v_max_i32_e32 %[hb], %[f], %[m1]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_or_b32_e32 %[k0], %[j0], %[m0]\n\t"
+        "v_max3_i32 %[f], %[f], %[t1], 0\n\t"
+        "v_min_i32_e32 %[l0], %[j1], %[m0]\n\t"
+        "v_lshl_or_b32 %[v1], %[x1], 16, %[ha]\n\t"
+        "v_lshlrev_b32_e32 %[m1], 16, %[hb]\n\t"
+        "v_max_i32_e32 %[ha], %[f], %[m2]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_or_b32_e32 %[k1], %[j1], %[m1]\n\t"
+        "v_max3_i32 %[f], %[f], %[t2], 0\n\t"
+        "v_min_i32_e32 %[l1], %[j2], %[m1]\n\t"
+        "v_lshl_or_b32 %[v2], %[x2], 16, %[hb]\n\t"
+        "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
+        "v_lshlrev_b32_e32 %[m2], 16, %[ha]\n\t"
+        "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
+        "v_max_i32_e32 %[h1], %[f], %[m3]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_or_b32_e32 %[k0], %[j2], %[m2]\n\t"
+        "v_max3_i32 %[f], %[f], %[t3], 0\n\t"
+        "v_min_i32_e32 %[l0], %[j3], %[m2]\n\t"
+        "v_lshl_or_b32 %[v3], %[x3], 16, %[ha]\n\t"
+        "v_lshlrev_b32_e32 %[m3], 16, %[h1]\n\t"
+        "v_or_b32_e32 %[k1], %[j3], %[m3]\n\t"
+        "v_min_i32_e32 %[l1], %[j4], %[m3]\n\t"
+        "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
+        "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
+        "s_branch 3f\n"
+        "2:\n\t"
+        "v_sub_u32_e32 %[d], %[j0], %[beg]\n\t"
+        "v_cmp_lt_u32_e32 vcc, %[d], %[span]\n\t"
+        "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
+        "v_cmp_gt_i32_e64 %[slt], 0, %[d]\n\t"
+        "v_max_i32_e32 %[tp], %[f], %[m0]\n\t"
+        "v_cndmask_b32_e32 %[ha], %[h1], %[tp], vcc\n\t"
+        "v_cndmask_b32_e32 %[tp], 0, %[tp], vcc\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_cndmask_b32_e32 %[x0], 0, %[x0], vcc\n\t"
+        "v_max3_i32 %[f], %[f], %[t0], 0\n\t"
+        "v_lshl_or_b32 %[d], %[x0], 16, %[h1]\n\t"
+        "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
+        "v_cndmask_b32_e64 %[v0], %[v0], %[d], %[sat]\n\t"
+        "v_lshlrev_b32_e32 %[tp], 16, %[tp]\n\t"
+        "v_or_b32_e32 %[k0], %[j0], %[tp]\n\t"
+        "v_min_i32_e32 %[l0], %[j1], %[tp]\n\t"
+        "v_sub_u32_e32 %[d], %[j1], %[beg]\n\t"
+        "v_cmp_lt_u32_e32 vcc, %[d], %[span]\n\t"
+        "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
+        "v_cmp_gt_i32_e64 %[slt], 0, %[d]\n\t"
+        "v_max_i32_e32 %[tp], %[f], %[m1]\n\t"
+        "v_cndmask_b32_e32 %[hb], %[ha], %[tp], vcc\n\t"
+        "v_cndmask_b32_e32 %[tp], 0, %[tp], vcc\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_cndmask_b32_e32 %[x1], 0, %[x1], vcc\n\t"
+        "v_max3_i32 %[f], %[f], %[t1], 0\n\t"
+        "v_lshl_or_b32 %[d], %[x1], 16, %[ha]\n\t"
+        "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
+        "v_cndmask_b32_e64 %[v1], %[v1], %[d], %[sat]\n\t"
+        "v_lshlrev_b32_e32 %[tp], 16, %[tp]\n\t"
+        "v_or_b32_e32 %[k1], %[j1], %[tp]\n\t"
+        "v_min_i32_e32 %[l1], %[j2], %[tp]\n\t"
+        "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
+        "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
+        "v_sub_u32_e32 %[d], %[j2], %[beg]\n\t"
+        "v_cmp_lt_u32_e32 vcc, %[d], %[span]\n\t"
+        "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
+        "v_cmp_gt_i32_e64 %[slt], 0, %[d]\n\t"
+        "v_max_i32_e32 %[tp], %[f], %[m2]\n\t"
+        "v_cndmask_b32_e32 %[ha], %[hb], %[tp], vcc\n\t"
+        "v_cndmask_b32_e32 %[tp], 0, %[tp], vcc\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_cndmask_b32_e32 %[x2], 0, %[x2], vcc\n\t"
+        "v_max3_i32 %[f], %[f], %[t2], 0\n\t"
+        "v_lshl_or_b32 %[d], %[x2], 16, %[hb]\n\t"
+        "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
+        "v_cndmask_b32_e64 %[v2], %[v2], %[d], %[sat]\n\t"
+        "v_lshlrev_b32_e32 %[tp], 16, %[tp]\n\t"
+        "v_or_b32_e32 %[k0], %[j2], %[tp]\n\t"
+        "v_min_i32_e32 %[l0], %[j3], %[tp]\n\t"
+        "v_sub_u32_e32 %[d], %[j3], %[beg]\n\t"
+        "v_cmp_lt_u32_e32 vcc, %[d], %[span]\n\t"
+        "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
+        "v_cmp_gt_i32_e64 %[slt], 0, %[d]\n\t"
+        "v_max_i32_e32 %[tp], %[f], %[m3]\n\t"
+        "v_cndmask_b32_e32 %[h1], %[ha], %[tp], vcc\n\t"
+        "v_cndmask_b32_e32 %[tp], 0, %[tp], vcc\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_cndmask_b32_e32 %[x3], 0, %[x3], vcc\n\t"
+        "v_max3_i32 %[f], %[f], %[t3], 0\n\t"
+        "v_lshl_or_b32 %[d], %[x3], 16, %[ha]\n\t"
+        "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
+        "v_cndmask_b32_e64 %[v3], %[v3], %[d], %[sat]\n\t"
+        "v_lshlrev_b32_e32 %[tp], 16, %[tp]\n\t"
+        "v_or_b32_e32 %[k1], %[j3], %[tp]\n\t"
+        "v_min_i32_e32 %[l1], %[j4], %[tp]\n\t"
+        "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
+        "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
+        "3:"
+        : [v0] "+v"(v0), [v1] "+v"(v1), [v2] "+v"(v2), [v3] "+v"(v3), [f] "+v"(f), [h1] "+v"(h1),
+          [key] "+v"(key), [lp] "+v"(lp1), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2),
+          [m3] "=&v"(m3), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2), [x3] "=&v"(x3), [ha] "=&v"(ha),
+          [hb] "=&v"(hb), [k0] "=&v"(k0), [k1] "=&v"(k1), [l0] "=&v"(l0), [l1] "=&v"(l1),
+          [pw] "=&v"(pw), [d] "=&v"(d), [tp] "=&v"(tp), [sat] "=&s"(sat), [slt] "=&s"(slt),
+          [st] "=&s"(st)
+        : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe] "s"(oe), [ed] "s"(ed),
+          [glo] "s"(glo), [gsp] "s"(gsp), [gfa] "s"(gfa), [gfn] "s"(gfn), [beg] "v"(beg),
+          [span] "v"(span), [g] "i"(G), [j0] "i"(4 * G), [j1] "i"(4 * G + 1),
+          [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [j4] "i"(4 * G + 4)
+        : "vcc", "scc");
 }
 
 template <int G, int QMAX, int SM, bool SYM>
-__device__ __forceinline__ void lane_group_edge(uint32_t (&eh)[QMAX + 1], const uint32_t (&q4)[QMAX / 4],
-                                                uint2 pr, int beg, int end, int &f, int &h1,
-                                                int &key, int &lp1, const LaneRow &r, const LaneCx &c)
+__device__ __forceinline__ void lane_group(uint32_t (&eh)[QMAX + 1], const uint32_t (&q4)[QMAX / 4],
+                                           uint2 pr, int beg, int end, int &f, int &h1, int &key,
+                                           int &lp1, const LaneRow &r, const LaneCx &c)
 {
     constexpr int J0 = 4 * G;
+    if constexpr (SM == 1 && SYM && J0 + 3 < QMAX) {
+        // skip / fast / masked decided inside the asm on SGPR group bounds
+        lane_group_asm<G>(eh[J0], eh[J0 + 1], eh[J0 + 2], eh[J0 + 3], q4[G], pr.x, pr.y, f, h1,
+                          key, lp1, c.oe_del, c.e_del, r.glo, r.gsp, r.gfa, r.gfn, beg, end - beg);
+        return;
+    }
     if (J0 + 3 < r.ulo || J0 > r.uhi) return;            // uniform skip
-    lane_col_edge<J0 + 0, QMAX, SM, SYM>(eh, q4, pr, beg, end, f, h1, key, lp1, r, c);
-    if constexpr (J0 + 1 <= QMAX) lane_col_edge<J0 + 1, QMAX, SM, SYM>(eh, q4, pr, beg, end, f, h1, key, lp1, r, c);
-    if constexpr (J0 + 2 <= QMAX) lane_col_edge<J0 + 2, QMAX, SM, SYM>(eh, q4, pr, beg, end, f, h1, key, lp1, r, c);
-    if constexpr (J0 + 3 <= QMAX) lane_col_edge<J0 + 3, QMAX, SM, SYM>(eh, q4, pr, beg, end, f, h1, key, lp1, r, c);
+    uint32_t pw = 0;
+    if constexpr (J0 < QMAX) pw = __builtin_amdgcn_perm(pr.y, pr.x, q4[G]);
+    if constexpr (J0 + 3 < QMAX) {
+        if (J0 >= r.fast_lo && J0 + 3 < r.fast_hi) {    // uniform: all lanes in band
+            lane_cell<J0 + 0, SM, SYM, QMAX + 1>(eh, (int)(int8_t)(pw), f, h1, key, lp1, c);
+            lane_cell<J0 + 1, SM, SYM, QMAX + 1>(eh, (int)(int8_t)(pw >> 8), f, h1, key, lp1, c);
+            lane_cell<J0 + 2, SM, SYM, QMAX + 1>(eh, (int)(int8_t)(pw >> 16), f, h1, key, lp1, c);
+            lane_cell<J0 + 3, SM, SYM, QMAX + 1>(eh, (int)(int8_t)(pw >> 24), f, h1, key, lp1, c);
+            return;
+        }
+    }
+    lane_col_masked<J0 + 0, QMAX, SM, SYM>(eh, (int)(int8_t)(pw), beg, end, f, h1, key, lp1, r, c);
+    if constexpr (J0 + 1 <= QMAX) lane_col_masked<J0 + 1, QMAX, SM, SYM>(eh, (int)(int8_t)(pw >> 8), beg, end, f, h1, key, lp1, r, c);
+    if constexpr (J0 + 2 <= QMAX) lane_col_masked<J0 + 2, QMAX, SM, SYM>(eh, (int)(int8_t)(pw >> 16), beg, end, f, h1, key, lp1, r, c);
+    if constexpr (J0 + 3 <= QMAX) lane_col_masked<J0 + 3, QMAX, SM, SYM>(eh, (int)(int8_t)(pw >> 24), beg, end, f, h1, key, lp1, r, c);
 }
 
 template <int QMAX, int SM, bool SYM, int... G>
 __device__ __forceinline__ void lane_row(std::integer_sequence<int, G...>, uint32_t (&eh)[QMAX + 1],
                                          const uint32_t (&q4)[QMAX / 4], uint2 pr, int beg, int end,
-                                         int &f, int &h1, int &key, int &lp1, const LaneRow &fast,
-                                         const LaneRow &edge, const LaneCx &c)
+                                         int &f, int &h1, int &key, int &lp1, const LaneRow &r,
+                                         const LaneCx &c)
 {
-    (lane_group_fast<G, QMAX, SM, SYM>(eh, q4, pr, f, h1, key, lp1, fast, c), ...);
-    (lane_group_edge<G, QMAX, SM, SYM>(eh, q4, pr, beg, end, f, h1, key, lp1, edge, c), ...);
+    (lane_group<G, QMAX, SM, SYM>(eh, q4, pr, beg, end, f, h1, key, lp1, r, c), ...);
 }
 
 __device__ __forceinline__ uint32_t load4(const uint8_t *p, int base, int len)
@@ -172,6 +359,10 @@ __device__ __forceinline__ uint32_t load4(const uint8_t *p, int base, int len)
     return w;
 }
 
+typedef const __attribute__((address_space(1))) void *gptr_t;
+typedef __attribute__((address_space(3))) void *lptr_t;
+constexpr int kTChunkDw = 17;            // dwords per lane per 64-row target chunk
+
 template <int QMAX, int SM, bool SYM>
 __global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const int32_t w,
                                                       SeqPair *__restrict__ pairs,
@@ -182,10 +373,7 @@ __global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const in
                                                       int32_t *__restrict__ err)
 {
     constexpr int NG = QMAX / 4;        // query words (4 codes each)
-    __shared__ uint2 tab[8];
-    if (threadIdx.x < 8) tab[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
-    __syncthreads();
-
+    __shared__ uint32_t s_tgt[4][2][kTChunkDw][64];   // 34.8 KB per 256-thread block
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = gid < n;
     const int idx = valid ? (order ? order[gid] : gid) : 0;
@@ -195,18 +383,25 @@ __global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const in
         idr = sp->idr; idq = sp->idq; tlen = sp->len1; qlen = sp->len2; h0 = sp->h0;
         if (qlen > QMAX || qlen < 0 || tlen < 0) { atomicOr(err, 1); valid = false; }
     }
-    // query codes -> perm selectors (codes > 7 clamp to 7 = ambig slot)
+    // query codes -> perm selectors (4 per VGPR).  Aligned dword loads (a dword holding at
+    // least one byte of the query never leaves that byte's page), all issued before use;
+    // bytes are realigned with v_alignbyte.  Codes must be 0..4 (upstream contract).
     uint32_t q4[NG];
-    const uint8_t *qp = qer + idq;
+    {
+        uint32_t wv[NG + 1];
+        const uintptr_t qa = (uintptr_t)(qer + idq);
+        const uint32_t *wp = (const uint32_t *)(qa & ~(uintptr_t)3);
+        const int sh = (int)(qa & 3);
+        const int nw = (valid && qlen > 0) ? (sh + qlen + 3) >> 2 : 0;
+        if (nw > 0) {
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        uint32_t word = 0;
+            for (int g = 0; g <= NG; ++g) wv[g] = wp[min(g, nw - 1)];
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int j = 4 * g + k;
-            if (valid && j < qlen) word |= (uint32_t)min((uint32_t)qp[j], 7u) << (8 * k);
+            for (int g = 0; g <= NG; ++g) wv[g] = 0;
         }
-        q4[g] = word;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) q4[g] = __builtin_amdgcn_alignbyte(wv[g + 1], wv[g], sh);
     }
     // A.1 first row: eh[j].h = max(h0 - oe_ins - (j-1) e_ins, 0), 1 <= j <= qlen
     uint32_t eh[QMAX + 1];
@@ -225,9 +420,26 @@ __global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const in
     // A.3 state
     int best = h0, best_i = -1, best_j = -1, max_ie = -1, gsc = -1, moff = 0, endc = qlen;
     bool alive = valid && tlen > 0;
+    // Target bases stream HBM -> LDS by LDS-DMA (global_load_lds_dword), no VGPRs involved:
+    // per wave two chunk buffers of 64 rows (17 aligned dwords per lane, layout [dword][lane]
+    // so each DMA instruction writes 256 contiguous bytes).  Chunk c covers rows
+    // [64c, 64c + 64) = dwords [16c, 16c + 17) of the lane's aligned window; it is issued one
+    // chunk ahead and waited for once (vmcnt) at its first row.  A dword holding >= 1 byte of
+    // the window never leaves that byte's page, so clamped aligned loads are always safe.
     const uint8_t *tp = ref + idr;
-    uint32_t tcur = 0, tnxt = 0;
-    if (alive) { tcur = load4(tp, 0, tlen); tnxt = load4(tp, 4, tlen); }
+    const int tsh = (int)((uintptr_t)tp & 3);
+    const uint32_t *twp = (const uint32_t *)(tp - tsh);
+    const int tlast = max((tsh + tlen - 1) >> 2, 0);      // last dword holding a valid byte
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    auto issue_chunk = [&](int ch) {
+        uint32_t *dst = &s_tgt[wv][ch & 1][0][0];
+#pragma unroll
+        for (int k = 0; k < kTChunkDw; ++k)
+            __builtin_amdgcn_global_load_lds((gptr_t)(twp + min(16 * ch + k, tlast)),
+                                             (lptr_t)(dst + 64 * k), 4, 0, 0);
+    };
+    if (alive) { issue_chunk(0); issue_chunk(1); }
+    uint32_t tcur = 0;
     const int wl_max = wave_max(alive ? wl : -1);
     const int wl_min = wave_min(alive ? wl : INT_MAX);
     const LaneCx cx{kp.e_del, kp.o_del + kp.e_del, kp.e_ins, kp.o_ins + kp.e_ins, kp.maxsc};
@@ -241,26 +453,46 @@ __global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const in
         endc = end;
         // uniform pass bounds: fast = [beg_u, min end) when every live lane shares beg,
         // edge = [fast_hi, max end] (or the whole [min beg, max end] otherwise)
+#ifdef BSW_EXP_NO_REDUCE
+        const int emax = 150, emin = 150;
+#else
         const int emax = wave_max(act ? end : -1);
         const int emin = wave_min(act ? end : INT_MAX);
-        LaneRow fast, edge;
-        if (wl_min == wl_max) {
-            fast.fast_lo = max(0, i - wl_min);
-            fast.fast_hi = emin;
-            edge.ulo = max(fast.fast_lo, emin);
-        } else {
-            fast.fast_lo = fast.fast_hi = 0;
-            edge.ulo = max(0, i - wl_max);
-        }
-        edge.uhi = emax;
+#endif
+        LaneRow r;
+        r.ulo = __builtin_amdgcn_readfirstlane(max(0, i - wl_max));      // min beg (live lanes)
+        r.uhi = __builtin_amdgcn_readfirstlane(emax);                    // max end
+        r.fast_lo = __builtin_amdgcn_readfirstlane(max(0, i - wl_min));  // max beg
+        r.fast_hi = __builtin_amdgcn_readfirstlane(emin);                // min end
+        r.glo = r.ulo >> 2;
+        r.gsp = max((r.uhi >> 2) - r.glo, -1);      // -1 (as unsigned: huge) never happens: uhi >= ulo
+        r.gfa = (r.fast_lo + 3) >> 2;
+        r.gfn = max((r.fast_hi >> 2) - r.gfa, 0);
         if (act) {
-            if ((i & 3) == 0 && i > 0) { tcur = tnxt; tnxt = load4(tp, i + 4, tlen); }
-            const uint32_t t = min((tcur >> (8 * (i & 3))) & 0xffu, 7u);
-            const uint2 pr = tab[t];
+            if ((i & 3) == 0) {            // new 4-row block: 4 target bases from LDS
+                if ((i & 63) == 0) {          // chunk boundary: its DMA was issued 64 rows ago
+                    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                const int k = (i >> 2) & 15;
+                const uint32_t *src = &s_tgt[wv][(i >> 6) & 1][k][ln];
+                tcur = __builtin_amdgcn_alignbyte(src[64], src[0], tsh);
+                if ((i & 63) == 0) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (i > 0) issue_chunk((i >> 6) + 1);   // refill the buffer just drained
+                }
+            }
+            // per-row score profile of target base t (8 bytes: mat[t][q], q = 0..7)
+            const uint32_t t = (tcur >> (8 * (i & 3))) & 0xffu;
+            uint2 pr = make_uint2(kp.prof[4][0], kp.prof[4][1]);
+            pr = (t == 3) ? make_uint2(kp.prof[3][0], kp.prof[3][1]) : pr;
+            pr = (t == 2) ? make_uint2(kp.prof[2][0], kp.prof[2][1]) : pr;
+            pr = (t == 1) ? make_uint2(kp.prof[1][0], kp.prof[1][1]) : pr;
+            pr = (t == 0) ? make_uint2(kp.prof[0][0], kp.prof[0][1]) : pr;
             int h1 = (beg == 0) ? max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) : 0;
             int f = 0, key = -1, lp1 = 0;
             lane_row<QMAX, SM, SYM>(std::make_integer_sequence<int, QMAX / 4 + 1>{}, eh, q4, pr,
-                                    beg, end, f, h1, key, lp1, fast, edge, cx);
+                                    beg, end, f, h1, key, lp1, r, cx);
             const int m = key >> 16, mj = key & 0xffff;
             if (end == qlen) {                    // A.4: j == qlen (beg <= end always)
                 if (!(gsc > h1)) max_ie = i;

@@ -1,0 +1,63 @@
+"""Summarise rocprofv3 CSV output (kernel trace + PMC passes) for the lane kernel.
+
+usage: python tools/pmc_summary.py gpurun_out/prof [profiles/<round>]
+Writes <dest>/kernel_stats.csv (copied), <dest>/pmc_summary.json and profiles/pmc_latest.json
+(read by bench.py for roofline.traffic).
+"""
+import csv, glob, json, os, shutil, sys
+from collections import defaultdict
+
+src = sys.argv[1]
+dest = sys.argv[2] if len(sys.argv) > 2 else None
+
+def rows(pattern):
+    out = []
+    for f in sorted(glob.glob(os.path.join(src, pattern), recursive=True)):
+        with open(f) as fh:
+            out.extend(csv.DictReader(fh))
+    return out
+
+def short(name):
+    if 'lane_kernel' in name:
+        for q in ('160', '128', '96', '64', '32'):
+            if f'ILi{q}E' in name or f'<{q},' in name:
+                return f'lane_kernel<{q}>'
+        return 'lane_kernel'
+    for k in ('wide_kernel', 'plan_kernel', 'Radix', 'radix', 'Onesweep', 'onesweep'):
+        if k in name:
+            return k
+    return name[:60]
+
+summary = {}
+stats = rows('**/*kernel_stats.csv')
+for r in stats:
+    n = short(r.get('Name', ''))
+    summary.setdefault(n, {})
+    summary[n]['calls'] = int(r.get('Calls', 0))
+    summary[n]['avg_ns'] = float(r.get('AverageNs', 0))
+    summary[n]['total_ns'] = float(r.get('TotalDurationNs', 0))
+    summary[n]['pct'] = float(r.get('Percentage', 0))
+# PMC: counter_collection.csv has one row per dispatch and counter
+acc = defaultdict(lambda: defaultdict(list))
+for r in rows('**/*counter_collection.csv'):
+    n = short(r.get('Kernel_Name', ''))
+    acc[n][r['Counter_Name']].append(float(r['Counter_Value']))
+for n, cs in acc.items():
+    d = summary.setdefault(n, {})
+    for c, v in cs.items():
+        d[c + '_per_launch'] = sum(v) / len(v)
+    if 'FETCH_SIZE' in cs or 'WRITE_SIZE' in cs:
+        f = d.get('FETCH_SIZE_per_launch', 0.0) * 1024
+        wr = d.get('WRITE_SIZE_per_launch', 0.0) * 1024
+        d['fetch_bytes_per_launch'] = f
+        d['write_bytes_per_launch'] = wr
+        d['hbm_bytes_per_launch'] = f + wr
+print(json.dumps(summary, indent=1))
+if dest:
+    os.makedirs(dest, exist_ok=True)
+    for f in glob.glob(os.path.join(src, '**/*kernel_stats.csv'), recursive=True)[:1]:
+        shutil.copy(f, os.path.join(dest, 'kernel_stats.csv'))
+    with open(os.path.join(dest, 'pmc_summary.json'), 'w') as fh:
+        json.dump(summary, fh, indent=1)
+    with open(os.path.join(os.path.dirname(dest.rstrip('/')), 'pmc_latest.json'), 'w') as fh:
+        json.dump(summary, fh, indent=1)
