@@ -1,0 +1,111 @@
+"""C-ABI checks that need no GPU: the product library loads, exports every symbol the
+public headers declare, SeqPair is byte-compatible with upstream's 56-byte layout, and the
+argument validation / error strings behave (no compute call is made here)."""
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import bsw
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "bsw.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(bsw_[a-z_0-9]+)\s*\(", src)
+    return sorted(set(names))
+
+
+def test_header_declares_expected_api():
+    assert set(declared_functions()) == set(bsw.ABI_SYMBOLS)
+
+
+def test_library_exports_all_declared_symbols():
+    lib = bsw.hip_lib()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", bsw.HIP_LIB], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (bsw_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_links_hip_runtime_not_torch():
+    out = subprocess.run(["readelf", "-d", bsw.HIP_LIB], capture_output=True, text=True).stdout
+    assert "libamdhip64.so" in out
+    assert "torch" not in out and "python" not in out
+
+
+def test_kernels_are_gfx950_code_objects():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", bsw.HIP_LIB],
+                         capture_output=True, text=True)
+    text = out.stdout + out.stderr
+    assert "gfx950" in text
+
+
+def test_seqpair_layout():
+    assert bsw.SEQPAIR_DTYPE.itemsize == 56
+    names = bsw.SEQPAIR_DTYPE.names
+    assert names[:6] == ("idr", "idq", "id", "len1", "len2", "h0")
+    assert names[8:] == bsw.OUT_FIELDS
+    assert bsw.SEQPAIR_DTYPE.fields["score"][1] == 32 and bsw.SEQPAIR_DTYPE.fields["max_off"][1] == 52
+    hdr = open(os.path.join(ROOT, "include", "bsw_seqpair.h")).read()
+    assert "sizeof(SeqPair) == 56" in hdr
+
+
+def test_params_default_and_abi_version():
+    lib = bsw.hip_lib()
+    p = bsw.Params()
+    lib.bsw_params_default(ctypes.byref(p))
+    assert (p.o_del, p.e_del, p.o_ins, p.e_ins, p.zdrop, p.end_bonus) == (6, 1, 6, 1, 100, 5)
+    mat = np.frombuffer(bytes(p.mat), np.int8).reshape(5, 5)
+    assert mat[0, 0] == 1 and mat[0, 1] == -4 and mat[4, 4] == -1 and mat[2, 4] == -1
+    assert lib.bsw_abi_version() == 1
+    ref = bsw.default_params()
+    assert bytes(ref.mat) == bytes(p.mat)
+
+
+def test_strerror_and_invalid_arguments():
+    lib = bsw.hip_lib()
+    for code in (0, -22, -12, -19, -5, -34):
+        assert lib.bsw_strerror(code)
+    # invalid arguments are rejected before any device work
+    P = ctypes.c_void_p
+    assert lib.bsw_create(None, 0, 1, ctypes.byref(P())) == -22
+    bad = bsw.default_params()
+    bad.e_del = 0
+    assert lib.bsw_create(ctypes.byref(bad), 0, 1, ctypes.byref(P())) == -22
+    assert lib.bsw_create(ctypes.byref(bsw.default_params()), 0, 0, ctypes.byref(P())) == -22
+    assert lib.bsw_get_scores(None, None, None, None, 0, 100, 16) == -22
+    st = bsw.Stats()
+    assert lib.bsw_last_stats(None, ctypes.byref(st)) == -22
+
+
+def test_create_without_gpu_fails_cleanly():
+    """Here (no GPU) bsw_create must return BSW_E_NODEV, never crash or fall back."""
+    import hiprt
+    if hiprt.device_count() > 0:
+        pytest.skip("a GPU is visible; covered by the gpu tests")
+    lib = bsw.hip_lib()
+    ctx = ctypes.c_void_p()
+    rc = lib.bsw_create(ctypes.byref(bsw.default_params()), 0, 1, ctypes.byref(ctx))
+    assert rc == -19 and not ctx.value
+    with pytest.raises(bsw.BswError):
+        bsw.Engine()
+
+
+def test_shim_header_compiles_against_c_abi(tmp_path):
+    """The upstream-compatible C++ shim (include/bandedSWA_gpu.h) compiles and links."""
+    src = tmp_path / "shim.cpp"
+    src.write_text('#include "bandedSWA_gpu.h"\nint main(){ int8_t mat[25]; for(int i=0;i<25;++i) mat[i]=-1;\n'
+                   ' BandedPairWiseSW* p = nullptr; (void)p; (void)mat; return 0; }\n')
+    r = subprocess.run(["g++", "-std=c++14", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                        str(tmp_path / "shim"), bsw.HIP_LIB, "-Wl,-rpath," + os.path.dirname(bsw.HIP_LIB)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

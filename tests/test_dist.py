@@ -1,0 +1,75 @@
+"""Multi-process sharding on CPU (gloo, world_size 2) -- the N > 1 path of bench.py.
+
+Pairs are independent: each rank generates and scores its own contiguous
+shard [rank*n, (rank+1)*n) of the global synthetic batch; no data-path collective exists.
+These tests check that the shards tile the single-process batch exactly, that per-shard
+results equal the single-process results, and that the max-over-ranks timing reduction
+used by bench.py behaves."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bsw
+import oracle
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    pairs, ref, qer = bsw.synth_batch(n, pair_base=rank * n)
+    oracle.sse41_get_scores16(oracle.make_params(), pairs, ref, qer, 100, 1)
+    out = torch.from_numpy(pairs.view(np.int32).reshape(n, 14).copy())
+    gathered = [torch.zeros_like(out) for _ in range(world)]
+    dist.all_gather(gathered, out)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        q.put((np.concatenate([g.numpy() for g in gathered]), float(t.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_equal_single_process():
+    n, world = 600, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, tmax = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert tmax == float(world)
+    full, ref, qer = bsw.synth_batch(n * world)
+    oracle.get_scores(oracle.make_params(), full, ref, qer, 100)
+    got = got.view(bsw.SEQPAIR_DTYPE).reshape(-1)
+    assert np.array_equal(got["id"], full["id"])
+    for f in ("len1", "len2", "h0") + bsw.OUT_FIELDS:
+        assert np.array_equal(got[f], full[f]), f
+
+
+def test_synth_shards_tile_global_batch():
+    a, ra, qa = bsw.synth_batch(300, pair_base=0)
+    b, rb, qb = bsw.synth_batch(300, pair_base=300)
+    full, rf, qf = bsw.synth_batch(600)
+    assert np.array_equal(np.concatenate([ra, rb]), rf)
+    assert np.array_equal(np.concatenate([qa, qb]), qf)
+    assert np.array_equal(np.concatenate([a["h0"], b["h0"]]), full["h0"])
