@@ -16,8 +16,8 @@ SYNTH    := $(LIBDIR)/libbsw_synth.so
 SHIMTEST := $(LIBDIR)/bsw_shim_example
 ORACLE   := oracle/liboracle.so
 
-HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_host.cpp
-HIP_HDRS := $(CSRC)/bsw_kernels.h include/bsw.h include/bsw_seqpair.h
+HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pk.hip $(CSRC)/bsw_host.cpp
+HIP_HDRS := $(CSRC)/bsw_kernels.h $(CSRC)/bsw_wave.h include/bsw.h include/bsw_seqpair.h
 
 all: product synth oracle
 
@@ -31,10 +31,13 @@ $(LIBDIR):
 $(LIBDIR)/bsw_kernels.o: $(CSRC)/bsw_kernels.hip $(HIP_HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(LIBDIR)/bsw_pk.o: $(CSRC)/bsw_pk.hip $(HIP_HDRS) | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/bsw_host.o: $(CSRC)/bsw_host.cpp $(HIP_HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_host.o
+$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pk.o $(LIBDIR)/bsw_host.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 $(SYNTH): $(CSRC)/bsw_synth.c include/bsw_seqpair.h | $(LIBDIR)

@@ -33,14 +33,43 @@
 namespace bsw {
 
 constexpr int kNumLaneClasses = 5;          // QMAX 32, 64, 96, 128, 160
-constexpr int kWideClass = kNumLaneClasses; // index of the wide-kernel class
-constexpr int kNumClasses = kNumLaneClasses + 1;
-constexpr int kKeyBits = 31;                // 3 class + 8 qlen + 12 tlen + 8 h0 bits
+constexpr int kPkClass = kNumLaneClasses;   // packed two-pairs-per-lane kernel (QMAX 160)
+constexpr int kWideClass = kPkClass + 1;    // index of the wide-kernel class
+constexpr int kNumClasses = kWideClass + 1;
+constexpr int kKeyBits = 32;                // 3 class + 8 qlen + 1 related + 12 tlen + 8 h0 bits
+
+// Lifetime predictor for the sort key (scheduling only, results never depend on it): does the
+// query look like an extension of the target near the seed?  Identity of query[10, 40) with
+// target[10 + s, 40 + s), best over |s| <= 6; > 18 of 30 matches = related.  Unrelated pairs
+// die within a few dozen rows and shrink their band ends on the way; giving them their own
+// wavefronts keeps the related waves' band edges uniform (masked groups
+// 25% -> 11% at C2 in simulation).
+__device__ __forceinline__ int seed_related(const uint8_t *__restrict__ q, int qlen,
+                                            const uint8_t *__restrict__ r, int tlen)
+{
+    if (qlen < 40 || tlen < 46) return 1;
+    uint8_t qb[30], rb[42];
+#pragma unroll
+    for (int j = 0; j < 30; ++j) qb[j] = q[10 + j];
+#pragma unroll
+    for (int j = 0; j < 42; ++j) rb[j] = r[4 + j];
+    int best = 0;
+#pragma unroll
+    for (int sft = 0; sft <= 12; ++sft) {
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < 30; ++j) c += qb[j] == rb[j + sft];
+        best = max(best, c);
+    }
+    return best > 18;
+}
 
 // Per pair: class + sort key.  Lane classes need qlen <= QMAX and int16-safe scores.
 __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_t maxsc,
-                            uint32_t *__restrict__ keys, int32_t *__restrict__ vals,
-                            int32_t *__restrict__ counts, int32_t *__restrict__ maxq_wide)
+                            int32_t pk_ok, const uint8_t *__restrict__ ref,
+                            const uint8_t *__restrict__ qer, uint32_t *__restrict__ keys,
+                            int32_t *__restrict__ vals, int32_t *__restrict__ counts,
+                            int32_t *__restrict__ maxq_wide)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < n;
@@ -55,13 +84,17 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
         else if (qlen <= 96) c = 2;
         else if (qlen <= 128) c = 3;
         else if (qlen <= 160) c = 4;
+        // packed kernel: bwa scoring, key H << 8 | j fits 16 bits (H <= h0 + min(qlen, tlen))
+        if (pk_ok && qlen > 128 && qlen <= kPkQmax && p.h0 + min(qlen, tlen) <= 255) c = kPkClass;
     }
     if (valid) {
         if (c == kWideClass) atomicMax(maxq_wide, qlen);
-        // (class, qlen desc, tlen desc, h0 desc): like-shaped pairs share a wavefront, and
-        // equal h0 gives lanes similar band-end trajectories (fewer masked edge groups)
-        keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
-                  ((uint32_t)(4095 - min(tlen, 4095)) << 8) | (uint32_t)(255 - min(max(p.h0, 0), 255));
+        // (class, qlen desc, related first, tlen desc, h0 desc): like-shaped pairs share a
+        // wavefront; equal h0 and relatedness give lanes similar band-end trajectories
+        const int rel = (c == kWideClass) ? 1 : seed_related(qer + p.idq, qlen, ref + p.idr, tlen);
+        keys[i] = ((uint32_t)c << 29) | ((uint32_t)(255 - min(qlen, 255)) << 21) |
+                  ((uint32_t)(1 - rel) << 20) | ((uint32_t)(4095 - min(tlen, 4095)) << 8) |
+                  (uint32_t)(255 - min(max(p.h0, 0), 255));
         vals[i] = i;
     }
     // one atomic per wave and class (1M same-address atomics cost ~11 ms)
@@ -191,6 +224,20 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
         kp.prof[t][0] = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
         kp.prof[t][1] = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
     }
+    // packed kernel scoring contract (bsw_pk.hip): match 1, one mismatch value in [-127, -1],
+    // every N entry -1, symmetric gap penalties.  Opt-in (BSW_PK=1): at one wave per SIMD it
+    // measures slower than the lane kernel on C2, so it is not the default.
+    bool ok = p.o_del == p.o_ins && p.e_del == p.e_ins && p.e_del > 0 && p.o_del + p.e_del < 16384;
+    const int mis = p.mat[1];
+    ok = ok && mis < 0 && mis >= -127;
+    for (int a = 0; a < 5 && ok; ++a)
+        for (int b = 0; b < 5 && ok; ++b) {
+            const int v = p.mat[a * 5 + b];
+            ok = (a == 4 || b == 4) ? v == -1 : (a == b ? v == 1 : v == mis);
+        }
+    const char *pk = getenv("BSW_PK");
+    if (!(pk && pk[0] == '1')) ok = false;
+    kp.pk_ok = ok ? 1 : 0;
 }
 
 // The device pipeline on one slot's device; d_* are device pointers valid on `stream`.
@@ -212,7 +259,8 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     BSW_TRY(hipMemsetAsync(s.d_meta, 0, 16 * sizeof(int32_t), stream));
     int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + 8, *d_err = s.d_meta + 9;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       d_pairs, n, kp.maxsc, s.d_keys, s.d_vals, d_counts, d_maxq);
+                       d_pairs, n, kp.maxsc, kp.pk_ok, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
+                       d_maxq);
     BSW_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
     BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals,
@@ -236,6 +284,13 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
             s.stats.n_i16 += counts[c];
         }
         off += counts[c];
+    }
+    if (counts[kPkClass] > 0) {
+        BSW_TRY(launch_pk_kernel(kPkQmax, kp, w, d_pairs, s.d_order + off, counts[kPkClass], d_ref,
+                                 d_qer, d_err, stream));
+        s.stats.n_launches++;
+        s.stats.n_i16 += counts[kPkClass];
+        off += counts[kPkClass];
     }
     if (counts[kWideClass] > 0) {
         const int32_t nw = counts[kWideClass];

@@ -4,6 +4,8 @@
 //   lane kernel  : one LANE per SeqPair, the whole DP row of the pair (eh[0..qlen], packed
 //                  {h:16, e:16} per column) held in VGPRs; 64 pairs per wavefront advance
 //                  through their target rows in lock-step.  qlen <= QMAX (template), int16 cells.
+//   pk kernel    : TWO SeqPairs per lane (16-bit halves of every DP register), every step a
+//                  packed v_pk_* instruction; bwa-style scoring, scores < 256 (bsw_pk.hip).
 //   wide kernel  : one lane per pair, eh row in HBM scratch, int32 cells; any length.
 //                  Used for qlen > QMAX or scores that could overflow int16.
 #pragma once
@@ -18,7 +20,8 @@ struct KParams {
     int32_t o_del, e_del, o_ins, e_ins;
     int32_t zdrop, end_bonus;
     int32_t maxsc;              // max(0, max(mat)) -- A.2 band cap and the M-gate bound
-    int32_t pad;
+    int32_t pk_ok;              // scoring fits the packed kernel (match 1, mismatch -b, N -1,
+                                //   symmetric gaps); set by the host, see bsw_pk.hip
     uint32_t prof[8][2];        // prof[t] = 8 score bytes mat[t][q], q = 0..7 (q>4 -> ambig)
     int8_t mat[25];
 };
@@ -32,6 +35,13 @@ constexpr int kLaneQmaxMax = 160;
 hipError_t launch_lane_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
                               const int32_t *order, int32_t n, const uint8_t *ref,
                               const uint8_t *qer, int32_t *err, hipStream_t s);
+
+// Packed two-pairs-per-lane kernel (bsw_pk.hip): kp.pk_ok scoring, qlen <= qmax (160),
+// h0 + min(len1, len2) <= 255.  order[] slice as for the lane kernel; 128 pairs per wave.
+constexpr int kPkQmax = 160;
+hipError_t launch_pk_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
+                            const int32_t *order, int32_t n, const uint8_t *ref,
+                            const uint8_t *qer, int32_t *err, hipStream_t s);
 
 // Wide kernel: any qlen/tlen, int32 cells, eh scratch of n * (max_qlen + 2) int2 in HBM.
 hipError_t launch_wide_kernel(const KParams &kp, int32_t w, SeqPair *pairs,

@@ -22,6 +22,7 @@
 #include <limits.h>
 #include <utility>
 #include "bsw_kernels.h"
+#include "bsw_wave.h"
 
 // Timing-only experiment hooks (never defined in product builds): extra dummy instructions
 // injected into the fast group, writing temps that are dead at that point.
@@ -45,30 +46,6 @@
 #endif
 
 namespace bsw {
-
-// ------------------------------------------------------------------ wave-level helpers
-// Wave-uniform max / min over all 64 lanes (exec must be full): DPP row_shr scan inside
-// each 16-lane row, then the four row results via v_readlane.
-__device__ __forceinline__ int wave_max(int x)
-{
-    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x111, 0xf, 0xf, false));
-    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x112, 0xf, 0xf, false));
-    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x114, 0xf, 0xf, false));
-    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x118, 0xf, 0xf, false));
-    int a = __builtin_amdgcn_readlane(x, 15), b = __builtin_amdgcn_readlane(x, 31);
-    int c = __builtin_amdgcn_readlane(x, 47), d = __builtin_amdgcn_readlane(x, 63);
-    return max(max(a, b), max(c, d));
-}
-__device__ __forceinline__ int wave_min(int x)
-{
-    x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x111, 0xf, 0xf, false));
-    x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x112, 0xf, 0xf, false));
-    x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x114, 0xf, 0xf, false));
-    x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x118, 0xf, 0xf, false));
-    int a = __builtin_amdgcn_readlane(x, 15), b = __builtin_amdgcn_readlane(x, 31);
-    int c = __builtin_amdgcn_readlane(x, 47), d = __builtin_amdgcn_readlane(x, 63);
-    return min(min(a, b), min(c, d));
-}
 
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
@@ -160,7 +137,7 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
                                                int glo, int gsp, int gfa, int gfn, int beg, int span)
 {
     int m0, m1, m2, m3, t0, t1, t2, t3, x0, x1, x2, x3, ha, hb, k0, k1, l0, l1, pw, st, d, tp;
-    uint64_t sat, slt;
+    uint64_t sat, slt, inb;
     asm volatile(
         "s_sub_u32 %[st], %[g], %[glo]\n\t"     // group outside [min beg, max end]: skip
         "s_cmp_le_u32 %[st], %[gsp]\n\t"
@@ -229,14 +206,14 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "s_branch 3f\n"
         "2:\n\t"
         "v_sub_u32_e32 %[d], %[j0], %[beg]\n\t"
-        "v_cmp_lt_u32_e32 vcc, %[d], %[span]\n\t"
+        "v_cmp_lt_u32_e64 %[inb], %[d], %[span]\n\t"
         "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
         "v_cmp_gt_i32_e64 %[slt], 0, %[d]\n\t"
         "v_max_i32_e32 %[tp], %[f], %[m0]\n\t"
-        "v_cndmask_b32_e32 %[ha], %[h1], %[tp], vcc\n\t"
-        "v_cndmask_b32_e32 %[tp], 0, %[tp], vcc\n\t"
+        "v_cndmask_b32_e64 %[ha], %[h1], %[tp], %[inb]\n\t"
+        "v_cndmask_b32_e64 %[tp], 0, %[tp], %[inb]\n\t"
         "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
-        "v_cndmask_b32_e32 %[x0], 0, %[x0], vcc\n\t"
+        "v_cndmask_b32_e64 %[x0], 0, %[x0], %[inb]\n\t"
         "v_max3_i32 %[f], %[f], %[t0], 0\n\t"
         "v_lshl_or_b32 %[d], %[x0], 16, %[h1]\n\t"
         "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
@@ -245,14 +222,14 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_or_b32_e32 %[k0], %[j0], %[tp]\n\t"
         "v_min_i32_e32 %[l0], %[j1], %[tp]\n\t"
         "v_sub_u32_e32 %[d], %[j1], %[beg]\n\t"
-        "v_cmp_lt_u32_e32 vcc, %[d], %[span]\n\t"
+        "v_cmp_lt_u32_e64 %[inb], %[d], %[span]\n\t"
         "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
         "v_cmp_gt_i32_e64 %[slt], 0, %[d]\n\t"
         "v_max_i32_e32 %[tp], %[f], %[m1]\n\t"
-        "v_cndmask_b32_e32 %[hb], %[ha], %[tp], vcc\n\t"
-        "v_cndmask_b32_e32 %[tp], 0, %[tp], vcc\n\t"
+        "v_cndmask_b32_e64 %[hb], %[ha], %[tp], %[inb]\n\t"
+        "v_cndmask_b32_e64 %[tp], 0, %[tp], %[inb]\n\t"
         "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
-        "v_cndmask_b32_e32 %[x1], 0, %[x1], vcc\n\t"
+        "v_cndmask_b32_e64 %[x1], 0, %[x1], %[inb]\n\t"
         "v_max3_i32 %[f], %[f], %[t1], 0\n\t"
         "v_lshl_or_b32 %[d], %[x1], 16, %[ha]\n\t"
         "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
@@ -263,14 +240,14 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
         "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
         "v_sub_u32_e32 %[d], %[j2], %[beg]\n\t"
-        "v_cmp_lt_u32_e32 vcc, %[d], %[span]\n\t"
+        "v_cmp_lt_u32_e64 %[inb], %[d], %[span]\n\t"
         "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
         "v_cmp_gt_i32_e64 %[slt], 0, %[d]\n\t"
         "v_max_i32_e32 %[tp], %[f], %[m2]\n\t"
-        "v_cndmask_b32_e32 %[ha], %[hb], %[tp], vcc\n\t"
-        "v_cndmask_b32_e32 %[tp], 0, %[tp], vcc\n\t"
+        "v_cndmask_b32_e64 %[ha], %[hb], %[tp], %[inb]\n\t"
+        "v_cndmask_b32_e64 %[tp], 0, %[tp], %[inb]\n\t"
         "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
-        "v_cndmask_b32_e32 %[x2], 0, %[x2], vcc\n\t"
+        "v_cndmask_b32_e64 %[x2], 0, %[x2], %[inb]\n\t"
         "v_max3_i32 %[f], %[f], %[t2], 0\n\t"
         "v_lshl_or_b32 %[d], %[x2], 16, %[hb]\n\t"
         "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
@@ -279,14 +256,14 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_or_b32_e32 %[k0], %[j2], %[tp]\n\t"
         "v_min_i32_e32 %[l0], %[j3], %[tp]\n\t"
         "v_sub_u32_e32 %[d], %[j3], %[beg]\n\t"
-        "v_cmp_lt_u32_e32 vcc, %[d], %[span]\n\t"
+        "v_cmp_lt_u32_e64 %[inb], %[d], %[span]\n\t"
         "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
         "v_cmp_gt_i32_e64 %[slt], 0, %[d]\n\t"
         "v_max_i32_e32 %[tp], %[f], %[m3]\n\t"
-        "v_cndmask_b32_e32 %[h1], %[ha], %[tp], vcc\n\t"
-        "v_cndmask_b32_e32 %[tp], 0, %[tp], vcc\n\t"
+        "v_cndmask_b32_e64 %[h1], %[ha], %[tp], %[inb]\n\t"
+        "v_cndmask_b32_e64 %[tp], 0, %[tp], %[inb]\n\t"
         "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
-        "v_cndmask_b32_e32 %[x3], 0, %[x3], vcc\n\t"
+        "v_cndmask_b32_e64 %[x3], 0, %[x3], %[inb]\n\t"
         "v_max3_i32 %[f], %[f], %[t3], 0\n\t"
         "v_lshl_or_b32 %[d], %[x3], 16, %[ha]\n\t"
         "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
@@ -302,7 +279,7 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
           [m3] "=&v"(m3), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
           [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2), [x3] "=&v"(x3), [ha] "=&v"(ha),
           [hb] "=&v"(hb), [k0] "=&v"(k0), [k1] "=&v"(k1), [l0] "=&v"(l0), [l1] "=&v"(l1),
-          [pw] "=&v"(pw), [d] "=&v"(d), [tp] "=&v"(tp), [sat] "=&s"(sat), [slt] "=&s"(slt),
+          [pw] "=&v"(pw), [d] "=&v"(d), [tp] "=&v"(tp), [inb] "=&s"(inb), [sat] "=&s"(sat), [slt] "=&s"(slt),
           [st] "=&s"(st)
         : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe] "s"(oe), [ed] "s"(ed),
           [glo] "s"(glo), [gsp] "s"(gsp), [gfa] "s"(gfa), [gfn] "s"(gfn), [beg] "v"(beg),
@@ -350,17 +327,6 @@ __device__ __forceinline__ void lane_row(std::integer_sequence<int, G...>, uint3
     (lane_group<G, QMAX, SM, SYM>(eh, q4, pr, beg, end, f, h1, key, lp1, r, c), ...);
 }
 
-__device__ __forceinline__ uint32_t load4(const uint8_t *p, int base, int len)
-{
-    uint32_t w = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (base + k < len) w |= (uint32_t)p[base + k] << (8 * k);
-    return w;
-}
-
-typedef const __attribute__((address_space(1))) void *gptr_t;
-typedef __attribute__((address_space(3))) void *lptr_t;
 constexpr int kTChunkDw = 17;            // dwords per lane per 64-row target chunk
 
 template <int QMAX, int SM, bool SYM>

@@ -194,6 +194,46 @@ def test_multi_gpu_context_shards(c2_full):
     _assert_same(want[:100_000], got, f"n_gpus={n}")
 
 
+@pytest.fixture(scope="module")
+def eng_pk():
+    """Engine with the opt-in packed two-pairs-per-lane kernel enabled (BSW_PK=1 at create)."""
+    import os
+    os.environ["BSW_PK"] = "1"
+    try:
+        e = bsw.Engine()
+    finally:
+        os.environ.pop("BSW_PK")
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("w", [0, 1, 7, 40, 100, 200])
+def test_packed_kernel_random(eng_pk, w):
+    """qlen 129..160 with h0 + min(qlen, tlen) <= 255 routes to bsw_pk.hip (1 launch)."""
+    pairs, ref, qer = bswgen.random_pairs(4000, seed=70 + w, qlen=(129, 160), tlen=(0, 330), h0=(0, 95))
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+    eng_pk.get_scores(got, ref, qer, w)
+    _assert_same(want, got, f"packed w={w}")
+    assert eng_pk.last_stats().n_launches == 1
+
+
+def test_packed_kernel_mixed_routing(eng_pk):
+    """h0 above the 8-bit key bound and short queries fall back to the lane kernels."""
+    pairs, ref, qer = bswgen.random_pairs(4000, seed=5, qlen=(0, 170), tlen=(0, 330), h0=(0, 160))
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    eng_pk.get_scores(got, ref, qer, 100)
+    _assert_same(want, got, "packed mixed routing")
+
+
+def test_packed_kernel_c2(eng_pk, c2_full):
+    pairs, ref, qer, want = c2_full
+    got = pairs[:300_000].copy()
+    eng_pk.get_scores(got, ref, qer, 100)
+    _assert_same(want[:300_000], got, "packed C2")
+
+
 def test_argument_errors(eng):
     pairs, ref, qer = bswgen.random_pairs(10, seed=1)
     lib = bsw.hip_lib()

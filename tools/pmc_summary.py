@@ -18,6 +18,8 @@ def rows(pattern):
     return out
 
 def short(name):
+    if 'pk_kernel' in name:
+        return 'pk_kernel<160>'
     if 'lane_kernel' in name:
         for q in ('160', '128', '96', '64', '32'):
             if f'ILi{q}E' in name or f'<{q},' in name:
