@@ -33,10 +33,13 @@
 namespace bsw {
 
 constexpr int kNumLaneClasses = 5;          // QMAX 32, 64, 96, 128, 160
-constexpr int kPkClass = kNumLaneClasses;   // packed two-pairs-per-lane kernel (QMAX 160)
-constexpr int kWideClass = kPkClass + 1;    // index of the wide-kernel class
+constexpr int kPkClass0 = kNumLaneClasses;  // packed kernel, same QMAX buckets (classes 5..9)
+constexpr int kWideClass = kPkClass0 + kNumLaneClasses;   // index of the wide-kernel class
 constexpr int kNumClasses = kWideClass + 1;
-constexpr int kKeyBits = 32;                // 3 class + 8 qlen + 1 related + 12 tlen + 8 h0 bits
+constexpr int kMetaCounts = 16;             // d_meta: counts[16], maxq_wide, err
+constexpr int kMetaWords = kMetaCounts + 2;
+constexpr int kKeyBits = 32;                // 4 class + 8 qlen + 1 related + 11 tlen + 8 h0 bits
+static_assert(kNumClasses <= kMetaCounts, "class counts");
 
 // Lifetime predictor for the sort key (scheduling only, results never depend on it): does the
 // query look like an extension of the target near the seed?  Identity of query[10, 40) with
@@ -84,16 +87,16 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
         else if (qlen <= 96) c = 2;
         else if (qlen <= 128) c = 3;
         else if (qlen <= 160) c = 4;
-        // packed kernel: bwa scoring, key H << 8 | j fits 16 bits (H <= h0 + min(qlen, tlen))
-        if (pk_ok && qlen > 128 && qlen <= kPkQmax && p.h0 + min(qlen, tlen) <= 255) c = kPkClass;
+        // 8-bit score regime -> packed kernel (key H << 8 | j fits 16 bits, H <= h0 + min(qlen, tlen))
+        if (pk_ok && c < kNumLaneClasses && p.h0 + min(qlen, tlen) <= 255) c += kPkClass0;
     }
     if (valid) {
         if (c == kWideClass) atomicMax(maxq_wide, qlen);
         // (class, qlen desc, related first, tlen desc, h0 desc): like-shaped pairs share a
         // wavefront; equal h0 and relatedness give lanes similar band-end trajectories
         const int rel = (c == kWideClass) ? 1 : seed_related(qer + p.idq, qlen, ref + p.idr, tlen);
-        keys[i] = ((uint32_t)c << 29) | ((uint32_t)(255 - min(qlen, 255)) << 21) |
-                  ((uint32_t)(1 - rel) << 20) | ((uint32_t)(4095 - min(tlen, 4095)) << 8) |
+        keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
+                  ((uint32_t)(1 - rel) << 19) | ((uint32_t)(2047 - min(tlen, 2047)) << 8) |
                   (uint32_t)(255 - min(max(p.h0, 0), 255));
         vals[i] = i;
     }
@@ -117,7 +120,7 @@ struct Slot {
     uint32_t *d_keys = nullptr, *d_keys2 = nullptr;
     int32_t *d_vals = nullptr, *d_order = nullptr; size_t cap_sort = 0;
     void *d_tmp = nullptr; size_t cap_tmp = 0;
-    int32_t *d_meta = nullptr;          // counts[8], maxq_wide, err
+    int32_t *d_meta = nullptr;          // counts[kMetaCounts], maxq_wide, err
     int32_t *h_meta = nullptr;          // pinned mirror
     int2 *d_scratch = nullptr; size_t cap_scratch = 0;
     bool timed = false;
@@ -184,8 +187,8 @@ struct DeviceCtx {
         if ((rc = hip_rc(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)))) return nullptr;
         if ((rc = hip_rc(hipEventCreate(&s->ev0)))) return nullptr;
         if ((rc = hip_rc(hipEventCreate(&s->ev1)))) return nullptr;
-        if ((rc = hip_rc(hipMalloc((void **)&s->d_meta, 16 * sizeof(int32_t))))) return nullptr;
-        if ((rc = hip_rc(hipHostMalloc((void **)&s->h_meta, 16 * sizeof(int32_t), 0)))) return nullptr;
+        if ((rc = hip_rc(hipMalloc((void **)&s->d_meta, kMetaWords * sizeof(int32_t))))) return nullptr;
+        if ((rc = hip_rc(hipHostMalloc((void **)&s->h_meta, kMetaWords * sizeof(int32_t), 0)))) return nullptr;
         return s;
     }
     void give_back(std::unique_ptr<Slot> s)
@@ -225,8 +228,9 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
         kp.prof[t][1] = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
     }
     // packed kernel scoring contract (bsw_pk.hip): match 1, one mismatch value in [-127, -1],
-    // every N entry -1, symmetric gap penalties.  Opt-in (BSW_PK=1): at one wave per SIMD it
-    // measures slower than the lane kernel on C2, so it is not the default.
+    // every N entry -1, symmetric gap penalties.  Used for cell_bits = 8 calls; on 16-bit calls
+    // only with BSW_PK=1 (at one wave per SIMD it measures slower than the lane kernel on C2,
+    // DESIGN.md §4.2).
     bool ok = p.o_del == p.o_ins && p.e_del == p.e_ins && p.e_del > 0 && p.o_del + p.e_del < 16384;
     const int mis = p.mat[1];
     ok = ok && mis < 0 && mis >= -127;
@@ -235,14 +239,14 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
             const int v = p.mat[a * 5 + b];
             ok = (a == 4 || b == 4) ? v == -1 : (a == b ? v == 1 : v == mis);
         }
-    const char *pk = getenv("BSW_PK");
-    if (!(pk && pk[0] == '1')) ok = false;
     kp.pk_ok = ok ? 1 : 0;
+    const char *pk = getenv("BSW_PK");
+    kp.pk_default = (pk && pk[0] == '1') ? 1 : 0;
 }
 
 // The device pipeline on one slot's device; d_* are device pointers valid on `stream`.
 static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_t *d_ref,
-                      const uint8_t *d_qer, int32_t n, int32_t w, hipStream_t stream)
+                      const uint8_t *d_qer, int32_t n, int32_t w, int cell_bits, hipStream_t stream)
 {
     s.stats = bsw_stats_t{};
     if (n == 0) return BSW_OK;
@@ -256,10 +260,13 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
         BSW_TRY(hipMalloc((void **)&s.d_order, cap * sizeof(int32_t)));
         s.cap_sort = cap;
     }
-    BSW_TRY(hipMemsetAsync(s.d_meta, 0, 16 * sizeof(int32_t), stream));
-    int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + 8, *d_err = s.d_meta + 9;
+    BSW_TRY(hipMemsetAsync(s.d_meta, 0, kMetaWords * sizeof(int32_t), stream));
+    int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaCounts, *d_err = s.d_meta + kMetaCounts + 1;
+    // cell_bits = 8 (getScores8): pairs in the 8-bit score regime take the packed kernel, the
+    // rest the int16 kernels (overflow fallback); cell_bits = 16: int16 kernels (BSW_PK=1: packed too)
+    const int use_pk = kp.pk_ok && (cell_bits == 8 || kp.pk_default);
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       d_pairs, n, kp.maxsc, kp.pk_ok, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
+                       d_pairs, n, kp.maxsc, use_pk, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
                        d_maxq);
     BSW_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
@@ -268,11 +275,11 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     BSW_TRY(grow(s.d_tmp, s.cap_tmp, tmp_bytes));
     BSW_TRY(hipcub::DeviceRadixSort::SortPairs(s.d_tmp, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals,
                                                s.d_order, n, 0, kKeyBits, stream));
-    BSW_TRY(hipMemcpyAsync(s.h_meta, s.d_meta, 16 * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    BSW_TRY(hipMemcpyAsync(s.h_meta, s.d_meta, kMetaWords * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
     BSW_TRY(hipStreamSynchronize(stream));
     int32_t counts[kNumClasses];
     memcpy(counts, s.h_meta, sizeof(counts));
-    const int32_t maxq_wide = s.h_meta[8];
+    const int32_t maxq_wide = s.h_meta[kMetaCounts];
     // DP kernels, one launch per non-empty class; event-timed as the hot region
     BSW_TRY(hipEventRecord(s.ev0, stream));
     int32_t off = 0;
@@ -285,12 +292,16 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
         }
         off += counts[c];
     }
-    if (counts[kPkClass] > 0) {
-        BSW_TRY(launch_pk_kernel(kPkQmax, kp, w, d_pairs, s.d_order + off, counts[kPkClass], d_ref,
-                                 d_qer, d_err, stream));
-        s.stats.n_launches++;
-        s.stats.n_i16 += counts[kPkClass];
-        off += counts[kPkClass];
+    for (int c = 0; c < kNumLaneClasses; ++c) {
+        const int32_t np = counts[kPkClass0 + c];
+        if (np > 0) {
+            BSW_TRY(launch_pk_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
+                                     d_err, stream));
+            s.stats.n_launches++;
+            if (cell_bits == 8) s.stats.n_u8 += np;
+            else s.stats.n_i16 += np;
+        }
+        off += np;
     }
     if (counts[kWideClass] > 0) {
         const int32_t nw = counts[kWideClass];
@@ -320,7 +331,7 @@ static int finish_stats(Slot &s)
 
 // One device's share of a host-buffer call.
 static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref,
-                      const uint8_t *qer, int32_t n, int32_t w, bsw_stats_t *st)
+                      const uint8_t *qer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *st)
 {
     if (n == 0) return BSW_OK;
     int rc = BSW_OK;
@@ -346,12 +357,12 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, ref + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
         if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, qer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
         // kernels index ref/qer by idr/idq: shift the base so d_ref[idr - r_lo] is byte idr
-        int r = run_device(kp, s, s.d_pairs, s.d_ref - r_lo, s.d_qer - q_lo, n, w, s.stream);
+        int r = run_device(kp, s, s.d_pairs, s.d_ref - r_lo, s.d_qer - q_lo, n, w, cell_bits, s.stream);
         if (r) return r;
         BSW_TRY(hipMemcpyAsync(pairs, s.d_pairs, (size_t)n * sizeof(SeqPair), hipMemcpyDeviceToHost, s.stream));
         BSW_TRY(hipStreamSynchronize(s.stream));
         if ((r = finish_stats(s))) return r;
-        if (s.h_meta[9] != 0) return BSW_E_RANGE;   // kernel guard tripped (routing bug)
+        if (s.h_meta[kMetaCounts + 1] != 0) return BSW_E_RANGE;   // kernel guard tripped (routing bug)
         if (st) *st = s.stats;
         return BSW_OK;
     }();
@@ -431,14 +442,14 @@ int bsw_get_scores(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef,
     std::vector<int> rcs(nd, BSW_OK);
     std::vector<bsw_stats_t> st(nd);
     if (nd == 1) {
-        rcs[0] = bsw::host_shard(ctx->kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, &st[0]);
+        rcs[0] = bsw::host_shard(ctx->kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, cell_bits, &st[0]);
     } else {
         std::vector<std::thread> th;
         for (int d = 0; d < nd; ++d) {
             const int32_t a = (int32_t)((int64_t)n * d / nd), b = (int32_t)((int64_t)n * (d + 1) / nd);
             th.emplace_back([&, d, a, b] {
                 rcs[d] = bsw::host_shard(ctx->kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer,
-                                         b - a, w, &st[d]);
+                                         b - a, w, cell_bits, &st[d]);
             });
         }
         for (auto &t : th) t.join();
@@ -469,10 +480,10 @@ int bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref
     rc = [&]() -> int {
         BSW_TRY(hipSetDevice(dc.device));
         hipStream_t st = stream ? (hipStream_t)stream : slot->stream;
-        int r = bsw::run_device(ctx->kp, *slot, d_pairs, d_ref, d_qer, n, w, st);
+        int r = bsw::run_device(ctx->kp, *slot, d_pairs, d_ref, d_qer, n, w, cell_bits, st);
         if (r) return r;
         if ((r = bsw::finish_stats(*slot))) return r;
-        if (slot->h_meta[9] != 0) return BSW_E_RANGE;
+        if (slot->h_meta[bsw::kMetaCounts + 1] != 0) return BSW_E_RANGE;
         std::lock_guard<std::mutex> g(ctx->stats_mu);
         ctx->last = slot->stats;
         return BSW_OK;

@@ -24,6 +24,8 @@ struct KParams {
                                 //   symmetric gaps); set by the host, see bsw_pk.hip
     uint32_t prof[8][2];        // prof[t] = 8 score bytes mat[t][q], q = 0..7 (q>4 -> ambig)
     int8_t mat[25];
+    int8_t pk_default;          // host: route 8-bit-regime pairs to the packed kernel on 16-bit
+                                //   calls too (BSW_PK=1)
 };
 
 // qlen limit of the register-resident kernel instantiations.
@@ -36,9 +38,9 @@ hipError_t launch_lane_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *p
                               const int32_t *order, int32_t n, const uint8_t *ref,
                               const uint8_t *qer, int32_t *err, hipStream_t s);
 
-// Packed two-pairs-per-lane kernel (bsw_pk.hip): kp.pk_ok scoring, qlen <= qmax (160),
-// h0 + min(len1, len2) <= 255.  order[] slice as for the lane kernel; 128 pairs per wave.
-constexpr int kPkQmax = 160;
+// Packed two-pairs-per-lane kernel (bsw_pk.hip): kp.pk_ok scoring, qlen <= qmax (one of
+// kLaneQmax), h0 + min(len1, len2) <= 255 (the 8-bit score regime: this is the engine's
+// cell_bits = 8 path).  order[] slice as for the lane kernel; 128 pairs per wave.
 hipError_t launch_pk_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
                             const int32_t *order, int32_t n, const uint8_t *ref,
                             const uint8_t *qer, int32_t *err, hipStream_t s);

@@ -228,8 +228,9 @@ __device__ __forceinline__ uint32_t pk_tenc(uint32_t t)
     return t < 4u ? (t | ((t ^ 12u) << 8)) : (8u | (9u << 8));
 }
 
+// QMAX <= 64 fits two waves per SIMD (<= 256 VGPR + AGPR); larger buckets run one.
 template <int QMAX>
-__global__ __launch_bounds__(256, 1) void pk_kernel(const KParams kp, const int32_t w,
+__global__ __launch_bounds__(256, QMAX <= 64 ? 2 : 1) void pk_kernel(const KParams kp, const int32_t w,
                                                     SeqPair *__restrict__ pairs,
                                                     const int32_t *__restrict__ order,
                                                     const int32_t n,
@@ -453,11 +454,12 @@ hipError_t launch_pk_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pai
     if (n <= 0) return hipSuccess;
     const dim3 block(256), grid((unsigned)((n + 511) / 512));
     switch (qmax) {
-    case 160:
-        hipLaunchKernelGGL(pk_kernel<160>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err);
-        break;
-    default:
-        return hipErrorInvalidValue;
+    case 32: hipLaunchKernelGGL(pk_kernel<32>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 64: hipLaunchKernelGGL(pk_kernel<64>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 96: hipLaunchKernelGGL(pk_kernel<96>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 128: hipLaunchKernelGGL(pk_kernel<128>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 160: hipLaunchKernelGGL(pk_kernel<160>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

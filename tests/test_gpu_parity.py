@@ -153,10 +153,28 @@ def test_c2_full_workload_host_api_permuted(eng, c2_full):
 
 
 def test_cell_bits_8_matches_16(eng, c2_full):
+    """getScores8 path: every C2 pair is in the 8-bit score regime (h0 + 150 <= 255) and takes
+    the packed kernel (n_u8); results equal the int16 path's / the oracle's."""
     pairs, ref, qer, want = c2_full
     got = pairs[:200_000].copy()
     eng.get_scores(got, ref, qer, 100, cell_bits=8)
     _assert_same(want[:200_000], got, "cell_bits=8")
+    st = eng.last_stats()
+    assert st.n_u8 == 200_000 and st.n_i16 == 0
+
+
+def test_cell_bits_8_overflow_fallback(eng):
+    """C3-style routing: pairs whose score could exceed 255 fall back to the int16 kernels."""
+    pairs, ref, qer = bswgen.random_pairs(5000, seed=33, qlen=(0, 170), tlen=(0, 330), h0=(0, 200))
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    eng.get_scores(got, ref, qer, 100, cell_bits=8)
+    _assert_same(want, got, "cell_bits=8 mixed")
+    st = eng.last_stats()
+    q, t, h0 = pairs["len2"], pairs["len1"], pairs["h0"]
+    narrow = (q <= 160) & (h0 + np.minimum(q, t) <= 255)
+    assert st.n_u8 == int(narrow.sum())
+    assert st.n_i16 + st.n_wide == len(pairs) - int(narrow.sum())
 
 
 def test_concurrent_callers(eng):
