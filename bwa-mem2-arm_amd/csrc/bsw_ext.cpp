@@ -1,0 +1,270 @@
+// bsw_ext.cpp -- seed-extension job builder + result interpreter (include/bsw_ext.h).
+//
+// Host C++ around the batch engine, restating the extension half of upstream's
+// mem_chain2aln / mem_chain2aln_across_reads_V2 (src/bwamem.cpp; semantics in bsw_ext.h and
+// SURVEY.md a9/§8(f) row 1).  Per call:
+//   phase 0  LEFT  jobs (qbeg > 0): reversed query prefix vs reversed target window, h0 = seed
+//            score, band w; phase 1: LEFT retries with w << 1 where the score changed and
+//            max_off >= 3/4 w (MAX_BAND_TRY); interpret local vs to-end with pen_clip5
+//   phase 2  RIGHT jobs (qe < l_query): query suffix vs target window, h0 = the LEFT score;
+//            phase 3: retries; interpret with pen_clip3
+// Each phase is ONE bsw batch over all reads (SeqPair AoS + concatenated code buffers in
+// upstream's layout); buffers are filled by a host thread pool.  The CPU restatement used as
+// the oracle is oracle/ext_ref.c.
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <thread>
+#include <vector>
+#include "../../include/bsw_ext.h"
+#include "bsw_internal.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+float ms_since(Clock::time_point t0)
+{
+    return std::chrono::duration<float, std::milli>(Clock::now() - t0).count();
+}
+
+struct Job {                       // one extension of one read
+    int32_t read;                  // read index
+    int32_t qlen, tlen;
+    int64_t qoff, toff;            // offsets into the phase's code buffers
+};
+
+int cal_max_gap(const bsw_params_t &p, int a, int w, int qlen)
+{
+    const int l_del = (int)((double)(qlen * a - p.o_del) / p.e_del + 1.);
+    const int l_ins = (int)((double)(qlen * a - p.o_ins) / p.e_ins + 1.);
+    int l = std::max(l_del, l_ins);
+    l = std::max(l, 1);
+    return std::min(l, w << 1);
+}
+
+template <class F>
+void parallel_for(int32_t n, F f)
+{
+    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < 4096 || nt == 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) {
+        const int32_t a = (int32_t)((int64_t)n * t / nt), b = (int32_t)((int64_t)n * (t + 1) / nt);
+        th.emplace_back([=] { f(a, b); });
+    }
+    for (auto &x : th) x.join();
+}
+
+struct Buf {                       // code buffer: pinned per-context staging when free, else heap
+    bsw_ctx_t *ctx = nullptr;
+    int which = 0;
+    uint8_t *p = nullptr;
+    bool pinned = false;
+    std::unique_ptr<uint8_t[]> heap;
+    void get(bsw_ctx_t *c, int w, size_t bytes)
+    {
+        ctx = c; which = w;
+        p = (uint8_t *)bsw::pinned_acquire(c, w, bytes);
+        pinned = p != nullptr;
+        if (!pinned) { heap.reset(new uint8_t[bytes]); p = heap.get(); }   // uninitialised
+    }
+    ~Buf() { if (pinned) bsw::pinned_release(ctx, which); }
+};
+
+struct Phase {                     // one batch: jobs + SeqPairs + code buffers
+    std::vector<Job> jobs;
+    std::vector<SeqPair> pairs;
+    Buf qbuf, tbuf;
+
+    // lay out buffers for jobs (qlen/tlen set), fill with `fill(job, qdst, tdst)`
+    template <class Fill>
+    void build(bsw_ctx_t *ctx, Fill fill)
+    {
+        int64_t qo = 0, to = 0;
+        for (auto &j : jobs) {
+            j.qoff = qo; j.toff = to;
+            qo += j.qlen; to += j.tlen;
+        }
+        qbuf.get(ctx, 0, (size_t)std::max<int64_t>(qo, 1));
+        tbuf.get(ctx, 1, (size_t)std::max<int64_t>(to, 1));
+        pairs.resize(jobs.size());
+        parallel_for((int32_t)jobs.size(), [&](int32_t a, int32_t b) {
+            for (int32_t k = a; k < b; ++k) {
+                const Job &j = jobs[k];
+                fill(j, qbuf.p + j.qoff, tbuf.p + j.toff);
+                SeqPair &p = pairs[k];
+                p = SeqPair{};
+                p.idr = (int32_t)j.toff; p.idq = (int32_t)j.qoff;
+                p.id = j.read; p.len1 = j.tlen; p.len2 = j.qlen;
+            }
+        });
+    }
+};
+
+}  // namespace
+
+extern "C" void bsw_ext_opt_default(bsw_ext_opt_t *opt)
+{
+    opt->w = 100;
+    opt->pen_clip5 = 5;
+    opt->pen_clip3 = 5;
+    opt->max_band_try = 2;
+}
+
+extern "C" int bsw_ext_last_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out)
+{
+    return bsw::get_ext_stats(ctx, out);
+}
+
+extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *ref,
+                                int64_t ref_len, const uint8_t *reads, const int64_t *read_off,
+                                const int32_t *read_len, const bsw_seed_t *seeds, int32_t n,
+                                bsw_alnreg_t *out)
+{
+    if (!ctx || !opt || n < 0 || (n > 0 && (!ref || !reads || !read_off || !read_len || !seeds || !out)))
+        return BSW_E_INVAL;
+    if (opt->w < 0 || opt->max_band_try < 1 || ref_len < 0) return BSW_E_INVAL;
+    bsw_params_t p;
+    bsw::ctx_params(ctx, &p);
+    const int a = p.mat[0];
+    bsw_ext_stats_t es{};
+    // per-read state (mem_alnreg_t subset + the window and scores the phases need)
+    std::vector<int64_t> rmax0(n), rmax1(n);
+    std::vector<int32_t> score(n, 0), lw(n, opt->w), rw(n, opt->w);   // aw[0], aw[1]
+    for (int32_t i = 0; i < n; ++i) {
+        bsw_alnreg_t &r = out[i];
+        memset(&r, 0, sizeof(r));
+        const bsw_seed_t &s = seeds[i];
+        if (s.len <= 0) continue;
+        const int32_t l = read_len[i];
+        if (s.qbeg < 0 || s.qbeg + s.len > l || s.rbeg < 0 || s.rbeg + s.len > ref_len || l > BSW_MAX_LEN)
+            return BSW_E_RANGE;
+        const int32_t qe = s.qbeg + s.len;
+        const int64_t b = s.rbeg - (s.qbeg + cal_max_gap(p, a, opt->w, s.qbeg));
+        const int64_t e = s.rbeg + s.len + ((l - qe) + cal_max_gap(p, a, opt->w, l - qe));
+        rmax0[i] = std::max<int64_t>(b, 0);
+        rmax1[i] = std::min<int64_t>(e, ref_len);
+        if (s.rbeg - rmax0[i] > BSW_MAX_LEN || rmax1[i] - (s.rbeg + s.len) > BSW_MAX_LEN) return BSW_E_RANGE;
+        r.seedlen0 = s.len;
+        // no-extension defaults (mem_chain2aln): qbeg == 0 / qe == l_query
+        r.score = r.truesc = s.len * a;
+        r.qb = 0; r.rb = s.rbeg;
+        r.qe = l; r.re = s.rbeg + s.len;
+        score[i] = s.len * a;
+    }
+
+    // run one side: build jobs, batch (+ retries), return per-job final SeqPair and band
+    auto run_side = [&](bool left, int phase0, std::vector<int32_t> &band) -> int {
+        auto tb = Clock::now();
+        Phase ph;
+        ph.jobs.reserve((size_t)n);
+        for (int32_t i = 0; i < n; ++i) {
+            const bsw_seed_t &s = seeds[i];
+            if (s.len <= 0) continue;
+            const int32_t qe = s.qbeg + s.len;
+            if (left ? s.qbeg == 0 : qe == read_len[i]) continue;
+            Job j{};
+            j.read = i;
+            j.qlen = left ? s.qbeg : read_len[i] - qe;
+            j.tlen = left ? (int32_t)(s.rbeg - rmax0[i]) : (int32_t)(rmax1[i] - (s.rbeg + s.len));
+            ph.jobs.push_back(j);
+        }
+        if (ph.jobs.empty()) return BSW_OK;
+        ph.build(ctx, [&](const Job &j, uint8_t *qd, uint8_t *td) {
+            const bsw_seed_t &s = seeds[j.read];
+            const uint8_t *q = reads + read_off[j.read];
+            if (left) {             // reversed prefix / reversed window ending at rbeg
+                for (int32_t k = 0; k < j.qlen; ++k) qd[k] = q[s.qbeg - 1 - k];
+                for (int32_t k = 0; k < j.tlen; ++k) td[k] = ref[s.rbeg - 1 - k];
+            } else {
+                memcpy(qd, q + s.qbeg + s.len, (size_t)j.qlen);
+                memcpy(td, ref + s.rbeg + s.len, (size_t)j.tlen);
+            }
+        });
+        const int32_t nj = (int32_t)ph.jobs.size();
+        std::vector<int32_t> prev(nj);
+        for (int32_t k = 0; k < nj; ++k) {
+            const int32_t i = ph.jobs[k].read;
+            ph.pairs[k].h0 = left ? seeds[i].len * a : score[i];
+            prev[k] = left ? 0 : score[i];     // a->score before the band loop
+            band[i] = opt->w;
+        }
+        const int32_t eb = left ? opt->pen_clip5 : opt->pen_clip3;
+        es.build_ms += ms_since(tb);
+        auto te = Clock::now();
+        bsw_stats_t st{};
+        int rc = bsw::scores_eb(ctx, eb, ph.pairs.data(), ph.tbuf.p, ph.qbuf.p, nj, opt->w, 16, &st);
+        if (rc) return rc;
+        es.n_pairs[phase0] += nj;
+        es.kernel_ms += st.kernel_ms;
+        // band retries: score changed and max_off >= 3/4 of the band -> redo with w << t
+        std::vector<int32_t> idx(nj);
+        for (int32_t k = 0; k < nj; ++k) idx[k] = k;
+        for (int t = 1; t < opt->max_band_try; ++t) {
+            const int32_t wt = opt->w << (t - 1), wn = opt->w << t;
+            std::vector<int32_t> redo;
+            for (int32_t k : idx) {
+                const SeqPair &sp = ph.pairs[k];
+                if (!(sp.score == prev[k] || sp.max_off < (wt >> 1) + (wt >> 2))) redo.push_back(k);
+            }
+            if (redo.empty()) break;
+            std::vector<SeqPair> sub(redo.size());
+            for (size_t r = 0; r < redo.size(); ++r) {
+                prev[redo[r]] = ph.pairs[redo[r]].score;
+                sub[r] = ph.pairs[redo[r]];
+            }
+            rc = bsw::scores_eb(ctx, eb, sub.data(), ph.tbuf.p, ph.qbuf.p, (int32_t)sub.size(), wn,
+                                16, &st);
+            if (rc) return rc;
+            es.n_pairs[phase0 + 1] += (int32_t)sub.size();
+            es.kernel_ms += st.kernel_ms;
+            for (size_t r = 0; r < redo.size(); ++r) {
+                ph.pairs[redo[r]] = sub[r];
+                band[ph.jobs[redo[r]].read] = wn;
+            }
+            idx = redo;
+        }
+        es.engine_ms += ms_since(te);
+        auto ti = Clock::now();
+        // interpret (mem_chain2aln local vs to-end)
+        for (int32_t k = 0; k < nj; ++k) {
+            const SeqPair &sp = ph.pairs[k];
+            const int32_t i = ph.jobs[k].read;
+            const bsw_seed_t &s = seeds[i];
+            bsw_alnreg_t &r = out[i];
+            if (left) {
+                r.score = sp.score;
+                if (sp.gscore <= 0 || sp.gscore <= sp.score - opt->pen_clip5) {
+                    r.qb = s.qbeg - sp.qle; r.rb = s.rbeg - sp.tle; r.truesc = sp.score;
+                } else {
+                    r.qb = 0; r.rb = s.rbeg - sp.gtle; r.truesc = sp.gscore;
+                }
+                score[i] = sp.score;
+            } else {
+                const int32_t sc0 = score[i];
+                const int32_t qe = s.qbeg + s.len;
+                r.score = sp.score;
+                if (sp.gscore <= 0 || sp.gscore <= sp.score - opt->pen_clip3) {
+                    r.qe = qe + sp.qle; r.re = s.rbeg + s.len + sp.tle; r.truesc += sp.score - sc0;
+                } else {
+                    r.qe = read_len[i]; r.re = s.rbeg + s.len + sp.gtle; r.truesc += sp.gscore - sc0;
+                }
+                score[i] = sp.score;
+            }
+        }
+        es.interp_ms += ms_since(ti);
+        return BSW_OK;
+    };
+    int rc = run_side(true, 0, lw);
+    if (rc) return rc;
+    rc = run_side(false, 2, rw);
+    if (rc) return rc;
+    for (int32_t i = 0; i < n; ++i)
+        if (seeds[i].len > 0) out[i].w = std::max(lw[i], rw[i]);
+    bsw::set_ext_stats(ctx, es);
+    return BSW_OK;
+}

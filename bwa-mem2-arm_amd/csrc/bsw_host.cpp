@@ -29,6 +29,7 @@
 #include <vector>
 #include "../../include/bsw.h"
 #include "bsw_kernels.h"
+#include "bsw_internal.h"
 
 namespace bsw {
 
@@ -206,6 +207,13 @@ struct bsw_ctx {
     std::vector<std::unique_ptr<bsw::DeviceCtx>> devs;
     std::mutex stats_mu;
     bsw_stats_t last{};
+    bsw_ext_stats_t ext_last{};
+    struct Pinned { std::mutex mu; void *p = nullptr; size_t cap = 0; } pin[2];
+    ~bsw_ctx()
+    {
+        for (auto &b : pin)
+            if (b.p) (void)hipHostFree(b.p);
+    }
 };
 
 namespace bsw {
@@ -426,30 +434,37 @@ static int validate(const SeqPair *pairs, int32_t n, int32_t w, int cell_bits)
     return BSW_OK;
 }
 
-int bsw_get_scores(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef,
-                   const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits)
+}  // extern "C"
+
+namespace bsw {
+
+int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *seqBufRef,
+              const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *out)
 {
     if (!ctx) return BSW_E_INVAL;
     int rc = validate(pairs, n, w, cell_bits);
     if (rc) return rc;
+    *out = bsw_stats_t{};
     if (n == 0) return BSW_OK;
     if (!seqBufRef || !seqBufQer) return BSW_E_INVAL;
     for (int32_t i = 0; i < n; ++i)
         if (pairs[i].len1 < 0 || pairs[i].len2 < 0 || pairs[i].len1 > BSW_MAX_LEN ||
             pairs[i].len2 > BSW_MAX_LEN || pairs[i].idr < 0 || pairs[i].idq < 0)
             return BSW_E_RANGE;
+    KParams kp = ctx->kp;
+    kp.end_bonus = end_bonus;
     const int nd = (int)ctx->devs.size();
     std::vector<int> rcs(nd, BSW_OK);
     std::vector<bsw_stats_t> st(nd);
     if (nd == 1) {
-        rcs[0] = bsw::host_shard(ctx->kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, cell_bits, &st[0]);
+        rcs[0] = host_shard(kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, cell_bits, &st[0]);
     } else {
         std::vector<std::thread> th;
         for (int d = 0; d < nd; ++d) {
             const int32_t a = (int32_t)((int64_t)n * d / nd), b = (int32_t)((int64_t)n * (d + 1) / nd);
             th.emplace_back([&, d, a, b] {
-                rcs[d] = bsw::host_shard(ctx->kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer,
-                                         b - a, w, cell_bits, &st[d]);
+                rcs[d] = host_shard(kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a, w,
+                                    cell_bits, &st[d]);
             });
         }
         for (auto &t : th) t.join();
@@ -461,8 +476,56 @@ int bsw_get_scores(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef,
         agg.n_i16 += st[d].n_i16; agg.n_u8 += st[d].n_u8; agg.n_wide += st[d].n_wide;
         agg.n_launches += st[d].n_launches;
     }
+    *out = agg;
+    return BSW_OK;
+}
+
+void ctx_params(const bsw_ctx_t *ctx, bsw_params_t *out) { *out = ctx->params; }
+
+void *pinned_acquire(bsw_ctx_t *ctx, int which, size_t bytes)
+{
+    auto &b = ctx->pin[which & 1];
+    if (!b.mu.try_lock()) return nullptr;
+    if (b.cap < bytes) {
+        if (b.p) (void)hipHostFree(b.p);
+        b.p = nullptr; b.cap = 0;
+        const size_t cap = std::max(bytes, b.cap + b.cap / 2);
+        if (hipHostMalloc(&b.p, cap, 0) != hipSuccess) { b.p = nullptr; b.mu.unlock(); return nullptr; }
+        b.cap = cap;
+    }
+    return b.p;
+}
+
+void pinned_release(bsw_ctx_t *ctx, int which) { ctx->pin[which & 1].mu.unlock(); }
+
+void set_ext_stats(bsw_ctx_t *ctx, const bsw_ext_stats_t &s)
+{
     std::lock_guard<std::mutex> g(ctx->stats_mu);
-    ctx->last = agg;
+    ctx->ext_last = s;
+}
+
+int get_ext_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out)
+{
+    if (!ctx || !out) return BSW_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    *out = ctx->ext_last;
+    return BSW_OK;
+}
+
+}  // namespace bsw
+
+extern "C" {
+
+int bsw_get_scores(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef,
+                   const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits)
+{
+    if (!ctx) return BSW_E_INVAL;
+    bsw_stats_t st{};
+    const int rc = bsw::scores_eb(ctx, ctx->params.end_bonus, pairs, seqBufRef, seqBufQer, n, w,
+                                  cell_bits, &st);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    ctx->last = st;
     return BSW_OK;
 }
 

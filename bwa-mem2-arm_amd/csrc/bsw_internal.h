@@ -1,0 +1,19 @@
+// bsw_internal.h -- engine hooks shared by the C ABI translation units (not installed).
+#pragma once
+#include "../../include/bsw.h"
+#include "../../include/bsw_ext.h"
+
+namespace bsw {
+// bsw_get_scores with a per-call end_bonus (LEFT uses pen_clip5, RIGHT pen_clip3) and the
+// call's stats returned instead of stored.
+int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *ref,
+              const uint8_t *qer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *st);
+void ctx_params(const bsw_ctx_t *ctx, bsw_params_t *out);
+// Per-context pinned host staging buffer `which` (0, 1) of at least `bytes`: DMA-speed H2D for
+// the extension pipeline's code buffers.  Returns nullptr when another call holds it (the
+// caller then uses pageable memory); release with pinned_release.
+void *pinned_acquire(bsw_ctx_t *ctx, int which, size_t bytes);
+void pinned_release(bsw_ctx_t *ctx, int which);
+void set_ext_stats(bsw_ctx_t *ctx, const bsw_ext_stats_t &s);
+int get_ext_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out);
+}  // namespace bsw

@@ -95,3 +95,106 @@ void bsw_synth_batch(const bsw_synth_cfg *c, int64_t pair_base, int32_t n, SeqPa
         p->regid = 0;
     }
 }
+
+/* ------------------------------------------------------------------ read-level workload
+ * C4/C5-shaped input for the extension pipeline (include/bsw_ext.h): a random reference and
+ * reads sampled from it with an edit script, each with ONE exact-match seed, as upstream's
+ * SMEM seeding would hand to mem_chain2aln.  Reads are forward-strand (the extension math is
+ * strand-independent).  A fraction p_unrelated of reads are random sequence with a planted
+ * 19..30 bp exact copy of a random reference position: a spurious seed hit whose extensions
+ * die early (the mis-seeded case the z-drop handles). */
+typedef struct bsw_seed_s { int64_t rbeg; int32_t qbeg; int32_t len; } bsw_seed_s; /* = bsw_seed_t */
+
+void bsw_synth_reference(uint64_t seed, int64_t len, double p_n, uint8_t *out)
+{
+    /* 64K-base blocks, each from its own stream: reproducible and parallelisable */
+    const int64_t B = 65536;
+    for (int64_t b0 = 0; b0 < len; b0 += B) {
+        uint64_t s = seed * 0x2545F4914F6CDD1Dull ^ ((uint64_t)(b0 / B + 1) * 0xD1B54A32D192ED03ull);
+        splitmix64(&s);
+        const int64_t e = b0 + B < len ? b0 + B : len;
+        for (int64_t i = b0; i < e; ++i) out[i] = (u01(&s) < p_n) ? 4 : (uint8_t)below(&s, 4);
+    }
+}
+
+typedef struct bsw_reads_cfg {
+    uint64_t seed;
+    int32_t read_len;           /* 150                                                   */
+    int32_t min_seed;           /* 19 (bwa -k)                                           */
+    double p_sub, p_indel;      /* per-base substitution / indel-start probability       */
+    double p_unrelated;         /* reads with a spurious planted seed                    */
+} bsw_reads_cfg;
+
+void bsw_reads_default(bsw_reads_cfg *c)
+{
+    c->seed = 42;
+    c->read_len = 150;
+    c->min_seed = 19;
+    c->p_sub = 0.02;
+    c->p_indel = 0.002;
+    c->p_unrelated = 0.10;
+}
+
+/* Reads [read_base, read_base + n): reads[k*read_len ..], seeds[k], origin[k] (may be NULL).
+ * Returns the number of reads that got a seed (seeds[k].len == 0 otherwise). */
+int32_t bsw_synth_reads(const bsw_reads_cfg *c, const uint8_t *ref, int64_t ref_len, int64_t read_base,
+                        int32_t n, uint8_t *reads, bsw_seed_s *seeds, int64_t *origin)
+{
+    const int32_t L = c->read_len;
+    int32_t nseeded = 0;
+    int64_t rp[4096];
+    if (L > 4096 || ref_len < 2 * (int64_t)L + 64) return -1;
+    for (int32_t k = 0; k < n; ++k) {
+        const int64_t gi = read_base + k;
+        uint64_t s = c->seed * 0x9E3779B97F4A7C15ull ^ ((uint64_t)gi * 0xBF58476D1CE4E5B9ull) ^ 0x5555;
+        splitmix64(&s);
+        uint8_t *q = reads + (int64_t)k * L;
+        bsw_seed_s *sd = &seeds[k];
+        sd->rbeg = 0; sd->qbeg = 0; sd->len = 0;
+        const int64_t org = (int64_t)(u01(&s) * (double)(ref_len - L - 64));
+        if (origin) origin[k] = org;
+        if (u01(&s) < c->p_unrelated) {
+            for (int32_t j = 0; j < L; ++j) q[j] = (uint8_t)below(&s, 4);
+            const int32_t sl = 19 + (int32_t)below(&s, 12);
+            const int32_t qb = (int32_t)below(&s, (uint32_t)(L - sl + 1));
+            int64_t rb = (int64_t)(u01(&s) * (double)(ref_len - sl));
+            int ok = 1;
+            for (int32_t t = 0; t < sl; ++t) { q[qb + t] = ref[rb + t]; if (ref[rb + t] > 3) ok = 0; }
+            if (ok) { sd->rbeg = rb; sd->qbeg = qb; sd->len = sl; ++nseeded; }
+            continue;
+        }
+        /* edit script: rp[j] = reference position read base j copies (-1: inserted) */
+        int64_t i = org;
+        int32_t j = 0;
+        while (j < L) {
+            const double u = u01(&s);
+            if (u < c->p_indel) {
+                const int32_t l = 1 + (int32_t)below(&s, 3);
+                if (splitmix64(&s) & 1) {
+                    for (int32_t t = 0; t < l && j < L; ++t) { rp[j] = -1; q[j++] = (uint8_t)below(&s, 4); }
+                } else {
+                    i += l;
+                }
+                continue;
+            }
+            uint8_t b = ref[i];
+            if (u01(&s) < c->p_sub) b = (uint8_t)((b < 4 ? b : 0) + 1 + below(&s, 3)) & 3;
+            rp[j] = i;
+            q[j++] = b;
+            ++i;
+        }
+        /* longest run of consecutive reference positions with identical, non-N bases */
+        int32_t best = 0, bq = 0, run = 0;
+        for (int32_t t = 0; t < L; ++t) {
+            const int ok = rp[t] >= 0 && ref[rp[t]] < 4 && q[t] == ref[rp[t]];
+            if (!ok) run = 0;
+            else if (run > 0 && rp[t] == rp[t - 1] + 1) ++run;
+            else run = 1;
+            if (run > best) { best = run; bq = t - run + 1; }
+        }
+        if (best >= c->min_seed) {
+            sd->rbeg = rp[bq]; sd->qbeg = bq; sd->len = best; ++nseeded;
+        }
+    }
+    return nseeded;
+}

@@ -27,7 +27,15 @@ assert SEQPAIR_DTYPE.itemsize == 56
 
 # Every symbol include/bsw.h declares (tests check the library exports all of them).
 ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_scores",
-               "bsw_get_scores_device", "bsw_last_stats", "bsw_strerror", "bsw_abi_version")
+               "bsw_get_scores_device", "bsw_last_stats", "bsw_strerror", "bsw_abi_version",
+               "bsw_ext_opt_default", "bsw_extend_seeds", "bsw_ext_last_stats")
+
+# include/bsw_ext.h structs
+SEED_DTYPE = np.dtype([("rbeg", np.int64), ("qbeg", np.int32), ("len", np.int32)])
+ALNREG_DTYPE = np.dtype([("rb", np.int64), ("re", np.int64), ("qb", np.int32), ("qe", np.int32),
+                         ("score", np.int32), ("truesc", np.int32), ("w", np.int32),
+                         ("seedlen0", np.int32)])
+assert SEED_DTYPE.itemsize == 16 and ALNREG_DTYPE.itemsize == 40
 
 
 class Params(ctypes.Structure):
@@ -83,8 +91,11 @@ def hip_lib():
         L.bsw_last_stats.argtypes = [P, P]
         L.bsw_strerror.restype = ctypes.c_char_p
         L.bsw_strerror.argtypes = [ctypes.c_int]
+        L.bsw_ext_opt_default.argtypes = [P]
+        L.bsw_extend_seeds.argtypes = [P, P, P, ctypes.c_int64, P, P, P, P, ctypes.c_int32, P]
+        L.bsw_ext_last_stats.argtypes = [P, P]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
-                  "bsw_abi_version"):
+                  "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -141,6 +152,46 @@ class Engine:
         return s
 
 
+# ---------------------------------------------------------------- extension pipeline
+class ExtOpt(ctypes.Structure):
+    """Mirror of bsw_ext_opt_t (include/bsw_ext.h)."""
+    _fields_ = [("w", ctypes.c_int32), ("pen_clip5", ctypes.c_int32), ("pen_clip3", ctypes.c_int32),
+                ("max_band_try", ctypes.c_int32)]
+
+
+class ExtStats(ctypes.Structure):
+    _fields_ = [("n_pairs", ctypes.c_int32 * 4), ("kernel_ms", ctypes.c_float), ("build_ms", ctypes.c_float),
+                ("engine_ms", ctypes.c_float), ("interp_ms", ctypes.c_float)]
+
+
+def ext_opt(**kw) -> ExtOpt:
+    o = ExtOpt()
+    hip_lib().bsw_ext_opt_default(ctypes.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def extend_seeds(engine, ref, reads, read_off, read_len, seeds, opt: ExtOpt | None = None):
+    """bsw_extend_seeds: one seed per read -> ALNREG_DTYPE regions (local / to-end ends)."""
+    opt = opt if opt is not None else ext_opt()
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    reads = np.ascontiguousarray(reads, dtype=np.uint8)
+    read_off = np.ascontiguousarray(read_off, dtype=np.int64)
+    read_len = np.ascontiguousarray(read_len, dtype=np.int32)
+    seeds = np.ascontiguousarray(seeds, dtype=SEED_DTYPE)
+    out = np.zeros(len(seeds), dtype=ALNREG_DTYPE)
+    _check(hip_lib().bsw_extend_seeds(engine._ctx, ctypes.byref(opt), _ptr(ref), len(ref), _ptr(reads),
+                                      _ptr(read_off), _ptr(read_len), _ptr(seeds), len(seeds), _ptr(out)))
+    return out
+
+
+def ext_last_stats(engine) -> ExtStats:
+    s = ExtStats()
+    _check(hip_lib().bsw_ext_last_stats(engine._ctx, ctypes.byref(s)))
+    return s
+
+
 # ---------------------------------------------------------------- synthetic batches
 class SynthCfg(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("tlen", ctypes.c_int32), ("qlen", ctypes.c_int32),
@@ -161,6 +212,11 @@ def synth_lib():
         L.bsw_synth_default.argtypes = [ctypes.c_void_p]
         L.bsw_synth_batch.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.bsw_synth_reference.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p]
+        L.bsw_reads_default.argtypes = [ctypes.c_void_p]
+        L.bsw_synth_reads.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.bsw_synth_reads.restype = ctypes.c_int32
         _synth = L
     return _synth
 
@@ -182,3 +238,39 @@ def synth_batch(n: int, pair_base: int = 0, cfg: SynthCfg | None = None):
     synth_lib().bsw_synth_batch(ctypes.byref(cfg), pair_base, n, _ptr(pairs), _ptr(ref),
                                 _ptr(qer))
     return pairs, ref, qer
+
+
+class ReadsCfg(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("read_len", ctypes.c_int32), ("min_seed", ctypes.c_int32),
+                ("p_sub", ctypes.c_double), ("p_indel", ctypes.c_double), ("p_unrelated", ctypes.c_double)]
+
+
+def reads_cfg(**kw) -> ReadsCfg:
+    c = ReadsCfg()
+    synth_lib().bsw_reads_default(ctypes.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def synth_reference(length: int, seed: int = 7, p_n: float = 0.0005) -> np.ndarray:
+    """Random reference (codes 0..3, N = 4 at rate p_n), reproducible per seed."""
+    ref = np.empty(length, dtype=np.uint8)
+    synth_lib().bsw_synth_reference(seed, length, p_n, _ptr(ref))
+    return ref
+
+
+def synth_reads(ref: np.ndarray, n: int, read_base: int = 0, cfg: ReadsCfg | None = None):
+    """Reads sampled from ref with one exact seed each: (reads, read_off, read_len, seeds, origin)."""
+    cfg = cfg if cfg is not None else reads_cfg()
+    L = cfg.read_len
+    reads = np.zeros(max(1, n * L), dtype=np.uint8)
+    seeds = np.zeros(n, dtype=SEED_DTYPE)
+    origin = np.zeros(n, dtype=np.int64)
+    r = synth_lib().bsw_synth_reads(ctypes.byref(cfg), _ptr(ref), len(ref), read_base, n, _ptr(reads),
+                                    _ptr(seeds), _ptr(origin))
+    if r < 0:
+        raise BswError("bsw_synth_reads: reference too short for the read length")
+    read_off = np.arange(n, dtype=np.int64) * L
+    read_len = np.full(n, L, dtype=np.int32)
+    return reads, read_off, read_len, seeds, origin

@@ -1,0 +1,83 @@
+/*
+ * bsw_ext.h -- seed-extension job builder + result interpreter on top of the batch engine
+ * (upstream consumer row a9).
+ *
+ * Replaces the extension half of upstream bwa-mem2's per-chain alignment step
+ * (mem_chain2aln / mem_chain2aln_across_reads_V2 in src/bwamem.cpp, the caller of
+ * BandedPairWiseSW::getScores16/8 -- docs-archive/INTEGRATION_COMPLETE.md:16-63,
+ * BUG_REPORT.md:28-41 for the call site), restated from bwa's ksw_extend2 consumer
+ * [UPSTREAM-RECALL, SURVEY.md a9]:
+ *
+ *   seed (qbeg, rbeg, len) of a read of length l_query, seed score sc = len * a
+ *   target window rmax = [rbeg - qbeg - gap(qbeg), rbeg + len + (l_query - qe) + gap(l_query - qe))
+ *     clipped to the reference, gap(l) = min(max((l*a - o)/e + 1, 1), 2w)   (cal_max_gap)
+ *   LEFT  (qbeg > 0): query = reverse(read[0, qbeg)), target = reverse(ref[rmax0, rbeg)),
+ *         h0 = sc, end_bonus = pen_clip5, band w << k for k < max_band_try (retry while the
+ *         score changed and max_off >= 3/4 of the band)
+ *         local  if gscore <= 0 || gscore <= score - pen_clip5: qb = qbeg - qle, rb = rbeg - tle
+ *         to-end otherwise:                                     qb = 0,          rb = rbeg - gtle
+ *   RIGHT (qe = qbeg + len < l_query): query = read[qe, l_query), target = ref[rbeg + len, rmax1),
+ *         h0 = the LEFT score (sc0), end_bonus = pen_clip3, same band retry
+ *         local  if gscore <= 0 || gscore <= score - pen_clip3: qe += qle, re = rbeg + len + tle
+ *         to-end otherwise:                                     qe = l_query, re = ... + gtle
+ *   truesc accumulates the chosen (local or to-end) scores; w = widest band used.
+ *
+ * All LEFT extensions of a call form one batch (then one retry batch), then all RIGHT
+ * extensions (their h0 depends on LEFT's result) -- the across-reads batching of
+ * mem_chain2aln_across_reads_V2.  One seed per read in this interface.
+ */
+#ifndef BSW_EXT_H
+#define BSW_EXT_H
+
+#include <stdint.h>
+#include "bsw.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bsw_seed_t {          /* one exact-match seed of read i (len == 0: no seed)     */
+    int64_t rbeg;                    /* reference position of the seed's first base            */
+    int32_t qbeg;                    /* read position of the seed's first base                 */
+    int32_t len;
+} bsw_seed_t;
+
+typedef struct bsw_ext_opt_t {
+    int32_t w;                       /* band width (bwa -w, default 100)                        */
+    int32_t pen_clip5, pen_clip3;    /* clipping penalties (bwa -L, default 5,5)                */
+    int32_t max_band_try;            /* band doublings incl. the first try (bwa: 2)             */
+} bsw_ext_opt_t;
+
+typedef struct bsw_alnreg_t {        /* the mem_alnreg_t fields the extension determines       */
+    int64_t rb, re;                  /* [rb, re): reference span                                */
+    int32_t qb, qe;                  /* [qb, qe): read span                                     */
+    int32_t score;                   /* best local score (last extension's)                     */
+    int32_t truesc;                  /* score of the chosen local / to-end ends                 */
+    int32_t w;                       /* band actually used (max over both sides)                */
+    int32_t seedlen0;                /* seed length                                             */
+} bsw_alnreg_t;
+
+void bsw_ext_opt_default(bsw_ext_opt_t *opt);
+
+/* Extend n seeds (read i = reads[read_off[i], read_off[i] + read_len[i]), codes 0..4) against
+ * ref[0, ref_len) on the context's devices; scoring = the context's params (a = mat[0]).
+ * Reads with seeds[i].len == 0 get a zeroed region.  Blocking; 0 or a BSW_E* code. */
+int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *ref, int64_t ref_len,
+                     const uint8_t *reads, const int64_t *read_off, const int32_t *read_len,
+                     const bsw_seed_t *seeds, int32_t n, bsw_alnreg_t *out);
+
+/* Batches issued by the last bsw_extend_seeds on ctx: SeqPairs per phase (left, left retry,
+ * right, right retry) and the summed DP kernel time. */
+typedef struct bsw_ext_stats_t {
+    int32_t n_pairs[4];
+    float   kernel_ms;               /* DP kernels (HIP events)                                  */
+    float   build_ms;                /* host: job lists + code buffers                           */
+    float   engine_ms;               /* bsw batches incl. PCIe, plan/sort and kernels            */
+    float   interp_ms;               /* host: local / to-end interpretation                      */
+} bsw_ext_stats_t;
+int bsw_ext_last_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSW_EXT_H */

@@ -1,0 +1,105 @@
+/*
+ * ext_ref.c -- CPU restatement of the seed-extension consumer (TEST INFRASTRUCTURE ONLY: the
+ * checker for bwa-mem2-arm_amd/csrc/bsw_ext.cpp; never linked into the product).
+ *
+ * Literal per-read form of the extension half of upstream mem_chain2aln (bwa 0.7.x
+ * src/bwamem.c, which bwa-mem2's src/bwamem.cpp keeps; [UPSTREAM-RECALL], SURVEY.md a9 /
+ * §8(f) row 1), one seed per read: target window via cal_max_gap, LEFT extension on reversed
+ * sequences with h0 = seed score and the MAX_BAND_TRY loop, local vs to-end by pen_clip5,
+ * RIGHT extension with h0 = the LEFT score, pen_clip3.  Scoring through oracle_ksw_extend2.
+ * Parity unpinned by the reference (no upstream fixtures for this step), like the oracle.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "../include/bsw_ext.h"
+
+int oracle_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m,
+                       const int8_t *mat, int o_del, int e_del, int o_ins, int e_ins, int w,
+                       int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
+                       int *_gscore, int *_max_off);
+
+typedef struct {
+    int32_t o_del, e_del, o_ins, e_ins, zdrop, end_bonus;
+    int8_t mat[25];
+} oracle_params_t;
+
+static int cal_max_gap(const oracle_params_t *p, int a, int w, int qlen)
+{
+    int l_del = (int)((double)(qlen * a - p->o_del) / p->e_del + 1.);
+    int l_ins = (int)((double)(qlen * a - p->o_ins) / p->e_ins + 1.);
+    int l = l_del > l_ins ? l_del : l_ins;
+    l = l > 1 ? l : 1;
+    return l < w << 1 ? l : w << 1;
+}
+
+void oracle_extend_seeds(const oracle_params_t *p, const bsw_ext_opt_t *opt, const uint8_t *ref,
+                         int64_t ref_len, const uint8_t *reads, const int64_t *read_off,
+                         const int32_t *read_len, const bsw_seed_t *seeds, int32_t n,
+                         bsw_alnreg_t *out)
+{
+    const int a = p->mat[0];
+    for (int32_t i = 0; i < n; ++i) {
+        bsw_alnreg_t *r = &out[i];
+        const bsw_seed_t *s = &seeds[i];
+        const uint8_t *query = reads + read_off[i];
+        const int l_query = read_len[i];
+        int qle, tle, gtle, gscore, max_off[2] = {0, 0}, aw[2];
+        memset(r, 0, sizeof(*r));
+        if (s->len <= 0) continue;
+        int64_t rmax0 = s->rbeg - (s->qbeg + cal_max_gap(p, a, opt->w, s->qbeg));
+        int64_t rmax1 = s->rbeg + s->len + ((l_query - s->qbeg - s->len) +
+                                            cal_max_gap(p, a, opt->w, l_query - s->qbeg - s->len));
+        rmax0 = rmax0 > 0 ? rmax0 : 0;
+        rmax1 = rmax1 < ref_len ? rmax1 : ref_len;
+        aw[0] = aw[1] = opt->w;
+        r->seedlen0 = s->len;
+        if (s->qbeg) {                                   /* left extension */
+            int tmp = (int)(s->rbeg - rmax0);
+            uint8_t *qs = (uint8_t *)malloc((size_t)s->qbeg), *rs = (uint8_t *)malloc((size_t)(tmp > 0 ? tmp : 1));
+            for (int k = 0; k < s->qbeg; ++k) qs[k] = query[s->qbeg - 1 - k];
+            for (int k = 0; k < tmp; ++k) rs[k] = ref[s->rbeg - 1 - k];
+            for (int t = 0; t < opt->max_band_try; ++t) {
+                int prev = r->score;
+                aw[0] = opt->w << t;
+                r->score = oracle_ksw_extend2(s->qbeg, qs, tmp, rs, 5, p->mat, p->o_del, p->e_del, p->o_ins,
+                                              p->e_ins, aw[0], opt->pen_clip5, p->zdrop, s->len * a, &qle,
+                                              &tle, &gtle, &gscore, &max_off[0]);
+                if (r->score == prev || max_off[0] < (aw[0] >> 1) + (aw[0] >> 2)) break;
+            }
+            if (gscore <= 0 || gscore <= r->score - opt->pen_clip5) {   /* local */
+                r->qb = s->qbeg - qle; r->rb = s->rbeg - tle;
+                r->truesc = r->score;
+            } else {                                                    /* to-end */
+                r->qb = 0; r->rb = s->rbeg - gtle;
+                r->truesc = gscore;
+            }
+            free(qs); free(rs);
+        } else {
+            r->score = r->truesc = s->len * a; r->qb = 0; r->rb = s->rbeg;
+        }
+        if (s->qbeg + s->len != l_query) {               /* right extension */
+            int qe = s->qbeg + s->len;
+            int64_t re = s->rbeg + s->len;
+            int sc0 = r->score;
+            for (int t = 0; t < opt->max_band_try; ++t) {
+                int prev = r->score;
+                aw[1] = opt->w << t;
+                r->score = oracle_ksw_extend2(l_query - qe, query + qe, (int)(rmax1 - re), ref + re, 5, p->mat,
+                                              p->o_del, p->e_del, p->o_ins, p->e_ins, aw[1], opt->pen_clip3,
+                                              p->zdrop, sc0, &qle, &tle, &gtle, &gscore, &max_off[1]);
+                if (r->score == prev || max_off[1] < (aw[1] >> 1) + (aw[1] >> 2)) break;
+            }
+            if (gscore <= 0 || gscore <= r->score - opt->pen_clip3) {   /* local */
+                r->qe = qe + qle; r->re = re + tle;
+                r->truesc += r->score - sc0;
+            } else {                                                    /* to-end */
+                r->qe = l_query; r->re = re + gtle;
+                r->truesc += gscore - sc0;
+            }
+        } else {
+            r->qe = l_query; r->re = s->rbeg + s->len;
+        }
+        r->w = aw[0] > aw[1] ? aw[0] : aw[1];
+    }
+}

@@ -95,3 +95,25 @@ def sse41_get_scores16(params: OracleParams, pairs: np.ndarray, ref: np.ndarray,
     assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
     return lib().sse41_get_scores16(ctypes.byref(params), _ptr(pairs), _ptr(ref), _ptr(qer),
                                     len(pairs), w, nthreads)
+
+
+def extend_seeds(params, opt, ref, reads, read_off, read_len, seeds):
+    """oracle/ext_ref.c: per-read CPU restatement of the extension consumer (test checker)."""
+    import sys as _sys
+    import os as _os
+    _sys.path.insert(0, _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
+                                      "bwa-mem2-arm_amd", "py"))
+    import bsw as _bsw
+    L = lib()
+    P = ctypes.c_void_p
+    L.oracle_extend_seeds.argtypes = [P, P, P, ctypes.c_int64, P, P, P, P, ctypes.c_int32, P]
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    reads = np.ascontiguousarray(reads, dtype=np.uint8)
+    read_off = np.ascontiguousarray(read_off, dtype=np.int64)
+    read_len = np.ascontiguousarray(read_len, dtype=np.int32)
+    seeds = np.ascontiguousarray(seeds, dtype=_bsw.SEED_DTYPE)
+    out = np.zeros(len(seeds), dtype=_bsw.ALNREG_DTYPE)
+    ptr = lambda a: ctypes.c_void_p(a.ctypes.data)
+    L.oracle_extend_seeds(ctypes.byref(params), ctypes.byref(opt), ptr(ref), len(ref), ptr(reads),
+                          ptr(read_off), ptr(read_len), ptr(seeds), len(seeds), ptr(out))
+    return out

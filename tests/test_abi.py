@@ -13,14 +13,16 @@ import pytest
 import bsw
 from conftest import ROOT
 
-HEADER = os.path.join(ROOT, "include", "bsw.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("bsw.h", "bsw_ext.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"\b(bsw_[a-z_0-9]+)\s*\(", src)
-    return sorted(set(names))
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(bsw_[a-z_0-9]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_header_declares_expected_api():
@@ -109,3 +111,20 @@ def test_shim_header_compiles_against_c_abi(tmp_path):
                         str(tmp_path / "shim"), bsw.HIP_LIB, "-Wl,-rpath," + os.path.dirname(bsw.HIP_LIB)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_ext_header_layouts_compile(tmp_path):
+    """include/bsw_ext.h structs match the Python mirrors (compiled by gcc, no GPU)."""
+    src = tmp_path / "t.c"
+    src.write_text(
+        '#include <stddef.h>\n#include "bsw_ext.h"\n'
+        "_Static_assert(sizeof(bsw_seed_t) == 16, \"seed\");\n"
+        "_Static_assert(sizeof(bsw_alnreg_t) == 40, \"alnreg\");\n"
+        "_Static_assert(offsetof(bsw_alnreg_t, qb) == 16, \"qb\");\n"
+        "_Static_assert(offsetof(bsw_alnreg_t, seedlen0) == 36, \"seedlen0\");\n"
+        "_Static_assert(sizeof(bsw_ext_opt_t) == 16, \"opt\");\n")
+    r = subprocess.run(["gcc", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert bsw.SEED_DTYPE.itemsize == 16 and bsw.ALNREG_DTYPE.itemsize == 40
+    assert ctypes.sizeof(bsw.ExtOpt) == 16
