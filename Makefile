@@ -17,7 +17,7 @@ SHIMTEST := $(LIBDIR)/bsw_shim_example
 ORACLE   := oracle/liboracle.so
 
 HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pk.hip $(CSRC)/bsw_host.cpp $(CSRC)/bsw_ext.cpp
-HIP_HDRS := $(CSRC)/bsw_kernels.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h
+HIP_HDRS := $(CSRC)/bsw_kernels.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h
 
 all: product synth oracle
 
@@ -40,7 +40,10 @@ $(LIBDIR)/bsw_host.o: $(CSRC)/bsw_host.cpp $(HIP_HDRS) | $(LIBDIR)
 $(LIBDIR)/bsw_ext.o: $(CSRC)/bsw_ext.cpp $(HIP_HDRS) | $(LIBDIR)
 	g++ -O3 -std=c++17 -fPIC -Wall -Iinclude -c $< -o $@
 
-$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pk.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o
+$(LIBDIR)/bsw_batch.o: $(CSRC)/bsw_batch.c include/bsw_batch.h include/bsw.h | $(LIBDIR)
+	gcc $(CFLAGS) -std=c11 -c $< -o $@
+
+$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pk.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_batch.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 $(SYNTH): $(CSRC)/bsw_synth.c include/bsw_seqpair.h | $(LIBDIR)

@@ -28,7 +28,8 @@ assert SEQPAIR_DTYPE.itemsize == 56
 # Every symbol include/bsw.h declares (tests check the library exports all of them).
 ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_scores",
                "bsw_get_scores_device", "bsw_last_stats", "bsw_strerror", "bsw_abi_version",
-               "bsw_ext_opt_default", "bsw_extend_seeds", "bsw_ext_last_stats")
+               "bsw_ext_opt_default", "bsw_extend_seeds", "bsw_ext_last_stats",
+               "bswb_write", "bswb_read_header", "bswb_read")
 
 # include/bsw_ext.h structs
 SEED_DTYPE = np.dtype([("rbeg", np.int64), ("qbeg", np.int32), ("len", np.int32)])
@@ -91,11 +92,16 @@ def hip_lib():
         L.bsw_last_stats.argtypes = [P, P]
         L.bsw_strerror.restype = ctypes.c_char_p
         L.bsw_strerror.argtypes = [ctypes.c_int]
+        L.bswb_write.argtypes = [ctypes.c_char_p, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int, P,
+                                 ctypes.c_int64, P, ctypes.c_int64, P, ctypes.c_int64]
+        L.bswb_read_header.argtypes = [ctypes.c_char_p, P]
+        L.bswb_read.argtypes = [ctypes.c_char_p, P, P, P, P]
         L.bsw_ext_opt_default.argtypes = [P]
         L.bsw_extend_seeds.argtypes = [P, P, P, ctypes.c_int64, P, P, P, P, ctypes.c_int32, P]
         L.bsw_ext_last_stats.argtypes = [P, P]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
-                  "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats"):
+                  "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
+                  "bswb_read_header", "bswb_read"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -150,6 +156,37 @@ class Engine:
         s = Stats()
         _check(hip_lib().bsw_last_stats(self._ctx, ctypes.byref(s)))
         return s
+
+
+# ---------------------------------------------------------------- .bswb batch files
+class BswbHeader(ctypes.Structure):
+    """Mirror of bswb_header_t (include/bsw_batch.h), 128 bytes."""
+    _fields_ = [("magic", ctypes.c_uint32), ("version", ctypes.c_uint32), ("header_bytes", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("n_pairs", ctypes.c_int64), ("ref_bytes", ctypes.c_int64),
+                ("qer_bytes", ctypes.c_int64), ("checksum", ctypes.c_uint64), ("w", ctypes.c_int32),
+                ("cell_bits", ctypes.c_int32), ("params", Params), ("reserved", ctypes.c_uint8 * 20)]
+
+
+def write_batch(path: str, pairs, ref, qer, w: int, cell_bits: int = 16, params=None,
+                has_outputs: bool = True):
+    """bswb_write: record a batch (+ outputs) for replay."""
+    params = params if params is not None else default_params()
+    pairs = np.ascontiguousarray(pairs, dtype=SEQPAIR_DTYPE)
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    qer = np.ascontiguousarray(qer, dtype=np.uint8)
+    _check(hip_lib().bswb_write(path.encode(), ctypes.byref(params), w, cell_bits, int(has_outputs),
+                                _ptr(pairs), len(pairs), _ptr(ref), len(ref), _ptr(qer), len(qer)))
+
+
+def read_batch(path: str):
+    """bswb_read: (header, pairs, ref, qer); raises BswError on a bad / corrupted file."""
+    h = BswbHeader()
+    _check(hip_lib().bswb_read_header(path.encode(), ctypes.byref(h)))
+    pairs = np.zeros(h.n_pairs, dtype=SEQPAIR_DTYPE)
+    ref = np.zeros(max(1, h.ref_bytes), dtype=np.uint8)
+    qer = np.zeros(max(1, h.qer_bytes), dtype=np.uint8)
+    _check(hip_lib().bswb_read(path.encode(), ctypes.byref(h), _ptr(pairs), _ptr(ref), _ptr(qer)))
+    return h, pairs, ref, qer
 
 
 # ---------------------------------------------------------------- extension pipeline

@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "bsw.h"
+#include "bsw_batch.h"
 
 #ifndef MAX_SEQ_LEN8
 #define MAX_SEQ_LEN8 BSW_MAX_SEQ_LEN8
@@ -47,6 +48,8 @@ public:
         const char *g = getenv("BSW_GPUS"), *d0 = getenv("BSW_DEVICE0");
         const int ngpu = g ? atoi(g) : 1, dev0 = d0 ? atoi(d0) : 0;
         check(bsw_create(&p, dev0, ngpu > 0 ? ngpu : 1, &ctx_), "bsw_create");
+        params_ = p;
+        record_ = getenv("BSW_RECORD");   // capture every batch as <prefix>.<n>.bswb (bsw_batch.h)
     }
     ~BandedPairWiseSW() { bsw_destroy(ctx_); }
     BandedPairWiseSW(const BandedPairWiseSW &) = delete;
@@ -57,12 +60,14 @@ public:
     {
         (void)numThreads;
         check(bsw_get_scores(ctx_, pairArray, seqBufRef, seqBufQer, numPairs, w, 16), "getScores16");
+        if (record_) record(pairArray, seqBufRef, seqBufQer, numPairs, w, 16);
     }
     void getScores8(SeqPair *pairArray, uint8_t *seqBufRef, uint8_t *seqBufQer, int32_t numPairs,
                     uint16_t numThreads, int32_t w)
     {
         (void)numThreads;
         check(bsw_get_scores(ctx_, pairArray, seqBufRef, seqBufQer, numPairs, w, 8), "getScores8");
+        if (record_) record(pairArray, seqBufRef, seqBufQer, numPairs, w, 8);
     }
     void scalarBandedSWAWrapper(SeqPair *seqPairArray, uint8_t *seqBufRef, uint8_t *seqBufQer,
                                 int numPairs, int nthreads, int32_t w)
@@ -87,6 +92,21 @@ public:
     }
 
 private:
+    // Record a finished batch (outputs included): the byte buffers up to the furthest byte
+    // any pair references.  Concurrent kt_for callers get distinct sequence numbers.
+    void record(const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t n, int32_t w,
+                int cell_bits)
+    {
+        int64_t rb = 0, qb = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            if ((int64_t)pairs[i].idr + pairs[i].len1 > rb) rb = (int64_t)pairs[i].idr + pairs[i].len1;
+            if ((int64_t)pairs[i].idq + pairs[i].len2 > qb) qb = (int64_t)pairs[i].idq + pairs[i].len2;
+        }
+        const unsigned k = __atomic_fetch_add(&seq_, 1u, __ATOMIC_RELAXED);
+        char path[4096];
+        snprintf(path, sizeof(path), "%s.%06u.bswb", record_, k);
+        check(bswb_write(path, &params_, w, cell_bits, 1, pairs, n, ref, rb, qer, qb), "BSW_RECORD");
+    }
     static void check(int rc, const char *what)
     {
         if (rc != BSW_OK) {
@@ -95,6 +115,9 @@ private:
         }
     }
     bsw_ctx_t *ctx_ = nullptr;
+    bsw_params_t params_{};
+    const char *record_ = nullptr;
+    unsigned seq_ = 0;
 };
 
 #endif  // BANDEDSWA_GPU_H

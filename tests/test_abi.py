@@ -13,7 +13,7 @@ import pytest
 import bsw
 from conftest import ROOT
 
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("bsw.h", "bsw_ext.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("bsw.h", "bsw_ext.h", "bsw_batch.h")]
 
 
 def declared_functions():
@@ -21,7 +21,7 @@ def declared_functions():
     for h in HEADERS:
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        names |= set(re.findall(r"\b(bsw_[a-z_0-9]+)\s*\(", src))
+        names |= set(re.findall(r"\b(bswb?_[a-z_0-9]+)\s*\(", src))
     return sorted(names)
 
 
@@ -34,7 +34,7 @@ def test_library_exports_all_declared_symbols():
     for name in declared_functions():
         assert hasattr(lib, name), name
     out = subprocess.run(["nm", "-D", "--defined-only", bsw.HIP_LIB], capture_output=True, text=True).stdout
-    exported = set(re.findall(r" T (bsw_\w+)", out))
+    exported = set(re.findall(r" T (bswb?_\w+)", out))
     assert set(declared_functions()) <= exported
 
 
