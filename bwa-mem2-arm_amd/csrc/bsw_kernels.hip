@@ -125,18 +125,20 @@ __device__ __forceinline__ void lane_col_masked(uint32_t (&eh)[QMAX + 1], int s,
 //   phase 1 : the four cells' independent work -- M (gated), E' = max(E-e, M-oe, 0),
 //             max(M, E), M - oe -- shared by both bodies;
 //   fast    : every live lane in band (scalar test): the F chain (2 dependent ops per
-//             cell) with H / pack / key / last-positive interleaved -- 56 VALU per 4 cells;
+//             cell) with H / pack / key interleaved -- 46 VALU per 4 cells (the last positive
+//             column is not tracked per cell: lane_lastpos recovers it at row end when needed);
 //   masked  : band edges by per-lane SELECTS (no EXEC changes): d = j - beg, in = d < span,
 //             inat = d <= span (j == end stores {H(i,end-1), 0}: E' forced to 0), j < beg
 //             resets F; out-of-band lanes pass H(i,j-1) along the chain but feed 0 to
-//             key / last-positive -- 92 VALU.
+//             key -- 82 VALU.
+// key = H << 16 | j by one v_lshl_or_b32 with j from an SGPR (VOP3 takes no literal on gfx9).
 template <int G>
 __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint32_t &v2, uint32_t &v3,
                                                uint32_t q, uint32_t plo, uint32_t phi, int &f,
-                                               int &h1, int &key, int &lp1, int oe, int ed,
+                                               int &h1, int &key, int oe, int ed,
                                                int glo, int gsp, int gfa, int gfn, int beg, int span)
 {
-    int m0, m1, m2, m3, t0, t1, t2, t3, x0, x1, x2, x3, ha, hb, k0, k1, l0, l1, pw, st, d, tp;
+    int m0, m1, m2, m3, t0, t1, t2, t3, x0, x1, x2, x3, ha, hb, k0, k1, pw, st, d, tp;
     uint64_t sat, slt, inb;
     asm volatile(
         "s_sub_u32 %[st], %[g], %[glo]\n\t"     // group outside [min beg, max end]: skip
@@ -175,34 +177,24 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
         "v_lshl_or_b32 %[v0], %[x0], 16, %[h1]\n\t"
         "v_max3_i32 %[f], %[f], %[t0], 0\n\t"
-        "v_lshlrev_b32_e32 %[m0], 16, %[ha]\n\t"
+        "v_lshl_or_b32 %[k0], %[ha], 16, %[s0]\n\t"
         "v_max_i32_e32 %[hb], %[f], %[m1]\n\t"
         "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
-        "v_or_b32_e32 %[k0], %[j0], %[m0]\n\t"
-        "v_max3_i32 %[f], %[f], %[t1], 0\n\t"
-        "v_min_i32_e32 %[l0], %[j1], %[m0]\n\t"
         "v_lshl_or_b32 %[v1], %[x1], 16, %[ha]\n\t"
-        "v_lshlrev_b32_e32 %[m1], 16, %[hb]\n\t"
+        "v_max3_i32 %[f], %[f], %[t1], 0\n\t"
+        "v_lshl_or_b32 %[k1], %[hb], 16, %[s1]\n\t"
         "v_max_i32_e32 %[ha], %[f], %[m2]\n\t"
         "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
-        "v_or_b32_e32 %[k1], %[j1], %[m1]\n\t"
-        "v_max3_i32 %[f], %[f], %[t2], 0\n\t"
-        "v_min_i32_e32 %[l1], %[j2], %[m1]\n\t"
         "v_lshl_or_b32 %[v2], %[x2], 16, %[hb]\n\t"
         "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
-        "v_lshlrev_b32_e32 %[m2], 16, %[ha]\n\t"
-        "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
+        "v_max3_i32 %[f], %[f], %[t2], 0\n\t"
+        "v_lshl_or_b32 %[k0], %[ha], 16, %[s2]\n\t"
         "v_max_i32_e32 %[h1], %[f], %[m3]\n\t"
         "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
-        "v_or_b32_e32 %[k0], %[j2], %[m2]\n\t"
-        "v_max3_i32 %[f], %[f], %[t3], 0\n\t"
-        "v_min_i32_e32 %[l0], %[j3], %[m2]\n\t"
         "v_lshl_or_b32 %[v3], %[x3], 16, %[ha]\n\t"
-        "v_lshlrev_b32_e32 %[m3], 16, %[h1]\n\t"
-        "v_or_b32_e32 %[k1], %[j3], %[m3]\n\t"
-        "v_min_i32_e32 %[l1], %[j4], %[m3]\n\t"
+        "v_max3_i32 %[f], %[f], %[t3], 0\n\t"
+        "v_lshl_or_b32 %[k1], %[h1], 16, %[s3]\n\t"
         "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
-        "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
         "s_branch 3f\n"
         "2:\n\t"
         "v_sub_u32_e32 %[d], %[j0], %[beg]\n\t"
@@ -218,9 +210,7 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_lshl_or_b32 %[d], %[x0], 16, %[h1]\n\t"
         "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
         "v_cndmask_b32_e64 %[v0], %[v0], %[d], %[sat]\n\t"
-        "v_lshlrev_b32_e32 %[tp], 16, %[tp]\n\t"
-        "v_or_b32_e32 %[k0], %[j0], %[tp]\n\t"
-        "v_min_i32_e32 %[l0], %[j1], %[tp]\n\t"
+        "v_lshl_or_b32 %[k0], %[tp], 16, %[s0]\n\t"
         "v_sub_u32_e32 %[d], %[j1], %[beg]\n\t"
         "v_cmp_lt_u32_e64 %[inb], %[d], %[span]\n\t"
         "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
@@ -234,11 +224,8 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_lshl_or_b32 %[d], %[x1], 16, %[ha]\n\t"
         "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
         "v_cndmask_b32_e64 %[v1], %[v1], %[d], %[sat]\n\t"
-        "v_lshlrev_b32_e32 %[tp], 16, %[tp]\n\t"
-        "v_or_b32_e32 %[k1], %[j1], %[tp]\n\t"
-        "v_min_i32_e32 %[l1], %[j2], %[tp]\n\t"
+        "v_lshl_or_b32 %[k1], %[tp], 16, %[s1]\n\t"
         "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
-        "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
         "v_sub_u32_e32 %[d], %[j2], %[beg]\n\t"
         "v_cmp_lt_u32_e64 %[inb], %[d], %[span]\n\t"
         "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
@@ -252,9 +239,7 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_lshl_or_b32 %[d], %[x2], 16, %[hb]\n\t"
         "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
         "v_cndmask_b32_e64 %[v2], %[v2], %[d], %[sat]\n\t"
-        "v_lshlrev_b32_e32 %[tp], 16, %[tp]\n\t"
-        "v_or_b32_e32 %[k0], %[j2], %[tp]\n\t"
-        "v_min_i32_e32 %[l0], %[j3], %[tp]\n\t"
+        "v_lshl_or_b32 %[k0], %[tp], 16, %[s2]\n\t"
         "v_sub_u32_e32 %[d], %[j3], %[beg]\n\t"
         "v_cmp_lt_u32_e64 %[inb], %[d], %[span]\n\t"
         "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
@@ -268,23 +253,21 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_lshl_or_b32 %[d], %[x3], 16, %[ha]\n\t"
         "v_cndmask_b32_e64 %[f], %[f], 0, %[slt]\n\t"
         "v_cndmask_b32_e64 %[v3], %[v3], %[d], %[sat]\n\t"
-        "v_lshlrev_b32_e32 %[tp], 16, %[tp]\n\t"
-        "v_or_b32_e32 %[k1], %[j3], %[tp]\n\t"
-        "v_min_i32_e32 %[l1], %[j4], %[tp]\n\t"
+        "v_lshl_or_b32 %[k1], %[tp], 16, %[s3]\n\t"
         "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
-        "v_max3_i32 %[lp], %[lp], %[l0], %[l1]\n\t"
         "3:"
         : [v0] "+v"(v0), [v1] "+v"(v1), [v2] "+v"(v2), [v3] "+v"(v3), [f] "+v"(f), [h1] "+v"(h1),
-          [key] "+v"(key), [lp] "+v"(lp1), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2),
+          [key] "+v"(key), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2),
           [m3] "=&v"(m3), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
           [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2), [x3] "=&v"(x3), [ha] "=&v"(ha),
-          [hb] "=&v"(hb), [k0] "=&v"(k0), [k1] "=&v"(k1), [l0] "=&v"(l0), [l1] "=&v"(l1),
+          [hb] "=&v"(hb), [k0] "=&v"(k0), [k1] "=&v"(k1),
           [pw] "=&v"(pw), [d] "=&v"(d), [tp] "=&v"(tp), [inb] "=&s"(inb), [sat] "=&s"(sat), [slt] "=&s"(slt),
           [st] "=&s"(st)
         : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe] "s"(oe), [ed] "s"(ed),
           [glo] "s"(glo), [gsp] "s"(gsp), [gfa] "s"(gfa), [gfn] "s"(gfn), [beg] "v"(beg),
           [span] "v"(span), [g] "i"(G), [j0] "i"(4 * G), [j1] "i"(4 * G + 1),
-          [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [j4] "i"(4 * G + 4)
+          [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [s0] "s"(4 * G), [s1] "s"(4 * G + 1),
+          [s2] "s"(4 * G + 2), [s3] "s"(4 * G + 3)
         : "vcc", "scc");
 }
 
@@ -297,7 +280,7 @@ __device__ __forceinline__ void lane_group(uint32_t (&eh)[QMAX + 1], const uint3
     if constexpr (SM == 1 && SYM && J0 + 3 < QMAX) {
         // skip / fast / masked decided inside the asm on SGPR group bounds
         lane_group_asm<G>(eh[J0], eh[J0 + 1], eh[J0 + 2], eh[J0 + 3], q4[G], pr.x, pr.y, f, h1,
-                          key, lp1, c.oe_del, c.e_del, r.glo, r.gsp, r.gfa, r.gfn, beg, end - beg);
+                          key, c.oe_del, c.e_del, r.glo, r.gsp, r.gfa, r.gfn, beg, end - beg);
         return;
     }
     if (J0 + 3 < r.ulo || J0 > r.uhi) return;            // uniform skip
@@ -325,6 +308,38 @@ __device__ __forceinline__ void lane_row(std::integer_sequence<int, G...>, uint3
                                          const LaneCx &c)
 {
     (lane_group<G, QMAX, SM, SYM>(eh, q4, pr, beg, end, f, h1, key, lp1, r, c), ...);
+}
+
+// Lazy last-positive column: end_{i+1} = min(lastH + 3, i + w + 2, qlen) needs
+// lastH = last j with H(i,j) > 0.  When H(i, end-1) > 0 (the chain value h1 at row end) that is
+// end - 1 and nothing is scanned; otherwise the lanes that need it scan the stored row
+// eh[j+1].h = H(i,j) right to left from their end - 1 and stop at the first positive cell
+// (one exists: m > 0).  Groups above every lane's end and groups after all lanes found one are
+// skipped by uniform tests.
+template <int QMAX, int GG>
+__device__ __forceinline__ bool lastpos_group(const uint32_t (&eh)[QMAX + 1], int end, bool pending,
+                                              int &lp1, int gstart)
+{
+    if (GG > gstart) return pending;                      // uniform
+    if (__ballot(pending) == 0) return false;             // uniform
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+        const int j = 4 * GG + k;
+        if (j < QMAX && pending && j < end && (eh[j + 1] & 0xffffu) != 0u) {
+            lp1 = j + 1;
+            pending = false;
+        }
+    }
+    return pending;
+}
+
+template <int QMAX, int... G>
+__device__ __forceinline__ void lane_lastpos(std::integer_sequence<int, G...>,
+                                             const uint32_t (&eh)[QMAX + 1], int end, bool need,
+                                             int &lp1, int gstart)
+{
+    bool pending = need;
+    ((pending = lastpos_group<QMAX, QMAX / 4 - G>(eh, end, pending, lp1, gstart)), ...);
 }
 
 constexpr int kTChunkDw = 17;            // dwords per lane per 64-row target chunk
@@ -475,7 +490,19 @@ __global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const in
                                          : best - m - (dj - di) * kp.e_ins;
                 if (dz > kp.zdrop) alive = false;
             }
-            if (alive) endc = min(lp1 + 2, qlen);   // = min(last nonzero eh + 2, qlen), DESIGN.md §3
+            if (alive) {                           // end_{i+1} = min(lastH + 3, ...), DESIGN.md §3
+                if constexpr (SM == 1 && SYM) {    // asm groups: lastH recovered lazily
+                    const bool need = h1 == 0;     // H(i, end-1) == 0 -> lastH < end - 1
+                    if (__ballot(need)) {
+                        lp1 = 0;
+                        lane_lastpos<QMAX>(std::make_integer_sequence<int, QMAX / 4 + 1>{}, eh, end, need,
+                                           lp1, (emax - 1) >> 2);
+                    }
+                    endc = min((need ? lp1 : end) + 2, qlen);
+                } else {
+                    endc = min(lp1 + 2, qlen);     // C++ cells track lp1 = 1 + lastH
+                }
+            }
         }
     }
     if (valid) {
