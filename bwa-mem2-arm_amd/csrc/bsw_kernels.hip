@@ -325,9 +325,10 @@ __device__ __forceinline__ bool lastpos_group(const uint32_t (&eh)[QMAX + 1], in
 #pragma unroll
     for (int k = 3; k >= 0; --k) {
         const int j = 4 * GG + k;
-        if (j < QMAX && pending && j < end && (eh[j + 1] & 0xffffu) != 0u) {
-            lp1 = j + 1;
-            pending = false;
+        if (j < QMAX) {                                   // branch-free selects
+            const bool hit = pending & (j < end) & ((eh[j + 1] & 0xffffu) != 0u);
+            lp1 = hit ? j + 1 : lp1;
+            pending = pending & !hit;
         }
     }
     return pending;

@@ -47,14 +47,14 @@ struct PkHalf {                          // one pair's scalar state (A = low hal
 };
 
 // One 4-column group (columns J0 = 4G .. J0+3) of both pairs as ONE asm statement
-// (in-place update of HH/EE/f/key/lp, no control-flow merge copies):
+// (in-place update of HH/EE/f/key, no control-flow merge copies):
 //   skip    : group outside [min beg, max end] of the live pairs (scalar test)
 //   phase 1 : scores, gated M = hold + min(S, hold), t = max(M - oe, 0), max(M, E), E - e
-//   fast    : every live pair in band: F chain, H, E', key = max(H<<8 | j),
-//             lp = max(min(key_j, 256 + j)) (-> last positive column), 10 instr per column
+//   fast    : every live pair in band: F chain, H, E', key = max(H<<8 | j); 8 instr per column
+//             (the last positive column is recovered lazily at row end, pk_lastpos)
 //   masked  : per-half masks OUT = (j >= end), GT = (j > end), LEFT = (j < beg) from packed
 //             arithmetic; stores beyond end preserved (A.7), E' = 0 at j == end, F reset left
-//             of beg, masked cells feed 0 to key/lp; hg passes H(i, end-1) along for gscore (only
+//             of beg, masked cells feed 0 to key; hg passes H(i, end-1) along for gscore (only
 //             in-band cells update it: an empty row keeps the boundary value).
 #ifdef PK_EXP_NO_AGPR
 #define PK_ACCR(d, a) "v_mov_b32 " d ", " a "\n\t"
@@ -79,7 +79,7 @@ template <int G>
 __device__ __forceinline__ void pk_group(uint32_t &h0, uint32_t &h1, uint32_t &h2, uint32_t &h3,
                                          uint32_t &e0, uint32_t &e1, uint32_t &e2, uint32_t &e3,
                                          uint32_t hn, uint32_t qa, uint32_t qb, uint32_t &hc,
-                                         uint32_t &hg, uint32_t &f, uint32_t &key, uint32_t &lp,
+                                         uint32_t &hg, uint32_t &f, uint32_t &key,
                                          uint32_t tw, uint32_t tl, uint32_t th, uint32_t end1,
                                          uint32_t begw, uint32_t oe2, uint32_t ed2,
                                          const PkRow &r)
@@ -87,10 +87,8 @@ __device__ __forceinline__ void pk_group(uint32_t &h0, uint32_t &h1, uint32_t &h
     constexpr uint32_t J0 = 4 * G;
     constexpr uint32_t P0 = J0 * 0x10001u, P1 = (J0 + 1) * 0x10001u, P2 = (J0 + 2) * 0x10001u,
                        P3 = (J0 + 3) * 0x10001u, PM = (J0 - 1) * 0x10001u;   // (j, j) packed
-    constexpr uint32_t L0 = (J0 + 256) * 0x10001u, L1 = (J0 + 257) * 0x10001u,
-                       L2 = (J0 + 258) * 0x10001u, L3 = (J0 + 259) * 0x10001u; // 256 + j
-    uint32_t m0, m1, m2, m3, t0, t1, t2, t3, x0, x1, x2, x3, ha, ka, kb, mo, mg, ml;
-    uint32_t sj, sl, st;
+    uint32_t m0, m1, m2, m3, t0, t1, t2, t3, x0, x1, x2, x3, ha, ka, mo, mg, ml;
+    uint32_t sj, st;
 #define PK_P1(K, QP, DUP)                                                                    \
     "v_perm_b32 %[m" #K "], %[" QP "], %[" QP "], %[" DUP "]\n\t"                              \
     PK_ACCR("%[x" #K "]", "%[e" #K "]")                                                       \
@@ -102,7 +100,7 @@ __device__ __forceinline__ void pk_group(uint32_t &h0, uint32_t &h1, uint32_t &h
     "v_pk_max_i16 %[t" #K "], %[t" #K "], 0\n\t"                                                \
     "v_pk_max_i16 %[m" #K "], %[m" #K "], %[x" #K "]\n\t"                                       \
     "v_pk_sub_i16 %[x" #K "], %[x" #K "], %[ed2]\n\t"
-#define PK_FAST(K, HOUT, PJ, LJ)                                                             \
+#define PK_FAST(K, HOUT, PJ)                                                             \
     "v_pk_max_i16 %[x" #K "], %[x" #K "], %[t" #K "]\n\t"                                       \
     PK_ACCW("%[e" #K "]", "%[x" #K "]")                                                       \
     "v_pk_max_i16 " HOUT ", %[m" #K "], %[f]\n\t"                                               \
@@ -110,12 +108,9 @@ __device__ __forceinline__ void pk_group(uint32_t &h0, uint32_t &h1, uint32_t &h
     "v_pk_max_i16 %[f], %[f], %[t" #K "]\n\t"                                                   \
     "v_pk_lshlrev_b16 %[ka], 8, " HOUT " op_sel_hi:[0,1]\n\t"                                  \
     "v_or_b32 %[ka], %[" PJ "], %[ka]\n\t"                                                      \
-    "v_pk_max_u16 %[key], %[key], %[ka]\n\t"                                                    \
-    "s_mov_b32 %[sl], %[" LJ "]\n\t"                                                            \
-    "v_pk_min_u16 %[kb], %[ka], %[sl]\n\t"                                                      \
-    "v_pk_max_u16 %[lp], %[lp], %[kb]\n\t"
+    "v_pk_max_u16 %[key], %[key], %[ka]\n\t"
     // masked cell: GTR holds GT (= OUT of the previous column), OUTR receives OUT of this one
-#define PK_MASK(K, HOUT, HOLD, PJ, LJ, GTR, OUTR)                                            \
+#define PK_MASK(K, HOUT, HOLD, PJ, GTR, OUTR)                                            \
     "s_mov_b32 %[sj], %[" PJ "]\n\t"                                                            \
     "v_pk_sub_i16 %[" OUTR "], %[end1], %[sj]\n\t"                                              \
     "v_pk_ashrrev_i16 %[" OUTR "], 15, %[" OUTR "] op_sel_hi:[0,1]\n\t"                        \
@@ -136,10 +131,7 @@ __device__ __forceinline__ void pk_group(uint32_t &h0, uint32_t &h1, uint32_t &h
     "v_pk_lshlrev_b16 %[ka], 8, %[ha] op_sel_hi:[0,1]\n\t"                                     \
     "v_or_b32 %[ka], %[" PJ "], %[ka]\n\t"                                                      \
     "v_bfi_b32 %[ka], %[ml], 0, %[ka]\n\t"                                                      \
-    "v_pk_max_u16 %[key], %[key], %[ka]\n\t"                                                    \
-    "s_mov_b32 %[sl], %[" LJ "]\n\t"                                                            \
-    "v_pk_min_u16 %[kb], %[ka], %[sl]\n\t"                                                      \
-    "v_pk_max_u16 %[lp], %[lp], %[kb]\n\t"
+    "v_pk_max_u16 %[key], %[key], %[ka]\n\t"
     asm volatile(
         PK_TESTS("s_sub_u32 %[st], %[g], %[glo]\n\t"
         "s_cmp_le_u32 %[st], %[gsp]\n\t", "s_cbranch_scc0 3f\n\t")
@@ -148,8 +140,8 @@ __device__ __forceinline__ void pk_group(uint32_t &h0, uint32_t &h1, uint32_t &h
         "v_mov_b32 %[h0], %[hc]\n\t"
         PK_TESTS("s_sub_u32 %[st], %[g], %[gfa]\n\t"
         "s_cmp_lt_u32 %[st], %[gfn]\n\t", "s_cbranch_scc0 2f\n\t")
-        PK_FAST(0, "%[h1]", "p0", "l0") PK_FAST(1, "%[h2]", "p1", "l1")
-        PK_FAST(2, "%[h3]", "p2", "l2") PK_FAST(3, "%[hc]", "p3", "l3")
+        PK_FAST(0, "%[h1]", "p0") PK_FAST(1, "%[h2]", "p1")
+        PK_FAST(2, "%[h3]", "p2") PK_FAST(3, "%[hc]", "p3")
         "v_mov_b32 %[hg], %[hc]\n\t"
         PK_TESTS("", "s_branch 3f\n")
         PK_SLOW(
@@ -157,24 +149,23 @@ __device__ __forceinline__ void pk_group(uint32_t &h0, uint32_t &h1, uint32_t &h
         "s_mov_b32 %[sj], %[pm]\n\t"
         "v_pk_sub_i16 %[mg], %[end1], %[sj]\n\t"
         "v_pk_ashrrev_i16 %[mg], 15, %[mg] op_sel_hi:[0,1]\n\t"
-        PK_MASK(0, "%[h1]", "%[h1]", "p0", "l0", "mg", "mo")
-        PK_MASK(1, "%[h2]", "%[h2]", "p1", "l1", "mo", "mg")
-        PK_MASK(2, "%[h3]", "%[h3]", "p2", "l2", "mg", "mo")
-        PK_MASK(3, "%[hc]", "%[hn]", "p3", "l3", "mo", "mg"))
+        PK_MASK(0, "%[h1]", "%[h1]", "p0", "mg", "mo")
+        PK_MASK(1, "%[h2]", "%[h2]", "p1", "mo", "mg")
+        PK_MASK(2, "%[h3]", "%[h3]", "p2", "mg", "mo")
+        PK_MASK(3, "%[hc]", "%[hn]", "p3", "mo", "mg"))
         "3:\n\t"
         : [h0] "+v"(h0), [h1] "+v"(h1), [h2] "+v"(h2), [h3] "+v"(h3), [e0] PK_ECON(e0), [e1] PK_ECON(e1),
           [e2] PK_ECON(e2), [e3] PK_ECON(e3), [hc] "+v"(hc), [hg] "+v"(hg), [f] "+v"(f), [key] "+v"(key),
-          [lp] "+v"(lp), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2), [m3] "=&v"(m3),
+          [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2), [m3] "=&v"(m3),
           [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [x0] "=&v"(x0),
           [x1] "=&v"(x1), [x2] "=&v"(x2), [x3] "=&v"(x3), [ha] "=&v"(ha), [ka] "=&v"(ka),
-          [kb] "=&v"(kb), [mo] "=&v"(mo), [mg] "=&v"(mg), [ml] "=&v"(ml), [sj] "=&s"(sj),
-          [sl] "=&s"(sl), [st] "=&s"(st)
+          [mo] "=&v"(mo), [mg] "=&v"(mg), [ml] "=&v"(ml), [sj] "=&s"(sj),
+          [st] "=&s"(st)
         : [hn] "v"(hn), [qa] PK_QCON(qa), [qb] PK_QCON(qb), [tw] "v"(tw), [tl] "v"(tl), [th] "v"(th),
           [end1] "v"(end1), [begw] "v"(begw), [oe2] "s"(oe2), [ed2] "s"(ed2),
           [d0] "s"(0x01010000u), [d1] "s"(0x03030202u), [g] "i"(G), [glo] "s"(r.glo),
           [gsp] "s"(r.gsp), [gfa] "s"(r.gfa), [gfn] "s"(r.gfn), [p0] "i"(P0), [p1] "i"(P1),
-          [p2] "i"(P2), [p3] "i"(P3), [pm] "i"(PM), [l0] "i"(L0), [l1] "i"(L1), [l2] "i"(L2),
-          [l3] "i"(L3)
+          [p2] "i"(P2), [p3] "i"(P3), [pm] "i"(PM)
         : "scc");
 #undef PK_P1
 #undef PK_FAST
@@ -185,20 +176,20 @@ template <int QMAX, int... G>
 __device__ __forceinline__ void pk_row(std::integer_sequence<int, G...>, uint32_t (&hh)[QMAX + 1],
                                        uint32_t (&ee)[QMAX], const uint32_t (&qp)[QMAX / 2],
                                        uint32_t &hc, uint32_t &hg, uint32_t &f, uint32_t &key,
-                                       uint32_t &lp, uint32_t tw, uint32_t tl, uint32_t th,
+                                       uint32_t tw, uint32_t tl, uint32_t th,
                                        uint32_t end1, uint32_t begw, uint32_t oe2, uint32_t ed2,
                                        const PkRow &r)
 {
     (pk_group<G>(hh[4 * G], hh[4 * G + 1], hh[4 * G + 2], hh[4 * G + 3], ee[4 * G], ee[4 * G + 1],
                  ee[4 * G + 2], ee[4 * G + 3], hh[4 * G + 4], qp[2 * G], qp[2 * G + 1], hc, hg, f,
-                 key, lp, tw, tl, th, end1, begw, oe2, ed2, r),
+                 key, tw, tl, th, end1, begw, oe2, ed2, r),
      ...);
 }
 
 // Row-end bookkeeping of one pair (A.4 tail): gscore at j == qlen, m == 0 termination, new
 // best, z-drop, next end = min(last positive + 3, qlen).
 __device__ __forceinline__ void pk_row_end(PkHalf &s, int i, int end, uint32_t key16,
-                                           uint32_t lp16, uint32_t hg16, const KParams &kp)
+                                           uint32_t hg16, const KParams &kp)
 {
     const int m = (int)(key16 >> 8), mj = (int)(key16 & 0xffu);
     const int h1 = (int)hg16;
@@ -216,10 +207,36 @@ __device__ __forceinline__ void pk_row_end(PkHalf &s, int i, int end, uint32_t k
         const int dz = (di > dj) ? s.best - m - (di - dj) * kp.e_del : s.best - m - (dj - di) * kp.e_ins;
         if (dz > kp.zdrop) s.alive = false;
     }
-    if (s.alive) {
-        const int lp1 = lp16 >= 256u ? (int)lp16 - 255 : 0;   // 1 + last column with H > 0
-        s.endc = min(lp1 + 2, s.qlen);
+}
+
+// Lazy last positive column (as the lane kernel's lane_lastpos): for the pairs whose
+// H(i, end-1) is 0, scan HH[j+1] = H(i, j) right to left from end - 1 (per half).
+template <int QMAX, int GG>
+__device__ __forceinline__ void pk_lastpos_group(const uint32_t (&hh)[QMAX + 1], const int (&end)[2],
+                                                 bool (&pend)[2], int (&lp1)[2], int gstart)
+{
+    if (GG > gstart) return;                                           // uniform
+    if (__ballot(pend[0] || pend[1]) == 0) return;                     // uniform
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+        const int j = 4 * GG + k;
+        if (j < QMAX) {
+            const uint32_t v = hh[j + 1];          // branch-free selects (no EXEC splits)
+            const bool a = pend[0] & (j < end[0]) & ((v & 0xffffu) != 0u);
+            const bool b = pend[1] & (j < end[1]) & ((v >> 16) != 0u);
+            lp1[0] = a ? j + 1 : lp1[0];
+            lp1[1] = b ? j + 1 : lp1[1];
+            pend[0] = pend[0] & !a;
+            pend[1] = pend[1] & !b;
+        }
     }
+}
+
+template <int QMAX, int... G>
+__device__ __forceinline__ void pk_lastpos(std::integer_sequence<int, G...>, const uint32_t (&hh)[QMAX + 1],
+                                           const int (&end)[2], bool (&pend)[2], int (&lp1)[2], int gstart)
+{
+    (pk_lastpos_group<QMAX, QMAX / 4 - 1 - G>(hh, end, pend, lp1, gstart), ...);
 }
 
 // Row-target encoding for the score XOR: lo selector t (N: 8), hi selector t ^ 12 (N: 5 ^ 12).
@@ -415,15 +432,27 @@ __global__ __launch_bounds__(256, QMAX <= 64 ? 2 : 1) void pk_kernel(const KPara
                 const int bB = (beg[1] == 0) ? max(hs[1].h0 - (kp.o_del + kp.e_del * (i + 1)), 0) : 0;
                 hc = (uint32_t)bA | ((uint32_t)bB << 16);
             }
-            uint32_t hg = hc, f = 0, key = 0, lp = 0;
+            uint32_t hg = hc, f = 0, key = 0;
             const uint32_t end1 = ((uint32_t)(end[0] - 1) & 0xffffu) | ((uint32_t)(end[1] - 1) << 16);
             const uint32_t begw = (uint32_t)beg[0] | ((uint32_t)beg[1] << 16);
             PK_STAMP(2);
-            pk_row<QMAX>(std::make_integer_sequence<int, NG>{}, hh, ee, qp, hc, hg, f, key, lp, tw, tl,
+            pk_row<QMAX>(std::make_integer_sequence<int, NG>{}, hh, ee, qp, hc, hg, f, key, tw, tl,
                          th, end1, begw, oe2, ed2, r);
             PK_STAMP(3);
-            if (act2[0]) pk_row_end(hs[0], i, end[0], key & 0xffffu, lp & 0xffffu, hg & 0xffffu, kp);
-            if (act2[1]) pk_row_end(hs[1], i, end[1], key >> 16, lp >> 16, hg >> 16, kp);
+            if (act2[0]) pk_row_end(hs[0], i, end[0], key & 0xffffu, hg & 0xffffu, kp);
+            if (act2[1]) pk_row_end(hs[1], i, end[1], key >> 16, hg >> 16, kp);
+            // next band end: lastH = end - 1 when H(i, end-1) > 0, else recovered
+            bool pend[2] = {act2[0] && hs[0].alive && (hg & 0xffffu) == 0u,
+                            act2[1] && hs[1].alive && (hg >> 16) == 0u};
+            int lp1[2] = {end[0], end[1]};
+            if (__ballot(pend[0] || pend[1])) {
+                if (pend[0]) lp1[0] = 0;
+                if (pend[1]) lp1[1] = 0;
+                pk_lastpos<QMAX>(std::make_integer_sequence<int, NG>{}, hh, end, pend, lp1, (emax - 1) >> 2);
+            }
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+                if (act2[hf] && hs[hf].alive) hs[hf].endc = min(lp1[hf] + 2, hs[hf].qlen);
         }
         PK_STAMP(4);
     }
