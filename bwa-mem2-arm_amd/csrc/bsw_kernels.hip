@@ -55,6 +55,8 @@ struct LaneRow {          // per-row uniform (SGPR) bounds
     int fast_lo, fast_hi; // max beg / min end over live lanes (columns inside: unmasked)
     int glo, gsp;         // groups touching [ulo, uhi]: glo <= G <= glo + gsp
     int gfa, gfn;         // groups fully inside [fast_lo, fast_hi): gfa <= G < gfa + gfn
+    int gua, gun;         // groups whose band edges are wave-uniform or absent: gua <= G < gua + gun
+    int usp;              // fast_hi - fast_lo (the uniform span inside those groups)
 };
 
 struct LaneCx {           // per-kernel constants
@@ -136,7 +138,8 @@ template <int G>
 __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint32_t &v2, uint32_t &v3,
                                                uint32_t q, uint32_t plo, uint32_t phi, int &f,
                                                int &h1, int &key, int oe, int ed,
-                                               int glo, int gsp, int gfa, int gfn, int beg, int span)
+                                               int glo, int gsp, int gfa, int gfn, int gua, int gun,
+                                               int bs, int usp, int beg, int span)
 {
     int m0, m1, m2, m3, t0, t1, t2, t3, x0, x1, x2, x3, ha, hb, k0, k1, pw, st, d, tp;
     uint64_t sat, slt, inb;
@@ -197,6 +200,11 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
         "s_branch 3f\n"
         "2:\n\t"
+        "s_sub_u32 %[st], %[g], %[gua]\n\t"   // both edges wave-uniform (or absent): U body
+        "s_cmp_lt_u32 %[st], %[gun]\n\t"
+        "s_cbranch_scc1 5f\n\t"
+        "s_cmp_ge_u32 %[g], %[gfa]\n\t"       // no cell left of any lane's beg: R body
+        "s_cbranch_scc1 6f\n\t"
         "v_sub_u32_e32 %[d], %[j0], %[beg]\n\t"
         "v_cmp_lt_u32_e64 %[inb], %[d], %[span]\n\t"
         "v_cmp_le_u32_e64 %[sat], %[d], %[span]\n\t"
@@ -255,6 +263,116 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "v_cndmask_b32_e64 %[v3], %[v3], %[d], %[sat]\n\t"
         "v_lshl_or_b32 %[k1], %[tp], 16, %[s3]\n\t"
         "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
+        "s_branch 3f\n"
+        "5:\n\t"
+        "s_sub_u32 %[st], %[j0], %[bs]\n\t"
+        "s_cmp_lt_u32 %[st], %[usp]\n\t"
+        "s_cbranch_scc0 110f\n\t"
+        "v_lshl_or_b32 %[v0], %[x0], 16, %[h1]\n\t"
+        "v_max_i32_e32 %[h1], %[f], %[m0]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_max3_i32 %[f], %[f], %[t0], 0\n\t"
+        "v_lshl_or_b32 %[k0], %[h1], 16, %[s0]\n\t"
+        "v_max_i32_e32 %[key], %[key], %[k0]\n"
+        "100:\n\t"
+        "s_sub_u32 %[st], %[j1], %[bs]\n\t"
+        "s_cmp_lt_u32 %[st], %[usp]\n\t"
+        "s_cbranch_scc0 111f\n\t"
+        "v_lshl_or_b32 %[v1], %[x1], 16, %[h1]\n\t"
+        "v_max_i32_e32 %[h1], %[f], %[m1]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_max3_i32 %[f], %[f], %[t1], 0\n\t"
+        "v_lshl_or_b32 %[k0], %[h1], 16, %[s1]\n\t"
+        "v_max_i32_e32 %[key], %[key], %[k0]\n"
+        "101:\n\t"
+        "s_sub_u32 %[st], %[j2], %[bs]\n\t"
+        "s_cmp_lt_u32 %[st], %[usp]\n\t"
+        "s_cbranch_scc0 112f\n\t"
+        "v_lshl_or_b32 %[v2], %[x2], 16, %[h1]\n\t"
+        "v_max_i32_e32 %[h1], %[f], %[m2]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_max3_i32 %[f], %[f], %[t2], 0\n\t"
+        "v_lshl_or_b32 %[k0], %[h1], 16, %[s2]\n\t"
+        "v_max_i32_e32 %[key], %[key], %[k0]\n"
+        "102:\n\t"
+        "s_sub_u32 %[st], %[j3], %[bs]\n\t"
+        "s_cmp_lt_u32 %[st], %[usp]\n\t"
+        "s_cbranch_scc0 113f\n\t"
+        "v_lshl_or_b32 %[v3], %[x3], 16, %[h1]\n\t"
+        "v_max_i32_e32 %[h1], %[f], %[m3]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_max3_i32 %[f], %[f], %[t3], 0\n\t"
+        "v_lshl_or_b32 %[k0], %[h1], 16, %[s3]\n\t"
+        "v_max_i32_e32 %[key], %[key], %[k0]\n"
+        "103:\n\t"
+        "s_branch 3f\n"
+        "110:\n\t"                          // cell 0 outside the uniform band
+        "s_cmp_eq_u32 %[st], %[usp]\n\t"       // j == end: {H(i,end-1), 0}
+        "s_cbranch_scc0 100b\n\t"
+        "v_mov_b32_e32 %[v0], %[h1]\n\t"
+        "s_branch 100b\n"
+        "111:\n\t"                          // cell 1 outside the uniform band
+        "s_cmp_eq_u32 %[st], %[usp]\n\t"       // j == end: {H(i,end-1), 0}
+        "s_cbranch_scc0 101b\n\t"
+        "v_mov_b32_e32 %[v1], %[h1]\n\t"
+        "s_branch 101b\n"
+        "112:\n\t"                          // cell 2 outside the uniform band
+        "s_cmp_eq_u32 %[st], %[usp]\n\t"       // j == end: {H(i,end-1), 0}
+        "s_cbranch_scc0 102b\n\t"
+        "v_mov_b32_e32 %[v2], %[h1]\n\t"
+        "s_branch 102b\n"
+        "113:\n\t"                          // cell 3 outside the uniform band
+        "s_cmp_eq_u32 %[st], %[usp]\n\t"       // j == end: {H(i,end-1), 0}
+        "s_cbranch_scc0 103b\n\t"
+        "v_mov_b32_e32 %[v3], %[h1]\n\t"
+        "s_branch 103b\n"
+        "6:\n\t"
+        "v_cmp_lt_i32_e64 %[inb], %[s0], %[endv]\n\t"
+        "v_cmp_le_i32_e64 %[sat], %[s0], %[endv]\n\t"
+        "v_max_i32_e32 %[tp], %[f], %[m0]\n\t"
+        "v_cndmask_b32_e64 %[ha], %[h1], %[tp], %[inb]\n\t"
+        "v_cndmask_b32_e64 %[tp], 0, %[tp], %[inb]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_cndmask_b32_e64 %[x0], 0, %[x0], %[inb]\n\t"
+        "v_max3_i32 %[f], %[f], %[t0], 0\n\t"
+        "v_lshl_or_b32 %[d], %[x0], 16, %[h1]\n\t"
+        "v_cndmask_b32_e64 %[v0], %[v0], %[d], %[sat]\n\t"
+        "v_lshl_or_b32 %[k0], %[tp], 16, %[s0]\n\t"
+        "v_cmp_lt_i32_e64 %[inb], %[s1], %[endv]\n\t"
+        "v_cmp_le_i32_e64 %[sat], %[s1], %[endv]\n\t"
+        "v_max_i32_e32 %[tp], %[f], %[m1]\n\t"
+        "v_cndmask_b32_e64 %[hb], %[ha], %[tp], %[inb]\n\t"
+        "v_cndmask_b32_e64 %[tp], 0, %[tp], %[inb]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_cndmask_b32_e64 %[x1], 0, %[x1], %[inb]\n\t"
+        "v_max3_i32 %[f], %[f], %[t1], 0\n\t"
+        "v_lshl_or_b32 %[d], %[x1], 16, %[ha]\n\t"
+        "v_cndmask_b32_e64 %[v1], %[v1], %[d], %[sat]\n\t"
+        "v_lshl_or_b32 %[k1], %[tp], 16, %[s1]\n\t"
+        "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
+        "v_cmp_lt_i32_e64 %[inb], %[s2], %[endv]\n\t"
+        "v_cmp_le_i32_e64 %[sat], %[s2], %[endv]\n\t"
+        "v_max_i32_e32 %[tp], %[f], %[m2]\n\t"
+        "v_cndmask_b32_e64 %[ha], %[hb], %[tp], %[inb]\n\t"
+        "v_cndmask_b32_e64 %[tp], 0, %[tp], %[inb]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_cndmask_b32_e64 %[x2], 0, %[x2], %[inb]\n\t"
+        "v_max3_i32 %[f], %[f], %[t2], 0\n\t"
+        "v_lshl_or_b32 %[d], %[x2], 16, %[hb]\n\t"
+        "v_cndmask_b32_e64 %[v2], %[v2], %[d], %[sat]\n\t"
+        "v_lshl_or_b32 %[k0], %[tp], 16, %[s2]\n\t"
+        "v_cmp_lt_i32_e64 %[inb], %[s3], %[endv]\n\t"
+        "v_cmp_le_i32_e64 %[sat], %[s3], %[endv]\n\t"
+        "v_max_i32_e32 %[tp], %[f], %[m3]\n\t"
+        "v_cndmask_b32_e64 %[h1], %[ha], %[tp], %[inb]\n\t"
+        "v_cndmask_b32_e64 %[tp], 0, %[tp], %[inb]\n\t"
+        "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"
+        "v_cndmask_b32_e64 %[x3], 0, %[x3], %[inb]\n\t"
+        "v_max3_i32 %[f], %[f], %[t3], 0\n\t"
+        "v_lshl_or_b32 %[d], %[x3], 16, %[ha]\n\t"
+        "v_cndmask_b32_e64 %[v3], %[v3], %[d], %[sat]\n\t"
+        "v_lshl_or_b32 %[k1], %[tp], 16, %[s3]\n\t"
+        "v_max3_i32 %[key], %[key], %[k0], %[k1]\n\t"
         "3:"
         : [v0] "+v"(v0), [v1] "+v"(v1), [v2] "+v"(v2), [v3] "+v"(v3), [f] "+v"(f), [h1] "+v"(h1),
           [key] "+v"(key), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2),
@@ -265,7 +383,8 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
           [st] "=&s"(st)
         : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe] "s"(oe), [ed] "s"(ed),
           [glo] "s"(glo), [gsp] "s"(gsp), [gfa] "s"(gfa), [gfn] "s"(gfn), [beg] "v"(beg),
-          [span] "v"(span), [g] "i"(G), [j0] "i"(4 * G), [j1] "i"(4 * G + 1),
+          [span] "v"(span), [endv] "v"(beg + span), [gua] "s"(gua), [gun] "s"(gun), [bs] "s"(bs),
+          [usp] "s"(usp), [g] "i"(G), [j0] "i"(4 * G), [j1] "i"(4 * G + 1),
           [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [s0] "s"(4 * G), [s1] "s"(4 * G + 1),
           [s2] "s"(4 * G + 2), [s3] "s"(4 * G + 3)
         : "vcc", "scc");
@@ -280,7 +399,8 @@ __device__ __forceinline__ void lane_group(uint32_t (&eh)[QMAX + 1], const uint3
     if constexpr (SM == 1 && SYM && J0 + 3 < QMAX) {
         // skip / fast / masked decided inside the asm on SGPR group bounds
         lane_group_asm<G>(eh[J0], eh[J0 + 1], eh[J0 + 2], eh[J0 + 3], q4[G], pr.x, pr.y, f, h1,
-                          key, c.oe_del, c.e_del, r.glo, r.gsp, r.gfa, r.gfn, beg, end - beg);
+                          key, c.oe_del, c.e_del, r.glo, r.gsp, r.gfa, r.gfn, r.gua, r.gun, r.fast_lo,
+                          r.usp, beg, end - beg);
         return;
     }
     if (J0 + 3 < r.ulo || J0 > r.uhi) return;            // uniform skip
@@ -450,6 +570,14 @@ __global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const in
         r.gsp = max((r.uhi >> 2) - r.glo, -1);      // -1 (as unsigned: huge) never happens: uhi >= ulo
         r.gfa = (r.fast_lo + 3) >> 2;
         r.gfn = max((r.fast_hi >> 2) - r.gfa, 0);
+        {   // U groups: left edge uniform (every lane's beg == fast_lo) or no cell left of it,
+            // and right edge uniform or every cell < fast_hi
+            const int gl = (r.ulo == r.fast_lo) ? 0 : r.gfa;
+            const int gr = (r.uhi == r.fast_hi) ? 64 : (r.fast_hi >> 2);
+            r.gua = gl;
+            r.gun = max(gr - gl, 0);
+            r.usp = r.fast_hi - r.fast_lo;
+        }
         if (act) {
             if ((i & 3) == 0) {            // new 4-row block: 4 target bases from LDS
                 if ((i & 63) == 0) {          // chunk boundary: its DMA was issued 64 rows ago
