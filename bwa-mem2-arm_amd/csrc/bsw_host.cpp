@@ -29,6 +29,7 @@
 #include <vector>
 #include "../../include/bsw.h"
 #include "bsw_kernels.h"
+#include "bsw_mate_k.h"
 #include "bsw_internal.h"
 
 namespace bsw {
@@ -124,6 +125,14 @@ struct Slot {
     int32_t *d_meta = nullptr;          // counts[kMetaCounts], maxq_wide, err
     int32_t *h_meta = nullptr;          // pinned mirror
     int2 *d_scratch = nullptr; size_t cap_scratch = 0;
+    // mate rescue (bsw_mate.h)
+    int32_t *d_mjobs = nullptr; size_t cap_mjobs = 0;
+    uint16_t *d_mrows = nullptr; size_t cap_mrows = 0;
+    int32_t *d_mmeta = nullptr, *h_mmeta = nullptr;
+    unsigned long long *d_mcells = nullptr;
+    SeqPair *d_mpairs = nullptr; size_t cap_mpairs = 0;
+    bsw_kswr_t *d_maln = nullptr; size_t cap_maln = 0;
+    hipEvent_t ev2 = nullptr, ev3 = nullptr;
     bool timed = false;
     bsw_stats_t stats{};
 };
@@ -165,6 +174,11 @@ struct DeviceCtx {
         (void)hipFree(s->d_pairs); (void)hipFree(s->d_ref); (void)hipFree(s->d_qer);
         (void)hipFree(s->d_keys); (void)hipFree(s->d_keys2); (void)hipFree(s->d_vals); (void)hipFree(s->d_order);
         (void)hipFree(s->d_tmp); (void)hipFree(s->d_meta); (void)hipFree(s->d_scratch);
+        (void)hipFree(s->d_mjobs); (void)hipFree(s->d_mrows); (void)hipFree(s->d_mmeta);
+        (void)hipFree(s->d_mcells); (void)hipFree(s->d_mpairs); (void)hipFree(s->d_maln);
+        if (s->h_mmeta) (void)hipHostFree(s->h_mmeta);
+        if (s->ev2) (void)hipEventDestroy(s->ev2);
+        if (s->ev3) (void)hipEventDestroy(s->ev3);
         if (s->h_meta) (void)hipHostFree(s->h_meta);
         if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -208,6 +222,7 @@ struct bsw_ctx {
     std::mutex stats_mu;
     bsw_stats_t last{};
     bsw_ext_stats_t ext_last{};
+    bsw_mate_stats_t mate_last{};
     struct Pinned { std::mutex mu; void *p = nullptr; size_t cap = 0; } pin[2];
     ~bsw_ctx()
     {
@@ -376,6 +391,79 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     }();
     dc.give_back(std::move(slot));
     return rc;
+}
+
+// ---------------------------------------------------------------- mate rescue (bsw_mate.h)
+static void make_mate_params(const bsw_params_t &p, MateParams &mp)
+{
+    memset(&mp, 0, sizeof(mp));
+    mp.e_del = p.e_del; mp.oe_del = p.o_del + p.e_del;
+    mp.e_ins = p.e_ins; mp.oe_ins = p.o_ins + p.e_ins;
+    int mn = 127, mx = 0;                                 // ksw_qinit: min(mat, 127), max(mat, 0)
+    for (int i = 0; i < 25; ++i) { mn = std::min(mn, (int)p.mat[i]); mx = std::max(mx, (int)p.mat[i]); }
+    mp.maxsc = mx;
+    mp.shift = (uint8_t)(256 - (uint8_t)(int8_t)mn);
+    for (int t = 0; t < 5; ++t) {
+        uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int q = 0; q < 5; ++q) b[q] = (uint8_t)p.mat[t * 5 + q];
+        memcpy(mp.prof[t], b, 8);
+    }
+}
+
+static bool mate_params_ok(const bsw_params_t &p)
+{
+    int mx = 0;
+    for (int i = 0; i < 25; ++i) mx = std::max(mx, (int)p.mat[i]);
+    return p.o_ins >= 1 && mx >= 1;
+}
+
+// Forward pass (ksw_u8 / ksw_i16 per job) then, for jobs with KSW_XSTART, the reverse pass;
+// each pass: device bucketing by (P, slen), one readback of the bucket ranges, one launch per
+// ncol class.  Blocking.
+static int mate_device(const MateParams &mp, Slot &s, const SeqPair *d_pairs, const uint8_t *d_ref,
+                       const uint8_t *d_qer, int32_t n, bsw_kswr_t *d_aln, hipStream_t st,
+                       bsw_mate_stats_t *stats)
+{
+    *stats = bsw_mate_stats_t{};
+    const size_t jcap = (size_t)n + 64 * kMateBuckets;
+    BSW_TRY(grow(s.d_mjobs, s.cap_mjobs, jcap));
+    if (!s.d_mmeta) BSW_TRY(hipMalloc((void **)&s.d_mmeta, kMateMetaWords * sizeof(int32_t)));
+    if (!s.h_mmeta) BSW_TRY(hipHostMalloc((void **)&s.h_mmeta, kMateMetaWords * sizeof(int32_t), 0));
+    if (!s.d_mcells) BSW_TRY(hipMalloc((void **)&s.d_mcells, sizeof(unsigned long long)));
+    if (!s.ev2) BSW_TRY(hipEventCreate(&s.ev2));
+    if (!s.ev3) BSW_TRY(hipEventCreate(&s.ev3));
+    BSW_TRY(hipMemsetAsync(s.d_mcells, 0, sizeof(unsigned long long), st));
+    for (int mode = 0; mode < 2; ++mode) {
+        BSW_TRY(launch_mate_prepare(d_pairs, d_aln, n, mode, s.d_mmeta, s.d_mjobs, (int32_t)jcap, st));
+        BSW_TRY(hipMemcpyAsync(s.h_mmeta, s.d_mmeta, kMateMetaWords * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        BSW_TRY(hipStreamSynchronize(st));
+        const int32_t *m = s.h_mmeta;
+        if (m[kMateMetaErr]) return BSW_E_RANGE;
+        int32_t njobs = 0;
+        for (int b = 0; b < kMateBuckets; ++b) njobs += m[kMateMetaCount + b];
+        const int64_t total = m[kMateMetaTotal];
+        uint16_t *rows = nullptr;
+        if (mode == 0 && njobs > 0) {
+            const size_t need = (size_t)std::max(m[kMateMetaTmax], 1) * (size_t)total;
+            BSW_TRY(grow(s.d_mrows, s.cap_mrows, need));
+            rows = s.d_mrows;
+        }
+        hipEvent_t e0 = mode == 0 ? s.ev0 : s.ev2, e1 = mode == 0 ? s.ev1 : s.ev3;
+        BSW_TRY(hipEventRecord(e0, st));
+        for (int c = 0; c < kMateClasses; ++c)
+            BSW_TRY(launch_mate_class(c, mp, d_pairs, s.d_mjobs, m[kMateMetaClass + 2 * c],
+                                      m[kMateMetaClass + 2 * c + 1], d_ref, d_qer, d_aln, mode, rows, total,
+                                      mode == 0 ? s.d_mcells : nullptr, st));
+        BSW_TRY(hipEventRecord(e1, st));
+        if (mode == 0) stats->n_fwd = njobs; else stats->n_rev = njobs;
+    }
+    unsigned long long cells = 0;
+    BSW_TRY(hipMemcpyAsync(&cells, s.d_mcells, sizeof(cells), hipMemcpyDeviceToHost, st));
+    BSW_TRY(hipStreamSynchronize(st));
+    BSW_TRY(hipEventElapsedTime(&stats->fwd_ms, s.ev0, s.ev1));
+    BSW_TRY(hipEventElapsedTime(&stats->rev_ms, s.ev2, s.ev3));
+    stats->cells_fwd = (int64_t)cells;
+    return BSW_OK;
 }
 
 }  // namespace bsw
@@ -553,6 +641,87 @@ int bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref
     }();
     dc.give_back(std::move(slot));
     return rc;
+}
+
+int bsw_ksw_align2_device(bsw_ctx_t *ctx, const SeqPair *d_pairs, const uint8_t *d_ref,
+                          const uint8_t *d_qer, int32_t n, bsw_kswr_t *d_aln, void *stream)
+{
+    if (!ctx || n < 0 || (n > 0 && (!d_pairs || !d_ref || !d_qer || !d_aln))) return BSW_E_INVAL;
+    if (!bsw::mate_params_ok(ctx->params)) return BSW_E_INVAL;
+    if (n == 0) return BSW_OK;
+    bsw::MateParams mp;
+    bsw::make_mate_params(ctx->params, mp);
+    bsw::DeviceCtx &dc = *ctx->devs[0];
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        hipStream_t st = stream ? (hipStream_t)stream : slot->stream;
+        bsw_mate_stats_t ms;
+        const int r = bsw::mate_device(mp, *slot, d_pairs, d_ref, d_qer, n, d_aln, st, &ms);
+        if (r) return r;
+        std::lock_guard<std::mutex> g(ctx->stats_mu);
+        ctx->mate_last = ms;
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+
+int bsw_ksw_align2(bsw_ctx_t *ctx, const SeqPair *pairs, const uint8_t *seqBufRef, const uint8_t *seqBufQer,
+                   int32_t n, bsw_kswr_t *aln)
+{
+    if (!ctx || n < 0 || (n > 0 && (!pairs || !seqBufRef || !seqBufQer || !aln))) return BSW_E_INVAL;
+    if (!bsw::mate_params_ok(ctx->params)) return BSW_E_INVAL;
+    if (n == 0) return BSW_OK;
+    for (int32_t i = 0; i < n; ++i)
+        if (pairs[i].len1 < 0 || pairs[i].len2 < 0 || pairs[i].len1 > BSW_MAX_LEN ||
+            pairs[i].len2 > BSW_MATE_MAX_QLEN || pairs[i].idr < 0 || pairs[i].idq < 0)
+            return BSW_E_RANGE;
+    bsw::MateParams mp;
+    bsw::make_mate_params(ctx->params, mp);
+    bsw::DeviceCtx &dc = *ctx->devs[0];
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    bsw::Slot &s = *slot;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            const SeqPair &p = pairs[i];
+            if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
+            if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
+        }
+        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+        BSW_TRY(bsw::grow(s.d_mpairs, s.cap_mpairs, (size_t)n));
+        BSW_TRY(bsw::grow(s.d_maln, s.cap_maln, (size_t)n));
+        BSW_TRY(bsw::grow(s.d_ref, s.cap_ref, (size_t)(r_hi - r_lo) + 1));
+        BSW_TRY(bsw::grow(s.d_qer, s.cap_qer, (size_t)(q_hi - q_lo) + 1));
+        BSW_TRY(hipMemcpyAsync(s.d_mpairs, pairs, (size_t)n * sizeof(SeqPair), hipMemcpyHostToDevice, s.stream));
+        if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, seqBufRef + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
+        if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, seqBufQer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
+        bsw_mate_stats_t ms;
+        int r = bsw::mate_device(mp, s, s.d_mpairs, s.d_ref - r_lo, s.d_qer - q_lo, n, s.d_maln, s.stream, &ms);
+        if (r) return r;
+        BSW_TRY(hipMemcpyAsync(aln, s.d_maln, (size_t)n * sizeof(bsw_kswr_t), hipMemcpyDeviceToHost, s.stream));
+        BSW_TRY(hipStreamSynchronize(s.stream));
+        std::lock_guard<std::mutex> g(ctx->stats_mu);
+        ctx->mate_last = ms;
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+
+int bsw_mate_last_stats(bsw_ctx_t *ctx, bsw_mate_stats_t *out)
+{
+    if (!ctx || !out) return BSW_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    *out = ctx->mate_last;
+    return BSW_OK;
 }
 
 int bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out)

@@ -198,3 +198,81 @@ int32_t bsw_synth_reads(const bsw_reads_cfg *c, const uint8_t *ref, int64_t ref_
     }
     return nseeded;
 }
+
+/* ---------------------------------------------------------------- mate-rescue jobs
+ * Jobs shaped like mem_matesw's (bwamem_pair.cpp; include/bsw_mate.h): the mate read
+ * (read_len bases sampled from the reference with substitutions / short indels) against a
+ * reference window of win_len bases -- insert-size window [mean - 4 sd, mean + 4 sd] plus
+ * the read length -- that holds the mate's true origin with probability p_true (a random
+ * window otherwise: the mate is unmapped or elsewhere).  pairs[k]: idr = window start in
+ * ref (seqBufRef = the reference), idq = k * read_len in qer, len1 = win_len,
+ * len2 = read_len, h0 = xtra = KSW_XSUBO | KSW_XSTART | (read_len * a < 250 ? KSW_XBYTE : 0)
+ * | min_seed * a, exactly bwa's mate-rescue flags for match score a. */
+typedef struct bsw_mates_cfg {
+    uint64_t seed;
+    int32_t read_len, win_len;   /* 150, 550                                             */
+    int32_t a, min_seed;         /* match score 1, bwa -k 19                             */
+    double p_true;               /* window holds the mate (0.8)                          */
+    double p_sub, p_indel;       /* read edit rates (0.02, 0.002)                        */
+} bsw_mates_cfg;
+
+void bsw_mates_default(bsw_mates_cfg *c)
+{
+    c->seed = 42;
+    c->read_len = 150;
+    c->win_len = 550;
+    c->a = 1;
+    c->min_seed = 19;
+    c->p_true = 0.8;
+    c->p_sub = 0.02;
+    c->p_indel = 0.002;
+}
+
+int32_t bsw_synth_mates(const bsw_mates_cfg *c, const uint8_t *ref, int64_t ref_len, int64_t base, int32_t n,
+                        SeqPair *pairs, uint8_t *qer)
+{
+    const int32_t L = c->read_len, W = c->win_len;
+    if (L <= 0 || W < L || ref_len < (int64_t)W + 2 * L + 64) return -1;
+    const int32_t xtra = 0x40000 | 0x80000 | (L * c->a < 250 ? 0x10000 : 0) | ((c->min_seed * c->a) & 0xffff);
+    int32_t ntrue = 0;
+    for (int32_t k = 0; k < n; ++k) {
+        const int64_t gi = base + k;
+        uint64_t s = c->seed * 0xA0761D6478BD642Full ^ ((uint64_t)gi * 0xE7037ED1A0B428DBull) ^ 0x3333;
+        splitmix64(&s);
+        const int64_t org = (int64_t)(u01(&s) * (double)(ref_len - W - L - 64)) + L;
+        uint8_t *q = qer + (int64_t)k * L;
+        int64_t i = org;
+        int32_t j = 0;
+        while (j < L) {
+            if (u01(&s) < c->p_indel) {
+                const int32_t l = 1 + (int32_t)below(&s, 3);
+                if (splitmix64(&s) & 1) {
+                    for (int32_t t = 0; t < l && j < L; ++t) q[j++] = (uint8_t)below(&s, 4);
+                } else {
+                    i += l;
+                }
+                continue;
+            }
+            uint8_t b = ref[i++];
+            if (u01(&s) < c->p_sub) b = (uint8_t)((b < 4 ? b : 0) + 1 + below(&s, 3)) & 3;
+            q[j++] = b;
+        }
+        int64_t w0;
+        if (u01(&s) < c->p_true) {
+            w0 = org - (int64_t)below(&s, (uint32_t)(W - L + 1));
+            if (w0 < 0) w0 = 0;
+            ++ntrue;
+        } else {
+            w0 = (int64_t)(u01(&s) * (double)(ref_len - W));
+        }
+        SeqPair *p = &pairs[k];
+        memset(p, 0, sizeof(*p));
+        p->idr = (int32_t)w0;
+        p->idq = (int32_t)((int64_t)k * L);
+        p->id = (int32_t)gi;
+        p->len1 = W;
+        p->len2 = L;
+        p->h0 = xtra;
+    }
+    return ntrue;
+}

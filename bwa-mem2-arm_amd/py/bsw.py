@@ -29,7 +29,8 @@ assert SEQPAIR_DTYPE.itemsize == 56
 ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_scores",
                "bsw_get_scores_device", "bsw_last_stats", "bsw_strerror", "bsw_abi_version",
                "bsw_ext_opt_default", "bsw_extend_seeds", "bsw_ext_last_stats",
-               "bswb_write", "bswb_read_header", "bswb_read")
+               "bswb_write", "bswb_read_header", "bswb_read",
+               "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats")
 
 # include/bsw_ext.h structs
 SEED_DTYPE = np.dtype([("rbeg", np.int64), ("qbeg", np.int32), ("len", np.int32)])
@@ -37,6 +38,11 @@ ALNREG_DTYPE = np.dtype([("rb", np.int64), ("re", np.int64), ("qb", np.int32), (
                          ("score", np.int32), ("truesc", np.int32), ("w", np.int32),
                          ("seedlen0", np.int32)])
 assert SEED_DTYPE.itemsize == 16 and ALNREG_DTYPE.itemsize == 40
+
+# include/bsw_mate.h
+KSW_XBYTE, KSW_XSTOP, KSW_XSUBO, KSW_XSTART = 0x10000, 0x20000, 0x40000, 0x80000
+KSWR_DTYPE = np.dtype([(n, "<i4") for n in ("score", "te", "qe", "score2", "te2", "tb", "qb")])
+assert KSWR_DTYPE.itemsize == 28
 
 
 class Params(ctypes.Structure):
@@ -99,9 +105,13 @@ def hip_lib():
         L.bsw_ext_opt_default.argtypes = [P]
         L.bsw_extend_seeds.argtypes = [P, P, P, ctypes.c_int64, P, P, P, P, ctypes.c_int32, P]
         L.bsw_ext_last_stats.argtypes = [P, P]
+        L.bsw_ksw_align2.argtypes = [P, P, P, P, ctypes.c_int32, P]
+        L.bsw_ksw_align2_device.argtypes = [P, P, P, P, ctypes.c_int32, P, P]
+        L.bsw_mate_last_stats.argtypes = [P, P]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
-                  "bswb_read_header", "bswb_read"):
+                  "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
+                  "bsw_mate_last_stats"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -229,6 +239,35 @@ def ext_last_stats(engine) -> ExtStats:
     return s
 
 
+# ---------------------------------------------------------------- mate rescue (bsw_mate.h)
+class MateStats(ctypes.Structure):
+    _fields_ = [("fwd_ms", ctypes.c_float), ("rev_ms", ctypes.c_float), ("n_fwd", ctypes.c_int32),
+                ("n_rev", ctypes.c_int32), ("cells_fwd", ctypes.c_int64)]
+
+
+def ksw_align2(engine, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray) -> np.ndarray:
+    """bsw_ksw_align2: per SeqPair (len1 = target, len2 = query, h0 = xtra) upstream
+    ksw_align2's kswr_t -> KSWR_DTYPE array."""
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    qer = np.ascontiguousarray(qer, dtype=np.uint8)
+    out = np.zeros(len(pairs), dtype=KSWR_DTYPE)
+    _check(hip_lib().bsw_ksw_align2(engine._ctx, _ptr(pairs), _ptr(ref), _ptr(qer), len(pairs), _ptr(out)))
+    return out
+
+
+def ksw_align2_device(engine, d_pairs: int, d_ref: int, d_qer: int, n: int, d_aln: int, stream: int = 0):
+    _check(hip_lib().bsw_ksw_align2_device(engine._ctx, ctypes.c_void_p(d_pairs), ctypes.c_void_p(d_ref),
+                                           ctypes.c_void_p(d_qer), n, ctypes.c_void_p(d_aln),
+                                           ctypes.c_void_p(stream or None)))
+
+
+def mate_last_stats(engine) -> MateStats:
+    s = MateStats()
+    _check(hip_lib().bsw_mate_last_stats(engine._ctx, ctypes.byref(s)))
+    return s
+
+
 # ---------------------------------------------------------------- synthetic batches
 class SynthCfg(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("tlen", ctypes.c_int32), ("qlen", ctypes.c_int32),
@@ -254,6 +293,10 @@ def synth_lib():
         L.bsw_synth_reads.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.bsw_synth_reads.restype = ctypes.c_int32
+        L.bsw_mates_default.argtypes = [ctypes.c_void_p]
+        L.bsw_synth_mates.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
+        L.bsw_synth_mates.restype = ctypes.c_int32
         _synth = L
     return _synth
 
@@ -311,3 +354,28 @@ def synth_reads(ref: np.ndarray, n: int, read_base: int = 0, cfg: ReadsCfg | Non
     read_off = np.arange(n, dtype=np.int64) * L
     read_len = np.full(n, L, dtype=np.int32)
     return reads, read_off, read_len, seeds, origin
+
+
+class MatesCfg(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("read_len", ctypes.c_int32), ("win_len", ctypes.c_int32),
+                ("a", ctypes.c_int32), ("min_seed", ctypes.c_int32), ("p_true", ctypes.c_double),
+                ("p_sub", ctypes.c_double), ("p_indel", ctypes.c_double)]
+
+
+def mates_cfg(**kw) -> MatesCfg:
+    c = MatesCfg()
+    synth_lib().bsw_mates_default(ctypes.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def synth_mates(ref: np.ndarray, n: int, base: int = 0, cfg: MatesCfg | None = None):
+    """Mate-rescue jobs against ref (bsw_synth_mates): (pairs, qer); seqBufRef is ref itself."""
+    cfg = cfg if cfg is not None else mates_cfg()
+    pairs = np.zeros(n, dtype=SEQPAIR_DTYPE)
+    qer = np.zeros(max(1, n * cfg.read_len), dtype=np.uint8)
+    r = synth_lib().bsw_synth_mates(ctypes.byref(cfg), _ptr(ref), len(ref), base, n, _ptr(pairs), _ptr(qer))
+    if r < 0:
+        raise BswError("bsw_synth_mates: reference too short for the window")
+    return pairs, qer

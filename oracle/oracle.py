@@ -117,3 +117,36 @@ def extend_seeds(params, opt, ref, reads, read_off, read_len, seeds):
     L.oracle_extend_seeds(ctypes.byref(params), ctypes.byref(opt), ptr(ref), len(ref), ptr(reads),
                           ptr(read_off), ptr(read_len), ptr(seeds), len(seeds), ptr(out))
     return out
+
+
+KSWR_DTYPE = np.dtype([(n, "<i4") for n in ("score", "te", "qe", "score2", "te2", "tb", "qb")])
+
+
+class _Kswr(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in KSWR_DTYPE.names]
+
+
+def ksw_align2(query, target, mat, o_del, e_del, o_ins, e_ins, xtra):
+    """oracle/ksw_align_ref.c: literal striped ksw_align2 (one pair) -> list of 7 ints."""
+    L = lib()
+    P = ctypes.c_void_p
+    L.oracle_ksw_align2.restype = _Kswr
+    L.oracle_ksw_align2.argtypes = [ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P] + [ctypes.c_int] * 5
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    t = np.ascontiguousarray(target, dtype=np.uint8)
+    m = np.ascontiguousarray(mat, dtype=np.int8)
+    r = L.oracle_ksw_align2(len(q), _ptr(q), len(t), _ptr(t), 5, _ptr(m), o_del, e_del, o_ins, e_ins, xtra)
+    return [getattr(r, n) for n in KSWR_DTYPE.names]
+
+
+def ksw_align2_batch(pairs, ref, qer, mat, o_del=6, e_del=1, o_ins=6, e_ins=1, nthreads=1):
+    """Batch over SeqPairs (len1 = target, len2 = query, h0 = xtra) -> KSWR_DTYPE array."""
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    L = lib()
+    P = ctypes.c_void_p
+    L.oracle_ksw_align2_batch.argtypes = [P, P, P, ctypes.c_int, P] + [ctypes.c_int] * 4 + [P, ctypes.c_int]
+    m = np.ascontiguousarray(mat, dtype=np.int8)
+    out = np.zeros(len(pairs), dtype=KSWR_DTYPE)
+    L.oracle_ksw_align2_batch(_ptr(pairs), _ptr(ref), _ptr(qer), len(pairs), _ptr(m), o_del, e_del, o_ins,
+                              e_ins, _ptr(out), nthreads)
+    return out
