@@ -13,7 +13,7 @@ HBM before timing starts.  N GPUs: one process per GPU (torchrun), each with its
 control plane (barriers, max-over-ranks timing) is torch.distributed/gloo.
 
 Reported beside the metric:
-  roofline     -- dominant kernel (lane_kernel<160>), integer-VALU bound: algorithmic ops
+  roofline     -- dominant kernel (pc_kernel<160> on C2), integer-VALU bound: algorithmic ops
                   = 14 int ops x 25,100 static band cells per pair per
                   launch / HIP-event-timed launch duration, vs the gfx950 packed-int16 VALU
                   peak; traffic = HBM bytes per launch from rocprofv3 PMC (profiles/).
@@ -188,9 +188,12 @@ def main():
     cells = STATIC_CELLS_C2 if (cfg.qlen, cfg.tlen, args.w) == (150, 300, 100) else \
         static_band_cells(cfg.qlen, cfg.tlen, args.w)
     achieved = (args.pairs * cells * OPS_PER_CELL) / (kms_mean * 1e-3) / 1e12
-    # the dominant launch: int16 lane kernel (C2), or the packed 8-bit-regime kernel when a
-    # cell_bits=8 call routed the batch there (C3: narrow kernel + int16 overflow fallback)
-    kname = "pk_kernel<160>" if st.n_u8 > st.n_i16 else "lane_kernel<160>"
+    # the dominant launch: the packed-column kernel when the batch is in the 8-bit score
+    # regime (C2: every pair; C3: most, the rest on the int16 lane kernel), else the lane
+    # kernel; BSW_PK=1 selects the two-pairs-per-lane kernel for those pairs instead
+    packed = 2 * st.n_packed > args.pairs
+    kname = ("pk_kernel<160>" if os.environ.get("BSW_PK") == "1" else "pc_kernel<160>") if packed \
+        else "lane_kernel<160>"
     roof = {
         "bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
         "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
@@ -211,7 +214,7 @@ def main():
                                f"{cfg.tlen} bp ref, band w={args.w}, cell_bits={args.cell_bits}, "
                                f"h0 U[{cfg.h0_lo},{cfg.h0_hi}]",
                    "pairs_per_gpu": args.pairs, "parallelism": f"shard{world} (independent pairs)",
-                   "routing": {"n_i16": st.n_i16, "n_u8": st.n_u8, "n_wide": st.n_wide,
+                   "routing": {"n_packed": st.n_packed, "n_i16": st.n_i16, "n_u8": st.n_u8, "n_wide": st.n_wide,
                                "int16_fallback_fraction": (round(st.n_i16 / max(1, st.n_i16 + st.n_u8), 4)
                                                            if args.cell_bits == 8 else None)}},
         "roofline": roof,

@@ -71,7 +71,7 @@ __device__ __forceinline__ int seed_related(const uint8_t *__restrict__ q, int q
 
 // Per pair: class + sort key.  Lane classes need qlen <= QMAX and int16-safe scores.
 __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_t maxsc,
-                            int32_t pk_ok, const uint8_t *__restrict__ ref,
+                            int32_t route8, const uint8_t *__restrict__ ref,
                             const uint8_t *__restrict__ qer, uint32_t *__restrict__ keys,
                             int32_t *__restrict__ vals, int32_t *__restrict__ counts,
                             int32_t *__restrict__ maxq_wide)
@@ -89,8 +89,13 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
         else if (qlen <= 96) c = 2;
         else if (qlen <= 128) c = 3;
         else if (qlen <= 160) c = 4;
-        // 8-bit score regime -> packed kernel (key H << 8 | j fits 16 bits, H <= h0 + min(qlen, tlen))
-        if (pk_ok && c < kNumLaneClasses && p.h0 + min(qlen, tlen) <= 255) c += kPkClass0;
+        // 8-bit score regime (key H << 8 | j fits 16 bits, H <= h0 + min(qlen, tlen)) -> the
+        // packed-column kernel (route 2: needs qlen < QMAX, so bucket by qlen + 1) or the
+        // two-pairs-per-lane kernel (route 1)
+        if (route8 && c < kNumLaneClasses && p.h0 + min(qlen, tlen) <= 255) {
+            if (route8 == 1) c += kPkClass0;
+            else if (qlen + 1 <= 160) c = kPkClass0 + (qlen + 1 <= 32 ? 0 : qlen + 1 <= 64 ? 1 : qlen + 1 <= 96 ? 2 : qlen + 1 <= 128 ? 3 : 4);
+        }
     }
     if (valid) {
         if (c == kWideClass) atomicMax(maxq_wide, qlen);
@@ -263,8 +268,12 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
             ok = (a == 4 || b == 4) ? v == -1 : (a == b ? v == 1 : v == mis);
         }
     kp.pk_ok = ok ? 1 : 0;
-    const char *pk = getenv("BSW_PK");
-    kp.pk_default = (pk && pk[0] == '1') ? 1 : 0;
+    // 8-bit-regime routing: 2 = packed-column kernel (default, both cell widths), 1 = the
+    // two-pairs-per-lane kernel (BSW_PK=1), 0 = the lane kernel (16-bit calls with BSW_PC=0)
+    const char *pk = getenv("BSW_PK"), *pc = getenv("BSW_PC");
+    const bool pk_on = pk && pk[0] == '1', pc_off = pc && pc[0] == '0';
+    kp.route16 = pk_on ? 1 : pc_off ? 0 : 2;
+    kp.route8 = (pk_on || pc_off) ? 1 : 2;
 }
 
 // The device pipeline on one slot's device; d_* are device pointers valid on `stream`.
@@ -285,11 +294,13 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     }
     BSW_TRY(hipMemsetAsync(s.d_meta, 0, kMetaWords * sizeof(int32_t), stream));
     int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaCounts, *d_err = s.d_meta + kMetaCounts + 1;
-    // cell_bits = 8 (getScores8): pairs in the 8-bit score regime take the packed kernel, the
-    // rest the int16 kernels (overflow fallback); cell_bits = 16: int16 kernels (BSW_PK=1: packed too)
-    const int use_pk = kp.pk_ok && (cell_bits == 8 || kp.pk_default);
+    // pairs in the 8-bit score regime (h0 + min(qlen, tlen) <= 255, bwa-style scoring) take the
+    // packed-column kernel on both entry points (getScores8 / getScores16: identical results,
+    // fewer instructions per cell), the rest the int16 kernels (cell_bits = 8: the overflow
+    // fallback); BSW_PK=1 / BSW_PC=0 select the older kernels for those pairs
+    const int route8 = kp.pk_ok ? (cell_bits == 8 ? kp.route8 : kp.route16) : 0;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       d_pairs, n, kp.maxsc, use_pk, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
+                       d_pairs, n, kp.maxsc, route8, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
                        d_maxq);
     BSW_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
@@ -318,9 +329,14 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     for (int c = 0; c < kNumLaneClasses; ++c) {
         const int32_t np = counts[kPkClass0 + c];
         if (np > 0) {
-            BSW_TRY(launch_pk_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
-                                     d_err, stream));
+            if (route8 == 1)
+                BSW_TRY(launch_pk_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
+                                         d_err, stream));
+            else
+                BSW_TRY(launch_pc_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
+                                         d_err, stream));
             s.stats.n_launches++;
+            s.stats.n_packed += np;
             if (cell_bits == 8) s.stats.n_u8 += np;
             else s.stats.n_i16 += np;
         }
@@ -561,7 +577,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
     for (int d = 0; d < nd; ++d) {
         if (rcs[d]) return rcs[d];
         agg.kernel_ms = std::max(agg.kernel_ms, st[d].kernel_ms);
-        agg.n_i16 += st[d].n_i16; agg.n_u8 += st[d].n_u8; agg.n_wide += st[d].n_wide;
+        agg.n_i16 += st[d].n_i16; agg.n_u8 += st[d].n_u8; agg.n_wide += st[d].n_wide; agg.n_packed += st[d].n_packed;
         agg.n_launches += st[d].n_launches;
     }
     *out = agg;

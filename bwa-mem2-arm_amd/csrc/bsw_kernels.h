@@ -6,6 +6,9 @@
 //                  through their target rows in lock-step.  qlen <= QMAX (template), int16 cells.
 //   pk kernel    : TWO SeqPairs per lane (16-bit halves of every DP register), every step a
 //                  packed v_pk_* instruction; bwa-style scoring, scores < 256 (bsw_pk.hip).
+//   pc kernel    : one SeqPair per lane, the DP row as an H plane and an E plane packed two
+//                  columns per VGPR, column-independent steps as v_pk_* (bsw_pc.hip);
+//                  bwa-style scoring, scores < 256.  The default 8-bit-regime kernel.
 //   wide kernel  : one lane per pair, eh row in HBM scratch, int32 cells; any length.
 //                  Used for qlen > QMAX or scores that could overflow int16.
 #pragma once
@@ -24,8 +27,8 @@ struct KParams {
                                 //   symmetric gaps); set by the host, see bsw_pk.hip
     uint32_t prof[8][2];        // prof[t] = 8 score bytes mat[t][q], q = 0..7 (q>4 -> ambig)
     int8_t mat[25];
-    int8_t pk_default;          // host: route 8-bit-regime pairs to the packed kernel on 16-bit
-                                //   calls too (BSW_PK=1)
+    int8_t route16, route8;     // host: kernel for 8-bit-regime pairs on 16-bit / 8-bit calls
+                                //   (2 = packed-column pc, 1 = two-pairs-per-lane pk, 0 = lane)
 };
 
 // qlen limit of the register-resident kernel instantiations.
@@ -42,6 +45,12 @@ hipError_t launch_lane_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *p
 // kLaneQmax), h0 + min(len1, len2) <= 255 (the 8-bit score regime: this is the engine's
 // cell_bits = 8 path).  order[] slice as for the lane kernel; 128 pairs per wave.
 hipError_t launch_pk_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
+                            const int32_t *order, int32_t n, const uint8_t *ref,
+                            const uint8_t *qer, int32_t *err, hipStream_t s);
+
+// Packed-column lane kernel (bsw_pc.hip): kp.pk_ok scoring, qlen < qmax (strictly: slot qlen
+// must fall inside a 4-column group), h0 + min(len1, len2) <= 255; 64 pairs per wave.
+hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
                             const int32_t *order, int32_t n, const uint8_t *ref,
                             const uint8_t *qer, int32_t *err, hipStream_t s);
 

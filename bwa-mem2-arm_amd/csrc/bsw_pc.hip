@@ -1,0 +1,435 @@
+// bsw_pc.hip -- the packed-COLUMN lane kernel for gfx950: one SeqPair per
+// lane as in the lane kernel (bsw_kernels.hip), but the pair's DP row is split into an H plane
+// and an E plane, each packed TWO COLUMNS per VGPR, so that every column-independent step of
+// the ksw_extend2 recurrence is one v_pk_* instruction for two cells.
+//
+//   HH[k] = {H(i-1, 2k-1), H(i-1, 2k)}   -- "slot" s holds eh[s].h = H(i-1, s-1), the hold of column s
+//   EE[k] = {E(i, 2k),     E(i, 2k+1)}   -- eh[s].e
+//   Q[g]  = query codes of columns 4g..4g+3 in byte order {c0, c2, c1, c3}
+//
+// Per 4-column group (two HH and two EE registers), default scoring (match 1, one mismatch
+// value, N -1, symmetric gaps; the host's pk_ok contract):
+//   scores   : Y = v_perm(profile[t], Q[g]) -> {S0, S2, S1, S3} bytes; {S0, S1} and {S2, S3}
+//              sign-extended by packed 16-bit shifts                         (4 instructions)
+//   phase 1  : M = hold + min(S, hold) (the A.5 gate), T = max(M - oe, 0), ME = max(M, E),
+//              E' = max(E - e, T) -- 7 packed instructions per 2 columns      (14)
+//   F chain  : h = max(F, ME_j), F = max(F - e, T_j) per column, 32-bit ops with SDWA
+//              word selects                                                   (12)
+//   pack/key : HH <- {h_{j-1}, h_j} (v_lshl_or), key = max(HH << 8 | j) by v_pk_max_u16 (6)
+// = 36 VALU per 4 cells, against 47 for the lane kernel's fast group.  ~200 VGPRs at
+// QMAX = 160: two waves per SIMD (the occupancy the packed two-pairs-per-lane kernel lacks).
+//
+// Eligibility (planner, bsw_host.cpp): pk_ok scoring, h0 + min(qlen, tlen) <= 255 (H <= 255:
+// the 8-bit key H << 8 | j and the 16-bit lanes), qlen < QMAX (slot qlen inside a group).
+//
+// Band edges (per lane [beg, end)): a group is FAST when every live lane has all
+// four columns in band and 4G > beg (so the entering F / H chain is valid); otherwise it is
+// MASKED: the same arithmetic, then per-lane packed masks write slots <= end only (slots
+// beyond end keep their stale values, A.7: a later row whose end grows by 2 reads them), put
+// E = 0 at slot end, drop slots > end (and < beg) from the key, and pass H(i, end-1) along the
+// chain (h1 at row end = H(i, end-1), for gscore and the lazy last-positive scan).  Groups that
+// contain some lane's beg also reset F and H to 0 entering column beg.  Slots left of beg may
+// take garbage: they are never read again (beg never decreases).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <limits.h>
+#include <utility>
+#include "bsw_kernels.h"
+#include "bsw_wave.h"
+
+namespace bsw {
+
+constexpr int kPcChunkDw = 17;           // dwords per lane per 64-row target chunk (as lane kernel)
+
+struct PcRow {                           // per-row uniform (SGPR) group bounds
+    int glo, gsp;                        // groups touching slots [min beg, max end]
+    int gfa, gfn;                        // FAST groups: gfa <= G < gfa + gfn
+    int gla, gln;                        // groups containing some lane's beg: gla <= G <= gla + gln
+};
+
+// {v, v} as two int16 halves
+__device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu) * 0x10001u; }
+
+#define PC_SDWA(op, d, a, b, sel) \
+    op "_sdwa " d ", " a ", " b " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" sel "\n\t"
+
+// phase 1 of one packed register X (columns 2k, 2k+1): S in %[sX] -> M -> ME; T in %[tX];
+// E' into EOUT (in place for FAST, %[xX] for MASKED).
+#define PC_PH1(X, EOUT)                                                                 \
+    "v_pk_min_i16 %[s" X "], %[s" X "], %[h" X "]\n\t"                                      \
+    "v_pk_add_u16 %[s" X "], %[s" X "], %[h" X "]\n\t"                                      \
+    "v_pk_sub_i16 %[t" X "], %[s" X "], %[oe2]\n\t"                                         \
+    "v_pk_max_i16 %[t" X "], %[t" X "], 0\n\t"                                              \
+    "v_pk_max_i16 %[s" X "], %[s" X "], %[e" X "]\n\t"                                      \
+    "v_pk_sub_i16 " EOUT ", %[e" X "], %[ed2]\n\t"                                          \
+    "v_pk_max_i16 " EOUT ", " EOUT ", %[t" X "]\n\t"
+
+#define PC_SCORES                                                                        \
+    "v_perm_b32 %[y], %[phi], %[plo], %[q]\n\t"                                              \
+    "v_pk_lshlrev_b16 %[sa], 8, %[y] op_sel_hi:[0,1]\n\t"                                    \
+    "v_pk_ashrrev_i16 %[sa], 8, %[sa] op_sel_hi:[0,1]\n\t"                                   \
+    "v_pk_ashrrev_i16 %[sb], 8, %[y] op_sel_hi:[0,1]\n\t"
+
+// one F-chain cell: H -> C, F updated.  X = a|b register, W = WORD_0|WORD_1 half
+#define PC_CELL(C, X, W)                                                                 \
+    PC_SDWA("v_max_i32", C, "%[f]", "%[s" X "]", W)                                          \
+    "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"                                                 \
+    PC_SDWA("v_max_i32", "%[f]", "%[f]", "%[t" X "]", W)
+
+// masked cell: optional reset entering column J (J == beg: F = 0, H(i, J-1) = 0), then the
+// cell, then C = (J < end) ? H : HP (H(i, end-1) travels on past end)
+#define PC_RESET(HP, RJ)                                                                 \
+    "v_cmp_ne_u32_e32 vcc, " RJ ", %[begv]\n\t"                                              \
+    "v_cndmask_b32_e32 " HP ", 0, " HP ", vcc\n\t"                                           \
+    "v_cndmask_b32_e32 %[f], 0, %[f], vcc\n\t"
+#define PC_MCELL(C, HP, X, W, J)                                                         \
+    PC_CELL(C, X, W)                                                                         \
+    "v_cmp_lt_i32_e32 vcc, " J ", %[endv]\n\t"                                               \
+    "v_cndmask_b32_e32 " C ", " HP ", " C ", vcc\n\t"
+
+// masked write-back of register X from packed new values in %[pX]:
+//   slot <= end : HH <- new (else stale kept);  slot < end : EE <- E';  slot == end : EE <- 0
+//   key over slots in [beg, end] (LEFT adds the slot >= beg mask)
+#define PC_MWRITE(X, KEYSRC, LEFT)                                                       \
+    "v_pk_sub_i16 %[y], %[jj" X "], %[endw]\n\t"                                             \
+    "v_pk_ashrrev_i16 %[y], 15, %[y] op_sel_hi:[0,1]\n\t"                                    \
+    "v_bfi_b32 %[h" X "], %[y], %[p" X "], %[h" X "]\n\t"                                    \
+    "v_bfi_b32 %[e" X "], %[y], 0, %[e" X "]\n\t"                                            \
+    KEYSRC                                                                                   \
+    "v_and_b32_e32 %[p" X "], %[p" X "], %[y]\n\t"                                           \
+    "v_pk_sub_i16 %[y], %[jj" X "], %[endm1w]\n\t"                                           \
+    "v_pk_ashrrev_i16 %[y], 15, %[y] op_sel_hi:[0,1]\n\t"                                    \
+    "v_bfi_b32 %[e" X "], %[y], %[x" X "], %[e" X "]\n\t"                                    \
+    LEFT                                                                                     \
+    "v_pk_max_u16 %[key], %[key], %[p" X "]\n\t"
+#define PC_LEFTMASK(X)                                                                   \
+    "v_pk_sub_i16 %[y], %[begm2w], %[jj" X "]\n\t"                                           \
+    "v_pk_ashrrev_i16 %[y], 15, %[y] op_sel_hi:[0,1]\n\t"                                    \
+    "v_and_b32_e32 %[p" X "], %[p" X "], %[y]\n\t"
+
+// masked body (chain variant CH), shared by the L (left-reset) and R forms
+#define PC_MASKED(CH0, CH1, CH2, CH3, KA, KB, LA, LB)                                    \
+    PC_PH1("a", "%[xa]") PC_PH1("b", "%[xb]")                                                \
+    CH0 CH1                                                                                  \
+    "v_lshl_or_b32 %[pa], %[c0], 16, %[h1]\n\t"                                              \
+    CH2 CH3                                                                                  \
+    "v_lshl_or_b32 %[pb], %[c2], 16, %[c1]\n\t"                                              \
+    PC_MWRITE("a", KA, LA) PC_MWRITE("b", KB, LB)
+
+#define PC_GROUP_ASM(KEYA_FAST, KEYA_MASK)                                                \
+    asm volatile(                                                                            \
+        "s_sub_u32 %[st], %[g], %[glo]\n\t"          /* outside [min beg, max end]: skip */ \
+        "s_cmp_le_u32 %[st], %[gsp]\n\t"                                                     \
+        "s_cbranch_scc0 3f\n\t"                                                              \
+        PC_SCORES                                                                            \
+        "s_sub_u32 %[st], %[g], %[gfa]\n\t"          /* every live lane in band: FAST */    \
+        "s_cmp_lt_u32 %[st], %[gfn]\n\t"                                                     \
+        "s_cbranch_scc0 2f\n\t"                                                              \
+        PC_PH1("a", "%[ea]") PC_PH1("b", "%[eb]")                                            \
+        PC_CELL("%[c0]", "a", "WORD_0")                                                      \
+        PC_CELL("%[c1]", "a", "WORD_1")                                                      \
+        "v_lshl_or_b32 %[ha], %[c0], 16, %[h1]\n\t"                                          \
+        PC_CELL("%[c2]", "b", "WORD_0")                                                      \
+        PC_CELL("%[h1]", "b", "WORD_1")                                                      \
+        "v_lshl_or_b32 %[hb], %[c2], 16, %[c1]\n\t"                                          \
+        KEYA_FAST                                                                            \
+        "v_pk_max_u16 %[key], %[key], %[pa]\n\t"                                             \
+        "v_lshl_or_b32 %[pb], %[hb], 8, %[jjb]\n\t"                                          \
+        "v_pk_max_u16 %[key], %[key], %[pb]\n\t"                                             \
+        "s_branch 3f\n"                                                                      \
+        "2:\n\t"                                                                             \
+        "s_sub_u32 %[st], %[g], %[gla]\n\t"          /* some lane's beg in this group: L */ \
+        "s_cmp_le_u32 %[st], %[gln]\n\t"                                                     \
+        "s_cbranch_scc1 4f\n\t"                                                              \
+        PC_MASKED(PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"),                        \
+                  PC_MCELL("%[c1]", "%[c0]", "a", "WORD_1", "%[j1]"),                        \
+                  PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"),                        \
+                  PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"),                        \
+                  KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t", "", "")           \
+        "s_branch 3f\n"                                                                      \
+        "4:\n\t"                                                                             \
+        PC_MASKED(PC_RESET("%[h1]", "%[r0]") PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"), \
+                  PC_RESET("%[c0]", "%[j1]") PC_MCELL("%[c1]", "%[c0]", "a", "WORD_1", "%[j1]"), \
+                  PC_RESET("%[c1]", "%[j2]") PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"), \
+                  PC_RESET("%[c2]", "%[j3]") PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"), \
+                  KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t",                    \
+                  PC_LEFTMASK("a"), PC_LEFTMASK("b"))                                        \
+        "3:"                                                                                 \
+        : [ha] "+v"(ha), [hb] "+v"(hb), [ea] "+v"(ea), [eb] "+v"(eb), [f] "+v"(f),           \
+          [h1] "+v"(h1), [key] "+v"(key), [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb),     \
+          [ta] "=&v"(ta), [tb] "=&v"(tb), [xa] "=&v"(xa), [xb] "=&v"(xb), [c0] "=&v"(c0),    \
+          [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb), [st] "=&s"(st)     \
+        : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe2] "s"(oe2), [ed2] "s"(ed2),        \
+          [ed] "s"(ed), [glo] "s"(r.glo), [gsp] "s"(r.gsp), [gfa] "s"(r.gfa), [gfn] "s"(r.gfn), \
+          [gla] "s"(r.gla), [gln] "s"(r.gln), [endw] "v"(endw), [endm1w] "v"(endm1w),       \
+          [begm2w] "v"(begm2w), [endv] "v"(endv), [begv] "v"(begv), [g] "i"(G),             \
+          [jja] "s"(JJA), [jjb] "s"(JJB), [j0] "i"(4 * G), [j1] "i"(4 * G + 1),              \
+          [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [r0] "i"(R0)                             \
+        : "vcc", "scc")
+
+// One 4-column group G (columns / slots 4G .. 4G+3) as ONE asm statement: skip / FAST /
+// MASKED (R: right edge only; L: also resets at beg) decided by scalar tests inside.
+template <int G>
+__device__ __forceinline__ void pc_group(uint32_t &ha, uint32_t &hb, uint32_t &ea, uint32_t &eb,
+                                         uint32_t q, uint32_t plo, uint32_t phi, int &f, int &h1,
+                                         uint32_t &key, uint32_t oe2, uint32_t ed2, int ed,
+                                         const PcRow &r, uint32_t endw, uint32_t endm1w,
+                                         uint32_t begm2w, int endv, int begv)
+{
+    // key slot s carries column j = s - 1: jj = {4G-1, 4G} and {4G+1, 4G+2}
+    constexpr uint32_t JJA = ((uint32_t)(4 * G - 1) & 0xffffu) | ((uint32_t)(4 * G) << 16);
+    constexpr uint32_t JJB = (uint32_t)(4 * G + 1) | ((uint32_t)(4 * G + 2) << 16);
+    constexpr int R0 = (G == 0) ? -1 : 4 * G;   // no reset entering column 0 (the boundary)
+    uint32_t y, sa, sb, ta, tb, xa, xb, c0, c1, c2, pa, pb, st;
+    if constexpr (G == 0) {
+        // slot 0 holds the column-0 boundary, not a cell: its key half is 0 (c0 << 24 | 0)
+        PC_GROUP_ASM("v_lshl_or_b32 %[pa], %[c0], 24, 0\n\t",
+                     "v_lshl_or_b32 %[pa], %[c0], 24, 0\n\t");
+    } else {
+        PC_GROUP_ASM("v_lshl_or_b32 %[pa], %[ha], 8, %[jja]\n\t",
+                     "v_lshl_or_b32 %[pa], %[pa], 8, %[jja]\n\t");
+    }
+}
+
+template <int QMAX, int... G>
+__device__ __forceinline__ void pc_row(std::integer_sequence<int, G...>, uint32_t (&hh)[QMAX / 2],
+                                       uint32_t (&ee)[QMAX / 2], const uint32_t (&qs)[QMAX / 4],
+                                       uint32_t plo, uint32_t phi, int &f, int &h1, uint32_t &key,
+                                       uint32_t oe2, uint32_t ed2, int ed, const PcRow &r,
+                                       uint32_t endw, uint32_t endm1w, uint32_t begm2w, int endv,
+                                       int begv)
+{
+    (pc_group<G>(hh[2 * G], hh[2 * G + 1], ee[2 * G], ee[2 * G + 1], qs[G], plo, phi, f, h1, key,
+                 oe2, ed2, ed, r, endw, endm1w, begm2w, endv, begv), ...);
+}
+
+// Lazy last positive column: when H(i, end-1) == 0 the lanes that need it
+// scan slots right to left (slot j+1 = H(i, j)) from end - 1; groups above every lane's end
+// and groups after all lanes found one are skipped by uniform tests.
+template <int QMAX, int GG>
+__device__ __forceinline__ bool pc_lastpos_group(const uint32_t (&hh)[QMAX / 2], int end, bool pending,
+                                                 int &lp1, int gstart)
+{
+    if (GG > gstart) return pending;                      // uniform
+    if (__ballot(pending) == 0) return false;             // uniform
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+        const int j = 4 * GG + k;                         // column; its H sits in slot j + 1
+        if (j + 1 < QMAX) {
+            const uint32_t hv = (hh[(j + 1) >> 1] >> (16 * ((j + 1) & 1))) & 0xffffu;
+            const bool hit = pending & (j < end) & (hv != 0u);
+            lp1 = hit ? j + 1 : lp1;
+            pending = pending & !hit;
+        }
+    }
+    return pending;
+}
+
+template <int QMAX, int... G>
+__device__ __forceinline__ void pc_lastpos(std::integer_sequence<int, G...>,
+                                           const uint32_t (&hh)[QMAX / 2], int end, bool need,
+                                           int &lp1, int gstart)
+{
+    bool pending = need;
+    ((pending = pc_lastpos_group<QMAX, QMAX / 4 - 1 - G>(hh, end, pending, lp1, gstart)), ...);
+}
+
+template <int QMAX>
+__global__ __launch_bounds__(256, 2) void pc_kernel(const KParams kp, const int32_t w,
+                                                    SeqPair *__restrict__ pairs,
+                                                    const int32_t *__restrict__ order,
+                                                    const int32_t n,
+                                                    const uint8_t *__restrict__ ref,
+                                                    const uint8_t *__restrict__ qer,
+                                                    int32_t *__restrict__ err)
+{
+    constexpr int NG = QMAX / 4;        // groups = query words (4 codes each)
+    __shared__ uint32_t s_tgt[4][2][kPcChunkDw][64];   // 34.8 KB per 256-thread block
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    bool valid = gid < n;
+    const int idx = valid ? (order ? order[gid] : gid) : 0;
+    SeqPair *sp = pairs + idx;
+    int idr = 0, idq = 0, tlen = 0, qlen = 0, h0 = 0;
+    if (valid) {
+        idr = sp->idr; idq = sp->idq; tlen = sp->len1; qlen = sp->len2; h0 = sp->h0;
+        if (qlen >= QMAX || qlen < 0 || tlen < 0 || h0 < 0 || h0 + min(qlen, tlen) > 255) {
+            atomicOr(err, 1);
+            valid = false;
+        }
+    }
+    // query codes, 4 per VGPR in byte order {c0, c2, c1, c3}: aligned dword loads (a dword
+    // holding a byte of the query never leaves that byte's page), realigned by v_alignbyte
+    uint32_t qs[NG];
+    {
+        uint32_t wv[NG + 1];
+        const uintptr_t qa = (uintptr_t)(qer + idq);
+        const uint32_t *wp = (const uint32_t *)(qa & ~(uintptr_t)3);
+        const int sh = (int)(qa & 3);
+        const int nw = (valid && qlen > 0) ? (sh + qlen + 3) >> 2 : 0;
+        if (nw > 0) {
+#pragma unroll
+            for (int g = 0; g <= NG; ++g) wv[g] = wp[min(g, nw - 1)];
+        } else {
+#pragma unroll
+            for (int g = 0; g <= NG; ++g) wv[g] = 0;
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const uint32_t c = __builtin_amdgcn_alignbyte(wv[g + 1], wv[g], sh);
+            qs[g] = __builtin_amdgcn_perm(c, c, 0x03010200u);
+        }
+    }
+    // A.1 first row: slot 0 = h0, slot j = max(h0 - oe_ins - (j-1) e_ins, 0) for 1 <= j <= qlen
+    uint32_t hh[QMAX / 2], ee[QMAX / 2];
+    {
+        const int oe_ins = kp.o_ins + kp.e_ins;
+#pragma unroll
+        for (int k = 0; k < QMAX / 2; ++k) {
+            const int j0 = 2 * k, j1 = 2 * k + 1;
+            const uint32_t a = (j0 == 0) ? (uint32_t)h0
+                             : (j0 <= qlen) ? (uint32_t)max(h0 - oe_ins - (j0 - 1) * kp.e_ins, 0) : 0u;
+            const uint32_t b = (j1 <= qlen) ? (uint32_t)max(h0 - oe_ins - (j1 - 1) * kp.e_ins, 0) : 0u;
+            hh[k] = a | (b << 16);
+            ee[k] = 0u;
+        }
+    }
+    // A.2 per-lane band cap, integer form of (int)((double)N / e + 1.)
+    int wl = w;
+    {
+        const int ni = qlen * kp.maxsc + kp.end_bonus - kp.o_ins;
+        const int nd = qlen * kp.maxsc + kp.end_bonus - kp.o_del;
+        wl = min(wl, max((ni + kp.e_ins) / kp.e_ins, 1));
+        wl = min(wl, max((nd + kp.e_del) / kp.e_del, 1));
+    }
+    int best = h0, best_i = -1, best_j = -1, max_ie = -1, gsc = -1, moff = 0, endc = qlen;
+    bool alive = valid && tlen > 0;
+    // target bases HBM -> LDS by LDS-DMA, 64-row chunks double-buffered (as the lane kernel)
+    const uint8_t *tp = ref + idr;
+    const int tsh = (int)((uintptr_t)tp & 3);
+    const uint32_t *twp = (const uint32_t *)(tp - tsh);
+    const int tlast = max((tsh + tlen - 1) >> 2, 0);
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    auto issue_chunk = [&](int ch) {
+        uint32_t *dst = &s_tgt[wv][ch & 1][0][0];
+#pragma unroll
+        for (int k = 0; k < kPcChunkDw; ++k)
+            __builtin_amdgcn_global_load_lds((gptr_t)(twp + min(16 * ch + k, tlast)),
+                                             (lptr_t)(dst + 64 * k), 4, 0, 0);
+    };
+    if (alive) { issue_chunk(0); issue_chunk(1); }
+    uint32_t tcur = 0;
+    const int wl_max = wave_max(alive ? wl : -1);
+    const int wl_min = wave_min(alive ? wl : INT_MAX);
+    const uint32_t oe2 = (uint32_t)(kp.o_del + kp.e_del) * 0x10001u;
+    const uint32_t ed2 = (uint32_t)kp.e_del * 0x10001u;
+
+    for (int i = 0;; ++i) {
+        const bool act = alive && i < tlen;
+        alive = act;
+        if (__ballot(act) == 0) break;
+        const int beg = max(0, i - wl);
+        const int end = min(min(endc, i + wl + 1), qlen);
+        endc = end;
+        const int emax = wave_max(act ? end : -1);
+        const int emin = wave_min(act ? end : INT_MAX);
+        PcRow r;
+        {
+            const int ulo = __builtin_amdgcn_readfirstlane(max(0, i - wl_max));  // min beg
+            const int uhi = __builtin_amdgcn_readfirstlane(emax);                // max end
+            const int flo = __builtin_amdgcn_readfirstlane(max(0, i - wl_min));  // max beg
+            const int fhi = __builtin_amdgcn_readfirstlane(emin);                // min end
+            r.glo = ulo >> 2;
+            r.gsp = max(min(uhi, QMAX - 1) / 4 - r.glo, -1);
+            // FAST needs 4G > every beg (entering chain valid) -- or one common beg == 4G with
+            // nothing computed before it -- and 4G + 4 <= every end
+            r.gfa = (ulo == flo && (flo & 3) == 0) ? (flo >> 2) : (flo >> 2) + 1;
+            r.gfn = max((fhi >> 2) - r.gfa, 0);
+            r.gla = ulo >> 2;
+            r.gln = (flo >> 2) - r.gla;
+        }
+        if (act) {
+            if ((i & 3) == 0) {            // new 4-row block: 4 target bases from LDS
+                if ((i & 63) == 0) {          // chunk boundary: its DMA was issued 64 rows ago
+                    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                const int k = (i >> 2) & 15;
+                const uint32_t *src = &s_tgt[wv][(i >> 6) & 1][k][ln];
+                tcur = __builtin_amdgcn_alignbyte(src[64], src[0], tsh);
+                if ((i & 63) == 0) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (i > 0) issue_chunk((i >> 6) + 1);   // refill the buffer just drained
+                }
+            }
+            // per-row score profile of target base t (8 bytes: mat[t][q], q = 0..7)
+            const uint32_t t = (tcur >> (8 * (i & 3))) & 0xffu;
+            uint2 pr = make_uint2(kp.prof[4][0], kp.prof[4][1]);
+            pr = (t == 3) ? make_uint2(kp.prof[3][0], kp.prof[3][1]) : pr;
+            pr = (t == 2) ? make_uint2(kp.prof[2][0], kp.prof[2][1]) : pr;
+            pr = (t == 1) ? make_uint2(kp.prof[1][0], kp.prof[1][1]) : pr;
+            pr = (t == 0) ? make_uint2(kp.prof[0][0], kp.prof[0][1]) : pr;
+            int h1 = (beg == 0) ? max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) : 0;
+            int f = 0;
+            uint32_t key = 0;
+            const uint32_t endw = pack2(end);
+            const uint32_t endm1w = pack2(end - 1);                         // end = 0: {-1, -1}
+            const uint32_t begm2w = pack2(beg - 2);
+            pc_row<QMAX>(std::make_integer_sequence<int, NG>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
+                         oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg);
+            const uint32_t k32 = max(key & 0xffffu, key >> 16);
+            const int m = (int)(k32 >> 8), mj = (int)(k32 & 0xffu);
+            if (end == qlen) {                    // A.4: j == qlen; h1 = H(i, qlen - 1)
+                if (!(gsc > h1)) max_ie = i;
+                gsc = max(gsc, h1);
+            }
+            if (m <= 0) {
+                alive = false;
+            } else if (m > best) {
+                best = m; best_i = i; best_j = mj;
+                moff = max(moff, abs(mj - i));
+            } else if (kp.zdrop > 0) {
+                const int di = i - best_i, dj = mj - best_j;
+                const int dz = (di > dj) ? best - m - (di - dj) * kp.e_del
+                                         : best - m - (dj - di) * kp.e_ins;
+                if (dz > kp.zdrop) alive = false;
+            }
+            if (alive) {                           // end_{i+1} = min(lastH + 3, ...), DESIGN.md §3
+                const bool need = h1 == 0;         // H(i, end-1) == 0 -> lastH < end - 1
+                int lp1 = end;
+                if (__ballot(need)) {
+                    if (need) lp1 = 0;
+                    pc_lastpos<QMAX>(std::make_integer_sequence<int, NG>{}, hh, end, need, lp1,
+                                     (emax - 1) >> 2);
+                }
+                endc = min(lp1 + 2, qlen);
+            }
+        }
+    }
+    if (valid) {
+        sp->score = best;
+        sp->tle = best_i + 1;
+        sp->gtle = max_ie + 1;
+        sp->qle = best_j + 1;
+        sp->gscore = gsc;
+        sp->max_off = moff;
+    }
+}
+
+hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
+                            const int32_t *order, int32_t n, const uint8_t *ref,
+                            const uint8_t *qer, int32_t *err, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    const dim3 block(256), grid((unsigned)((n + 255) / 256));
+    switch (qmax) {
+    case 32: hipLaunchKernelGGL(pc_kernel<32>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 64: hipLaunchKernelGGL(pc_kernel<64>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 96: hipLaunchKernelGGL(pc_kernel<96>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 128: hipLaunchKernelGGL(pc_kernel<128>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 160: hipLaunchKernelGGL(pc_kernel<160>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace bsw

@@ -57,7 +57,7 @@ class Params(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_float), ("n_i16", ctypes.c_int32),
                 ("n_u8", ctypes.c_int32), ("n_wide", ctypes.c_int32),
-                ("n_launches", ctypes.c_int32)]
+                ("n_launches", ctypes.c_int32), ("n_packed", ctypes.c_int32)]
 
 
 def default_params(a=1, b=4, o_del=6, e_del=1, o_ins=6, e_ins=1, zdrop=100, end_bonus=5,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BSW_ABI_VERSION 1
+#define BSW_ABI_VERSION 2
 
 enum {
     BSW_OK = 0,
@@ -93,6 +93,8 @@ typedef struct bsw_stats_t {
     float   kernel_ms;          /* sum of DP-kernel durations (HIP events, same stream) */
     int32_t n_i16, n_u8, n_wide; /* pairs per kernel class                               */
     int32_t n_launches;         /* DP-kernel launches                                    */
+    int32_t n_packed;           /* of n_i16 + n_u8: pairs run on the 8-bit-regime packed
+                                   kernels (v_pk_* cells; ABI version 2)                 */
 } bsw_stats_t;
 int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
 

@@ -117,3 +117,17 @@ def edge_pairs(seed=7):
         items.append((rr, mutate(rng, rr, L, 0.05, 0.02), 250))  # large h0
         items.append((rr, mutate(rng, rr, L, 0.05, 0.02), 1))    # tiny h0
     return assemble(items)
+
+
+def pairs_from_shapes(shapes, seed, p_unrelated=0.2):
+    """shapes: list of (tlen, qlen, h0); related (mutated-prefix) queries unless unrelated."""
+    rng = np.random.default_rng(seed)
+    items = []
+    for T, Q, h0 in shapes:
+        r = rng.integers(0, 4, T).astype(np.uint8)
+        if rng.random() < p_unrelated:
+            q = rng.integers(0, 4, Q).astype(np.uint8)
+        else:
+            q = mutate(rng, r, Q, rng.uniform(0.0, 0.08), rng.uniform(0.0, 0.03), 0.01)
+        items.append((r, q, int(h0)))
+    return assemble(items)

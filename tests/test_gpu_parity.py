@@ -172,7 +172,7 @@ def test_cell_bits_8_overflow_fallback(eng):
     _assert_same(want, got, "cell_bits=8 mixed")
     st = eng.last_stats()
     q, t, h0 = pairs["len2"], pairs["len1"], pairs["h0"]
-    narrow = (q <= 160) & (h0 + np.minimum(q, t) <= 255)
+    narrow = (q < 160) & (h0 + np.minimum(q, t) <= 255)      # packed-column kernel: qlen < QMAX
     assert st.n_u8 == int(narrow.sum())
     assert st.n_i16 + st.n_wide == len(pairs) - int(narrow.sum())
 
@@ -212,15 +212,81 @@ def test_multi_gpu_context_shards(c2_full):
     _assert_same(want[:100_000], got, f"n_gpus={n}")
 
 
+def _engine_with(env):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return bsw.Engine()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def eng_lane():
+    """Engine with the packed-column kernel disabled (BSW_PC=0 at create): every 16-bit pair
+    runs on the lane kernel (bsw_kernels.hip)."""
+    e = _engine_with({"BSW_PC": "0"})
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("w", [0, 1, 7, 40, 100, 200])
+def test_pc_kernel_random(eng, w):
+    """8-bit-regime pairs (h0 + min(qlen, tlen) <= 255, qlen < 160) run on bsw_pc.hip."""
+    pairs, ref, qer = bswgen.random_pairs(6000, seed=170 + w, qlen=(0, 159), tlen=(0, 330), h0=(0, 95))
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+    eng.get_scores(got, ref, qer, w)
+    _assert_same(want, got, f"pc w={w}")
+    assert eng.last_stats().n_packed == len(pairs)
+
+
+@pytest.mark.parametrize("cell_bits", [16, 8])
+def test_pc_kernel_bucket_edges(eng, cell_bits):
+    """qlen at every bucket edge (31/32/33 ... 159/160/161: 160 goes to the lane kernel,
+    161 to the wide kernel), h0 at the 8-bit bound, tiny and long targets."""
+    rng = np.random.default_rng(11)
+    shapes = []
+    for q in (0, 1, 2, 3, 4, 5, 31, 32, 33, 63, 64, 65, 95, 96, 97, 127, 128, 129, 159, 160, 161):
+        for t in (0, 1, 3, q, q + 1, 2 * q + 7, 300):
+            h0 = int(min(rng.integers(0, 120), max(0, 255 - min(q, t))))
+            shapes.append((t, q, h0))
+            shapes.append((t, q, max(0, 255 - min(q, t))))         # exactly at the bound
+            shapes.append((t, q, 256 - min(q, t)))                 # one above: lane kernel
+    pairs, ref, qer = bswgen.pairs_from_shapes(shapes, seed=12)
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    eng.get_scores(got, ref, qer, 100, cell_bits=cell_bits)
+    _assert_same(want, got, f"pc bucket edges cb={cell_bits}")
+    assert eng.last_stats().n_packed > 0
+
+
+def test_lane_kernel_random(eng_lane):
+    pairs, ref, qer = bswgen.random_pairs(6000, seed=77, qlen=(0, 160), tlen=(0, 330), h0=(0, 95))
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    eng_lane.get_scores(got, ref, qer, 100)
+    _assert_same(want, got, "lane kernel random")
+    assert eng_lane.last_stats().n_packed == 0
+
+
+def test_lane_kernel_c2(eng_lane, c2_full):
+    pairs, ref, qer, want = c2_full
+    got = pairs[:300_000].copy()
+    eng_lane.get_scores(got, ref, qer, 100)
+    _assert_same(want[:300_000], got, "lane kernel C2")
+    assert eng_lane.last_stats().n_packed == 0
+
+
 @pytest.fixture(scope="module")
 def eng_pk():
     """Engine with the opt-in packed two-pairs-per-lane kernel enabled (BSW_PK=1 at create)."""
-    import os
-    os.environ["BSW_PK"] = "1"
-    try:
-        e = bsw.Engine()
-    finally:
-        os.environ.pop("BSW_PK")
+    e = _engine_with({"BSW_PK": "1"})
     yield e
     e.close()
 
