@@ -18,13 +18,12 @@ def rows(pattern):
     return out
 
 def short(name):
-    if 'pk_kernel' in name:
-        return 'pk_kernel<160>'
-    if 'lane_kernel' in name:
-        for q in ('160', '128', '96', '64', '32'):
-            if f'ILi{q}E' in name or f'<{q},' in name:
-                return f'lane_kernel<{q}>'
-        return 'lane_kernel'
+    for kern in ('pc_kernel', 'pk_kernel', 'lane_kernel', 'mate_kernel'):
+        if kern in name:
+            for q in ('160', '128', '96', '64', '32'):
+                if f'ILi{q}E' in name or f'<{q},' in name or f'<{q}>' in name:
+                    return f'{kern}<{q}>'
+            return kern
     for k in ('wide_kernel', 'plan_kernel', 'Radix', 'radix', 'Onesweep', 'onesweep'):
         if k in name:
             return k
