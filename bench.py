@@ -138,9 +138,10 @@ def main():
     ap.add_argument("--cell-bits", type=int, default=16, choices=(8, 16))
     ap.add_argument("--h0-hi", type=int, default=100, help="h0 upper bound (C3 uses 105)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--workload", default="c2", choices=("c2", "c4", "mate"),
+    ap.add_argument("--workload", default="c2", choices=("c2", "c4", "mate", "global"),
                     help="c2 (default): resident SeqPair batch; c4: extension pipeline on synthetic reads; "
-                         "mate: resident mate-rescue batch (ksw_align2 jobs, SURVEY.md §8(f) row 2)")
+                         "mate: resident mate-rescue batch (ksw_align2 jobs, SURVEY.md §8(f) row 2); "
+                         "global: resident ksw_global2 + CIGAR batch (SURVEY.md §8(f) row 4)")
     ap.add_argument("--jobs", type=int, default=1_000_000, help="mate: jobs per GPU")
     ap.add_argument("--reads", type=int, default=1_000_000, help="c4: reads per GPU per step")
     ap.add_argument("--ref-mb", type=int, default=64, help="c4: random reference size (Mb)")
@@ -155,6 +156,8 @@ def main():
         return main_c4(args, rank, local, world)
     if args.workload == "mate":
         return main_mate(args, rank, local, world)
+    if args.workload == "global":
+        return main_global(args, rank, local, world)
 
     cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
     t0 = time.perf_counter()
@@ -375,6 +378,87 @@ def main_mate(args, rank, local, world):
                       f"loops over the SIMD lanes), {cores} threads",
             "outputs_identical_to_gpu": bool(all(np.array_equal(want[f], aln[:S][f])
                                                  for f in bsw.KSWR_DTYPE.names)),
+        }
+    out["synth_gen_s"] = round(gen_s, 2)
+    print(json.dumps(out), flush=True)
+
+
+def main_global(args, rank, local, world):
+    """Global alignment + CIGAR batch (include/bsw_global.h): per GPU `--jobs` ksw_global2 jobs as
+    bwa_gen_cigar2 issues them for final alignments -- a 150 bp read vs exactly the reference span
+    it covers (2% substitutions, 0.2% short indels), band w by bwa_gen_cigar2's rule (~35) --
+    resident in HBM.  A step = one bsw_ksw_global2_device over the batch (plan, sort, banded DP
+    with the traceback matrix in HBM, per-lane traceback, CIGARs written to HBM)."""
+    t0 = time.perf_counter()
+    ref = bsw.synth_reference(args.ref_mb * 1_000_000, seed=7)
+    pairs, qer = bsw.synth_globals(ref, args.jobs, base=rank * args.jobs)
+    gen_s = time.perf_counter() - t0
+    stride = 64
+    d_pairs = hiprt.DeviceBuffer.from_array(pairs)
+    d_ref = hiprt.DeviceBuffer.from_array(ref)
+    d_qer = hiprt.DeviceBuffer.from_array(qer)
+    d_cig = hiprt.DeviceBuffer(args.jobs * stride * 4)
+    d_nc = hiprt.DeviceBuffer(args.jobs * 4)
+    eng = bsw.Engine(device=local)
+
+    def step():
+        bsw.ksw_global2_device(eng, d_pairs.ptr, d_ref.ptr, d_qer.ptr, args.jobs, d_cig.ptr, stride, d_nc.ptr)
+        return bsw.global_last_stats(eng)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    t = time.perf_counter()
+    sts = [step() for _ in range(args.steps)]
+    barrier(world)
+    dt = time.perf_counter() - t
+    dt_max = allreduce_max(dt, world)
+    res = np.empty_like(pairs)
+    d_pairs.download(res)
+    cig = np.empty((args.jobs, stride), dtype=np.uint32)
+    d_cig.download(cig)
+    nc = np.empty(args.jobs, dtype=np.int32)
+    d_nc.download(nc)
+    if rank != 0:
+        return
+    st = sts[-1]
+    kms = float(np.mean([x.kernel_ms for x in sts]))
+    value = args.jobs * world * args.steps / dt_max / 1e6
+    out = {
+        "metric": "M global alignments with CIGAR/sec (150 bp read vs its reference span, ksw_global2)",
+        "value": round(value, 3), "unit": "M alignments/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int16", "data": "synthetic (bsw_synth.c globals, seed 42)",
+        "config": {"workload": f"global + CIGAR: {args.jobs} jobs/GPU resident in HBM, 150 bp read vs its "
+                               f"reference span, w by bwa_gen_cigar2 (opt->w 100), CIGAR stride {stride}",
+                   "jobs_per_gpu": args.jobs, "parallelism": f"shard{world} (independent jobs)",
+                   "n_lane": st.n_lane, "n_wide": st.n_wide, "n_launches": st.n_launches},
+        "roofline": {"bound": "valu", "achieved": round(st.cells * OPS_PER_CELL / (kms * 1e-3) / 1e12, 3),
+                     "peak": round(VALU_PEAK_TOPS, 1), "unit": "TOP/s",
+                     "frac": round(st.cells * OPS_PER_CELL / (kms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
+                     "traffic": None, "kernel": "glob_lane_kernel<160> (DP + traceback)", "launch_ms": round(kms, 4),
+                     "cells_per_s": round(st.cells / (kms * 1e-3) / 1e12, 4),
+                     "traceback_matrix_GBps": round(st.z_bytes / (kms * 1e-3) / 1e9, 1),
+                     "algorithmic": f"{OPS_PER_CELL} int ops x {st.cells} band cells per step"},
+        "cigar_ops_mean": round(float(np.mean(nc[nc > 0])), 3),
+    }
+    if world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # CPU baseline leg only (test infrastructure)
+        cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        S = min(args.jobs, 200_000)
+        mat = list(bsw.default_params().mat)
+        t = time.perf_counter()
+        ws, wc, wn = oracle.ksw_global2_batch(pairs[:S], ref, qer, mat, stride=stride, nthreads=cores)
+        dt_cpu = time.perf_counter() - t
+        same = bool(np.array_equal(ws, res["score"][:S]) and np.array_equal(wn, nc[:S]) and
+                    all(np.array_equal(wc[i, :wn[i]], cig[i, :wn[i]]) for i in range(0, S, 97) if wn[i] > 0))
+        out["cpu_baseline"] = {
+            "value": round(S / dt_cpu / 1e6, 4), "unit": "M alignments/s", "cores": cores, "kind": "port",
+            "sample": f"first {S} jobs; oracle/ksw_global_ref.c (scalar ksw_global2 restated, as bwa-mem2 "
+                      f"runs it per alignment), {cores} threads",
+            "outputs_identical_to_gpu": same,
         }
     out["synth_gen_s"] = round(gen_s, 2)
     print(json.dumps(out), flush=True)

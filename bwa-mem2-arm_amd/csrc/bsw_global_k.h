@@ -1,0 +1,49 @@
+// bsw_global_k.h -- host-visible launch interface of the global-alignment kernels (bsw_global.hip).
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+#include "../../include/bsw_seqpair.h"
+#include "../../include/bsw_global.h"
+
+namespace bsw {
+
+struct GlobParams {
+    int32_t o_del, e_del, o_ins, e_ins, oe_del, oe_ins;
+    int32_t maxabs;             // max |mat| -- the int16 safety bound of the register kernel
+    uint32_t prof[8][2];        // prof[t] = score bytes mat[t][q], q = 0..4; q = 5..7 score as N
+    int8_t mat[25];
+};
+
+// Job classes: register kernel for qlen <= 32, 64, 96, 128, 160 (int16-safe scores), then the
+// int32 wide kernel (eh row in HBM) for everything else.
+constexpr int kGlobLaneClasses = 5;
+constexpr int kGlobQmax[kGlobLaneClasses] = {32, 64, 96, 128, 160};
+constexpr int kGlobWideClass = kGlobLaneClasses;
+constexpr int kGlobClasses = kGlobLaneClasses + 1;
+// meta words: counts, max tlen, max w, max qlen per class; error flag
+constexpr int kGMetaCount = 0, kGMetaTmax = 8, kGMetaWmax = 16, kGMetaQmax = 24, kGMetaErr = 32;
+constexpr int kGMetaWords = 40;
+constexpr int kGlobKeyBits = 32;
+
+// Traceback-matrix dwords per row of a class's waves (8 nibbles per dword): the row window
+// starting at dword max(i - wmax, 0) >> 3 covers every lane's band [max(i - w, 0), i + w].
+inline int glob_cap_dw(int cls, int qmax, int wmax)
+{
+    const int band = ((2 * wmax) >> 3) + 2;
+    const int full = cls < kGlobLaneClasses ? kGlobQmax[cls] / 8 : (qmax + 7) / 8 + 1;
+    return band < full ? band : full;
+}
+
+// Per job: class + scheduling key (class, w desc, qlen desc, tlen desc); meta per class.
+hipError_t launch_glob_plan(const SeqPair *pairs, int32_t n, const GlobParams &gp, uint32_t *keys,
+                            int32_t *vals, int32_t *meta, hipStream_t s);
+
+// DP + traceback of class cls over jobs order[0, n).  z: traceback matrix, zstride uint32 per
+// wave (>= max tlen * cap_dw * 64), null for scores only; ehs: int32 row scratch of the wide
+// class, (max qlen + 1) * n int2.
+hipError_t launch_glob_class(int cls, const GlobParams &gp, SeqPair *pairs, const int32_t *order, int32_t n,
+                             const uint8_t *ref, const uint8_t *qer, uint32_t *z, int64_t zstride,
+                             int32_t cap_dw, int2 *ehs, uint32_t *cigar, int32_t stride, int32_t *n_cigar,
+                             unsigned long long *cells, hipStream_t s);
+
+}  // namespace bsw

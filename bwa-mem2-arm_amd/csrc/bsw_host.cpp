@@ -30,6 +30,7 @@
 #include "../../include/bsw.h"
 #include "bsw_kernels.h"
 #include "bsw_mate_k.h"
+#include "bsw_global_k.h"
 #include "bsw_internal.h"
 
 namespace bsw {
@@ -138,6 +139,11 @@ struct Slot {
     SeqPair *d_mpairs = nullptr; size_t cap_mpairs = 0;
     bsw_kswr_t *d_maln = nullptr; size_t cap_maln = 0;
     hipEvent_t ev2 = nullptr, ev3 = nullptr;
+    // global alignment (bsw_global.h)
+    uint32_t *d_gz = nullptr; size_t cap_gz = 0;
+    int32_t *d_gmeta = nullptr, *h_gmeta = nullptr;
+    uint32_t *d_gcig = nullptr; size_t cap_gcig = 0;
+    int32_t *d_gncig = nullptr; size_t cap_gncig = 0;
     bool timed = false;
     bsw_stats_t stats{};
 };
@@ -182,6 +188,8 @@ struct DeviceCtx {
         (void)hipFree(s->d_mjobs); (void)hipFree(s->d_mrows); (void)hipFree(s->d_mmeta);
         (void)hipFree(s->d_mcells); (void)hipFree(s->d_mpairs); (void)hipFree(s->d_maln);
         if (s->h_mmeta) (void)hipHostFree(s->h_mmeta);
+        (void)hipFree(s->d_gz); (void)hipFree(s->d_gmeta); (void)hipFree(s->d_gcig); (void)hipFree(s->d_gncig);
+        if (s->h_gmeta) (void)hipHostFree(s->h_gmeta);
         if (s->ev2) (void)hipEventDestroy(s->ev2);
         if (s->ev3) (void)hipEventDestroy(s->ev3);
         if (s->h_meta) (void)hipHostFree(s->h_meta);
@@ -228,6 +236,7 @@ struct bsw_ctx {
     bsw_stats_t last{};
     bsw_ext_stats_t ext_last{};
     bsw_mate_stats_t mate_last{};
+    bsw_global_stats_t glob_last{};
     struct Pinned { std::mutex mu; void *p = nullptr; size_t cap = 0; } pin[2];
     ~bsw_ctx()
     {
@@ -276,22 +285,29 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.route8 = (pk_on || pc_off) ? 1 : 2;
 }
 
+// keys / keys2 / vals / order (radix-sort buffers) grow together
+static hipError_t grow_sort(Slot &s, int32_t n)
+{
+    if ((size_t)n <= s.cap_sort) return hipSuccess;
+    (void)hipFree(s.d_keys); (void)hipFree(s.d_keys2); (void)hipFree(s.d_vals); (void)hipFree(s.d_order);
+    s.d_keys = s.d_keys2 = nullptr; s.d_vals = s.d_order = nullptr; s.cap_sort = 0;
+    const size_t cap = std::max((size_t)n, (size_t)1024);
+    hipError_t e;
+    if ((e = hipMalloc((void **)&s.d_keys, cap * sizeof(uint32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc((void **)&s.d_keys2, cap * sizeof(uint32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc((void **)&s.d_vals, cap * sizeof(int32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc((void **)&s.d_order, cap * sizeof(int32_t))) != hipSuccess) return e;
+    s.cap_sort = cap;
+    return hipSuccess;
+}
+
 // The device pipeline on one slot's device; d_* are device pointers valid on `stream`.
 static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_t *d_ref,
                       const uint8_t *d_qer, int32_t n, int32_t w, int cell_bits, hipStream_t stream)
 {
     s.stats = bsw_stats_t{};
     if (n == 0) return BSW_OK;
-    if ((size_t)n > s.cap_sort) {           // keys / keys2 / vals / order grow together
-        (void)hipFree(s.d_keys); (void)hipFree(s.d_keys2); (void)hipFree(s.d_vals); (void)hipFree(s.d_order);
-        s.d_keys = s.d_keys2 = nullptr; s.d_vals = s.d_order = nullptr; s.cap_sort = 0;
-        const size_t cap = std::max((size_t)n, (size_t)1024);
-        BSW_TRY(hipMalloc((void **)&s.d_keys, cap * sizeof(uint32_t)));
-        BSW_TRY(hipMalloc((void **)&s.d_keys2, cap * sizeof(uint32_t)));
-        BSW_TRY(hipMalloc((void **)&s.d_vals, cap * sizeof(int32_t)));
-        BSW_TRY(hipMalloc((void **)&s.d_order, cap * sizeof(int32_t)));
-        s.cap_sort = cap;
-    }
+    BSW_TRY(grow_sort(s, n));
     BSW_TRY(hipMemsetAsync(s.d_meta, 0, kMetaWords * sizeof(int32_t), stream));
     int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaCounts, *d_err = s.d_meta + kMetaCounts + 1;
     // pairs in the 8-bit score regime (h0 + min(qlen, tlen) <= 255, bwa-style scoring) take the
@@ -479,6 +495,90 @@ static int mate_device(const MateParams &mp, Slot &s, const SeqPair *d_pairs, co
     BSW_TRY(hipEventElapsedTime(&stats->fwd_ms, s.ev0, s.ev1));
     BSW_TRY(hipEventElapsedTime(&stats->rev_ms, s.ev2, s.ev3));
     stats->cells_fwd = (int64_t)cells;
+    return BSW_OK;
+}
+
+// ---------------------------------------------------------------- global alignment (bsw_global.h)
+static void make_glob_params(const bsw_params_t &p, GlobParams &gp)
+{
+    memset(&gp, 0, sizeof(gp));
+    gp.o_del = p.o_del; gp.e_del = p.e_del; gp.o_ins = p.o_ins; gp.e_ins = p.e_ins;
+    gp.oe_del = p.o_del + p.e_del; gp.oe_ins = p.o_ins + p.e_ins;
+    int mx = 0;
+    for (int i = 0; i < 25; ++i) mx = std::max(mx, std::abs((int)p.mat[i]));
+    gp.maxabs = mx;
+    memcpy(gp.mat, p.mat, 25);
+    for (int t = 0; t < 8; ++t) {                        // codes > 4 score as N (as prof in KParams)
+        const int tt = std::min(t, 4);
+        uint8_t b[8];
+        for (int q = 0; q < 8; ++q) b[q] = (uint8_t)p.mat[tt * 5 + std::min(q, 4)];
+        gp.prof[t][0] = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+        gp.prof[t][1] = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+    }
+}
+
+constexpr int64_t kGlobZCapWords = (int64_t)2 << 30;     // traceback matrix per launch <= 8 GB
+
+// plan -> sort (class, w, qlen, tlen) -> one readback of the class statistics -> per class the
+// DP + traceback kernel over its slice of order[] (chunked so the matrix stays under the cap).
+static int glob_device(const GlobParams &gp, Slot &s, SeqPair *d_pairs, const uint8_t *d_ref,
+                       const uint8_t *d_qer, int32_t n, uint32_t *d_cigar, int32_t stride, int32_t *d_ncig,
+                       hipStream_t st, bsw_global_stats_t *stats)
+{
+    *stats = bsw_global_stats_t{};
+    stats->n_jobs = n;
+    if (n == 0) return BSW_OK;
+    BSW_TRY(grow_sort(s, n));
+    if (!s.d_gmeta) BSW_TRY(hipMalloc((void **)&s.d_gmeta, kGMetaWords * sizeof(int32_t)));
+    if (!s.h_gmeta) BSW_TRY(hipHostMalloc((void **)&s.h_gmeta, kGMetaWords * sizeof(int32_t), 0));
+    if (!s.d_mcells) BSW_TRY(hipMalloc((void **)&s.d_mcells, sizeof(unsigned long long)));
+    BSW_TRY(launch_glob_plan(d_pairs, n, gp, s.d_keys, s.d_vals, s.d_gmeta, st));
+    size_t tmp_bytes = 0;
+    BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals, s.d_order, n,
+                                               0, kGlobKeyBits, st));
+    BSW_TRY(grow(s.d_tmp, s.cap_tmp, tmp_bytes));
+    BSW_TRY(hipcub::DeviceRadixSort::SortPairs(s.d_tmp, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals, s.d_order, n,
+                                               0, kGlobKeyBits, st));
+    BSW_TRY(hipMemcpyAsync(s.h_gmeta, s.d_gmeta, kGMetaWords * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    BSW_TRY(hipMemsetAsync(s.d_mcells, 0, sizeof(unsigned long long), st));
+    BSW_TRY(hipStreamSynchronize(st));
+    int32_t m[kGMetaWords];
+    memcpy(m, s.h_gmeta, sizeof(m));
+    if (m[kGMetaErr]) return BSW_E_RANGE;
+    const bool want = d_cigar && stride > 0;
+    BSW_TRY(hipEventRecord(s.ev0, st));
+    int32_t off = 0;
+    for (int c = 0; c < kGlobClasses; ++c) {
+        const int32_t cnt = m[kGMetaCount + c];
+        if (cnt <= 0) continue;
+        const int tm = m[kGMetaTmax + c], wm = m[kGMetaWmax + c], qm = m[kGMetaQmax + c];
+        const int cap_dw = glob_cap_dw(c, qm, wm);
+        const int64_t zstride = (int64_t)std::max(tm, 1) * cap_dw * 64;
+        int32_t chunk = cnt;
+        if (want) {
+            const int64_t waves = std::max<int64_t>(1, kGlobZCapWords / zstride);
+            chunk = (int32_t)std::min<int64_t>(cnt, waves * 64);
+            BSW_TRY(grow(s.d_gz, s.cap_gz, (size_t)((chunk + 63) / 64) * (size_t)zstride));
+        }
+        if (c == kGlobWideClass) BSW_TRY(grow(s.d_scratch, s.cap_scratch, (size_t)(qm + 1) * (size_t)chunk));
+        for (int32_t a = 0; a < cnt; a += chunk) {
+            const int32_t b = std::min(cnt, a + chunk);
+            BSW_TRY(launch_glob_class(c, gp, d_pairs, s.d_order + off + a, b - a, d_ref, d_qer,
+                                      want ? s.d_gz : nullptr, zstride, cap_dw, s.d_scratch, d_cigar, stride,
+                                      d_ncig, s.d_mcells, st));
+            stats->n_launches++;
+            if (want) stats->z_bytes += (int64_t)((b - a + 63) / 64) * zstride * 4;
+        }
+        if (c == kGlobWideClass) stats->n_wide += cnt;
+        else stats->n_lane += cnt;
+        off += cnt;
+    }
+    BSW_TRY(hipEventRecord(s.ev1, st));
+    unsigned long long cells = 0;
+    BSW_TRY(hipMemcpyAsync(&cells, s.d_mcells, sizeof(cells), hipMemcpyDeviceToHost, st));
+    BSW_TRY(hipStreamSynchronize(st));
+    BSW_TRY(hipEventElapsedTime(&stats->kernel_ms, s.ev0, s.ev1));
+    stats->cells = (int64_t)cells;
     return BSW_OK;
 }
 
@@ -737,6 +837,100 @@ int bsw_mate_last_stats(bsw_ctx_t *ctx, bsw_mate_stats_t *out)
     if (!ctx || !out) return BSW_E_INVAL;
     std::lock_guard<std::mutex> g(ctx->stats_mu);
     *out = ctx->mate_last;
+    return BSW_OK;
+}
+
+int bsw_ksw_global2_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref, const uint8_t *d_qer,
+                           int32_t n, uint32_t *d_cigar, int32_t cigar_stride, int32_t *d_n_cigar,
+                           void *stream)
+{
+    if (!ctx || n < 0 || cigar_stride < 0 || (n > 0 && (!d_pairs || !d_ref || !d_qer)) ||
+        (n > 0 && cigar_stride > 0 && (!d_cigar || !d_n_cigar)))
+        return BSW_E_INVAL;
+    if (n == 0) return BSW_OK;
+    bsw::GlobParams gp;
+    bsw::make_glob_params(ctx->params, gp);
+    bsw::DeviceCtx &dc = *ctx->devs[0];
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        hipStream_t st = stream ? (hipStream_t)stream : slot->stream;
+        bsw_global_stats_t gs;
+        const int r = bsw::glob_device(gp, *slot, d_pairs, d_ref, d_qer, n, cigar_stride > 0 ? d_cigar : nullptr,
+                                       cigar_stride, d_n_cigar, st, &gs);
+        if (r) return r;
+        std::lock_guard<std::mutex> g(ctx->stats_mu);
+        ctx->glob_last = gs;
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+
+int bsw_ksw_global2(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef, const uint8_t *seqBufQer,
+                    int32_t n, uint32_t *cigar, int32_t cigar_stride, int32_t *n_cigar)
+{
+    if (!ctx || n < 0 || cigar_stride < 0 || (n > 0 && (!pairs || !seqBufRef || !seqBufQer)) ||
+        (n > 0 && cigar_stride > 0 && (!cigar || !n_cigar)))
+        return BSW_E_INVAL;
+    if (n == 0) return BSW_OK;
+    for (int32_t i = 0; i < n; ++i)
+        if (pairs[i].len1 < 0 || pairs[i].len2 < 0 || pairs[i].len1 > BSW_MAX_LEN || pairs[i].len2 > BSW_MAX_LEN ||
+            pairs[i].idr < 0 || pairs[i].idq < 0 || pairs[i].h0 < 0)
+            return BSW_E_RANGE;
+    bsw::GlobParams gp;
+    bsw::make_glob_params(ctx->params, gp);
+    bsw::DeviceCtx &dc = *ctx->devs[0];
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    bsw::Slot &s = *slot;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            const SeqPair &p = pairs[i];
+            if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
+            if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
+        }
+        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+        const bool want = cigar_stride > 0;
+        BSW_TRY(bsw::grow(s.d_pairs, s.cap_pairs, (size_t)n));
+        BSW_TRY(bsw::grow(s.d_ref, s.cap_ref, (size_t)(r_hi - r_lo) + 1));
+        BSW_TRY(bsw::grow(s.d_qer, s.cap_qer, (size_t)(q_hi - q_lo) + 1));
+        if (want) {
+            BSW_TRY(bsw::grow(s.d_gcig, s.cap_gcig, (size_t)n * (size_t)cigar_stride));
+            BSW_TRY(bsw::grow(s.d_gncig, s.cap_gncig, (size_t)n));
+        }
+        BSW_TRY(hipMemcpyAsync(s.d_pairs, pairs, (size_t)n * sizeof(SeqPair), hipMemcpyHostToDevice, s.stream));
+        if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, seqBufRef + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
+        if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, seqBufQer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
+        bsw_global_stats_t gs;
+        int r = bsw::glob_device(gp, s, s.d_pairs, s.d_ref - r_lo, s.d_qer - q_lo, n, want ? s.d_gcig : nullptr,
+                                 cigar_stride, want ? s.d_gncig : nullptr, s.stream, &gs);
+        if (r) return r;
+        BSW_TRY(hipMemcpyAsync(pairs, s.d_pairs, (size_t)n * sizeof(SeqPair), hipMemcpyDeviceToHost, s.stream));
+        if (want) {
+            BSW_TRY(hipMemcpyAsync(cigar, s.d_gcig, (size_t)n * cigar_stride * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+            BSW_TRY(hipMemcpyAsync(n_cigar, s.d_gncig, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
+        }
+        BSW_TRY(hipStreamSynchronize(s.stream));
+        std::lock_guard<std::mutex> g(ctx->stats_mu);
+        ctx->glob_last = gs;
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+
+int bsw_global_last_stats(bsw_ctx_t *ctx, bsw_global_stats_t *out)
+{
+    if (!ctx || !out) return BSW_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    *out = ctx->glob_last;
     return BSW_OK;
 }
 

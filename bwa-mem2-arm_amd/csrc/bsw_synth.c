@@ -276,3 +276,79 @@ int32_t bsw_synth_mates(const bsw_mates_cfg *c, const uint8_t *ref, int64_t ref_
     }
     return ntrue;
 }
+
+/* ---------------------------------------------------------------- global (CIGAR) jobs
+ * Jobs shaped like bwa_gen_cigar2's ksw_global2 calls (mem_reg2aln, src/bwa.cpp;
+ * include/bsw_global.h): a read of read_len bases sampled from the reference with
+ * substitutions / short indels, against exactly the reference span it covers (rb..re), band w
+ * by bwa_gen_cigar2's rule with opt->w = w_cap.  pairs[k]: idr = span start in ref (seqBufRef =
+ * the reference), idq = k * read_len in qer, len1 = span length, len2 = read_len, h0 = w. */
+typedef struct bsw_globals_cfg {
+    uint64_t seed;
+    int32_t read_len, w_cap;     /* 150, opt->w = 100                                    */
+    int32_t a, o_del, e_del, o_ins, e_ins;   /* bwa defaults 1, 6, 1, 6, 1               */
+    double p_sub, p_indel;       /* read edit rates (0.02, 0.002)                        */
+} bsw_globals_cfg;
+
+void bsw_globals_default(bsw_globals_cfg *c)
+{
+    c->seed = 42;
+    c->read_len = 150;
+    c->w_cap = 100;
+    c->a = 1;
+    c->o_del = c->o_ins = 6;
+    c->e_del = c->e_ins = 1;
+    c->p_sub = 0.02;
+    c->p_indel = 0.002;
+}
+
+static int32_t gen_cigar_band(int l_query, int rlen, int w_, int a, int o_del, int e_del, int o_ins, int e_ins)
+{
+    int max_ins = (int)((double)(((l_query + 1) >> 1) * a - o_ins) / e_ins + 1.);
+    int max_del = (int)((double)(((l_query + 1) >> 1) * a - o_del) / e_del + 1.);
+    int max_gap = max_ins > max_del ? max_ins : max_del;
+    int d = rlen > l_query ? rlen - l_query : l_query - rlen;
+    max_gap = max_gap > 1 ? max_gap : 1;
+    int w = (max_gap + d + 1) >> 1;
+    w = w < w_ ? w : w_;
+    return w > d + 3 ? w : d + 3;
+}
+
+int32_t bsw_synth_globals(const bsw_globals_cfg *c, const uint8_t *ref, int64_t ref_len, int64_t base, int32_t n,
+                          SeqPair *pairs, uint8_t *qer)
+{
+    const int32_t L = c->read_len;
+    if (L <= 0 || ref_len < 4 * (int64_t)L + 64) return -1;
+    for (int32_t k = 0; k < n; ++k) {
+        const int64_t gi = base + k;
+        uint64_t s = c->seed * 0x8EBC6AF09C88C6E3ull ^ ((uint64_t)gi * 0x589965CC75374CC3ull) ^ 0x5555;
+        splitmix64(&s);
+        const int64_t org = (int64_t)(u01(&s) * (double)(ref_len - 3 * L - 64));
+        uint8_t *q = qer + (int64_t)k * L;
+        int64_t i = org;
+        int32_t j = 0;
+        while (j < L) {
+            if (j > 0 && j < L - 4 && u01(&s) < c->p_indel) {       /* no indel at the read ends */
+                const int32_t l = 1 + (int32_t)below(&s, 3);
+                if (splitmix64(&s) & 1) {
+                    for (int32_t t = 0; t < l && j < L - 1; ++t) q[j++] = (uint8_t)below(&s, 4);
+                } else {
+                    i += l;
+                }
+                continue;
+            }
+            uint8_t b = ref[i++];
+            if (u01(&s) < c->p_sub) b = (uint8_t)((b < 4 ? b : 0) + 1 + below(&s, 3)) & 3;
+            q[j++] = b;
+        }
+        SeqPair *p = &pairs[k];
+        memset(p, 0, sizeof(*p));
+        p->idr = (int32_t)org;
+        p->idq = (int32_t)((int64_t)k * L);
+        p->id = (int32_t)gi;
+        p->len1 = (int32_t)(i - org);
+        p->len2 = L;
+        p->h0 = gen_cigar_band(L, p->len1, c->w_cap, c->a, c->o_del, c->e_del, c->o_ins, c->e_ins);
+    }
+    return 0;
+}

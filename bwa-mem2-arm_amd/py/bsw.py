@@ -30,7 +30,8 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
                "bsw_get_scores_device", "bsw_last_stats", "bsw_strerror", "bsw_abi_version",
                "bsw_ext_opt_default", "bsw_extend_seeds", "bsw_ext_last_stats",
                "bswb_write", "bswb_read_header", "bswb_read",
-               "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats")
+               "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats",
+               "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats")
 
 # include/bsw_ext.h structs
 SEED_DTYPE = np.dtype([("rbeg", np.int64), ("qbeg", np.int32), ("len", np.int32)])
@@ -108,10 +109,13 @@ def hip_lib():
         L.bsw_ksw_align2.argtypes = [P, P, P, P, ctypes.c_int32, P]
         L.bsw_ksw_align2_device.argtypes = [P, P, P, P, ctypes.c_int32, P, P]
         L.bsw_mate_last_stats.argtypes = [P, P]
+        L.bsw_ksw_global2.argtypes = [P, P, P, P, ctypes.c_int32, P, ctypes.c_int32, P]
+        L.bsw_ksw_global2_device.argtypes = [P, P, P, P, ctypes.c_int32, P, ctypes.c_int32, P, P]
+        L.bsw_global_last_stats.argtypes = [P, P]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
-                  "bsw_mate_last_stats"):
+                  "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -268,6 +272,41 @@ def mate_last_stats(engine) -> MateStats:
     return s
 
 
+class GlobalStats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_float), ("n_jobs", ctypes.c_int32), ("n_lane", ctypes.c_int32),
+                ("n_wide", ctypes.c_int32), ("n_launches", ctypes.c_int32), ("cells", ctypes.c_int64),
+                ("z_bytes", ctypes.c_int64)]
+
+
+def ksw_global2(engine, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray, stride: int = 64):
+    """bsw_ksw_global2 (include/bsw_global.h): per SeqPair (len1 = target, len2 = query, h0 = w)
+    upstream ksw_global2 -> (score, cigar[n, stride] uint32 or None, n_cigar); scores are also
+    written into pairs['score']."""
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    qer = np.ascontiguousarray(qer, dtype=np.uint8)
+    n = len(pairs)
+    cig = np.zeros((n, stride), dtype=np.uint32) if stride > 0 else None
+    ncig = np.zeros(n, dtype=np.int32)
+    _check(hip_lib().bsw_ksw_global2(engine._ctx, _ptr(pairs), _ptr(ref), _ptr(qer), n,
+                                     _ptr(cig) if cig is not None else None, stride, _ptr(ncig)))
+    return pairs["score"].copy(), cig, ncig
+
+
+def ksw_global2_device(engine, d_pairs: int, d_ref: int, d_qer: int, n: int, d_cigar: int, stride: int,
+                       d_ncig: int, stream: int = 0):
+    _check(hip_lib().bsw_ksw_global2_device(engine._ctx, ctypes.c_void_p(d_pairs), ctypes.c_void_p(d_ref),
+                                            ctypes.c_void_p(d_qer), n, ctypes.c_void_p(d_cigar or None),
+                                            stride, ctypes.c_void_p(d_ncig or None),
+                                            ctypes.c_void_p(stream or None)))
+
+
+def global_last_stats(engine) -> GlobalStats:
+    s = GlobalStats()
+    _check(hip_lib().bsw_global_last_stats(engine._ctx, ctypes.byref(s)))
+    return s
+
+
 # ---------------------------------------------------------------- synthetic batches
 class SynthCfg(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("tlen", ctypes.c_int32), ("qlen", ctypes.c_int32),
@@ -297,6 +336,10 @@ def synth_lib():
         L.bsw_synth_mates.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
         L.bsw_synth_mates.restype = ctypes.c_int32
+        L.bsw_globals_default.argtypes = [ctypes.c_void_p]
+        L.bsw_synth_globals.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
+        L.bsw_synth_globals.restype = ctypes.c_int32
         _synth = L
     return _synth
 
@@ -378,4 +421,31 @@ def synth_mates(ref: np.ndarray, n: int, base: int = 0, cfg: MatesCfg | None = N
     r = synth_lib().bsw_synth_mates(ctypes.byref(cfg), _ptr(ref), len(ref), base, n, _ptr(pairs), _ptr(qer))
     if r < 0:
         raise BswError("bsw_synth_mates: reference too short for the window")
+    return pairs, qer
+
+
+class GlobalsCfg(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("read_len", ctypes.c_int32), ("w_cap", ctypes.c_int32),
+                ("a", ctypes.c_int32), ("o_del", ctypes.c_int32), ("e_del", ctypes.c_int32),
+                ("o_ins", ctypes.c_int32), ("e_ins", ctypes.c_int32), ("p_sub", ctypes.c_double),
+                ("p_indel", ctypes.c_double)]
+
+
+def globals_cfg(**kw) -> GlobalsCfg:
+    c = GlobalsCfg()
+    synth_lib().bsw_globals_default(ctypes.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def synth_globals(ref: np.ndarray, n: int, base: int = 0, cfg: GlobalsCfg | None = None):
+    """ksw_global2 jobs shaped like bwa_gen_cigar2's (bsw_synth_globals): (pairs, qer); seqBufRef
+    is ref itself, h0 = the band w."""
+    cfg = cfg if cfg is not None else globals_cfg()
+    pairs = np.zeros(n, dtype=SEQPAIR_DTYPE)
+    qer = np.zeros(max(1, n * cfg.read_len), dtype=np.uint8)
+    r = synth_lib().bsw_synth_globals(ctypes.byref(cfg), _ptr(ref), len(ref), base, n, _ptr(pairs), _ptr(qer))
+    if r < 0:
+        raise BswError("bsw_synth_globals: reference too short for the read length")
     return pairs, qer

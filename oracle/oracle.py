@@ -150,3 +150,43 @@ def ksw_align2_batch(pairs, ref, qer, mat, o_del=6, e_del=1, o_ins=6, e_ins=1, n
     L.oracle_ksw_align2_batch(_ptr(pairs), _ptr(ref), _ptr(qer), len(pairs), _ptr(m), o_del, e_del, o_ins,
                               e_ins, _ptr(out), nthreads)
     return out
+
+
+def ksw_global2(query, target, mat, o_del, e_del, o_ins, e_ins, w):
+    """oracle/ksw_global_ref.c: literal ksw_global2 (one pair) -> (score, [(op, len), ...])."""
+    L = lib()
+    P = ctypes.c_void_p
+    L.oracle_ksw_global2.restype = ctypes.c_int
+    L.oracle_ksw_global2.argtypes = [ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P] + \
+        [ctypes.c_int] * 5 + [P, P]
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    t = np.ascontiguousarray(target, dtype=np.uint8)
+    m = np.ascontiguousarray(mat, dtype=np.int8)
+    nc = ctypes.c_int(0)
+    cg = ctypes.POINTER(ctypes.c_uint32)()
+    sc = L.oracle_ksw_global2(len(q), _ptr(q), len(t), _ptr(t), 5, _ptr(m), o_del, e_del, o_ins, e_ins,
+                              w, ctypes.byref(nc), ctypes.byref(cg))
+    ops = [(cg[k] & 0xf, cg[k] >> 4) for k in range(nc.value)]
+    if cg:
+        ctypes.CDLL(None).free(cg)
+    return sc, ops
+
+
+def ksw_global2_batch(pairs, ref, qer, mat, o_del=6, e_del=1, o_ins=6, e_ins=1, stride=64, nthreads=1):
+    """Batch over SeqPairs (len1 = target, len2 = query, h0 = w) -> (score, cigar[n, stride],
+    n_cigar) with n_cigar -1 (more than `stride` ops) / -2 (qlen < tlen - w, undefined);
+    stride 0: scores only (cigar None, n_cigar zeros)."""
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    L = lib()
+    P = ctypes.c_void_p
+    L.oracle_ksw_global2_batch.argtypes = [P, P, P, ctypes.c_int, P] + [ctypes.c_int] * 4 + \
+        [P, P, ctypes.c_int, P, ctypes.c_int]
+    m = np.ascontiguousarray(mat, dtype=np.int8)
+    n = len(pairs)
+    score = np.zeros(n, dtype=np.int32)
+    ncig = np.zeros(n, dtype=np.int32)
+    cig = np.zeros((n, stride), dtype=np.uint32) if stride > 0 else None
+    L.oracle_ksw_global2_batch(_ptr(pairs), _ptr(ref), _ptr(qer), n, _ptr(m), o_del, e_del, o_ins, e_ins,
+                               _ptr(score), _ptr(cig) if cig is not None else None, stride, _ptr(ncig),
+                               nthreads)
+    return score, cig, ncig
