@@ -31,6 +31,8 @@
 #include "bsw_kernels.h"
 #include "bsw_mate_k.h"
 #include "bsw_global_k.h"
+#include "bsw_ext_k.h"
+#include <chrono>
 #include "bsw_internal.h"
 
 namespace bsw {
@@ -144,6 +146,10 @@ struct Slot {
     int32_t *d_gmeta = nullptr, *h_gmeta = nullptr;
     uint32_t *d_gcig = nullptr; size_t cap_gcig = 0;
     int32_t *d_gncig = nullptr; size_t cap_gncig = 0;
+    // device extension pipeline (bsw_ext_dev.hip)
+    SeqPair *d_xpairs = nullptr, *d_xsub = nullptr; size_t cap_xpairs = 0, cap_xsub = 0;
+    uint8_t *d_xq = nullptr, *d_xt = nullptr; size_t cap_xq = 0, cap_xt = 0;
+    ExtState *d_xst = nullptr; size_t cap_xst = 0;
     bool timed = false;
     bsw_stats_t stats{};
 };
@@ -174,10 +180,13 @@ struct DeviceCtx {
     int device = 0;
     std::mutex mu;
     std::vector<std::unique_ptr<Slot>> free_slots;
+    uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
+    int64_t refres_len = -1;
 
     ~DeviceCtx()
     {
         for (auto &s : free_slots) release_slot(s.get());
+        if (d_refres) { (void)hipSetDevice(device); (void)hipFree(d_refres); }
     }
     static void release_slot(Slot *s)
     {
@@ -190,6 +199,8 @@ struct DeviceCtx {
         if (s->h_mmeta) (void)hipHostFree(s->h_mmeta);
         (void)hipFree(s->d_gz); (void)hipFree(s->d_gmeta); (void)hipFree(s->d_gcig); (void)hipFree(s->d_gncig);
         if (s->h_gmeta) (void)hipHostFree(s->h_gmeta);
+        (void)hipFree(s->d_xpairs); (void)hipFree(s->d_xsub); (void)hipFree(s->d_xq); (void)hipFree(s->d_xt);
+        (void)hipFree(s->d_xst);
         if (s->ev2) (void)hipEventDestroy(s->ev2);
         if (s->ev3) (void)hipEventDestroy(s->ev3);
         if (s->h_meta) (void)hipHostFree(s->h_meta);
@@ -582,6 +593,40 @@ static int glob_device(const GlobParams &gp, Slot &s, SeqPair *d_pairs, const ui
     return BSW_OK;
 }
 
+// ---------------------------------------------------------------- device extension pipeline
+// One side of bsw_extend_seeds on the GPU: build (sparse job per read) -> engine -> band retries
+// -> interpretation.  Every step on `st`; the only host syncs are the engine's class-count
+// readback and one retry count per retry round.
+static int ext_side_device(const KParams &kp0, Slot &s, const ExtDevParams &xp, int left, const bsw_ext_opt_t &opt,
+                           const uint8_t *d_reads, const int64_t *d_off, const int32_t *d_len,
+                           const bsw_seed_t *d_seeds, int32_t n, const uint8_t *d_ref, bsw_alnreg_t *d_out,
+                           int32_t *d_cnt, hipStream_t st, bsw_ext_stats_t &es)
+{
+    KParams kp = kp0;
+    kp.end_bonus = left ? opt.pen_clip5 : opt.pen_clip3;
+    BSW_TRY(launch_ext_build(left, xp, d_reads, d_off, d_len, d_seeds, n, d_ref, s.d_xst, s.d_xpairs, s.d_xq,
+                             s.d_xt, d_out, st));
+    int r = run_device(kp, s, s.d_xpairs, s.d_xt, s.d_xq, n, opt.w, 16, st);
+    if (r) return r;
+    if ((r = finish_stats(s))) return r;
+    es.kernel_ms += s.stats.kernel_ms;
+    for (int t = 1; t < opt.max_band_try; ++t) {
+        const int32_t wt = opt.w << (t - 1), wn = opt.w << t;
+        BSW_TRY(launch_ext_retry_mark(t == 1 ? s.d_xpairs : s.d_xsub, s.d_xsub, s.d_xst, n, wt, d_cnt, st));
+        int32_t cnt = 0;
+        BSW_TRY(hipMemcpyAsync(&cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
+        BSW_TRY(hipStreamSynchronize(st));
+        if (cnt == 0) break;
+        es.n_pairs[(left ? 0 : 2) + 1] += cnt;
+        if ((r = run_device(kp, s, s.d_xsub, s.d_xt, s.d_xq, n, wn, 16, st))) return r;
+        if ((r = finish_stats(s))) return r;
+        es.kernel_ms += s.stats.kernel_ms;
+        BSW_TRY(launch_ext_retry_merge(s.d_xpairs, s.d_xsub, s.d_xst, n, wn, left, st));
+    }
+    BSW_TRY(launch_ext_interp(left, xp, d_len, d_seeds, n, s.d_xpairs, s.d_xst, d_out, st));
+    return BSW_OK;
+}
+
 }  // namespace bsw
 
 // ====================================================================== C ABI
@@ -931,6 +976,85 @@ int bsw_global_last_stats(bsw_ctx_t *ctx, bsw_global_stats_t *out)
     if (!ctx || !out) return BSW_E_INVAL;
     std::lock_guard<std::mutex> g(ctx->stats_mu);
     *out = ctx->glob_last;
+    return BSW_OK;
+}
+
+int bsw_set_reference(bsw_ctx_t *ctx, const uint8_t *ref, int64_t ref_len)
+{
+    if (!ctx || ref_len < 0 || (ref_len > 0 && !ref)) return BSW_E_INVAL;
+    for (auto &dcp : ctx->devs) {
+        bsw::DeviceCtx &dc = *dcp;
+        std::lock_guard<std::mutex> g(dc.mu);
+        BSW_TRY(hipSetDevice(dc.device));
+        if (dc.d_refres) (void)hipFree(dc.d_refres);
+        dc.d_refres = nullptr;
+        dc.refres_len = -1;
+        BSW_TRY(hipMalloc((void **)&dc.d_refres, (size_t)ref_len + 64));
+        if (ref_len > 0) BSW_TRY(hipMemcpy(dc.d_refres, ref, (size_t)ref_len, hipMemcpyHostToDevice));
+        dc.refres_len = ref_len;
+    }
+    return BSW_OK;
+}
+
+int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
+                            const int64_t *d_read_off, const int32_t *d_read_len, const bsw_seed_t *d_seeds,
+                            int32_t n, bsw_alnreg_t *d_out, void *stream)
+{
+    if (!ctx || !opt || n < 0 || (n > 0 && (!d_reads || !d_read_off || !d_read_len || !d_seeds || !d_out)))
+        return BSW_E_INVAL;
+    if (opt->w < 0 || opt->max_band_try < 1) return BSW_E_INVAL;
+    bsw::DeviceCtx &dc = *ctx->devs[0];
+    if (!dc.d_refres) return BSW_E_INVAL;
+    if (n == 0) return BSW_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    bsw::Slot &s = *slot;
+    bsw_ext_stats_t es{};
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        hipStream_t st = stream ? (hipStream_t)stream : s.stream;
+        const bsw_params_t &p = ctx->params;
+        // scan: max read length, input errors, job counts
+        BSW_TRY(bsw::launch_ext_scan(d_read_len, d_seeds, n, dc.refres_len, s.d_meta, st));
+        int32_t m[4];
+        BSW_TRY(hipMemcpyAsync(m, s.d_meta, sizeof(m), hipMemcpyDeviceToHost, st));
+        BSW_TRY(hipStreamSynchronize(st));
+        if (m[1]) return BSW_E_RANGE;
+        es.n_pairs[0] = m[2];
+        es.n_pairs[2] = m[3];
+        bsw::ExtDevParams xp{};
+        xp.w = opt->w; xp.pen_clip5 = opt->pen_clip5; xp.pen_clip3 = opt->pen_clip3; xp.a = p.mat[0];
+        xp.o_del = p.o_del; xp.e_del = p.e_del; xp.o_ins = p.o_ins; xp.e_ins = p.e_ins;
+        xp.qstride = std::max(m[0], 1);
+        xp.tstride = m[0] + 2 * opt->w + 1;             // cal_max_gap <= 2w
+        xp.ref_len = dc.refres_len;
+        if ((int64_t)xp.tstride > BSW_MAX_LEN) return BSW_E_RANGE;
+        // SeqPair idr / idq are int32: chunk so i * tstride stays below 2^31
+        const int32_t chunk = (int32_t)std::min<int64_t>(n, (int64_t)INT32_MAX / xp.tstride - 1);
+        BSW_TRY(bsw::grow(s.d_xpairs, s.cap_xpairs, (size_t)chunk));
+        BSW_TRY(bsw::grow(s.d_xsub, s.cap_xsub, (size_t)chunk));
+        BSW_TRY(bsw::grow(s.d_xst, s.cap_xst, (size_t)chunk));
+        BSW_TRY(bsw::grow(s.d_xq, s.cap_xq, (size_t)chunk * xp.qstride));
+        BSW_TRY(bsw::grow(s.d_xt, s.cap_xt, (size_t)chunk * xp.tstride));
+        if (!s.d_mcells) BSW_TRY(hipMalloc((void **)&s.d_mcells, sizeof(unsigned long long)));
+        int32_t *d_cnt = (int32_t *)s.d_mcells;
+        for (int32_t a = 0; a < n; a += chunk) {
+            const int32_t b = std::min(n, a + chunk);
+            for (int left = 1; left >= 0; --left) {
+                const int r = bsw::ext_side_device(ctx->kp, s, xp, left, *opt, d_reads, d_read_off + a, d_read_len + a,
+                                                   d_seeds + a, b - a, dc.d_refres, d_out + a, d_cnt, st, es);
+                if (r) return r;
+            }
+        }
+        BSW_TRY(hipStreamSynchronize(st));
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    if (rc) return rc;
+    es.engine_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    bsw::set_ext_stats(ctx, es);
     return BSW_OK;
 }
 

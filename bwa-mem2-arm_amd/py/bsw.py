@@ -31,7 +31,8 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
                "bsw_ext_opt_default", "bsw_extend_seeds", "bsw_ext_last_stats",
                "bswb_write", "bswb_read_header", "bswb_read",
                "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats",
-               "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats")
+               "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
+               "bsw_set_reference", "bsw_extend_seeds_device")
 
 # include/bsw_ext.h structs
 SEED_DTYPE = np.dtype([("rbeg", np.int64), ("qbeg", np.int32), ("len", np.int32)])
@@ -112,10 +113,13 @@ def hip_lib():
         L.bsw_ksw_global2.argtypes = [P, P, P, P, ctypes.c_int32, P, ctypes.c_int32, P]
         L.bsw_ksw_global2_device.argtypes = [P, P, P, P, ctypes.c_int32, P, ctypes.c_int32, P, P]
         L.bsw_global_last_stats.argtypes = [P, P]
+        L.bsw_set_reference.argtypes = [P, P, ctypes.c_int64]
+        L.bsw_extend_seeds_device.argtypes = [P, P, P, P, P, P, ctypes.c_int32, P, P]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
-                  "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats"):
+                  "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
+                  "bsw_set_reference", "bsw_extend_seeds_device"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -234,6 +238,34 @@ def extend_seeds(engine, ref, reads, read_off, read_len, seeds, opt: ExtOpt | No
     out = np.zeros(len(seeds), dtype=ALNREG_DTYPE)
     _check(hip_lib().bsw_extend_seeds(engine._ctx, ctypes.byref(opt), _ptr(ref), len(ref), _ptr(reads),
                                       _ptr(read_off), _ptr(read_len), _ptr(seeds), len(seeds), _ptr(out)))
+    return out
+
+
+def set_reference(engine, ref: np.ndarray):
+    """bsw_set_reference: keep ref resident in HBM (for extend_seeds_device)."""
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    _check(hip_lib().bsw_set_reference(engine._ctx, _ptr(ref), len(ref)))
+
+
+def extend_seeds_device(engine, d_reads: int, d_off: int, d_len: int, d_seeds: int, n: int, d_out: int,
+                        opt: ExtOpt | None = None, stream: int = 0):
+    """bsw_extend_seeds_device on raw device pointers (resident reference required)."""
+    opt = opt if opt is not None else ext_opt()
+    V = ctypes.c_void_p
+    _check(hip_lib().bsw_extend_seeds_device(engine._ctx, ctypes.byref(opt), V(d_reads), V(d_off), V(d_len),
+                                             V(d_seeds), n, V(d_out), V(stream or None)))
+
+
+def extend_seeds_resident(engine, reads, read_off, read_len, seeds, opt: ExtOpt | None = None):
+    """Upload reads / seeds, run bsw_extend_seeds_device against the resident reference, download
+    the regions (ALNREG_DTYPE)."""
+    import hiprt
+    bufs = [hiprt.DeviceBuffer.from_array(np.ascontiguousarray(a, dtype=dt)) for a, dt in
+            ((reads, np.uint8), (read_off, np.int64), (read_len, np.int32), (seeds, SEED_DTYPE))]
+    out = np.zeros(len(seeds), dtype=ALNREG_DTYPE)
+    d_out = hiprt.DeviceBuffer(out.nbytes)
+    extend_seeds_device(engine, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, len(seeds), d_out.ptr, opt)
+    d_out.download(out)
     return out
 
 

@@ -66,14 +66,28 @@ int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *re
                      const uint8_t *reads, const int64_t *read_off, const int32_t *read_len,
                      const bsw_seed_t *seeds, int32_t n, bsw_alnreg_t *out);
 
+/* Keep ref[0, ref_len) RESIDENT in HBM of every device of the context (replacing any earlier
+ * one) for bsw_extend_seeds_device: a 3 Gb genome is ~1% of an MI355X's 288 GB.  Blocking. */
+int bsw_set_reference(bsw_ctx_t *ctx, const uint8_t *ref, int64_t ref_len);
+
+/* Device-resident form of bsw_extend_seeds against the resident reference: d_reads, d_read_off,
+ * d_read_len, d_seeds and d_out in HBM of the context's first device, `stream` a hipStream_t
+ * or NULL.  Job building, band retries and the local / to-end interpretation run on the GPU
+ * (bsw_ext_dev.hip); results equal bsw_extend_seeds's.  BSW_E_INVAL without a resident
+ * reference.  Returns when d_out holds the regions. */
+int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
+                            const int64_t *d_read_off, const int32_t *d_read_len, const bsw_seed_t *d_seeds,
+                            int32_t n, bsw_alnreg_t *d_out, void *stream);
+
 /* Batches issued by the last bsw_extend_seeds on ctx: SeqPairs per phase (left, left retry,
  * right, right retry) and the summed DP kernel time. */
 typedef struct bsw_ext_stats_t {
     int32_t n_pairs[4];
     float   kernel_ms;               /* DP kernels (HIP events)                                  */
-    float   build_ms;                /* host: job lists + code buffers                           */
-    float   engine_ms;               /* bsw batches incl. PCIe, plan/sort and kernels            */
-    float   interp_ms;               /* host: local / to-end interpretation                      */
+    float   build_ms;                /* host: job lists + code buffers (device form: 0)          */
+    float   engine_ms;               /* bsw batches incl. PCIe, plan/sort and kernels (device
+                                        form: the whole call)                                    */
+    float   interp_ms;               /* host: local / to-end interpretation (device form: 0)     */
 } bsw_ext_stats_t;
 int bsw_ext_last_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out);
 

@@ -177,3 +177,55 @@ def test_gpu_pipeline_edges():
     got = bsw.extend_seeds(eng, ref, reads, off, lens, seeds, opt)
     _same(want, got, "GPU pipeline edges")
     eng.close()
+
+
+# ---------------------------------------------------------------- GPU: device-resident pipeline
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,try_,clip", [(100, 2, (5, 5)), (10, 2, (5, 5)), (20, 1, (0, 100)),
+                                          (3, 3, (2, 9))])
+def test_gpu_device_pipeline_matches_oracle(w, try_, clip):
+    """bsw_extend_seeds_device (job build / retries / interpretation on the GPU, resident
+    reference) == the CPU restatement == the host-built pipeline."""
+    ref, reads, off, lens, seeds, _ = _workload(20_000, seed=21 + w, ref_len=2_000_000, p_sub=0.03,
+                                               p_indel=0.005)
+    opt = bsw.ExtOpt(w=w, pen_clip5=clip[0], pen_clip3=clip[1], max_band_try=try_)
+    want = oracle.extend_seeds(oracle.make_params(), opt, ref, reads, off, lens, seeds)
+    eng = bsw.Engine()
+    bsw.set_reference(eng, ref)
+    got = bsw.extend_seeds_resident(eng, reads, off, lens, seeds, opt)
+    _same(want, got, f"device pipeline w={w}")
+    st = bsw.ext_last_stats(eng)
+    assert st.n_pairs[0] > 0 and st.n_pairs[2] > 0
+    if try_ > 1 and w <= 10:
+        assert st.n_pairs[1] + st.n_pairs[3] > 0
+    _same(bsw.extend_seeds(eng, ref, reads, off, lens, seeds, opt), got, "host vs device pipeline")
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_device_pipeline_edges():
+    """Seeds at read/reference ends, reads without seeds, N-rich reference, varying read
+    lengths; no resident reference -> BSW_E_INVAL; bad seed -> BSW_E_RANGE."""
+    ref = bsw.synth_reference(5000, seed=2, p_n=0.05)
+    reads, off, lens, seeds, origin = bsw.synth_reads(ref, 2000, cfg=bsw.reads_cfg(seed=4, read_len=120))
+    seeds[::7]["len"] = 0
+    seeds[1::7]["qbeg"] = 0
+    seeds[2::7]["qbeg"] = lens[2::7] - seeds[2::7]["len"]
+    for i in range(3, len(seeds), 7):
+        seeds[i]["rbeg"], seeds[i]["qbeg"], seeds[i]["len"] = 0, 10, 19
+    lens = lens.copy()
+    lens[5::11] = np.maximum(seeds[5::11]["qbeg"] + seeds[5::11]["len"], lens[5::11] - 30)   # shorter reads
+    opt = bsw.ext_opt()
+    want = oracle.extend_seeds(oracle.make_params(), opt, ref, reads, off, lens, seeds)
+    eng = bsw.Engine()
+    with pytest.raises(bsw.BswError):
+        bsw.extend_seeds_resident(eng, reads, off, lens, seeds, opt)        # no resident reference
+    bsw.set_reference(eng, ref)
+    got = bsw.extend_seeds_resident(eng, reads, off, lens, seeds, opt)
+    _same(want, got, "device pipeline edges")
+    bad = seeds.copy()
+    bad[0]["rbeg"] = len(ref)
+    bad[0]["len"] = 5
+    with pytest.raises(bsw.BswError):
+        bsw.extend_seeds_resident(eng, reads, off, lens, bad, opt)
+    eng.close()
