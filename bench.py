@@ -445,6 +445,8 @@ def main_global(args, rank, local, world):
     st = sts[-1]
     kms = float(np.mean([x.kernel_ms for x in sts]))
     value = args.jobs * world * args.steps / dt_max / 1e6
+    bsw.ksw_global2_device(eng, d_pairs.ptr, d_ref.ptr, d_qer.ptr, args.jobs, 0, 0, 0)   # scores only
+    so_ms = bsw.global_last_stats(eng).kernel_ms
     out = {
         "metric": "M global alignments with CIGAR/sec (150 bp read vs its reference span, ksw_global2)",
         "value": round(value, 3), "unit": "M alignments/s", "n_gpus": world,
@@ -463,6 +465,7 @@ def main_global(args, rank, local, world):
                      "traceback_matrix_GBps": round(st.z_bytes / (kms * 1e-3) / 1e9, 1),
                      "algorithmic": f"{OPS_PER_CELL} int ops x {st.cells} band cells per step"},
         "cigar_ops_mean": round(float(np.mean(nc[nc > 0])), 3),
+        "score_only_kernel_ms": round(so_ms, 4),
     }
     if world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

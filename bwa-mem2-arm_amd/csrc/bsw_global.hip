@@ -36,6 +36,9 @@ namespace bsw {
 constexpr int kGNeg = -16384;                 // -inf of the int16 register rows
 constexpr int32_t kGMinusInf = -0x40000000;   // upstream MINUS_INF
 
+// Routing: the column kernel when the job fits it (measured faster on bwa-shaped jobs: 9.55 vs
+// 9.76 ms per 1M 150-bp jobs), else the band kernel when 2w + 2 <= 96, else the wide kernel;
+// gp.prefer_band (BSW_GLOB_BAND=1) puts every band-eligible job on the band kernel.
 __device__ __forceinline__ int glob_class(const SeqPair &p, const GlobParams &gp)
 {
     const int q = p.len2, t = p.len1, w = p.h0;
@@ -44,14 +47,24 @@ __device__ __forceinline__ int glob_class(const SeqPair &p, const GlobParams &gp
     // the row-0 / column-0 boundaries, one more gap open for E' / F')
     const int64_t bound = (int64_t)gp.maxabs * min(q, t) + gp.o_del + (int64_t)gp.e_del * (t + 1) +
                           gp.o_ins + (int64_t)gp.e_ins * (q + 1) + max(gp.oe_del, gp.oe_ins) + 8;
+    int col = -1;
     if (bound < 15000) {
-        if (q <= 32) return 0;
-        if (q <= 64) return 1;
-        if (q <= 96) return 2;
-        if (q <= 128) return 3;
-        if (q <= 160) return 4;
+        if (q <= 32) col = 0;
+        else if (q <= 64) col = 1;
+        else if (q <= 96) col = 2;
+        else if (q <= 128) col = 3;
+        else if (q <= 160) col = 4;
     }
-    return kGlobWideClass;
+    const int need = 2 * w + 2;                          // band slots incl. the end slot
+    int band = -1, bw = 0;
+    if (need <= 32) { band = 0; bw = 32; }
+    else if (need <= 48) { band = 1; bw = 48; }
+    else if (need <= 64) { band = 2; bw = 64; }
+    else if (need <= 80) { band = 3; bw = 80; }
+    else if (need <= 96) { band = 4; bw = 96; }
+    (void)bw;
+    if (band >= 0 && (col < 0 || gp.prefer_band)) return band;
+    return col >= 0 ? kGlobLane0 + col : kGlobWideClass;
 }
 
 __global__ void glob_plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, const GlobParams gp,
@@ -284,6 +297,213 @@ __global__ __launch_bounds__(256, 2) void glob_lane_kernel(
     if (zw) glob_traceback(zw, cap_dw, wmax, lane, qlen, tlen, w, cigar + (int64_t)idx * stride, stride, n_cigar + idx);
 }
 
+// ------------------------------------------------------------------ band-coordinate kernel
+// Slot s of row i holds column j = i - w + s (w = the lane's band), so the band is a fixed
+// window of 2w + 1 slots: the diagonal H(i-1, j-1) sits in the SAME slot, E(i, j) was written
+// into slot s by the cell of slot s + 1 one row earlier, and the query codes shift one nibble
+// per row.  H and E live in separate int32 register arrays (upstream's int32 values and
+// MINUS_INF, no packing); the per-row bounds are per-wave scalars computed from wmin / wmax /
+// min and max of qlen + w, with no cross-lane reduction in the row loop.
+template <bool MASKED>
+__device__ __forceinline__ uint32_t glob_bcell(int &H, int &Ecur, int *Eprev, int sc, int &h1, int &f,
+                                               const GCx &c, bool in, bool atend, bool lb, int bnd)
+{
+    const int m = H + sc, e = Ecur;
+    int h = max(m, e);
+    uint32_t d = m < e ? 1u : 0u;
+    d = h < f ? 2u : d;
+    h = max(h, f);
+    const int t = m - c.oe_del, ee = e - c.e_del;
+    const uint32_t eb = ee > t ? 4u : 0u;
+    const int e2 = max(ee, t);
+    const int t2 = m - c.oe_ins, ff = f - c.e_ins;
+    const uint32_t fb = ff > t2 ? 8u : 0u;
+    const int f2 = max(ff, t2);
+    if (!MASKED) {
+        H = h;
+        if (Eprev) *Eprev = e2;
+        h1 = h; f = f2;
+    } else {
+        H = in ? h : (lb ? bnd : H);
+        if (Eprev) *Eprev = in ? e2 : (atend ? kGMinusInf : *Eprev);
+        h1 = in ? h : h1;
+        f = in ? f2 : f;
+    }
+    return d | eb | fb;
+}
+
+struct GBand {                      // per-lane slot bounds of a row
+    int sb, se, bnd;                // valid slots [sb, se); slot se takes E = -inf; slot sb - 1 (when
+    bool left;                      //   the band touches column 0) takes H(i, -1) = bnd
+};
+
+template <int G, int BW, bool MASKED>
+__device__ __forceinline__ uint32_t glob_bgroup(int (&H)[BW], int (&E)[BW], const uint32_t (&Qb)[BW / 8], uint2 pr,
+                                                int &h1, int &f, const GCx &c, const GBand &b)
+{
+    const uint32_t sel0 = Qb[G] & 0x0f0f0f0fu, sel1 = (Qb[G] >> 4) & 0x0f0f0f0fu;
+    const uint32_t pw0 = __builtin_amdgcn_perm(pr.y, pr.x, sel0), pw1 = __builtin_amdgcn_perm(pr.y, pr.x, sel1);
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int s = 8 * G + k;
+        const int sc = (int)(int8_t)(((k & 1) ? pw1 : pw0) >> (8 * (k >> 1)));
+        const bool in = MASKED ? (s >= b.sb && s < b.se) : true;
+        const bool atend = MASKED ? (s == b.se) : false;
+        const bool lb = MASKED ? (b.left && s == b.sb - 1) : false;
+        word |= glob_bcell<MASKED>(H[s], E[s], s > 0 ? &E[s - 1] : nullptr, sc, h1, f, c, in, atend, lb, b.bnd)
+                << (4 * k);
+    }
+    return word;
+}
+
+template <int G, int BW>
+__device__ __forceinline__ void glob_bgroup_at(int (&H)[BW], int (&E)[BW], const uint32_t (&Qb)[BW / 8], uint2 pr,
+                                               int &h1, int &f, const GCx &c, const GBand &b, int lo, int hi, int fb,
+                                               int fe, uint32_t *__restrict__ zrow, int lane)
+{
+    if (8 * G + 8 <= lo || 8 * G >= hi) return;          // uniform
+    uint32_t word;
+    if (8 * G >= fb && 8 * G + 8 <= fe) word = glob_bgroup<G, BW, false>(H, E, Qb, pr, h1, f, c, b);
+    else word = glob_bgroup<G, BW, true>(H, E, Qb, pr, h1, f, c, b);
+    if (zrow) zrow[G * 64 + lane] = word;
+}
+
+template <int BW, int... G>
+__device__ __forceinline__ void glob_brow(std::integer_sequence<int, G...>, int (&H)[BW], int (&E)[BW],
+                                          const uint32_t (&Qb)[BW / 8], uint2 pr, int &h1, int &f, const GCx &c,
+                                          const GBand &b, int lo, int hi, int fb, int fe, uint32_t *__restrict__ zrow,
+                                          int lane)
+{
+    (glob_bgroup_at<G, BW>(H, E, Qb, pr, h1, f, c, b, lo, hi, fb, fe, zrow, lane), ...);
+}
+
+// traceback over band-coordinate nibbles: cell (i, k) sits in slot k - i + w
+__device__ void glob_traceback_band(const uint32_t *__restrict__ zw, int ng, int lane, int qlen, int tlen, int w,
+                                    uint32_t *__restrict__ out, int stride, int32_t *__restrict__ nout)
+{
+    if (qlen >= 1 && tlen >= 1 && qlen < tlen - w) { *nout = -2; return; }
+    int i = tlen - 1, k = min(i + w + 1, qlen) - 1, which = 0, n = 0;
+    uint32_t cur = 0;
+    auto push = [&](uint32_t op, uint32_t len) {
+        if (n > 0 && (cur & 0xfu) == op) { cur += len << 4; return; }
+        if (n > 0 && n - 1 < stride) out[n - 1] = cur;
+        cur = len << 4 | op;
+        ++n;
+    };
+    while (i >= 0 && k >= 0) {
+        const int s = k - i + w;
+        const uint32_t word = zw[((int64_t)i * ng + (s >> 3)) * 64 + lane];
+        const uint32_t nib = (word >> ((s & 7) * 4)) & 15u;
+        which = which == 0 ? (int)(nib & 3u) : which == 1 ? (int)((nib >> 2) & 1u) : ((nib & 8u) ? 2 : 0);
+        if (which == 0) { push(0, 1); --i; --k; }
+        else if (which == 1) { push(2, 1); --i; }
+        else { push(1, 1); --k; }
+    }
+    if (i >= 0) push(2, (uint32_t)(i + 1));
+    if (k >= 0) push(1, (uint32_t)(k + 1));
+    if (n > 0 && n - 1 < stride) out[n - 1] = cur;
+    if (n > stride) { *nout = -1; return; }
+    for (int a = 0, b = n - 1; a < b; ++a, --b) {
+        const uint32_t t = out[a];
+        out[a] = out[b];
+        out[b] = t;
+    }
+    *nout = n;
+}
+
+template <int BW>
+__global__ __launch_bounds__(256, 2) void glob_band_kernel(
+    const GlobParams gp, SeqPair *__restrict__ pairs, const int32_t *__restrict__ order, int32_t n,
+    const uint8_t *__restrict__ ref, const uint8_t *__restrict__ qer, uint32_t *__restrict__ z, int64_t zstride,
+    uint32_t *__restrict__ cigar, int32_t stride, int32_t *__restrict__ n_cigar, unsigned long long *__restrict__ cells)
+{
+    constexpr int NG = BW / 8;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool live = tid < n;
+    const int idx = live ? order[tid] : 0;
+    SeqPair p{};
+    if (live) p = pairs[idx];
+    const int qlen = live ? p.len2 : 0, tlen = live ? p.len1 : 0, w = live ? p.h0 : 0;
+    const int wmax = __builtin_amdgcn_readfirstlane(wave_max(live ? w : -1));
+    if (wmax < 0) return;                                   // whole wave empty
+    const int wmin = __builtin_amdgcn_readfirstlane(wave_min(live ? w : INT_MAX));
+    const int tmax = __builtin_amdgcn_readfirstlane(wave_max(tlen));
+    const int qwmin = __builtin_amdgcn_readfirstlane(wave_min(live ? qlen + w : INT_MAX));
+    const int qwmax = __builtin_amdgcn_readfirstlane(wave_max(live ? qlen + w : 0));
+    uint32_t *zw = z ? z + (int64_t)(tid >> 6) * zstride : nullptr;
+    const uint8_t *q = qer + p.idq;
+    // query codes of row 0 in band coordinates: slot s <-> column s - w, 8 nibbles per dword
+    uint32_t Qb[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        uint32_t w8 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = 8 * g + k - w;
+            const uint32_t code = (live && j >= 0 && j < qlen) ? q[j] : 4u;
+            w8 |= min(code, 7u) << (4 * k);
+        }
+        Qb[g] = w8;
+    }
+    // row -1: H(-1, j - 1) = eh[j].h of upstream's first row, E(0, j) = -inf
+    int H[BW], E[BW];
+#pragma unroll
+    for (int s = 0; s < BW; ++s) {
+        const int j = s - w;
+        H[s] = j == 0 ? 0 : ((j >= 1 && j <= w && j <= qlen) ? -(gp.o_ins + gp.e_ins * j) : kGMinusInf);
+        E[s] = kGMinusInf;
+    }
+    int score = qlen == 0 ? 0 : (qlen <= w ? -(gp.o_ins + gp.e_ins * qlen) : kGMinusInf);
+    const GCx cx{gp.e_del, gp.oe_del, gp.e_ins, gp.oe_ins};
+    unsigned long long ncell = 0;
+    uint32_t tnext = (live && tlen > 0) ? ref[p.idr] : 4u;
+    int jn = BW - w;                                        // column entering the top slot next row
+    uint32_t qnext = (live && jn >= 0 && jn < qlen) ? q[jn] : 4u;
+    for (int i = 0; i < tmax; ++i) {
+        const bool act = live && i < tlen;
+        const uint32_t t = min(tnext, 7u);
+        if (act && i + 1 < tlen) tnext = ref[p.idr + i + 1];
+        uint2 pr = make_uint2(gp.prof[4][0], gp.prof[4][1]);
+        pr = (t == 3) ? make_uint2(gp.prof[3][0], gp.prof[3][1]) : pr;
+        pr = (t == 2) ? make_uint2(gp.prof[2][0], gp.prof[2][1]) : pr;
+        pr = (t == 1) ? make_uint2(gp.prof[1][0], gp.prof[1][1]) : pr;
+        pr = (t == 0) ? make_uint2(gp.prof[0][0], gp.prof[0][1]) : pr;
+        const int beg = max(i - w, 0), end = min(i + w + 1, qlen);
+        GBand b;
+        b.sb = act ? beg - i + w : BW + 1;
+        b.se = act ? end - i + w : -1;
+        b.bnd = -(gp.o_del + gp.e_del * (i + 1));
+        b.left = act && beg == 0;
+        // uniform bounds: slots any lane touches [lo, hi) (incl. the boundary slot sb - 1 and the
+        // end slot se), slots every active lane has in band [fb, fe)
+        const int lo = max(wmin - i - 1, 0);
+        const int hi = min(BW, min(2 * wmax + 1, qwmax - i) + 1);
+        const int fb = max(wmax - i, 0);
+        const int fe = min(2 * wmin + 1, qwmin - i);
+        int h1 = b.left ? b.bnd : kGMinusInf;
+        int f = kGMinusInf;
+        glob_brow<BW>(std::make_integer_sequence<int, NG>{}, H, E, Qb, pr, h1, f, cx, b, lo, hi, fb, fe,
+                      zw ? zw + (int64_t)i * NG * 64 : nullptr, lane);
+        if (act) {
+            ncell += (unsigned long long)max(end - beg, 0);
+            if (end == qlen) score = beg < end ? h1 : (beg == 0 ? b.bnd : kGMinusInf);
+        }
+        // next row's query window: shift one slot (nibble) down, the new top slot from qnext
+#pragma unroll
+        for (int g = 0; g < NG - 1; ++g) Qb[g] = __builtin_amdgcn_alignbit(Qb[g + 1], Qb[g], 4);
+        Qb[NG - 1] = (Qb[NG - 1] >> 4) | (min(qnext, 7u) << 28);
+        ++jn;
+        qnext = (live && jn >= 0 && jn < qlen) ? q[jn] : 4u;
+    }
+    for (int o = 32; o > 0; o >>= 1) ncell += __shfl_xor(ncell, o);
+    if (lane == 0 && cells) atomicAdd(cells, ncell);
+    if (!live) return;
+    pairs[idx].score = score;
+    if (zw) glob_traceback_band(zw, NG, lane, qlen, tlen, w, cigar + (int64_t)idx * stride, stride, n_cigar + idx);
+}
+
 // ------------------------------------------------------------------ wide kernel
 __global__ __launch_bounds__(256) void glob_wide_kernel(
     const GlobParams gp, SeqPair *__restrict__ pairs, const int32_t *__restrict__ order, int32_t n,
@@ -390,11 +610,18 @@ hipError_t launch_glob_class(int cls, const GlobParams &gp, SeqPair *pairs, cons
 {
     if (n <= 0) return hipSuccess;
     switch (cls) {
-    case 0: launch_lane_q<32>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
-    case 1: launch_lane_q<64>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
-    case 2: launch_lane_q<96>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
-    case 3: launch_lane_q<128>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
-    case 4: launch_lane_q<160>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
+#define GB(C, BW)                                                                                           \
+    case C:                                                                                                 \
+        hipLaunchKernelGGL(glob_band_kernel<BW>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gp, pairs, \
+                           order, n, ref, qer, z, zstride, cigar, stride, n_cigar, cells);                 \
+        break;
+    GB(0, 32) GB(1, 48) GB(2, 64) GB(3, 80) GB(4, 96)
+#undef GB
+    case kGlobLane0 + 0: launch_lane_q<32>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
+    case kGlobLane0 + 1: launch_lane_q<64>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
+    case kGlobLane0 + 2: launch_lane_q<96>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
+    case kGlobLane0 + 3: launch_lane_q<128>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
+    case kGlobLane0 + 4: launch_lane_q<160>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
     case kGlobWideClass:
         hipLaunchKernelGGL(glob_wide_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gp, pairs, order,
                            n, ref, qer, z, zstride, cap_dw, ehs, cigar, stride, n_cigar, cells);

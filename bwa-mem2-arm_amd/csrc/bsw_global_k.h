@@ -12,25 +12,33 @@ struct GlobParams {
     int32_t maxabs;             // max |mat| -- the int16 safety bound of the register kernel
     uint32_t prof[8][2];        // prof[t] = score bytes mat[t][q], q = 0..4; q = 5..7 score as N
     int8_t mat[25];
+    int8_t prefer_band;         // route band-eligible jobs to the band kernel (BSW_GLOB_BAND=1)
 };
 
-// Job classes: register kernel for qlen <= 32, 64, 96, 128, 160 (int16-safe scores), then the
-// int32 wide kernel (eh row in HBM) for everything else.
+// Job classes: band-coordinate register kernel (int32 cells, 2w + 2 <= BW slots), column
+// register kernel for qlen <= QMAX (int16-safe scores), then the int32 wide kernel (eh row in
+// HBM).  Routing in glob_class (bsw_global.hip).
+constexpr int kGlobBandClasses = 5;
+constexpr int kGlobBandW[kGlobBandClasses] = {32, 48, 64, 80, 96};
 constexpr int kGlobLaneClasses = 5;
 constexpr int kGlobQmax[kGlobLaneClasses] = {32, 64, 96, 128, 160};
-constexpr int kGlobWideClass = kGlobLaneClasses;
-constexpr int kGlobClasses = kGlobLaneClasses + 1;
+constexpr int kGlobLane0 = kGlobBandClasses;                       // first column class
+constexpr int kGlobWideClass = kGlobLane0 + kGlobLaneClasses;
+constexpr int kGlobClasses = kGlobWideClass + 1;
 // meta words: counts, max tlen, max w, max qlen per class; error flag
-constexpr int kGMetaCount = 0, kGMetaTmax = 8, kGMetaWmax = 16, kGMetaQmax = 24, kGMetaErr = 32;
-constexpr int kGMetaWords = 40;
+constexpr int kGMetaCount = 0, kGMetaTmax = 16, kGMetaWmax = 32, kGMetaQmax = 48, kGMetaErr = 64;
+constexpr int kGMetaWords = 72;
+static_assert(kGlobClasses <= 16, "meta layout");
 constexpr int kGlobKeyBits = 32;
 
 // Traceback-matrix dwords per row of a class's waves (8 nibbles per dword): the row window
 // starting at dword max(i - wmax, 0) >> 3 covers every lane's band [max(i - w, 0), i + w].
+// (Band classes: one dword per 8 slots of the fixed band window, BW / 8.)
 inline int glob_cap_dw(int cls, int qmax, int wmax)
 {
+    if (cls < kGlobBandClasses) return kGlobBandW[cls] / 8;
     const int band = ((2 * wmax) >> 3) + 2;
-    const int full = cls < kGlobLaneClasses ? kGlobQmax[cls] / 8 : (qmax + 7) / 8 + 1;
+    const int full = cls < kGlobWideClass ? kGlobQmax[cls - kGlobLane0] / 8 : (qmax + 7) / 8 + 1;
     return band < full ? band : full;
 }
 

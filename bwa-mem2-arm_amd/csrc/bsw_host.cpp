@@ -519,6 +519,8 @@ static void make_glob_params(const bsw_params_t &p, GlobParams &gp)
     for (int i = 0; i < 25; ++i) mx = std::max(mx, std::abs((int)p.mat[i]));
     gp.maxabs = mx;
     memcpy(gp.mat, p.mat, 25);
+    const char *band = getenv("BSW_GLOB_BAND");
+    gp.prefer_band = (band && band[0] == '1') ? 1 : 0;
     for (int t = 0; t < 8; ++t) {                        // codes > 4 score as N (as prof in KParams)
         const int tt = std::min(t, 4);
         uint8_t b[8];

@@ -169,9 +169,20 @@ def _check(want, got, tag):
                              f"{gc[i, :k] if gc is not None else ''}")
 
 
+@pytest.fixture(params=["column", "band"])
+def routing(request, monkeypatch):
+    """Default routing (column kernel first) or BSW_GLOB_BAND=1 (band kernel first); the
+    variable is read on every bsw_ksw_global2 call."""
+    if request.param == "band":
+        monkeypatch.setenv("BSW_GLOB_BAND", "1")
+    else:
+        monkeypatch.delenv("BSW_GLOB_BAND", raising=False)
+    return request.param
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("scoring", [(1, 4, 6, 1, 6, 1), (1, 3, 5, 2, 3, 1), (2, 5, 0, 1, 1, 2)])
-def test_gpu_random_jobs_match_oracle(scoring):
+def test_gpu_random_jobs_match_oracle(scoring, routing):
     a, b, od, ed, oi, ei = scoring
     pairs, ref, qer = _random_batch(4000, seed=a * 100 + od + b)
     p = bsw.default_params(a=a, b=b, o_del=od, e_del=ed, o_ins=oi, e_ins=ei)
@@ -185,7 +196,7 @@ def test_gpu_random_jobs_match_oracle(scoring):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("read_len", [150, 101, 250])
-def test_gpu_bwa_shaped_jobs_match_oracle(read_len):
+def test_gpu_bwa_shaped_jobs_match_oracle(read_len, routing):
     ref = bsw.synth_reference(4_000_000, seed=13)
     pairs, qer = bsw.synth_globals(ref, 20_000, cfg=bsw.globals_cfg(seed=read_len, read_len=read_len))
     want = oracle.ksw_global2_batch(pairs, ref, qer, bwa_fill_scmat(), stride=64, nthreads=16)
@@ -193,12 +204,13 @@ def test_gpu_bwa_shaped_jobs_match_oracle(read_len):
     got = bsw.ksw_global2(eng, pairs, ref, qer, stride=64)
     _check(want, got, f"bwa-shaped {read_len}")
     st = bsw.global_last_stats(eng)
-    assert st.n_jobs == len(pairs) and (st.n_wide > 0) == (read_len > 160)
+    assert st.n_jobs == len(pairs) and (st.n_wide > 0) == (read_len > 160)   # 250 bp: w ~ 60 -> wide
+    assert st.n_lane + st.n_wide == len(pairs)
     eng.close()
 
 
 @pytest.mark.gpu
-def test_gpu_edges_and_flags():
+def test_gpu_edges_and_flags(routing):
     """Empty sequences, w = 0, wide routing (qlen > 160 and int16-unsafe scores), the
     undefined geometry (-2), CIGAR overflow (-1) and the score-only mode."""
     rnd = random.Random(77)
@@ -236,5 +248,6 @@ def test_gpu_edges_and_flags():
     got = bsw.ksw_global2(eng, pr, rf, qr, stride=160)
     _check(want, got, "wide scoring")
     st = bsw.global_last_stats(eng)              # the larger jobs exceed the int16 bound
-    assert st.n_wide > 0 and st.n_lane > 0 and st.n_wide + st.n_lane == len(pr)
+    assert st.n_lane > 0 and st.n_wide + st.n_lane == len(pr)
+    assert st.n_wide > 0 or routing == "band"    # (band kernel: int32 cells, takes them when w is small)
     eng.close()
