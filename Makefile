@@ -67,4 +67,12 @@ $(ORACLE): oracle/ksw_ext_ref.c oracle/bsw_sse41.c oracle/ext_ref.c oracle/ksw_a
 clean:
 	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so $(ORACLE)
 
-.PHONY: all product synth oracle clean
+# experiment build: pc_kernel group-path counters (tools/pc_stats.py), never loaded by the product
+STATSLIB := $(LIBDIR)/libbsw_hip_stats.so
+stats: $(STATSLIB)
+$(LIBDIR)/bsw_pc_stats.o: $(CSRC)/bsw_pc.hip $(HIP_HDRS) | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DBSW_PC_STATS -c $< -o $@
+$(STATSLIB): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pk.o $(LIBDIR)/bsw_pc_stats.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_batch.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+
+.PHONY: all product synth oracle clean stats

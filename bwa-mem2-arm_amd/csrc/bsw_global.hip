@@ -218,7 +218,7 @@ __device__ __forceinline__ void glob_row(std::integer_sequence<int, G...>, uint3
 }
 
 template <int QMAX>
-__global__ __launch_bounds__(256, 2) void glob_lane_kernel(
+__global__ __launch_bounds__(64, 2) void glob_lane_kernel(
     const GlobParams gp, SeqPair *__restrict__ pairs, const int32_t *__restrict__ order, int32_t n,
     const uint8_t *__restrict__ ref, const uint8_t *__restrict__ qer, uint32_t *__restrict__ z, int64_t zstride,
     int32_t cap_dw, uint32_t *__restrict__ cigar, int32_t stride, int32_t *__restrict__ n_cigar,
@@ -413,7 +413,7 @@ __device__ void glob_traceback_band(const uint32_t *__restrict__ zw, int ng, int
 }
 
 template <int BW>
-__global__ __launch_bounds__(256, 2) void glob_band_kernel(
+__global__ __launch_bounds__(64, 2) void glob_band_kernel(
     const GlobParams gp, SeqPair *__restrict__ pairs, const int32_t *__restrict__ order, int32_t n,
     const uint8_t *__restrict__ ref, const uint8_t *__restrict__ qer, uint32_t *__restrict__ z, int64_t zstride,
     uint32_t *__restrict__ cigar, int32_t stride, int32_t *__restrict__ n_cigar, unsigned long long *__restrict__ cells)
@@ -599,7 +599,7 @@ static void launch_lane_q(const GlobParams &gp, SeqPair *pairs, const int32_t *o
                           uint32_t *cigar, int32_t stride, int32_t *n_cigar, unsigned long long *cells,
                           hipStream_t s)
 {
-    hipLaunchKernelGGL(glob_lane_kernel<QMAX>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gp, pairs,
+    hipLaunchKernelGGL(glob_lane_kernel<QMAX>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, gp, pairs,
                        order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells);
 }
 
@@ -612,7 +612,7 @@ hipError_t launch_glob_class(int cls, const GlobParams &gp, SeqPair *pairs, cons
     switch (cls) {
 #define GB(C, BW)                                                                                           \
     case C:                                                                                                 \
-        hipLaunchKernelGGL(glob_band_kernel<BW>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gp, pairs, \
+        hipLaunchKernelGGL(glob_band_kernel<BW>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, gp, pairs,    \
                            order, n, ref, qer, z, zstride, cigar, stride, n_cigar, cells);                 \
         break;
     GB(0, 32) GB(1, 48) GB(2, 64) GB(3, 80) GB(4, 96)

@@ -194,7 +194,7 @@ __device__ __forceinline__ void mate_row(std::integer_sequence<int, G...>, uint3
 }
 
 template <int NC>
-__global__ __launch_bounds__(256, NC <= 160 ? 2 : 1) void mate_kernel(
+__global__ __launch_bounds__(64, NC <= 160 ? 2 : 1) void mate_kernel(
     const MateParams mp, const SeqPair *__restrict__ pairs, const int32_t *__restrict__ jobs, int32_t j0,
     int32_t j1, const uint8_t *__restrict__ ref, const uint8_t *__restrict__ qer, bsw_kswr_t *__restrict__ aln,
     int mode, uint16_t *__restrict__ scratch, int64_t sstride, unsigned long long *__restrict__ cells)
@@ -324,7 +324,7 @@ static hipError_t launch_nc(const MateParams &mp, const SeqPair *pairs, const in
                             uint16_t *scratch, int64_t sstride, unsigned long long *cells, hipStream_t s)
 {
     const int n = j1 - j0;
-    hipLaunchKernelGGL(mate_kernel<NC>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mp, pairs, jobs,
+    hipLaunchKernelGGL(mate_kernel<NC>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, mp, pairs, jobs,
                        j0, j1, ref, qer, aln, mode, scratch, sstride, cells);
     return hipGetLastError();
 }

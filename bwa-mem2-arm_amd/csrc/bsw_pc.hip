@@ -32,6 +32,7 @@
 // take garbage: they are never read again (beg never decreases).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <limits.h>
 #include <utility>
 #include "bsw_kernels.h"
@@ -39,7 +40,10 @@
 
 namespace bsw {
 
-constexpr int kPcChunkDw = 17;           // dwords per lane per 64-row target chunk (as lane kernel)
+constexpr int kPcChunkDw = 17;
+#ifdef BSW_PC_STATS
+__device__ unsigned long long g_pc_stats[8];
+#endif           // dwords per lane per 64-row target chunk (as lane kernel)
 
 struct PcRow {                           // per-row uniform (SGPR) group bounds
     int glo, gsp;                        // groups touching slots [min beg, max end]
@@ -116,15 +120,25 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
     "v_lshl_or_b32 %[pb], %[c2], 16, %[c1]\n\t"                                              \
     PC_MWRITE("a", KA, LA) PC_MWRITE("b", KB, LB)
 
+#ifdef BSW_PC_STATS          // group-path counters (tools/pc_stats.py; never in the product build)
+#define PC_CNT(k) "v_add_u32_e32 %[ct" #k "], 1, %[ct" #k "]\n\t"
+#define PC_CNT_OPS , [ct0] "+v"(ctr[0]), [ct1] "+v"(ctr[1]), [ct2] "+v"(ctr[2]), [ct3] "+v"(ctr[3])
+#else
+#define PC_CNT(k)
+#define PC_CNT_OPS
+#endif
+
 #define PC_GROUP_ASM(KEYA_FAST, KEYA_MASK)                                                \
     asm volatile(                                                                            \
         "s_sub_u32 %[st], %[g], %[glo]\n\t"          /* outside [min beg, max end]: skip */ \
         "s_cmp_le_u32 %[st], %[gsp]\n\t"                                                     \
         "s_cbranch_scc0 3f\n\t"                                                              \
+        PC_CNT(0)                                                                            \
         PC_SCORES                                                                            \
         "s_sub_u32 %[st], %[g], %[gfa]\n\t"          /* every live lane in band: FAST */    \
         "s_cmp_lt_u32 %[st], %[gfn]\n\t"                                                     \
         "s_cbranch_scc0 2f\n\t"                                                              \
+        PC_CNT(1)                                                                            \
         PC_PH1("a", "%[ea]") PC_PH1("b", "%[eb]")                                            \
         PC_CELL("%[c0]", "a", "WORD_0")                                                      \
         PC_CELL("%[c1]", "a", "WORD_1")                                                      \
@@ -141,6 +155,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
         "s_sub_u32 %[st], %[g], %[gla]\n\t"          /* some lane's beg in this group: L */ \
         "s_cmp_le_u32 %[st], %[gln]\n\t"                                                     \
         "s_cbranch_scc1 4f\n\t"                                                              \
+        PC_CNT(2)                                                                            \
         PC_MASKED(PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"),                        \
                   PC_MCELL("%[c1]", "%[c0]", "a", "WORD_1", "%[j1]"),                        \
                   PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"),                        \
@@ -148,6 +163,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
                   KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t", "", "")           \
         "s_branch 3f\n"                                                                      \
         "4:\n\t"                                                                             \
+        PC_CNT(3)                                                                            \
         PC_MASKED(PC_RESET("%[h1]", "%[r0]") PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"), \
                   PC_RESET("%[c0]", "%[j1]") PC_MCELL("%[c1]", "%[c0]", "a", "WORD_1", "%[j1]"), \
                   PC_RESET("%[c1]", "%[j2]") PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"), \
@@ -159,6 +175,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
           [h1] "+v"(h1), [key] "+v"(key), [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb),     \
           [ta] "=&v"(ta), [tb] "=&v"(tb), [xa] "=&v"(xa), [xb] "=&v"(xb), [c0] "=&v"(c0),    \
           [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb), [st] "=&s"(st)     \
+          PC_CNT_OPS                                                                         \
         : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe2] "s"(oe2), [ed2] "s"(ed2),        \
           [ed] "s"(ed), [glo] "s"(r.glo), [gsp] "s"(r.gsp), [gfa] "s"(r.gfa), [gfn] "s"(r.gfn), \
           [gla] "s"(r.gla), [gln] "s"(r.gln), [endw] "v"(endw), [endm1w] "v"(endm1w),       \
@@ -174,8 +191,9 @@ __device__ __forceinline__ void pc_group(uint32_t &ha, uint32_t &hb, uint32_t &e
                                          uint32_t q, uint32_t plo, uint32_t phi, int &f, int &h1,
                                          uint32_t &key, uint32_t oe2, uint32_t ed2, int ed,
                                          const PcRow &r, uint32_t endw, uint32_t endm1w,
-                                         uint32_t begm2w, int endv, int begv)
+                                         uint32_t begm2w, int endv, int begv, uint32_t (&ctr)[4])
 {
+    (void)ctr;
     // key slot s carries column j = s - 1: jj = {4G-1, 4G} and {4G+1, 4G+2}
     constexpr uint32_t JJA = ((uint32_t)(4 * G - 1) & 0xffffu) | ((uint32_t)(4 * G) << 16);
     constexpr uint32_t JJB = (uint32_t)(4 * G + 1) | ((uint32_t)(4 * G + 2) << 16);
@@ -197,10 +215,10 @@ __device__ __forceinline__ void pc_row(std::integer_sequence<int, G...>, uint32_
                                        uint32_t plo, uint32_t phi, int &f, int &h1, uint32_t &key,
                                        uint32_t oe2, uint32_t ed2, int ed, const PcRow &r,
                                        uint32_t endw, uint32_t endm1w, uint32_t begm2w, int endv,
-                                       int begv)
+                                       int begv, uint32_t (&ctr)[4])
 {
     (pc_group<G>(hh[2 * G], hh[2 * G + 1], ee[2 * G], ee[2 * G + 1], qs[G], plo, phi, f, h1, key,
-                 oe2, ed2, ed, r, endw, endm1w, begm2w, endv, begv), ...);
+                 oe2, ed2, ed, r, endw, endm1w, begm2w, endv, begv, ctr), ...);
 }
 
 // Lazy last positive column: when H(i, end-1) == 0 the lanes that need it
@@ -234,8 +252,10 @@ __device__ __forceinline__ void pc_lastpos(std::integer_sequence<int, G...>,
     ((pending = pc_lastpos_group<QMAX, QMAX / 4 - 1 - G>(hh, end, pending, lp1, gstart)), ...);
 }
 
-template <int QMAX>
-__global__ __launch_bounds__(256, 2) void pc_kernel(const KParams kp, const int32_t w,
+// WPB waves per workgroup: with 1, a wave's slot (and its LDS) is reused as soon as that wave
+// ends, instead of when the slowest of its block's waves ends.
+template <int QMAX, int WPB>
+__global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const int32_t w,
                                                     SeqPair *__restrict__ pairs,
                                                     const int32_t *__restrict__ order,
                                                     const int32_t n,
@@ -244,7 +264,7 @@ __global__ __launch_bounds__(256, 2) void pc_kernel(const KParams kp, const int3
                                                     int32_t *__restrict__ err)
 {
     constexpr int NG = QMAX / 4;        // groups = query words (4 codes each)
-    __shared__ uint32_t s_tgt[4][2][kPcChunkDw][64];   // 34.8 KB per 256-thread block
+    __shared__ uint32_t s_tgt[WPB][2][kPcChunkDw][64];   // 8.7 KB per wave
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = gid < n;
     const int idx = valid ? (order ? order[gid] : gid) : 0;
@@ -322,6 +342,10 @@ __global__ __launch_bounds__(256, 2) void pc_kernel(const KParams kp, const int3
     const int wl_min = wave_min(alive ? wl : INT_MAX);
     const uint32_t oe2 = (uint32_t)(kp.o_del + kp.e_del) * 0x10001u;
     const uint32_t ed2 = (uint32_t)kp.e_del * 0x10001u;
+    uint32_t ctr[4] = {0, 0, 0, 0};                       // BSW_PC_STATS group-path counters
+#ifdef BSW_PC_STATS
+    uint32_t nrows = 0, nlast = 0;
+#endif
 
     for (int i = 0;; ++i) {
         const bool act = alive && i < tlen;
@@ -375,7 +399,7 @@ __global__ __launch_bounds__(256, 2) void pc_kernel(const KParams kp, const int3
             const uint32_t endm1w = pack2(end - 1);                         // end = 0: {-1, -1}
             const uint32_t begm2w = pack2(beg - 2);
             pc_row<QMAX>(std::make_integer_sequence<int, NG>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
-                         oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg);
+                         oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg, ctr);
             const uint32_t k32 = max(key & 0xffffu, key >> 16);
             const int m = (int)(k32 >> 8), mj = (int)(k32 & 0xffu);
             if (end == qlen) {                    // A.4: j == qlen; h1 = H(i, qlen - 1)
@@ -393,10 +417,16 @@ __global__ __launch_bounds__(256, 2) void pc_kernel(const KParams kp, const int3
                                          : best - m - (dj - di) * kp.e_ins;
                 if (dz > kp.zdrop) alive = false;
             }
+#ifdef BSW_PC_STATS
+            nrows += 1;
+#endif
             if (alive) {                           // end_{i+1} = min(lastH + 3, ...), DESIGN.md §3
                 const bool need = h1 == 0;         // H(i, end-1) == 0 -> lastH < end - 1
                 int lp1 = end;
                 if (__ballot(need)) {
+#ifdef BSW_PC_STATS
+                    nlast += 1;
+#endif
                     if (need) lp1 = 0;
                     pc_lastpos<QMAX>(std::make_integer_sequence<int, NG>{}, hh, end, need, lp1,
                                      (emax - 1) >> 2);
@@ -405,6 +435,20 @@ __global__ __launch_bounds__(256, 2) void pc_kernel(const KParams kp, const int3
             }
         }
     }
+#ifdef BSW_PC_STATS
+    {   // per wave: rows (max over lanes), group paths, lastpos scans; lane 0 adds
+        const unsigned rows = (unsigned)wave_max((int)nrows);
+        const unsigned nl = (unsigned)wave_max((int)nlast);
+        unsigned cmax[4];
+        for (int k = 0; k < 4; ++k) cmax[k] = (unsigned)wave_max((int)ctr[k]);   // the longest lane
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&g_pc_stats[0], (unsigned long long)rows);
+            for (int k = 0; k < 4; ++k) atomicAdd(&g_pc_stats[1 + k], (unsigned long long)cmax[k]);
+            atomicAdd(&g_pc_stats[5], (unsigned long long)nl);
+            atomicAdd(&g_pc_stats[6], 1ull);
+        }
+    }
+#endif
     if (valid) {
         sp->score = best;
         sp->tle = best_i + 1;
@@ -415,18 +459,46 @@ __global__ __launch_bounds__(256, 2) void pc_kernel(const KParams kp, const int3
     }
 }
 
+#ifdef BSW_PC_STATS
+// [rows, groups entered, fast, masked-R, masked-L, lastpos scans, waves] summed over waves
+extern "C" int bsw_pc_stats(unsigned long long *out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pc_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return -5;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pc_stats), z, sizeof(z)) != hipSuccess) return -5;
+    }
+    return 0;
+}
+#endif
+
+template <int QMAX>
+static void launch_pc_q(int wpb, const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order, int32_t n,
+                        const uint8_t *ref, const uint8_t *qer, int32_t *err, hipStream_t s)
+{
+    if (wpb == 4)
+        hipLaunchKernelGGL((pc_kernel<QMAX, 4>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, kp, w, pairs,
+                           order, n, ref, qer, err);
+    else
+        hipLaunchKernelGGL((pc_kernel<QMAX, 1>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, kp, w, pairs, order,
+                           n, ref, qer, err);
+}
+
 hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
                             const int32_t *order, int32_t n, const uint8_t *ref,
                             const uint8_t *qer, int32_t *err, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
-    const dim3 block(256), grid((unsigned)((n + 255) / 256));
+    static const int wpb = [] {
+        const char *e = getenv("BSW_PC_WPB");
+        return (e && e[0] == '4') ? 4 : 1;
+    }();
     switch (qmax) {
-    case 32: hipLaunchKernelGGL(pc_kernel<32>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
-    case 64: hipLaunchKernelGGL(pc_kernel<64>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
-    case 96: hipLaunchKernelGGL(pc_kernel<96>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
-    case 128: hipLaunchKernelGGL(pc_kernel<128>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
-    case 160: hipLaunchKernelGGL(pc_kernel<160>, grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err); break;
+    case 32: launch_pc_q<32>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 64: launch_pc_q<64>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 96: launch_pc_q<96>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 128: launch_pc_q<128>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 160: launch_pc_q<160>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -15,7 +15,7 @@ import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBDIR = os.path.join(PKG, "lib")
-HIP_LIB = os.path.join(LIBDIR, "libbsw_hip.so")
+HIP_LIB = os.environ.get("BSW_HIP_LIB") or os.path.join(LIBDIR, "libbsw_hip.so")   # override: experiment builds
 SYNTH_LIB = os.path.join(LIBDIR, "libbsw_synth.so")
 
 SEQPAIR_DTYPE = np.dtype(
