@@ -466,7 +466,7 @@ __device__ __forceinline__ void lane_lastpos(std::integer_sequence<int, G...>,
 constexpr int kTChunkDw = 17;            // dwords per lane per 64-row target chunk
 
 template <int QMAX, int SM, bool SYM>
-__global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const int32_t w,
+__global__ __launch_bounds__(64, 2) void lane_kernel(const KParams kp, const int32_t w,
                                                       SeqPair *__restrict__ pairs,
                                                       const int32_t *__restrict__ order,
                                                       const int32_t n,
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(256, 2) void lane_kernel(const KParams kp, const in
                                                       int32_t *__restrict__ err)
 {
     constexpr int NG = QMAX / 4;        // query words (4 codes each)
-    __shared__ uint32_t s_tgt[4][2][kTChunkDw][64];   // 34.8 KB per 256-thread block
+    __shared__ uint32_t s_tgt[1][2][kTChunkDw][64];   // 8.7 KB: one wave per workgroup (as pc_kernel)
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = gid < n;
     const int idx = valid ? (order ? order[gid] : gid) : 0;
@@ -733,7 +733,7 @@ static hipError_t launch_lane_q(const KParams &kp, int32_t w, SeqPair *pairs, co
                                 int32_t n, const uint8_t *ref, const uint8_t *qer, int32_t *err,
                                 hipStream_t s)
 {
-    const dim3 block(256), grid((unsigned)((n + 255) / 256));
+    const dim3 block(64), grid((unsigned)((n + 63) / 64));
     const bool sym = kp.o_del == kp.o_ins && kp.e_del == kp.e_ins;
     if (kp.maxsc == 1 && sym)
         hipLaunchKernelGGL((lane_kernel<QMAX, 1, true>), grid, block, 0, s, kp, w, pairs, order, n, ref, qer, err);

@@ -31,6 +31,16 @@ typedef struct { int32_t h, e; } eh_t;
 
 /* ksw_extend2 (Appendix A).  Row i walks the target (ref, len1), column j the query
  * (len2).  Returns the best score; out-params as upstream. */
+/* Band cells the literal loop visits (sum of end - beg over rows), per thread: the "actual cells"
+ * of SURVEY.md §8(d), read by bench.py on a sample. */
+static __thread long long g_oracle_cells;
+long long oracle_cells_take(void)
+{
+    const long long c = g_oracle_cells;
+    g_oracle_cells = 0;
+    return c;
+}
+
 int oracle_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target,
                        int m, const int8_t *mat, int o_del, int e_del, int o_ins,
                        int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle,
@@ -80,6 +90,7 @@ int oracle_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
             if (h1 < 0) h1 = 0;
         } else
             h1 = 0;
+        if (end > beg) g_oracle_cells += end - beg;
         for (j = beg; j < end; ++j) {
             /* eh[j] = { H(i-1,j-1), E(i,j) }, f = F(i,j), h1 = H(i,j-1) */
             eh_t *p = &eh[j];

@@ -90,6 +90,16 @@ def get_scores(params: OracleParams, pairs: np.ndarray, ref: np.ndarray, qer: np
                                 len(pairs), w)
 
 
+def band_cells(params: OracleParams, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray, w: int) -> int:
+    """DP cells the literal ksw_extend2 loop visits on `pairs` (sum of end - beg over rows;
+    narrowed band, early z-drop / m == 0 exits) -- one thread, pairs copied."""
+    L = lib()
+    L.oracle_cells_take.restype = ctypes.c_longlong
+    L.oracle_cells_take()
+    get_scores(params, pairs.copy(), ref, qer, w)
+    return int(L.oracle_cells_take())
+
+
 def sse41_get_scores16(params: OracleParams, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray,
                        w: int, nthreads: int = 1) -> int:
     assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous

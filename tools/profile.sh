@@ -4,6 +4,7 @@
 #   2. PMC FETCH_SIZE              -> gpurun_out/prof/pmc_fetch
 #   3. PMC WRITE_SIZE              -> gpurun_out/prof/pmc_write
 #   4. PMC SQ occupancy/VALU       -> gpurun_out/prof/pmc_sq
+#   5. PMC LDS bank conflicts + L2 hit/miss -> gpurun_out/prof/pmc_lds
 # Counters are collected in their own passes with --kernel-trace only (never with
 # sys/runtime traces).  Every pass runs under its own timeout; any failure stops the script.
 set -euo pipefail
@@ -15,4 +16,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -- python3 bench.py $ARGS > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -- python3 bench.py $ARGS > "$OUT/pmc_write.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS --output-format csv -d "$OUT/pmc_sq" -- python3 bench.py $ARGS > "$OUT/pmc_sq.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_lds" -- python3 bench.py $ARGS > "$OUT/pmc_lds.log" 2>&1
 echo profile-done
