@@ -265,6 +265,9 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
 {
     constexpr int NG = QMAX / 4;        // groups = query words (4 codes each)
     __shared__ uint32_t s_tgt[WPB][2][kPcChunkDw][64];   // 8.7 KB per wave
+    __shared__ uint2 s_prof[8];                           // per-row score profiles, by target code
+    if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
+    __syncthreads();
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = gid < n;
     const int idx = valid ? (order ? order[gid] : gid) : 0;
@@ -387,11 +390,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             }
             // per-row score profile of target base t (8 bytes: mat[t][q], q = 0..7)
             const uint32_t t = (tcur >> (8 * (i & 3))) & 0xffu;
-            uint2 pr = make_uint2(kp.prof[4][0], kp.prof[4][1]);
-            pr = (t == 3) ? make_uint2(kp.prof[3][0], kp.prof[3][1]) : pr;
-            pr = (t == 2) ? make_uint2(kp.prof[2][0], kp.prof[2][1]) : pr;
-            pr = (t == 1) ? make_uint2(kp.prof[1][0], kp.prof[1][1]) : pr;
-            pr = (t == 0) ? make_uint2(kp.prof[0][0], kp.prof[0][1]) : pr;
+            const uint2 pr = s_prof[min(t, 7u)];         // one ds_read_b64 (codes > 4 score as N)
             int h1 = (beg == 0) ? max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) : 0;
             int f = 0;
             uint32_t key = 0;
