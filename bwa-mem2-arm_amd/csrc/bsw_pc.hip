@@ -357,8 +357,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
         const int beg = max(0, i - wl);
         const int end = min(min(endc, i + wl + 1), qlen);
         endc = end;
-        const int emax = wave_max(act ? end : -1);
-        const int emin = wave_min(act ? end : INT_MAX);
+        const int emax = wave_max_bc(act ? end : -1);
+        const int emin = wave_min_bc(act ? end : INT_MAX);
         PcRow r;
         {
             const int ulo = __builtin_amdgcn_readfirstlane(max(0, i - wl_max));  // min beg
@@ -412,8 +412,9 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
                 moff = max(moff, abs(mj - i));
             } else if (kp.zdrop > 0) {
                 const int di = i - best_i, dj = mj - best_j;
-                const int dz = (di > dj) ? best - m - (di - dj) * kp.e_del
-                                         : best - m - (dj - di) * kp.e_ins;
+                // |di - dj| and e are small and non-negative: 24-bit multiplies (full rate)
+                const int dz = (di > dj) ? best - m - (int)__umul24((unsigned)(di - dj), (unsigned)kp.e_del)
+                                         : best - m - (int)__umul24((unsigned)(dj - di), (unsigned)kp.e_ins);
                 if (dz > kp.zdrop) alive = false;
             }
 #ifdef BSW_PC_STATS
