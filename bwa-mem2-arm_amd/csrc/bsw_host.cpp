@@ -832,6 +832,68 @@ int bsw_ksw_align2_device(bsw_ctx_t *ctx, const SeqPair *d_pairs, const uint8_t 
     return rc;
 }
 
+}  // extern "C"
+
+namespace bsw {
+// One device's share of a host-buffer mate-rescue call (contiguous job range).
+static int mate_host_shard(const MateParams &mp, DeviceCtx &dc, const SeqPair *pairs, const uint8_t *seqBufRef,
+                           const uint8_t *seqBufQer, int32_t n, bsw_kswr_t *aln, bsw_mate_stats_t *ms)
+{
+    *ms = bsw_mate_stats_t{};
+    if (n == 0) return BSW_OK;
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    Slot &s = *slot;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            const SeqPair &p = pairs[i];
+            if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
+            if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
+        }
+        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+        BSW_TRY(grow(s.d_mpairs, s.cap_mpairs, (size_t)n));
+        BSW_TRY(grow(s.d_maln, s.cap_maln, (size_t)n));
+        BSW_TRY(grow(s.d_ref, s.cap_ref, (size_t)(r_hi - r_lo) + 1));
+        BSW_TRY(grow(s.d_qer, s.cap_qer, (size_t)(q_hi - q_lo) + 1));
+        BSW_TRY(hipMemcpyAsync(s.d_mpairs, pairs, (size_t)n * sizeof(SeqPair), hipMemcpyHostToDevice, s.stream));
+        if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, seqBufRef + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
+        if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, seqBufQer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
+        int r = mate_device(mp, s, s.d_mpairs, s.d_ref - r_lo, s.d_qer - q_lo, n, s.d_maln, s.stream, ms);
+        if (r) return r;
+        BSW_TRY(hipMemcpyAsync(aln, s.d_maln, (size_t)n * sizeof(bsw_kswr_t), hipMemcpyDeviceToHost, s.stream));
+        BSW_TRY(hipStreamSynchronize(s.stream));
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+
+// Run shard(d, a, b) for contiguous job ranges [a, b) on every device of the context (one host
+// thread per device; jobs are independent), first non-zero status wins.
+template <class F>
+static int shard_devices(bsw_ctx_t *ctx, int32_t n, F shard)
+{
+    const int nd = (int)ctx->devs.size();
+    if (nd == 1) return shard(0, 0, n);
+    std::vector<int> rcs(nd, BSW_OK);
+    std::vector<std::thread> th;
+    for (int d = 0; d < nd; ++d) {
+        const int32_t a = (int32_t)((int64_t)n * d / nd), b = (int32_t)((int64_t)n * (d + 1) / nd);
+        th.emplace_back([&, d, a, b] { rcs[d] = shard(d, a, b); });
+    }
+    for (auto &t : th) t.join();
+    for (int r : rcs)
+        if (r) return r;
+    return BSW_OK;
+}
+}  // namespace bsw
+
+extern "C" {
+
 int bsw_ksw_align2(bsw_ctx_t *ctx, const SeqPair *pairs, const uint8_t *seqBufRef, const uint8_t *seqBufQer,
                    int32_t n, bsw_kswr_t *aln)
 {
@@ -844,39 +906,19 @@ int bsw_ksw_align2(bsw_ctx_t *ctx, const SeqPair *pairs, const uint8_t *seqBufRe
             return BSW_E_RANGE;
     bsw::MateParams mp;
     bsw::make_mate_params(ctx->params, mp);
-    bsw::DeviceCtx &dc = *ctx->devs[0];
-    int rc = BSW_OK;
-    auto slot = dc.acquire(rc);
-    if (!slot) return rc;
-    bsw::Slot &s = *slot;
-    rc = [&]() -> int {
-        BSW_TRY(hipSetDevice(dc.device));
-        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
-        for (int32_t i = 0; i < n; ++i) {
-            const SeqPair &p = pairs[i];
-            if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
-            if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
-        }
-        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
-        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
-        BSW_TRY(bsw::grow(s.d_mpairs, s.cap_mpairs, (size_t)n));
-        BSW_TRY(bsw::grow(s.d_maln, s.cap_maln, (size_t)n));
-        BSW_TRY(bsw::grow(s.d_ref, s.cap_ref, (size_t)(r_hi - r_lo) + 1));
-        BSW_TRY(bsw::grow(s.d_qer, s.cap_qer, (size_t)(q_hi - q_lo) + 1));
-        BSW_TRY(hipMemcpyAsync(s.d_mpairs, pairs, (size_t)n * sizeof(SeqPair), hipMemcpyHostToDevice, s.stream));
-        if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, seqBufRef + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
-        if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, seqBufQer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
-        bsw_mate_stats_t ms;
-        int r = bsw::mate_device(mp, s, s.d_mpairs, s.d_ref - r_lo, s.d_qer - q_lo, n, s.d_maln, s.stream, &ms);
-        if (r) return r;
-        BSW_TRY(hipMemcpyAsync(aln, s.d_maln, (size_t)n * sizeof(bsw_kswr_t), hipMemcpyDeviceToHost, s.stream));
-        BSW_TRY(hipStreamSynchronize(s.stream));
-        std::lock_guard<std::mutex> g(ctx->stats_mu);
-        ctx->mate_last = ms;
-        return BSW_OK;
-    }();
-    dc.give_back(std::move(slot));
-    return rc;
+    std::vector<bsw_mate_stats_t> st(ctx->devs.size());
+    const int rc = bsw::shard_devices(ctx, n, [&](int d, int32_t a, int32_t b) {
+        return bsw::mate_host_shard(mp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a, aln + a, &st[d]);
+    });
+    if (rc) return rc;
+    bsw_mate_stats_t agg{};
+    for (const auto &x : st) {
+        agg.fwd_ms = std::max(agg.fwd_ms, x.fwd_ms); agg.rev_ms = std::max(agg.rev_ms, x.rev_ms);
+        agg.n_fwd += x.n_fwd; agg.n_rev += x.n_rev; agg.cells_fwd += x.cells_fwd;
+    }
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    ctx->mate_last = agg;
+    return BSW_OK;
 }
 
 int bsw_mate_last_stats(bsw_ctx_t *ctx, bsw_mate_stats_t *out)
@@ -916,6 +958,59 @@ int bsw_ksw_global2_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_re
     return rc;
 }
 
+}  // extern "C"
+
+namespace bsw {
+// One device's share of a host-buffer global-alignment call (contiguous job range).
+static int glob_host_shard(const GlobParams &gp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *seqBufRef,
+                           const uint8_t *seqBufQer, int32_t n, uint32_t *cigar, int32_t cigar_stride,
+                           int32_t *n_cigar, bsw_global_stats_t *gs)
+{
+    *gs = bsw_global_stats_t{};
+    if (n == 0) return BSW_OK;
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    Slot &s = *slot;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            const SeqPair &p = pairs[i];
+            if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
+            if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
+        }
+        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+        const bool want = cigar_stride > 0;
+        BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)n));
+        BSW_TRY(grow(s.d_ref, s.cap_ref, (size_t)(r_hi - r_lo) + 1));
+        BSW_TRY(grow(s.d_qer, s.cap_qer, (size_t)(q_hi - q_lo) + 1));
+        if (want) {
+            BSW_TRY(grow(s.d_gcig, s.cap_gcig, (size_t)n * (size_t)cigar_stride));
+            BSW_TRY(grow(s.d_gncig, s.cap_gncig, (size_t)n));
+        }
+        BSW_TRY(hipMemcpyAsync(s.d_pairs, pairs, (size_t)n * sizeof(SeqPair), hipMemcpyHostToDevice, s.stream));
+        if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, seqBufRef + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
+        if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, seqBufQer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
+        int r = glob_device(gp, s, s.d_pairs, s.d_ref - r_lo, s.d_qer - q_lo, n, want ? s.d_gcig : nullptr,
+                            cigar_stride, want ? s.d_gncig : nullptr, s.stream, gs);
+        if (r) return r;
+        BSW_TRY(hipMemcpyAsync(pairs, s.d_pairs, (size_t)n * sizeof(SeqPair), hipMemcpyDeviceToHost, s.stream));
+        if (want) {
+            BSW_TRY(hipMemcpyAsync(cigar, s.d_gcig, (size_t)n * cigar_stride * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+            BSW_TRY(hipMemcpyAsync(n_cigar, s.d_gncig, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
+        }
+        BSW_TRY(hipStreamSynchronize(s.stream));
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+}  // namespace bsw
+
+extern "C" {
+
 int bsw_ksw_global2(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef, const uint8_t *seqBufQer,
                     int32_t n, uint32_t *cigar, int32_t cigar_stride, int32_t *n_cigar)
 {
@@ -929,48 +1024,22 @@ int bsw_ksw_global2(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef, co
             return BSW_E_RANGE;
     bsw::GlobParams gp;
     bsw::make_glob_params(ctx->params, gp);
-    bsw::DeviceCtx &dc = *ctx->devs[0];
-    int rc = BSW_OK;
-    auto slot = dc.acquire(rc);
-    if (!slot) return rc;
-    bsw::Slot &s = *slot;
-    rc = [&]() -> int {
-        BSW_TRY(hipSetDevice(dc.device));
-        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
-        for (int32_t i = 0; i < n; ++i) {
-            const SeqPair &p = pairs[i];
-            if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
-            if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
-        }
-        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
-        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
-        const bool want = cigar_stride > 0;
-        BSW_TRY(bsw::grow(s.d_pairs, s.cap_pairs, (size_t)n));
-        BSW_TRY(bsw::grow(s.d_ref, s.cap_ref, (size_t)(r_hi - r_lo) + 1));
-        BSW_TRY(bsw::grow(s.d_qer, s.cap_qer, (size_t)(q_hi - q_lo) + 1));
-        if (want) {
-            BSW_TRY(bsw::grow(s.d_gcig, s.cap_gcig, (size_t)n * (size_t)cigar_stride));
-            BSW_TRY(bsw::grow(s.d_gncig, s.cap_gncig, (size_t)n));
-        }
-        BSW_TRY(hipMemcpyAsync(s.d_pairs, pairs, (size_t)n * sizeof(SeqPair), hipMemcpyHostToDevice, s.stream));
-        if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, seqBufRef + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
-        if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, seqBufQer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
-        bsw_global_stats_t gs;
-        int r = bsw::glob_device(gp, s, s.d_pairs, s.d_ref - r_lo, s.d_qer - q_lo, n, want ? s.d_gcig : nullptr,
-                                 cigar_stride, want ? s.d_gncig : nullptr, s.stream, &gs);
-        if (r) return r;
-        BSW_TRY(hipMemcpyAsync(pairs, s.d_pairs, (size_t)n * sizeof(SeqPair), hipMemcpyDeviceToHost, s.stream));
-        if (want) {
-            BSW_TRY(hipMemcpyAsync(cigar, s.d_gcig, (size_t)n * cigar_stride * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
-            BSW_TRY(hipMemcpyAsync(n_cigar, s.d_gncig, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
-        }
-        BSW_TRY(hipStreamSynchronize(s.stream));
-        std::lock_guard<std::mutex> g(ctx->stats_mu);
-        ctx->glob_last = gs;
-        return BSW_OK;
-    }();
-    dc.give_back(std::move(slot));
-    return rc;
+    std::vector<bsw_global_stats_t> st(ctx->devs.size());
+    const int rc = bsw::shard_devices(ctx, n, [&](int d, int32_t a, int32_t b) {
+        return bsw::glob_host_shard(gp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a,
+                                    cigar_stride > 0 ? cigar + (size_t)a * cigar_stride : nullptr, cigar_stride,
+                                    cigar_stride > 0 ? n_cigar + a : nullptr, &st[d]);
+    });
+    if (rc) return rc;
+    bsw_global_stats_t agg{};
+    for (const auto &x : st) {
+        agg.kernel_ms = std::max(agg.kernel_ms, x.kernel_ms);
+        agg.n_jobs += x.n_jobs; agg.n_lane += x.n_lane; agg.n_wide += x.n_wide; agg.n_launches += x.n_launches;
+        agg.cells += x.cells; agg.z_bytes += x.z_bytes;
+    }
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    ctx->glob_last = agg;
+    return BSW_OK;
 }
 
 int bsw_global_last_stats(bsw_ctx_t *ctx, bsw_global_stats_t *out)

@@ -251,3 +251,17 @@ def test_gpu_edges_and_flags(routing):
     assert st.n_lane > 0 and st.n_wide + st.n_lane == len(pr)
     assert st.n_wide > 0 or routing == "band"    # (band kernel: int32 cells, takes them when w is small)
     eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_all_devices_context():
+    """A context over every visible device shards host-buffer calls by contiguous job ranges."""
+    import hiprt
+    ref = bsw.synth_reference(2_000_000, seed=17)
+    pairs, qer = bsw.synth_globals(ref, 9_000)
+    want = oracle.ksw_global2_batch(pairs, ref, qer, bwa_fill_scmat(), stride=64, nthreads=16)
+    eng = bsw.Engine(n_gpus=hiprt.device_count())
+    got = bsw.ksw_global2(eng, pairs, ref, qer, stride=64)
+    _check(want, got, f"n_gpus={hiprt.device_count()}")
+    assert bsw.global_last_stats(eng).n_jobs == len(pairs)
+    eng.close()

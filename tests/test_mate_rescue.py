@@ -204,3 +204,17 @@ def test_gpu_rejects_unsupported():
     with pytest.raises(bsw.BswError):
         bsw.ksw_align2(eng, pairs, np.zeros(10_000, np.uint8), np.zeros(10_000, np.uint8))
     eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_all_devices_context():
+    """A context over every visible device shards host-buffer calls by contiguous job ranges."""
+    import hiprt
+    ref = bsw.synth_reference(2_000_000, seed=19)
+    pairs, qer = bsw.synth_mates(ref, 9_000)
+    want = oracle.ksw_align2_batch(pairs, ref, qer, bwa_fill_scmat(), nthreads=16)
+    eng = bsw.Engine(n_gpus=hiprt.device_count())
+    got = bsw.ksw_align2(eng, pairs, ref, qer)
+    _same(want, got, f"n_gpus={hiprt.device_count()}")
+    assert bsw.mate_last_stats(eng).n_fwd == len(pairs)
+    eng.close()
