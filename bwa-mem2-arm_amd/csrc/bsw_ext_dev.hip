@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "bsw_ext_k.h"
+#include "bsw_wave.h"
 
 namespace bsw {
 
@@ -26,20 +27,45 @@ __device__ __forceinline__ int cal_max_gap_d(const ExtDevParams &p, int qlen)
     return min(l, p.w << 1);
 }
 
-// meta[0] = max read length, meta[1] = input error, meta[2] / [3] = LEFT / RIGHT job counts
+// Per block (LDS), then one global atomic per block and word into slot blockIdx % 32 (own 64-B
+// line): meta[slot * 16 + k], k = 0 max read length, 1 input error, 2 / 3 LEFT / RIGHT job counts.
 __global__ void ext_scan_kernel(const int32_t *__restrict__ read_len, const bsw_seed_t *__restrict__ seeds,
                                 int32_t n, int64_t ref_len, int32_t *__restrict__ meta)
 {
+    __shared__ int s_m[4];
+    if (threadIdx.x < 4) s_m[threadIdx.x] = 0;
+    __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int l = read_len[i];
-    const bsw_seed_t s = seeds[i];
-    if (l < 0 || l > BSW_MAX_LEN) { atomicOr(&meta[1], 1); return; }
-    atomicMax(&meta[0], l);
-    if (s.len <= 0) return;
-    if (s.qbeg < 0 || s.qbeg + s.len > l || s.rbeg < 0 || s.rbeg + s.len > ref_len) { atomicOr(&meta[1], 1); return; }
-    if (s.qbeg > 0) atomicAdd(&meta[2], 1);
-    if (s.qbeg + s.len < l) atomicAdd(&meta[3], 1);
+    int l = 0, err = 0, nl = 0, nr = 0;
+    if (i < n) {
+        l = read_len[i];
+        const bsw_seed_t s = seeds[i];
+        if (l < 0 || l > BSW_MAX_LEN) {
+            err = 1;
+            l = 0;
+        } else if (s.len > 0) {
+            if (s.qbeg < 0 || s.qbeg + s.len > l || s.rbeg < 0 || s.rbeg + s.len > ref_len) err = 1;
+            else {
+                nl = s.qbeg > 0;
+                nr = s.qbeg + s.len < l;
+            }
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    const int wl = wave_max(l);
+    const unsigned long long be = __ballot(err), bl = __ballot(nl), br = __ballot(nr);
+    if (lane == 0) {
+        atomicMax(&s_m[0], wl);
+        if (be) atomicOr(&s_m[1], 1);
+        if (bl) atomicAdd(&s_m[2], __popcll(bl));
+        if (br) atomicAdd(&s_m[3], __popcll(br));
+    }
+    __syncthreads();
+    int32_t *slot = meta + (blockIdx.x % kExtMetaSpread) * 16;
+    if (threadIdx.x == 0 && s_m[0]) atomicMax(&slot[0], s_m[0]);
+    if (threadIdx.x == 1 && s_m[1]) atomicOr(&slot[1], 1);
+    if (threadIdx.x == 2 && s_m[2]) atomicAdd(&slot[2], s_m[2]);
+    if (threadIdx.x == 3 && s_m[3]) atomicAdd(&slot[3], s_m[3]);
 }
 
 __global__ void ext_left_build_kernel(const ExtDevParams p, const uint8_t *__restrict__ reads,
@@ -69,12 +95,8 @@ __global__ void ext_left_build_kernel(const ExtDevParams p, const uint8_t *__res
         r.qb = 0; r.rb = s.rbeg;
         r.qe = l; r.re = s.rbeg + s.len;
         x.score = s.len * p.a;
-        if (s.qbeg > 0) {                               // reversed prefix / reversed window
-            const uint8_t *q = reads + read_off[i];
-            uint8_t *qd = qbuf + (int64_t)i * p.qstride, *td = tbuf + (int64_t)i * p.tstride;
+        if (s.qbeg > 0) {                               // reversed prefix / reversed window (ext_copy)
             const int tlen = (int)(s.rbeg - x.rmax0);
-            for (int k = 0; k < s.qbeg; ++k) qd[k] = q[s.qbeg - 1 - k];
-            for (int k = 0; k < tlen; ++k) td[k] = ref[s.rbeg - 1 - k];
             sp.idr = i * p.tstride; sp.idq = i * p.qstride;
             sp.len1 = tlen; sp.len2 = s.qbeg; sp.h0 = s.len * p.a;
         }
@@ -96,19 +118,43 @@ __global__ void ext_right_build_kernel(const ExtDevParams p, const uint8_t *__re
     sp.id = i;
     const bsw_seed_t s = seeds[i];
     const int l = read_len[i], qe = s.qbeg + s.len;
-    if (s.len > 0 && qe < l) {                          // forward suffix / forward window
+    if (s.len > 0 && qe < l) {                          // forward suffix / forward window (ext_copy)
         ExtState &x = st[i];
-        const uint8_t *q = reads + read_off[i] + qe;
         const int64_t t0 = s.rbeg + s.len;
         const int tlen = (int)(x.rmax1 - t0);
-        uint8_t *qd = qbuf + (int64_t)i * p.qstride, *td = tbuf + (int64_t)i * p.tstride;
-        for (int k = 0; k < l - qe; ++k) qd[k] = q[k];
-        for (int k = 0; k < tlen; ++k) td[k] = ref[t0 + k];
         sp.idr = i * p.tstride; sp.idq = i * p.qstride;
         sp.len1 = tlen; sp.len2 = l - qe; sp.h0 = x.score;
         x.prev = x.score;                               // a->score before the band loop
     }
     pairs[i] = sp;
+}
+
+// Code-buffer fill for the jobs the build kernel laid out: 16 lanes per job, so each byte
+// load / store instruction covers 16 consecutive bytes of 4 jobs (the one-thread-per-read form
+// touched 64 cache lines per instruction).  LEFT: reversed prefix / window ending at rbeg;
+// RIGHT: forward suffix / window from rbeg + len.
+__global__ void ext_copy_kernel(int left, const uint8_t *__restrict__ reads, const int64_t *__restrict__ read_off,
+                                const bsw_seed_t *__restrict__ seeds, int32_t n, const uint8_t *__restrict__ ref,
+                                const SeqPair *__restrict__ pairs, uint8_t *__restrict__ qbuf,
+                                uint8_t *__restrict__ tbuf)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = (int)(t >> 4), sub = (int)(t & 15);
+    if (i >= n) return;
+    const SeqPair sp = pairs[i];
+    if (sp.len2 <= 0) return;
+    const bsw_seed_t s = seeds[i];
+    const uint8_t *q = reads + read_off[i];
+    uint8_t *qd = qbuf + sp.idq, *td = tbuf + sp.idr;
+    if (left) {
+        for (int k = sub; k < sp.len2; k += 16) qd[k] = q[s.qbeg - 1 - k];
+        for (int k = sub; k < sp.len1; k += 16) td[k] = ref[s.rbeg - 1 - k];
+    } else {
+        const int qe = s.qbeg + s.len;
+        const int64_t t0 = s.rbeg + s.len;
+        for (int k = sub; k < sp.len2; k += 16) qd[k] = q[qe + k];
+        for (int k = sub; k < sp.len1; k += 16) td[k] = ref[t0 + k];
+    }
 }
 
 // Band retry t: a job of src (pairs for t == 1, the previous retry batch after) is redone with
@@ -184,7 +230,7 @@ static inline dim3 grid_of(int32_t n) { return dim3((unsigned)((n + 255) / 256))
 hipError_t launch_ext_scan(const int32_t *read_len, const bsw_seed_t *seeds, int32_t n, int64_t ref_len,
                            int32_t *meta, hipStream_t s)
 {
-    hipError_t e = hipMemsetAsync(meta, 0, 4 * sizeof(int32_t), s);
+    hipError_t e = hipMemsetAsync(meta, 0, kExtMetaSpread * 16 * sizeof(int32_t), s);
     if (e != hipSuccess || n <= 0) return e;
     hipLaunchKernelGGL(ext_scan_kernel, grid_of(n), dim3(256), 0, s, read_len, seeds, n, ref_len, meta);
     return hipGetLastError();
@@ -202,6 +248,8 @@ hipError_t launch_ext_build(int left, const ExtDevParams &p, const uint8_t *read
     else
         hipLaunchKernelGGL(ext_right_build_kernel, grid_of(n), dim3(256), 0, s, p, reads, read_off, read_len, seeds,
                            n, ref, st, pairs, qbuf, tbuf);
+    hipLaunchKernelGGL(ext_copy_kernel, dim3((unsigned)(((int64_t)n * 16 + 255) / 256)), dim3(256), 0, s, left, reads,
+                       read_off, seeds, n, ref, pairs, qbuf, tbuf);
     return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ struct ExtState {                       // per read, between the phases
     int32_t lw, rw;                     // band used per side
 };
 
+constexpr int kExtMetaSpread = 32;     // ext_scan writes meta[slot * 16 + k], slot < 32
+
 hipError_t launch_ext_scan(const int32_t *read_len, const bsw_seed_t *seeds, int32_t n, int64_t ref_len,
                            int32_t *meta, hipStream_t s);
 hipError_t launch_ext_build(int left, const ExtDevParams &p, const uint8_t *reads, const int64_t *read_off,

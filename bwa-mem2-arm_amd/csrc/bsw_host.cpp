@@ -41,8 +41,11 @@ constexpr int kNumLaneClasses = 5;          // QMAX 32, 64, 96, 128, 160
 constexpr int kPkClass0 = kNumLaneClasses;  // packed kernel, same QMAX buckets (classes 5..9)
 constexpr int kWideClass = kPkClass0 + kNumLaneClasses;   // index of the wide-kernel class
 constexpr int kNumClasses = kWideClass + 1;
-constexpr int kMetaCounts = 16;             // d_meta: counts[16], maxq_wide, err
-constexpr int kMetaWords = kMetaCounts + 2;
+constexpr int kMetaCounts = 16;             // class counters per slot (one 64-B line per slot)
+constexpr int kMetaSpread = 32;             // slots: block b adds into slot b % 32 (no hot line)
+constexpr int kMetaMaxq = kMetaCounts * kMetaSpread;   // d_meta: counts[32][16], maxq_wide, err
+constexpr int kMetaErr = kMetaMaxq + 1;
+constexpr int kMetaWords = kMetaErr + 1;
 constexpr int kKeyBits = 32;                // 4 class + 8 qlen + 1 related + 11 tlen + 8 h0 bits
 static_assert(kNumClasses <= kMetaCounts, "class counts");
 
@@ -110,13 +113,21 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
                   (uint32_t)(255 - min(max(p.h0, 0), 255));
         vals[i] = i;
     }
-    // one atomic per wave and class (1M same-address atomics cost ~11 ms)
+    // class counts: wave ballots -> LDS per block -> one global add per block and class into the
+    // block's slot (32 slots in separate 64-B lines; same-line atomics from every wave cost
+    // ~10 ns each, 0.16-0.7 ms per 1M pairs)
+    __shared__ int s_cnt[kNumClasses];
+    if (threadIdx.x < kNumClasses) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < kNumClasses; ++k) {
         const unsigned long long m = __ballot(valid && c == k);
-        if (m && lane == __ffsll((long long)m) - 1) atomicAdd(&counts[k], __popcll(m));
+        if (m && lane == __ffsll((long long)m) - 1) atomicAdd(&s_cnt[k], __popcll(m));
     }
+    __syncthreads();
+    if (threadIdx.x < kNumClasses && s_cnt[threadIdx.x])
+        atomicAdd(&counts[(blockIdx.x % kMetaSpread) * kMetaCounts + threadIdx.x], s_cnt[threadIdx.x]);
 }
 
 struct Slot {
@@ -320,7 +331,7 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     if (n == 0) return BSW_OK;
     BSW_TRY(grow_sort(s, n));
     BSW_TRY(hipMemsetAsync(s.d_meta, 0, kMetaWords * sizeof(int32_t), stream));
-    int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaCounts, *d_err = s.d_meta + kMetaCounts + 1;
+    int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaMaxq, *d_err = s.d_meta + kMetaErr;
     // pairs in the 8-bit score regime (h0 + min(qlen, tlen) <= 255, bwa-style scoring) take the
     // packed-column kernel on both entry points (getScores8 / getScores16: identical results,
     // fewer instructions per cell), the rest the int16 kernels (cell_bits = 8: the overflow
@@ -338,9 +349,10 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
                                                s.d_order, n, 0, kKeyBits, stream));
     BSW_TRY(hipMemcpyAsync(s.h_meta, s.d_meta, kMetaWords * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
     BSW_TRY(hipStreamSynchronize(stream));
-    int32_t counts[kNumClasses];
-    memcpy(counts, s.h_meta, sizeof(counts));
-    const int32_t maxq_wide = s.h_meta[kMetaCounts];
+    int32_t counts[kNumClasses] = {};
+    for (int sl = 0; sl < kMetaSpread; ++sl)
+        for (int c = 0; c < kNumClasses; ++c) counts[c] += s.h_meta[sl * kMetaCounts + c];
+    const int32_t maxq_wide = s.h_meta[kMetaMaxq];
     // DP kernels, one launch per non-empty class; event-timed as the hot region
     BSW_TRY(hipEventRecord(s.ev0, stream));
     int32_t off = 0;
@@ -428,7 +440,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         BSW_TRY(hipMemcpyAsync(pairs, s.d_pairs, (size_t)n * sizeof(SeqPair), hipMemcpyDeviceToHost, s.stream));
         BSW_TRY(hipStreamSynchronize(s.stream));
         if ((r = finish_stats(s))) return r;
-        if (s.h_meta[kMetaCounts + 1] != 0) return BSW_E_RANGE;   // kernel guard tripped (routing bug)
+        if (s.h_meta[kMetaErr] != 0) return BSW_E_RANGE;   // kernel guard tripped (routing bug)
         if (st) *st = s.stats;
         return BSW_OK;
     }();
@@ -797,7 +809,7 @@ int bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref
         int r = bsw::run_device(ctx->kp, *slot, d_pairs, d_ref, d_qer, n, w, cell_bits, st);
         if (r) return r;
         if ((r = bsw::finish_stats(*slot))) return r;
-        if (slot->h_meta[bsw::kMetaCounts + 1] != 0) return BSW_E_RANGE;
+        if (slot->h_meta[bsw::kMetaErr] != 0) return BSW_E_RANGE;
         std::lock_guard<std::mutex> g(ctx->stats_mu);
         ctx->last = slot->stats;
         return BSW_OK;
@@ -1089,9 +1101,14 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
         const bsw_params_t &p = ctx->params;
         // scan: max read length, input errors, job counts
         BSW_TRY(bsw::launch_ext_scan(d_read_len, d_seeds, n, dc.refres_len, s.d_meta, st));
-        int32_t m[4];
-        BSW_TRY(hipMemcpyAsync(m, s.d_meta, sizeof(m), hipMemcpyDeviceToHost, st));
+        static_assert(bsw::kExtMetaSpread * 16 <= bsw::kMetaWords, "ext meta fits d_meta");
+        BSW_TRY(hipMemcpyAsync(s.h_meta, s.d_meta, bsw::kExtMetaSpread * 16 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         BSW_TRY(hipStreamSynchronize(st));
+        int32_t m[4] = {0, 0, 0, 0};
+        for (int sl = 0; sl < bsw::kExtMetaSpread; ++sl) {
+            const int32_t *v = s.h_meta + sl * 16;
+            m[0] = std::max(m[0], v[0]); m[1] |= v[1]; m[2] += v[2]; m[3] += v[3];
+        }
         if (m[1]) return BSW_E_RANGE;
         es.n_pairs[0] = m[2];
         es.n_pairs[2] = m[3];
