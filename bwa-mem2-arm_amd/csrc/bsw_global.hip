@@ -78,26 +78,40 @@ __global__ void glob_plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, c
         p = pairs[i];
         c = glob_class(p, gp);
         if (c < 0) {
-            atomicOr(&meta[kGMetaErr], 1);
+            atomicOr(&meta[kGMetaErr], 1);                  // slot 0 (rare)
             c = kGlobWideClass;
         }
         keys[i] = ((uint32_t)c << 28) | ((uint32_t)(1023 - min(max(p.h0, 0), 1023)) << 18) |
                   ((uint32_t)(255 - min(max(p.len2, 0), 255)) << 10) | (uint32_t)(1023 - min(max(p.len1, 0), 1023));
         vals[i] = i;
     }
+    // class statistics: per wave (ballot / DPP max) -> per block in LDS -> one global atomic per
+    // block, class and statistic into slot blockIdx % kGMetaSpread (slots in separate lines)
+    __shared__ int s_st[4][kGlobClasses];
+    if (threadIdx.x < 4 * kGlobClasses) (&s_st[0][0])[threadIdx.x] = 0;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
-    for (int k = 0; k < kGlobClasses; ++k) {               // wave-aggregated class statistics
+    for (int k = 0; k < kGlobClasses; ++k) {
         const bool mine = c == k;
         const unsigned long long m = __ballot(mine);
         if (!m) continue;                                   // uniform
         const int tm = wave_max(mine ? p.len1 : 0), wm = wave_max(mine ? p.h0 : 0);
         const int qm = wave_max(mine ? p.len2 : 0);
         if (lane == 0) {
-            atomicAdd(&meta[kGMetaCount + k], __popcll(m));
-            atomicMax(&meta[kGMetaTmax + k], tm);
-            atomicMax(&meta[kGMetaWmax + k], wm);
-            atomicMax(&meta[kGMetaQmax + k], qm);
+            atomicAdd(&s_st[0][k], __popcll(m));
+            atomicMax(&s_st[1][k], tm);
+            atomicMax(&s_st[2][k], wm);
+            atomicMax(&s_st[3][k], qm);
         }
+    }
+    __syncthreads();
+    if (threadIdx.x < kGlobClasses && s_st[0][threadIdx.x]) {
+        const int k = threadIdx.x;
+        int32_t *slot = meta + (blockIdx.x % kGMetaSpread) * kGMetaWordsPerSlot;
+        atomicAdd(&slot[kGMetaCount + k], s_st[0][k]);
+        atomicMax(&slot[kGMetaTmax + k], s_st[1][k]);
+        atomicMax(&slot[kGMetaWmax + k], s_st[2][k]);
+        atomicMax(&slot[kGMetaQmax + k], s_st[3][k]);
     }
 }
 
@@ -586,7 +600,7 @@ __global__ __launch_bounds__(256) void glob_wide_kernel(
 hipError_t launch_glob_plan(const SeqPair *pairs, int32_t n, const GlobParams &gp, uint32_t *keys,
                             int32_t *vals, int32_t *meta, hipStream_t s)
 {
-    hipError_t e = hipMemsetAsync(meta, 0, sizeof(int32_t) * kGMetaWords, s);
+    hipError_t e = hipMemsetAsync(meta, 0, sizeof(int32_t) * kGMetaWords, s);   // all slots
     if (e != hipSuccess || n <= 0) return e;
     hipLaunchKernelGGL(glob_plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pairs, n, gp, keys,
                        vals, meta);

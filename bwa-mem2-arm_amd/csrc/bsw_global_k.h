@@ -26,8 +26,12 @@ constexpr int kGlobLane0 = kGlobBandClasses;                       // first colu
 constexpr int kGlobWideClass = kGlobLane0 + kGlobLaneClasses;
 constexpr int kGlobClasses = kGlobWideClass + 1;
 // meta words: counts, max tlen, max w, max qlen per class; error flag
+// per slot (kGMetaSpread slots, each in its own lines; the host reduces them): counts, max
+// tlen, max w, max qlen per class, error flag
 constexpr int kGMetaCount = 0, kGMetaTmax = 16, kGMetaWmax = 32, kGMetaQmax = 48, kGMetaErr = 64;
-constexpr int kGMetaWords = 72;
+constexpr int kGMetaWordsPerSlot = 80;
+constexpr int kGMetaSpread = 16;
+constexpr int kGMetaWords = kGMetaWordsPerSlot * kGMetaSpread;
 static_assert(kGlobClasses <= 16, "meta layout");
 constexpr int kGlobKeyBits = 32;
 

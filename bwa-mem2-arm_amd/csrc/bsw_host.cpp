@@ -567,8 +567,17 @@ static int glob_device(const GlobParams &gp, Slot &s, SeqPair *d_pairs, const ui
     BSW_TRY(hipMemcpyAsync(s.h_gmeta, s.d_gmeta, kGMetaWords * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     BSW_TRY(hipMemsetAsync(s.d_mcells, 0, sizeof(unsigned long long), st));
     BSW_TRY(hipStreamSynchronize(st));
-    int32_t m[kGMetaWords];
-    memcpy(m, s.h_gmeta, sizeof(m));
+    int32_t m[kGMetaWordsPerSlot] = {};
+    for (int sl = 0; sl < kGMetaSpread; ++sl) {
+        const int32_t *v = s.h_gmeta + sl * kGMetaWordsPerSlot;
+        for (int c = 0; c < kGlobClasses; ++c) {
+            m[kGMetaCount + c] += v[kGMetaCount + c];
+            m[kGMetaTmax + c] = std::max(m[kGMetaTmax + c], v[kGMetaTmax + c]);
+            m[kGMetaWmax + c] = std::max(m[kGMetaWmax + c], v[kGMetaWmax + c]);
+            m[kGMetaQmax + c] = std::max(m[kGMetaQmax + c], v[kGMetaQmax + c]);
+        }
+        m[kGMetaErr] |= v[kGMetaErr];
+    }
     if (m[kGMetaErr]) return BSW_E_RANGE;
     const bool want = d_cigar && stride > 0;
     BSW_TRY(hipEventRecord(s.ev0, st));
