@@ -154,6 +154,10 @@ def main():
     rank, local, world = dist_init()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = hiprt.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no HIP device visible")
+    local = local % ndev              # one GPU per rank; more ranks than GPUs share (rehearsal only)
     hiprt.set_device(local)
     if args.workload == "c1":          # BASELINE configs[0]: 10K exact 150 bp SE reads vs 1 Mb
         args.reads, args.ref_mb, args.exact = 10_000, 1, True
