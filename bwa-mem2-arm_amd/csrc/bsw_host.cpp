@@ -54,11 +54,12 @@ static_assert(kNumClasses <= kMetaCounts, "class counts");
 // target[10 + s, 40 + s), best over |s| <= 6; > 18 of 30 matches = related.  Unrelated pairs
 // die within a few dozen rows and shrink their band ends on the way; giving them their own
 // wavefronts keeps the related waves' band edges uniform (masked groups
-// 25% -> 11% at C2 in simulation).
-__device__ __forceinline__ int seed_related(const uint8_t *__restrict__ q, int qlen,
+// 25% -> 11% at C2 in simulation).  The identity count itself is the next sort field: it tracks
+// the pair's score along the first rows, hence its band-end trajectory and its lifetime.
+__device__ __forceinline__ int seed_matches(const uint8_t *__restrict__ q, int qlen,
                                             const uint8_t *__restrict__ r, int tlen)
 {
-    if (qlen < 40 || tlen < 46) return 1;
+    if (qlen < 40 || tlen < 46) return 31;
     uint8_t qb[30], rb[42];
 #pragma unroll
     for (int j = 0; j < 30; ++j) qb[j] = q[10 + j];
@@ -72,7 +73,7 @@ __device__ __forceinline__ int seed_related(const uint8_t *__restrict__ q, int q
         for (int j = 0; j < 30; ++j) c += qb[j] == rb[j + sft];
         best = max(best, c);
     }
-    return best > 18;
+    return best;                    // identities of the best shift (of 30); > 18: related
 }
 
 // Per pair: class + sort key.  Lane classes need qlen <= QMAX and int16-safe scores.
@@ -80,7 +81,7 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
                             int32_t route8, const uint8_t *__restrict__ ref,
                             const uint8_t *__restrict__ qer, uint32_t *__restrict__ keys,
                             int32_t *__restrict__ vals, int32_t *__restrict__ counts,
-                            int32_t *__restrict__ maxq_wide)
+                            int32_t *__restrict__ maxq_wide, int keymode)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < n;
@@ -107,10 +108,20 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
         if (c == kWideClass) atomicMax(maxq_wide, qlen);
         // (class, qlen desc, related first, tlen desc, h0 desc): like-shaped pairs share a
         // wavefront; equal h0 and relatedness give lanes similar band-end trajectories
-        const int rel = (c == kWideClass) ? 1 : seed_related(qer + p.idq, qlen, ref + p.idr, tlen);
-        keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
-                  ((uint32_t)(1 - rel) << 19) | ((uint32_t)(2047 - min(tlen, 2047)) << 8) |
-                  (uint32_t)(255 - min(max(p.h0, 0), 255));
+        const int mt = (c == kWideClass) ? 31 : seed_matches(qer + p.idq, qlen, ref + p.idr, tlen);
+        const int rel = mt > 18;
+        // sort key (scheduling only; results never depend on it).  Default: (class, qlen desc,
+        // related first, tlen / 32 desc, seed identities desc, h0 desc) -- pairs that align
+        // alike share a wavefront, so their band ends move together (C2 kernel 9.58 -> 8.60 ms vs
+        // the h0-only order, BSW_SORTKEY=0)
+        if (keymode == 0)
+            keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
+                      ((uint32_t)(1 - rel) << 19) | ((uint32_t)(2047 - min(tlen, 2047)) << 8) |
+                      (uint32_t)(255 - min(max(p.h0, 0), 255));
+        else
+            keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
+                      ((uint32_t)(1 - rel) << 19) | ((uint32_t)(63 - min(tlen >> 5, 63)) << 13) |
+                      ((uint32_t)(31 - min(mt, 31)) << 8) | (uint32_t)(255 - min(max(p.h0, 0), 255));
         vals[i] = i;
     }
     // class counts: wave ballots -> LDS per block -> one global add per block and class into the
@@ -304,6 +315,8 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     const char *pk = getenv("BSW_PK"), *pc = getenv("BSW_PC");
     const bool pk_on = pk && pk[0] == '1', pc_off = pc && pc[0] == '0';
     kp.route16 = pk_on ? 1 : pc_off ? 0 : 2;
+    const char *km = getenv("BSW_SORTKEY");
+    kp.keymode = (km && km[0] == '0') ? 0 : 2;
     kp.route8 = (pk_on || pc_off) ? 1 : 2;
 }
 
@@ -339,7 +352,7 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     const int route8 = kp.pk_ok ? (cell_bits == 8 ? kp.route8 : kp.route16) : 0;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                        d_pairs, n, kp.maxsc, route8, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
-                       d_maxq);
+                       d_maxq, kp.keymode);
     BSW_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
     BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals,

@@ -29,6 +29,7 @@ struct KParams {
     int8_t mat[25];
     int8_t route16, route8;     // host: kernel for 8-bit-regime pairs on 16-bit / 8-bit calls
                                 //   (2 = packed-column pc, 1 = two-pairs-per-lane pk, 0 = lane)
+    int8_t keymode;             // host: plan sort-key variant (BSW_SORTKEY)
 };
 
 // qlen limit of the register-resident kernel instantiations.

@@ -10,9 +10,20 @@ from collections import defaultdict
 src = sys.argv[1]
 dest = sys.argv[2] if len(sys.argv) > 2 else None
 
+def newest(pattern):
+    """Per directory only the newest run's file: gpurun merges every call's output into the same
+    local gpurun_out/, so older runs' CSVs (other process ids) sit beside the current ones."""
+    best = {}
+    for f in glob.glob(os.path.join(src, pattern), recursive=True):
+        d = os.path.dirname(f)
+        if d not in best or os.path.getmtime(f) > os.path.getmtime(best[d]):
+            best[d] = f
+    return sorted(best.values())
+
+
 def rows(pattern):
     out = []
-    for f in sorted(glob.glob(os.path.join(src, pattern), recursive=True)):
+    for f in newest(pattern):
         with open(f) as fh:
             out.extend(csv.DictReader(fh))
     return out
@@ -60,7 +71,7 @@ for n, cs in acc.items():
 print(json.dumps(summary, indent=1))
 if dest:
     os.makedirs(dest, exist_ok=True)
-    for f in glob.glob(os.path.join(src, '**/*kernel_stats.csv'), recursive=True)[:1]:
+    for f in newest('**/*kernel_stats.csv')[:1]:
         shutil.copy(f, os.path.join(dest, 'kernel_stats.csv'))
     with open(os.path.join(dest, 'pmc_summary.json'), 'w') as fh:
         json.dump(summary, fh, indent=1)
