@@ -128,6 +128,30 @@ extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const 
     if (!ctx || !opt || n < 0 || (n > 0 && (!ref || !reads || !read_off || !read_len || !seeds || !out)))
         return BSW_E_INVAL;
     if (opt->w < 0 || opt->max_band_try < 1 || ref_len < 0) return BSW_E_INVAL;
+    // SeqPair idr / idq are int32 offsets into one phase's code buffers: split calls whose
+    // buffers could pass 2^31 bytes (window <= read + 2 cal_max_gap <= read + 4w per read)
+    {
+        int64_t maxlen = 0;
+        for (int32_t i = 0; i < n; ++i) maxlen = std::max<int64_t>(maxlen, read_len[i]);
+        const int64_t per_read = maxlen + ((int64_t)opt->w << 2) + 2;
+        const int64_t chunk = std::max<int64_t>(1, (int64_t)INT32_MAX / per_read - 1);
+        if (n > chunk) {
+            bsw_ext_stats_t agg{};
+            for (int64_t a0 = 0; a0 < n; a0 += chunk) {
+                const int32_t m = (int32_t)std::min<int64_t>(chunk, n - a0);
+                const int rc = bsw_extend_seeds(ctx, opt, ref, ref_len, reads, read_off + a0,
+                                                read_len + a0, seeds + a0, m, out + a0);
+                if (rc) return rc;
+                bsw_ext_stats_t st{};
+                bsw::get_ext_stats(ctx, &st);
+                for (int k = 0; k < 4; ++k) agg.n_pairs[k] += st.n_pairs[k];
+                agg.kernel_ms += st.kernel_ms; agg.build_ms += st.build_ms;
+                agg.engine_ms += st.engine_ms; agg.interp_ms += st.interp_ms;
+            }
+            bsw::set_ext_stats(ctx, agg);
+            return BSW_OK;
+        }
+    }
     bsw_params_t p;
     bsw::ctx_params(ctx, &p);
     const int a = p.mat[0];
