@@ -45,11 +45,19 @@ constexpr int kPcChunkDw = 17;
 __device__ unsigned long long g_pc_stats[8];
 #endif           // dwords per lane per 64-row target chunk (as lane kernel)
 
-struct PcRow {                           // per-row uniform (SGPR) group bounds
-    int glo, gsp;                        // groups touching slots [min beg, max end]
-    int gfa, gfn;                        // FAST groups: gfa <= G < gfa + gfn
-    int gla, gln;                        // groups containing some lane's beg: gla <= G <= gla + gln
+struct PcRow {                           // per-row uniform (SGPR) group sets, bit G = group G
+    uint64_t enter;                      // groups touching slots [min beg, max end]
+    uint64_t fast;                       // FAST groups
+    uint64_t left;                       // groups containing some lane's beg (masked-L)
 };
+
+// groups lo .. lo + n - 1 as a bit set (uniform; bits >= 64 dropped, only bits < QMAX / 4 are read)
+__device__ __forceinline__ uint64_t gbits(int lo, int n)
+{
+    if (lo >= 64 || n <= 0) return 0;
+    n = min(n, 64 - lo);
+    return (n >= 64 ? ~0ull : ((1ull << n) - 1)) << lo;
+}
 
 // {v, v} as two int16 halves
 __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu) * 0x10001u; }
@@ -130,13 +138,11 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
 
 #define PC_GROUP_ASM(KEYA_FAST, KEYA_MASK)                                                \
     asm volatile(                                                                            \
-        "s_sub_u32 %[st], %[g], %[glo]\n\t"          /* outside [min beg, max end]: skip */ \
-        "s_cmp_le_u32 %[st], %[gsp]\n\t"                                                     \
+        "s_bitcmp1_b64 %[men], %[g]\n\t"             /* outside [min beg, max end]: skip */ \
         "s_cbranch_scc0 3f\n\t"                                                              \
         PC_CNT(0)                                                                            \
         PC_SCORES                                                                            \
-        "s_sub_u32 %[st], %[g], %[gfa]\n\t"          /* every live lane in band: FAST */    \
-        "s_cmp_lt_u32 %[st], %[gfn]\n\t"                                                     \
+        "s_bitcmp1_b64 %[mfa], %[g]\n\t"             /* every live lane in band: FAST */    \
         "s_cbranch_scc0 2f\n\t"                                                              \
         PC_CNT(1)                                                                            \
         PC_PH1("a", "%[ea]") PC_PH1("b", "%[eb]")                                            \
@@ -152,8 +158,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
         "v_pk_max_u16 %[key], %[key], %[pb]\n\t"                                             \
         "s_branch 3f\n"                                                                      \
         "2:\n\t"                                                                             \
-        "s_sub_u32 %[st], %[g], %[gla]\n\t"          /* some lane's beg in this group: L */ \
-        "s_cmp_le_u32 %[st], %[gln]\n\t"                                                     \
+        "s_bitcmp1_b64 %[mle], %[g]\n\t"             /* some lane's beg in this group: L */ \
         "s_cbranch_scc1 4f\n\t"                                                              \
         PC_CNT(2)                                                                            \
         PC_MASKED(PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"),                        \
@@ -174,11 +179,11 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
         : [ha] "+v"(ha), [hb] "+v"(hb), [ea] "+v"(ea), [eb] "+v"(eb), [f] "+v"(f),           \
           [h1] "+v"(h1), [key] "+v"(key), [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb),     \
           [ta] "=&v"(ta), [tb] "=&v"(tb), [xa] "=&v"(xa), [xb] "=&v"(xb), [c0] "=&v"(c0),    \
-          [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb), [st] "=&s"(st)     \
+          [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb)                     \
           PC_CNT_OPS                                                                         \
         : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe2] "s"(oe2), [ed2] "s"(ed2),        \
-          [ed] "s"(ed), [glo] "s"(r.glo), [gsp] "s"(r.gsp), [gfa] "s"(r.gfa), [gfn] "s"(r.gfn), \
-          [gla] "s"(r.gla), [gln] "s"(r.gln), [endw] "v"(endw), [endm1w] "v"(endm1w),       \
+          [ed] "s"(ed), [men] "s"(r.enter), [mfa] "s"(r.fast), [mle] "s"(r.left),           \
+          [endw] "v"(endw), [endm1w] "v"(endm1w),                                            \
           [begm2w] "v"(begm2w), [endv] "v"(endv), [begv] "v"(begv), [g] "i"(G),             \
           [jja] "s"(JJA), [jjb] "s"(JJB), [j0] "i"(4 * G), [j1] "i"(4 * G + 1),              \
           [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [r0] "i"(R0)                             \
@@ -198,7 +203,7 @@ __device__ __forceinline__ void pc_group(uint32_t &ha, uint32_t &hb, uint32_t &e
     constexpr uint32_t JJA = ((uint32_t)(4 * G - 1) & 0xffffu) | ((uint32_t)(4 * G) << 16);
     constexpr uint32_t JJB = (uint32_t)(4 * G + 1) | ((uint32_t)(4 * G + 2) << 16);
     constexpr int R0 = (G == 0) ? -1 : 4 * G;   // no reset entering column 0 (the boundary)
-    uint32_t y, sa, sb, ta, tb, xa, xb, c0, c1, c2, pa, pb, st;
+    uint32_t y, sa, sb, ta, tb, xa, xb, c0, c1, c2, pa, pb;
     if constexpr (G == 0) {
         // slot 0 holds the column-0 boundary, not a cell: its key half is 0 (c0 << 24 | 0)
         PC_GROUP_ASM("v_lshl_or_b32 %[pa], %[c0], 24, 0\n\t",
@@ -365,14 +370,16 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             const int uhi = __builtin_amdgcn_readfirstlane(emax);                // max end
             const int flo = __builtin_amdgcn_readfirstlane(max(0, i - wl_min));  // max beg
             const int fhi = __builtin_amdgcn_readfirstlane(emin);                // min end
-            r.glo = ulo >> 2;
-            r.gsp = max(min(uhi, QMAX - 1) / 4 - r.glo, -1);
+            const int glo = ulo >> 2;
+            const int gsp = max(min(uhi, QMAX - 1) / 4 - glo, -1);
             // FAST needs 4G > every beg (entering chain valid) -- or one common beg == 4G with
             // nothing computed before it -- and 4G + 4 <= every end
-            r.gfa = (ulo == flo && (flo & 3) == 0) ? (flo >> 2) : (flo >> 2) + 1;
-            r.gfn = max((fhi >> 2) - r.gfa, 0);
-            r.gla = ulo >> 2;
-            r.gln = (flo >> 2) - r.gla;
+            const int gfa = (ulo == flo && (flo & 3) == 0) ? (flo >> 2) : (flo >> 2) + 1;
+            const int gfn = max((fhi >> 2) - gfa, 0);
+            const int gln = (flo >> 2) - glo;
+            r.enter = gbits(glo, gsp + 1);
+            r.fast = gbits(gfa, gfn);
+            r.left = gbits(glo, gln + 1);
         }
         if (act) {
             if ((i & 3) == 0) {            // new 4-row block: 4 target bases from LDS
