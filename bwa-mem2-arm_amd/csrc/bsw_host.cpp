@@ -783,6 +783,15 @@ void *pinned_acquire(bsw_ctx_t *ctx, int which, size_t bytes)
 
 void pinned_release(bsw_ctx_t *ctx, int which) { ctx->pin[which & 1].mu.unlock(); }
 
+// reads per extension call chunk: the int32-offset bound, optionally lowered by the environment
+// (BSW_EXT_CHUNK_READS, tests only: exercises the chunked paths at small sizes)
+int64_t ext_chunk_cap()
+{
+    const char *e = getenv("BSW_EXT_CHUNK_READS");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (int64_t)v : (int64_t)INT32_MAX;
+}
+
 void set_ext_stats(bsw_ctx_t *ctx, const bsw_ext_stats_t &s)
 {
     std::lock_guard<std::mutex> g(ctx->stats_mu);
@@ -1142,7 +1151,8 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
         xp.ref_len = dc.refres_len;
         if ((int64_t)xp.tstride > BSW_MAX_LEN) return BSW_E_RANGE;
         // SeqPair idr / idq are int32: chunk so i * tstride stays below 2^31
-        const int32_t chunk = (int32_t)std::min<int64_t>(n, (int64_t)INT32_MAX / xp.tstride - 1);
+        const int32_t chunk = (int32_t)std::min<int64_t>(std::min<int64_t>(n, (int64_t)INT32_MAX / xp.tstride - 1),
+                                                         bsw::ext_chunk_cap());
         BSW_TRY(bsw::grow(s.d_xpairs, s.cap_xpairs, (size_t)chunk));
         BSW_TRY(bsw::grow(s.d_xsub, s.cap_xsub, (size_t)chunk));
         BSW_TRY(bsw::grow(s.d_xst, s.cap_xst, (size_t)chunk));

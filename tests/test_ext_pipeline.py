@@ -229,3 +229,22 @@ def test_gpu_device_pipeline_edges():
     with pytest.raises(bsw.BswError):
         bsw.extend_seeds_resident(eng, reads, off, lens, bad, opt)
     eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pipelines_chunked(monkeypatch):
+    """Calls split into read chunks (the int32 SeqPair-offset guard that applies above ~3.9M reads,
+    forced small by BSW_EXT_CHUNK_READS) give the unsplit results on both pipeline forms."""
+    ref, reads, off, lens, seeds, _ = _workload(5_000, seed=5, ref_len=500_000, p_sub=0.03, p_indel=0.005)
+    opt = bsw.ext_opt()
+    want = oracle.extend_seeds(oracle.make_params(), opt, ref, reads, off, lens, seeds)
+    monkeypatch.setenv("BSW_EXT_CHUNK_READS", "1234")
+    eng = bsw.Engine()
+    host = bsw.extend_seeds(eng, ref, reads, off, lens, seeds, opt)
+    st = bsw.ext_last_stats(eng)
+    assert st.n_pairs[0] > 0 and st.n_pairs[2] > 0                 # aggregated over the chunks
+    bsw.set_reference(eng, ref)
+    dev = bsw.extend_seeds_resident(eng, reads, off, lens, seeds, opt)
+    _same(want, host, "host-built pipeline, chunked")
+    _same(want, dev, "device pipeline, chunked")
+    eng.close()
