@@ -172,6 +172,11 @@ struct Slot {
     SeqPair *d_xpairs = nullptr, *d_xsub = nullptr; size_t cap_xpairs = 0, cap_xsub = 0;
     uint8_t *d_xq = nullptr, *d_xt = nullptr; size_t cap_xq = 0, cap_xt = 0;
     ExtState *d_xst = nullptr; size_t cap_xst = 0;
+    // class launches of one batch fork over side streams (independent pairs; small batches are
+    // bound by the longest wave of each class, so classes run side by side instead of in turn)
+    static constexpr int kSide = 3;
+    hipStream_t side[kSide] = {};
+    hipEvent_t evf = nullptr, evj[kSide] = {};
     bool timed = false;
     bsw_stats_t stats{};
 };
@@ -229,6 +234,11 @@ struct DeviceCtx {
         if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         if (s->stream) (void)hipStreamDestroy(s->stream);
+        for (int k = 0; k < Slot::kSide; ++k) {
+            if (s->side[k]) (void)hipStreamDestroy(s->side[k]);
+            if (s->evj[k]) (void)hipEventDestroy(s->evj[k]);
+        }
+        if (s->evf) (void)hipEventDestroy(s->evf);
     }
     std::unique_ptr<Slot> acquire(int &rc)
     {
@@ -366,13 +376,32 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     for (int sl = 0; sl < kMetaSpread; ++sl)
         for (int c = 0; c < kNumClasses; ++c) counts[c] += s.h_meta[sl * kMetaCounts + c];
     const int32_t maxq_wide = s.h_meta[kMetaMaxq];
-    // DP kernels, one launch per non-empty class; event-timed as the hot region
+    // DP kernels, one launch per non-empty class; event-timed as the hot region.  With more than
+    // one class the launches fork over the slot's side streams and join back on `stream`.
+    int nclass = 0;
+    for (int c = 0; c < kNumClasses; ++c) nclass += counts[c] > 0;
+    const bool fork = nclass > 1 && getenv("BSW_NO_FORK") == nullptr;
     BSW_TRY(hipEventRecord(s.ev0, stream));
+    if (fork) {
+        if (!s.evf) BSW_TRY(hipEventCreateWithFlags(&s.evf, hipEventDisableTiming));
+        for (int k = 0; k < Slot::kSide; ++k)
+            if (!s.side[k]) {
+                BSW_TRY(hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking));
+                BSW_TRY(hipEventCreateWithFlags(&s.evj[k], hipEventDisableTiming));
+            }
+        BSW_TRY(hipEventRecord(s.evf, stream));
+        for (int k = 0; k < Slot::kSide; ++k) BSW_TRY(hipStreamWaitEvent(s.side[k], s.evf, 0));
+    }
+    int nl = 0;                        // launch k runs on stream k mod (1 + kSide)
+    auto next_stream = [&]() {
+        const int k = nl++ % (1 + Slot::kSide);
+        return (fork && k > 0) ? s.side[k - 1] : stream;
+    };
     int32_t off = 0;
     for (int c = 0; c < kNumLaneClasses; ++c) {
         if (counts[c] > 0) {
             BSW_TRY(launch_lane_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, counts[c],
-                                       d_ref, d_qer, d_err, stream));
+                                       d_ref, d_qer, d_err, next_stream()));
             s.stats.n_launches++;
             s.stats.n_i16 += counts[c];
         }
@@ -383,10 +412,10 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
         if (np > 0) {
             if (route8 == 1)
                 BSW_TRY(launch_pk_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
-                                         d_err, stream));
+                                         d_err, next_stream()));
             else
                 BSW_TRY(launch_pc_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
-                                         d_err, stream));
+                                         d_err, next_stream()));
             s.stats.n_launches++;
             s.stats.n_packed += np;
             if (cell_bits == 8) s.stats.n_u8 += np;
@@ -399,10 +428,15 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
         const size_t need = (size_t)(maxq_wide + 2) * (size_t)nw;
         BSW_TRY(grow(s.d_scratch, s.cap_scratch, need));
         BSW_TRY(launch_wide_kernel(kp, w, d_pairs, s.d_order + off, nw, d_ref, d_qer, s.d_scratch,
-                                   nw, stream));
+                                   nw, next_stream()));
         s.stats.n_launches++;
         s.stats.n_wide += nw;
     }
+    if (fork)
+        for (int k = 0; k < Slot::kSide; ++k) {
+            BSW_TRY(hipEventRecord(s.evj[k], s.side[k]));
+            BSW_TRY(hipStreamWaitEvent(stream, s.evj[k], 0));
+        }
     BSW_TRY(hipEventRecord(s.ev1, stream));
     s.timed = true;
     return BSW_OK;
