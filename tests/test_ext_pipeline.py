@@ -248,3 +248,20 @@ def test_gpu_pipelines_chunked(monkeypatch):
     _same(want, host, "host-built pipeline, chunked")
     _same(want, dev, "device pipeline, chunked")
     eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pipelines_no_fork(monkeypatch):
+    """Class launches run serially on the caller's stream (BSW_NO_FORK=1) give the forked
+    results on both pipeline forms."""
+    ref, reads, off, lens, seeds, _ = _workload(3_000, seed=6, ref_len=400_000, p_sub=0.03, p_indel=0.005)
+    opt = bsw.ext_opt()
+    want = oracle.extend_seeds(oracle.make_params(), opt, ref, reads, off, lens, seeds)
+    monkeypatch.setenv("BSW_NO_FORK", "1")
+    eng = bsw.Engine()
+    host = bsw.extend_seeds(eng, ref, reads, off, lens, seeds, opt)
+    bsw.set_reference(eng, ref)
+    dev = bsw.extend_seeds_resident(eng, reads, off, lens, seeds, opt)
+    _same(want, host, "host-built pipeline, no fork")
+    _same(want, dev, "device pipeline, no fork")
+    eng.close()

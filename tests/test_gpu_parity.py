@@ -82,6 +82,27 @@ def test_random_mixed_shapes(eng, w):
     assert st.n_i16 + st.n_u8 + st.n_wide == len(pairs)
 
 
+@pytest.mark.parametrize("no_fork", [False, True])
+def test_class_launch_fork(eng, monkeypatch, no_fork):
+    """A batch spanning every kernel class (short/long queries up to the wide kernel) gives the
+    oracle's results whether its class launches fork over the slot's side streams (default) or
+    run serially on the caller's stream (BSW_NO_FORK=1, read per call)."""
+    if no_fork:
+        monkeypatch.setenv("BSW_NO_FORK", "1")
+    else:
+        monkeypatch.delenv("BSW_NO_FORK", raising=False)
+    pairs, ref, qer = bswgen.random_pairs(4000, seed=77, tlen=(0, 700), qlen=(0, 400))
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    for _ in range(2):                                  # second call reuses the side streams
+        got[:] = pairs
+        eng.get_scores(got, ref, qer, 100)
+        _assert_same(want, got, f"class launches no_fork={no_fork}")
+    st = eng.last_stats()
+    assert st.n_launches >= 3 and st.n_wide > 0
+    assert st.n_i16 + st.n_u8 + st.n_wide == len(pairs)
+
+
 def test_long_queries_wide_kernel(eng):
     pairs, ref, qer = bswgen.random_pairs(300, seed=9, tlen=(100, 700), qlen=(161, 600))
     want, got = pairs.copy(), pairs.copy()
