@@ -135,7 +135,7 @@ extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const 
         for (int32_t i = 0; i < n; ++i) maxlen = std::max<int64_t>(maxlen, read_len[i]);
         const int64_t per_read = maxlen + ((int64_t)opt->w << 2) + 2;
         int64_t chunk = std::max<int64_t>(1, (int64_t)INT32_MAX / per_read - 1);
-        chunk = std::min<int64_t>(chunk, bsw::ext_chunk_cap());     // test knob BSW_EXT_CHUNK_READS
+        chunk = std::min<int64_t>(chunk, bsw::ext_chunk_cap(ctx));  // BSW_OPT_EXT_CHUNK
         if (n > chunk) {
             bsw_ext_stats_t agg{};
             for (int64_t a0 = 0; a0 < n; a0 += chunk) {

@@ -38,14 +38,14 @@ __global__ void ext_scan_kernel(const int32_t *__restrict__ read_len, const bsw_
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     int l = 0, err = 0, nl = 0, nr = 0;
     if (i < n) {
-        l = read_len[i];
         const bsw_seed_t s = seeds[i];
-        if (l < 0 || l > BSW_MAX_LEN) {
-            err = 1;
-            l = 0;
-        } else if (s.len > 0) {
-            if (s.qbeg < 0 || s.qbeg + s.len > l || s.rbeg < 0 || s.rbeg + s.len > ref_len) err = 1;
-            else {
+        if (s.len > 0) {            // only seeded reads are validated and sized (as bsw_extend_seeds)
+            l = read_len[i];
+            if (l < 0 || l > BSW_MAX_LEN || s.qbeg < 0 || s.qbeg + s.len > l || s.rbeg < 0 ||
+                s.rbeg + s.len > ref_len) {
+                err = 1;
+                l = 0;
+            } else {
                 nl = s.qbeg > 0;
                 nr = s.qbeg + s.len < l;
             }

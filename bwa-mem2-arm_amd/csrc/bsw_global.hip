@@ -38,7 +38,7 @@ constexpr int32_t kGMinusInf = -0x40000000;   // upstream MINUS_INF
 
 // Routing: the column kernel when the job fits it (measured faster on bwa-shaped jobs: 9.55 vs
 // 9.76 ms per 1M 150-bp jobs), else the band kernel when 2w + 2 <= 96, else the wide kernel;
-// gp.prefer_band (BSW_GLOB_BAND=1) puts every band-eligible job on the band kernel.
+// gp.prefer_band (BSW_OPT_GLOB_BAND) puts every band-eligible job on the band kernel.
 __device__ __forceinline__ int glob_class(const SeqPair &p, const GlobParams &gp)
 {
     const int q = p.len2, t = p.len1, w = p.h0;

@@ -12,7 +12,7 @@ struct GlobParams {
     int32_t maxabs;             // max |mat| -- the int16 safety bound of the register kernel
     uint32_t prof[8][2];        // prof[t] = score bytes mat[t][q], q = 0..4; q = 5..7 score as N
     int8_t mat[25];
-    int8_t prefer_band;         // route band-eligible jobs to the band kernel (BSW_GLOB_BAND=1)
+    int8_t prefer_band;         // route band-eligible jobs to the band kernel (BSW_OPT_GLOB_BAND)
 };
 
 // Job classes: band-coordinate register kernel (int32 cells, 2w + 2 <= BW slots), column

@@ -25,6 +25,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 #include "../../include/bsw.h"
@@ -78,10 +79,10 @@ __device__ __forceinline__ int seed_matches(const uint8_t *__restrict__ q, int q
 
 // Per pair: class + sort key.  Lane classes need qlen <= QMAX and int16-safe scores.
 __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_t maxsc,
-                            int32_t route8, const uint8_t *__restrict__ ref,
+                            int32_t pc_route, const uint8_t *__restrict__ ref,
                             const uint8_t *__restrict__ qer, uint32_t *__restrict__ keys,
                             int32_t *__restrict__ vals, int32_t *__restrict__ counts,
-                            int32_t *__restrict__ maxq_wide, int keymode)
+                            int32_t *__restrict__ maxq_wide, int keymode, int misroute)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < n;
@@ -97,13 +98,11 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
         else if (qlen <= 128) c = 3;
         else if (qlen <= 160) c = 4;
         // 8-bit score regime (key H << 8 | j fits 16 bits, H <= h0 + min(qlen, tlen)) -> the
-        // packed-column kernel (route 2: needs qlen < QMAX, so bucket by qlen + 1) or the
-        // two-pairs-per-lane kernel (route 1)
-        if (route8 && c < kNumLaneClasses && p.h0 + min(qlen, tlen) <= 255) {
-            if (route8 == 1) c += kPkClass0;
-            else if (qlen + 1 <= 160) c = kPkClass0 + (qlen + 1 <= 32 ? 0 : qlen + 1 <= 64 ? 1 : qlen + 1 <= 96 ? 2 : qlen + 1 <= 128 ? 3 : 4);
-        }
+        // packed-column kernel (needs qlen < QMAX: bucket by qlen + 1)
+        if (pc_route && c < kNumLaneClasses && p.h0 + min(qlen, tlen) <= 255 && qlen + 1 <= 160)
+            c = kPkClass0 + (qlen + 1 <= 32 ? 0 : qlen + 1 <= 64 ? 1 : qlen + 1 <= 96 ? 2 : qlen + 1 <= 128 ? 3 : 4);
     }
+    if (misroute) c = 0;          // BSW_OPT_TEST_MISROUTE: the QMAX=32 lane kernel's guard must trip
     if (valid) {
         if (c == kWideClass) atomicMax(maxq_wide, qlen);
         // (class, qlen desc, related first, tlen desc, h0 desc): like-shaped pairs share a
@@ -178,6 +177,7 @@ struct Slot {
     hipStream_t side[kSide] = {};
     hipEvent_t evf = nullptr, evj[kSide] = {};
     bool timed = false;
+    hipStream_t run_stream = nullptr;   // stream of the last run_device (finish_stats waits on it)
     bsw_stats_t stats{};
 };
 
@@ -209,6 +209,7 @@ struct DeviceCtx {
     std::vector<std::unique_ptr<Slot>> free_slots;
     uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
     int64_t refres_len = -1;
+    std::shared_mutex refmu;            // extension calls hold it shared while they use d_refres
 
     ~DeviceCtx()
     {
@@ -281,6 +282,8 @@ struct bsw_ctx {
     bsw_mate_stats_t mate_last{};
     bsw_global_stats_t glob_last{};
     struct Pinned { std::mutex mu; void *p = nullptr; size_t cap = 0; } pin[2];
+    int glob_band = 0;                  // BSW_OPT_GLOB_BAND
+    int64_t ext_chunk = 0;              // BSW_OPT_EXT_CHUNK (0: the int32-offset bound)
     ~bsw_ctx()
     {
         for (auto &b : pin)
@@ -307,10 +310,8 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
         kp.prof[t][0] = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
         kp.prof[t][1] = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
     }
-    // packed kernel scoring contract (bsw_pk.hip): match 1, one mismatch value in [-127, -1],
-    // every N entry -1, symmetric gap penalties.  Used for cell_bits = 8 calls; on 16-bit calls
-    // only with BSW_PK=1 (at one wave per SIMD it measures slower than the lane kernel on C2,
-    // DESIGN.md §4.2).
+    // packed-column kernel scoring contract (bsw_pc.hip): match 1, one mismatch value in
+    // [-127, -1], every N entry -1, symmetric gap penalties.
     bool ok = p.o_del == p.o_ins && p.e_del == p.e_ins && p.e_del > 0 && p.o_del + p.e_del < 16384;
     const int mis = p.mat[1];
     ok = ok && mis < 0 && mis >= -127;
@@ -320,14 +321,11 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
             ok = (a == 4 || b == 4) ? v == -1 : (a == b ? v == 1 : v == mis);
         }
     kp.pk_ok = ok ? 1 : 0;
-    // 8-bit-regime routing: 2 = packed-column kernel (default, both cell widths), 1 = the
-    // two-pairs-per-lane kernel (BSW_PK=1), 0 = the lane kernel (16-bit calls with BSW_PC=0)
-    const char *pk = getenv("BSW_PK"), *pc = getenv("BSW_PC");
-    const bool pk_on = pk && pk[0] == '1', pc_off = pc && pc[0] == '0';
-    kp.route16 = pk_on ? 1 : pc_off ? 0 : 2;
-    const char *km = getenv("BSW_SORTKEY");
-    kp.keymode = (km && km[0] == '0') ? 0 : 2;
-    kp.route8 = (pk_on || pc_off) ? 1 : 2;
+    // routing / scheduling defaults; bsw_set_option changes them per context
+    kp.kern8 = 1;
+    kp.keymode = 2;
+    kp.misroute = 0;
+    kp.fork = 1;
 }
 
 // keys / keys2 / vals / order (radix-sort buffers) grow together
@@ -347,22 +345,28 @@ static hipError_t grow_sort(Slot &s, int32_t n)
 }
 
 // The device pipeline on one slot's device; d_* are device pointers valid on `stream`.
+// Enqueues plan -> sort -> (one class-count readback) -> DP kernels -> a readback of the
+// kernels' range-guard word into h_meta[kMetaErr]; finish_stats() waits for it and turns a
+// tripped guard into BSW_E_RANGE.
 static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_t *d_ref,
                       const uint8_t *d_qer, int32_t n, int32_t w, int cell_bits, hipStream_t stream)
 {
+    (void)cell_bits;      // 8 and 16 route alike: the cell width is the planner's per-pair choice
     s.stats = bsw_stats_t{};
+    s.timed = false;
+    s.run_stream = stream;
     if (n == 0) return BSW_OK;
     BSW_TRY(grow_sort(s, n));
     BSW_TRY(hipMemsetAsync(s.d_meta, 0, kMetaWords * sizeof(int32_t), stream));
     int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaMaxq, *d_err = s.d_meta + kMetaErr;
     // pairs in the 8-bit score regime (h0 + min(qlen, tlen) <= 255, bwa-style scoring) take the
     // packed-column kernel on both entry points (getScores8 / getScores16: identical results,
-    // fewer instructions per cell), the rest the int16 kernels (cell_bits = 8: the overflow
-    // fallback); BSW_PK=1 / BSW_PC=0 select the older kernels for those pairs
-    const int route8 = kp.pk_ok ? (cell_bits == 8 ? kp.route8 : kp.route16) : 0;
+    // fewer instructions per cell), the rest the int16 lane kernel (on cell_bits = 8: the
+    // overflow fallback) or the int32 wide kernel
+    const int pc_route = (kp.pk_ok && kp.kern8) ? 1 : 0;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       d_pairs, n, kp.maxsc, route8, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
-                       d_maxq, kp.keymode);
+                       d_pairs, n, kp.maxsc, pc_route, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
+                       d_maxq, (int)kp.keymode, (int)kp.misroute);
     BSW_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
     BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals,
@@ -380,7 +384,7 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     // one class the launches fork over the slot's side streams and join back on `stream`.
     int nclass = 0;
     for (int c = 0; c < kNumClasses; ++c) nclass += counts[c] > 0;
-    const bool fork = nclass > 1 && getenv("BSW_NO_FORK") == nullptr;
+    const bool fork = nclass > 1 && kp.fork;
     BSW_TRY(hipEventRecord(s.ev0, stream));
     if (fork) {
         if (!s.evf) BSW_TRY(hipEventCreateWithFlags(&s.evf, hipEventDisableTiming));
@@ -397,59 +401,70 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
         const int k = nl++ % (1 + Slot::kSide);
         return (fork && k > 0) ? s.side[k - 1] : stream;
     };
-    int32_t off = 0;
-    for (int c = 0; c < kNumLaneClasses; ++c) {
-        if (counts[c] > 0) {
-            BSW_TRY(launch_lane_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, counts[c],
-                                       d_ref, d_qer, d_err, next_stream()));
-            s.stats.n_launches++;
-            s.stats.n_i16 += counts[c];
+    // every launch of the fork; the join below runs whatever happens here, so no side stream
+    // can still be reading this slot's buffers when the slot goes back to the pool
+    const int lrc = [&]() -> int {
+        int32_t off = 0;
+        for (int c = 0; c < kNumLaneClasses; ++c) {
+            if (counts[c] > 0) {
+                BSW_TRY(launch_lane_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, counts[c],
+                                           d_ref, d_qer, d_err, next_stream()));
+                s.stats.n_launches++;
+                s.stats.n_i16 += counts[c];
+            }
+            off += counts[c];
         }
-        off += counts[c];
-    }
-    for (int c = 0; c < kNumLaneClasses; ++c) {
-        const int32_t np = counts[kPkClass0 + c];
-        if (np > 0) {
-            if (route8 == 1)
-                BSW_TRY(launch_pk_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
-                                         d_err, next_stream()));
-            else
+        for (int c = 0; c < kNumLaneClasses; ++c) {
+            const int32_t np = counts[kPkClass0 + c];
+            if (np > 0) {
                 BSW_TRY(launch_pc_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
                                          d_err, next_stream()));
-            s.stats.n_launches++;
-            s.stats.n_packed += np;
-            if (cell_bits == 8) s.stats.n_u8 += np;
-            else s.stats.n_i16 += np;
+                s.stats.n_launches++;
+                s.stats.n_packed += np;
+                if (cell_bits == 8) s.stats.n_u8 += np;
+                else s.stats.n_i16 += np;
+            }
+            off += np;
         }
-        off += np;
-    }
-    if (counts[kWideClass] > 0) {
-        const int32_t nw = counts[kWideClass];
-        const size_t need = (size_t)(maxq_wide + 2) * (size_t)nw;
-        BSW_TRY(grow(s.d_scratch, s.cap_scratch, need));
-        BSW_TRY(launch_wide_kernel(kp, w, d_pairs, s.d_order + off, nw, d_ref, d_qer, s.d_scratch,
-                                   nw, next_stream()));
-        s.stats.n_launches++;
-        s.stats.n_wide += nw;
-    }
+        if (counts[kWideClass] > 0) {
+            const int32_t nw = counts[kWideClass];
+            const size_t need = (size_t)(maxq_wide + 2) * (size_t)nw;
+            BSW_TRY(grow(s.d_scratch, s.cap_scratch, need));
+            BSW_TRY(launch_wide_kernel(kp, w, d_pairs, s.d_order + off, nw, d_ref, d_qer, s.d_scratch,
+                                       nw, next_stream()));
+            s.stats.n_launches++;
+            s.stats.n_wide += nw;
+        }
+        return BSW_OK;
+    }();
     if (fork)
         for (int k = 0; k < Slot::kSide; ++k) {
             BSW_TRY(hipEventRecord(s.evj[k], s.side[k]));
             BSW_TRY(hipStreamWaitEvent(stream, s.evj[k], 0));
         }
+    if (lrc) {
+        (void)hipStreamSynchronize(stream);         // drain what was queued before the failure
+        return lrc;
+    }
     BSW_TRY(hipEventRecord(s.ev1, stream));
+    // the DP kernels' range guard (a pair routed to a class that cannot hold it) -> host,
+    // after every DP launch of this batch
+    BSW_TRY(hipMemcpyAsync(s.h_meta + kMetaErr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
     s.timed = true;
     return BSW_OK;
 }
 
+// Wait for run_device's work (through the guard readback), record the DP kernel time; a
+// tripped range guard is BSW_E_RANGE (the affected pairs' outputs were not written).
 static int finish_stats(Slot &s)
 {
     if (s.timed) {
         float ms = 0.f;
-        BSW_TRY(hipEventSynchronize(s.ev1));
+        s.timed = false;
+        BSW_TRY(hipStreamSynchronize(s.run_stream));
         BSW_TRY(hipEventElapsedTime(&ms, s.ev0, s.ev1));
         s.stats.kernel_ms = ms;
-        s.timed = false;
+        if (s.h_meta[kMetaErr] != 0) return BSW_E_RANGE;
     }
     return BSW_OK;
 }
@@ -485,9 +500,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         int r = run_device(kp, s, s.d_pairs, s.d_ref - r_lo, s.d_qer - q_lo, n, w, cell_bits, s.stream);
         if (r) return r;
         BSW_TRY(hipMemcpyAsync(pairs, s.d_pairs, (size_t)n * sizeof(SeqPair), hipMemcpyDeviceToHost, s.stream));
-        BSW_TRY(hipStreamSynchronize(s.stream));
-        if ((r = finish_stats(s))) return r;
-        if (s.h_meta[kMetaErr] != 0) return BSW_E_RANGE;   // kernel guard tripped (routing bug)
+        if ((r = finish_stats(s))) return r;             // also BSW_E_RANGE: kernel guard tripped
         if (st) *st = s.stats;
         return BSW_OK;
     }();
@@ -569,7 +582,7 @@ static int mate_device(const MateParams &mp, Slot &s, const SeqPair *d_pairs, co
 }
 
 // ---------------------------------------------------------------- global alignment (bsw_global.h)
-static void make_glob_params(const bsw_params_t &p, GlobParams &gp)
+static void make_glob_params(const bsw_params_t &p, int prefer_band, GlobParams &gp)
 {
     memset(&gp, 0, sizeof(gp));
     gp.o_del = p.o_del; gp.e_del = p.e_del; gp.o_ins = p.o_ins; gp.e_ins = p.e_ins;
@@ -578,8 +591,7 @@ static void make_glob_params(const bsw_params_t &p, GlobParams &gp)
     for (int i = 0; i < 25; ++i) mx = std::max(mx, std::abs((int)p.mat[i]));
     gp.maxabs = mx;
     memcpy(gp.mat, p.mat, 25);
-    const char *band = getenv("BSW_GLOB_BAND");
-    gp.prefer_band = (band && band[0] == '1') ? 1 : 0;
+    gp.prefer_band = prefer_band ? 1 : 0;
     for (int t = 0; t < 8; ++t) {                        // codes > 4 score as N (as prof in KParams)
         const int tt = std::min(t, 4);
         uint8_t b[8];
@@ -817,13 +829,11 @@ void *pinned_acquire(bsw_ctx_t *ctx, int which, size_t bytes)
 
 void pinned_release(bsw_ctx_t *ctx, int which) { ctx->pin[which & 1].mu.unlock(); }
 
-// reads per extension call chunk: the int32-offset bound, optionally lowered by the environment
-// (BSW_EXT_CHUNK_READS, tests only: exercises the chunked paths at small sizes)
-int64_t ext_chunk_cap()
+// reads per extension call chunk: the int32-offset bound, optionally lowered per context
+// (BSW_OPT_EXT_CHUNK: exercises the chunked paths at small sizes)
+int64_t ext_chunk_cap(const bsw_ctx_t *ctx)
 {
-    const char *e = getenv("BSW_EXT_CHUNK_READS");
-    const long long v = e ? atoll(e) : 0;
-    return v > 0 ? (int64_t)v : (int64_t)INT32_MAX;
+    return ctx->ext_chunk > 0 ? ctx->ext_chunk : (int64_t)INT32_MAX;
 }
 
 void set_ext_stats(bsw_ctx_t *ctx, const bsw_ext_stats_t &s)
@@ -874,7 +884,6 @@ int bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref
         int r = bsw::run_device(ctx->kp, *slot, d_pairs, d_ref, d_qer, n, w, cell_bits, st);
         if (r) return r;
         if ((r = bsw::finish_stats(*slot))) return r;
-        if (slot->h_meta[bsw::kMetaErr] != 0) return BSW_E_RANGE;
         std::lock_guard<std::mutex> g(ctx->stats_mu);
         ctx->last = slot->stats;
         return BSW_OK;
@@ -1015,7 +1024,7 @@ int bsw_ksw_global2_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_re
         return BSW_E_INVAL;
     if (n == 0) return BSW_OK;
     bsw::GlobParams gp;
-    bsw::make_glob_params(ctx->params, gp);
+    bsw::make_glob_params(ctx->params, ctx->glob_band, gp);
     bsw::DeviceCtx &dc = *ctx->devs[0];
     int rc = BSW_OK;
     auto slot = dc.acquire(rc);
@@ -1100,7 +1109,7 @@ int bsw_ksw_global2(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef, co
             pairs[i].idr < 0 || pairs[i].idq < 0 || pairs[i].h0 < 0)
             return BSW_E_RANGE;
     bsw::GlobParams gp;
-    bsw::make_glob_params(ctx->params, gp);
+    bsw::make_glob_params(ctx->params, ctx->glob_band, gp);
     std::vector<bsw_global_stats_t> st(ctx->devs.size());
     const int rc = bsw::shard_devices(ctx, n, [&](int d, int32_t a, int32_t b) {
         return bsw::glob_host_shard(gp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a,
@@ -1132,7 +1141,7 @@ int bsw_set_reference(bsw_ctx_t *ctx, const uint8_t *ref, int64_t ref_len)
     if (!ctx || ref_len < 0 || (ref_len > 0 && !ref)) return BSW_E_INVAL;
     for (auto &dcp : ctx->devs) {
         bsw::DeviceCtx &dc = *dcp;
-        std::lock_guard<std::mutex> g(dc.mu);
+        std::unique_lock<std::shared_mutex> g(dc.refmu);   // waits for running extension calls
         BSW_TRY(hipSetDevice(dc.device));
         if (dc.d_refres) (void)hipFree(dc.d_refres);
         dc.d_refres = nullptr;
@@ -1152,6 +1161,7 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
         return BSW_E_INVAL;
     if (opt->w < 0 || opt->max_band_try < 1) return BSW_E_INVAL;
     bsw::DeviceCtx &dc = *ctx->devs[0];
+    std::shared_lock<std::shared_mutex> refg(dc.refmu);   // the resident reference stays put
     if (!dc.d_refres) return BSW_E_INVAL;
     if (n == 0) return BSW_OK;
     const auto t0 = std::chrono::steady_clock::now();
@@ -1186,7 +1196,7 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
         if ((int64_t)xp.tstride > BSW_MAX_LEN) return BSW_E_RANGE;
         // SeqPair idr / idq are int32: chunk so i * tstride stays below 2^31
         const int32_t chunk = (int32_t)std::min<int64_t>(std::min<int64_t>(n, (int64_t)INT32_MAX / xp.tstride - 1),
-                                                         bsw::ext_chunk_cap());
+                                                         bsw::ext_chunk_cap(ctx));
         BSW_TRY(bsw::grow(s.d_xpairs, s.cap_xpairs, (size_t)chunk));
         BSW_TRY(bsw::grow(s.d_xsub, s.cap_xsub, (size_t)chunk));
         BSW_TRY(bsw::grow(s.d_xst, s.cap_xst, (size_t)chunk));
@@ -1210,6 +1220,21 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
     es.engine_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     bsw::set_ext_stats(ctx, es);
     return BSW_OK;
+}
+
+int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
+{
+    if (!ctx) return BSW_E_INVAL;
+    const bool b01 = value == 0 || value == 1;
+    switch (option) {
+    case BSW_OPT_KERNEL8: if (!b01) return BSW_E_INVAL; ctx->kp.kern8 = (int8_t)value; return BSW_OK;
+    case BSW_OPT_FORK: if (!b01) return BSW_E_INVAL; ctx->kp.fork = (int8_t)value; return BSW_OK;
+    case BSW_OPT_SORTKEY: if (!b01) return BSW_E_INVAL; ctx->kp.keymode = value ? 2 : 0; return BSW_OK;
+    case BSW_OPT_GLOB_BAND: if (!b01) return BSW_E_INVAL; ctx->glob_band = (int)value; return BSW_OK;
+    case BSW_OPT_EXT_CHUNK: if (value < 0) return BSW_E_INVAL; ctx->ext_chunk = value; return BSW_OK;
+    case BSW_OPT_TEST_MISROUTE: if (!b01) return BSW_E_INVAL; ctx->kp.misroute = (int8_t)value; return BSW_OK;
+    default: return BSW_E_INVAL;
+    }
 }
 
 int bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out)

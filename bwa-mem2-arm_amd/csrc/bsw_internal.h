@@ -15,6 +15,6 @@ void ctx_params(const bsw_ctx_t *ctx, bsw_params_t *out);
 void *pinned_acquire(bsw_ctx_t *ctx, int which, size_t bytes);
 void pinned_release(bsw_ctx_t *ctx, int which);
 void set_ext_stats(bsw_ctx_t *ctx, const bsw_ext_stats_t &s);
-int64_t ext_chunk_cap();
+int64_t ext_chunk_cap(const bsw_ctx_t *ctx);   // reads per extension chunk (BSW_OPT_EXT_CHUNK)
 int get_ext_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out);
 }  // namespace bsw

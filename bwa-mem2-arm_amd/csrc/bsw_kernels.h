@@ -4,8 +4,6 @@
 //   lane kernel  : one LANE per SeqPair, the whole DP row of the pair (eh[0..qlen], packed
 //                  {h:16, e:16} per column) held in VGPRs; 64 pairs per wavefront advance
 //                  through their target rows in lock-step.  qlen <= QMAX (template), int16 cells.
-//   pk kernel    : TWO SeqPairs per lane (16-bit halves of every DP register), every step a
-//                  packed v_pk_* instruction; bwa-style scoring, scores < 256 (bsw_pk.hip).
 //   pc kernel    : one SeqPair per lane, the DP row as an H plane and an E plane packed two
 //                  columns per VGPR, column-independent steps as v_pk_* (bsw_pc.hip);
 //                  bwa-style scoring, scores < 256.  The default 8-bit-regime kernel.
@@ -23,13 +21,16 @@ struct KParams {
     int32_t o_del, e_del, o_ins, e_ins;
     int32_t zdrop, end_bonus;
     int32_t maxsc;              // max(0, max(mat)) -- A.2 band cap and the M-gate bound
-    int32_t pk_ok;              // scoring fits the packed kernel (match 1, mismatch -b, N -1,
-                                //   symmetric gaps); set by the host, see bsw_pk.hip
+    int32_t pk_ok;              // scoring fits the packed-column kernel (match 1, mismatch -b,
+                                //   N -1, symmetric gaps); set by the host, see bsw_pc.hip
     uint32_t prof[8][2];        // prof[t] = 8 score bytes mat[t][q], q = 0..7 (q>4 -> ambig)
     int8_t mat[25];
-    int8_t route16, route8;     // host: kernel for 8-bit-regime pairs on 16-bit / 8-bit calls
-                                //   (2 = packed-column pc, 1 = two-pairs-per-lane pk, 0 = lane)
-    int8_t keymode;             // host: plan sort-key variant (BSW_SORTKEY)
+    int8_t kern8;               // host: 8-bit-regime pairs -> 1 packed-column kernel, 0 lane
+                                //   kernel (BSW_OPT_KERNEL8)
+    int8_t keymode;             // host: plan sort-key variant (BSW_OPT_SORTKEY)
+    int8_t fork;                // host: class launches fork over side streams (BSW_OPT_FORK)
+    int8_t misroute;            // host, tests only: every pair to the QMAX=32 lane class
+                                //   (BSW_OPT_TEST_MISROUTE: trips the kernels' range guard)
 };
 
 // qlen limit of the register-resident kernel instantiations.
@@ -41,13 +42,6 @@ constexpr int kLaneQmaxMax = 160;
 hipError_t launch_lane_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
                               const int32_t *order, int32_t n, const uint8_t *ref,
                               const uint8_t *qer, int32_t *err, hipStream_t s);
-
-// Packed two-pairs-per-lane kernel (bsw_pk.hip): kp.pk_ok scoring, qlen <= qmax (one of
-// kLaneQmax), h0 + min(len1, len2) <= 255 (the 8-bit score regime: this is the engine's
-// cell_bits = 8 path).  order[] slice as for the lane kernel; 128 pairs per wave.
-hipError_t launch_pk_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
-                            const int32_t *order, int32_t n, const uint8_t *ref,
-                            const uint8_t *qer, int32_t *err, hipStream_t s);
 
 // Packed-column lane kernel (bsw_pc.hip): kp.pk_ok scoring, qlen < qmax (strictly: slot qlen
 // must fall inside a 4-column group), h0 + min(len1, len2) <= 255; 64 pairs per wave.

@@ -24,22 +24,6 @@
 #include "bsw_kernels.h"
 #include "bsw_wave.h"
 
-// Timing-only experiment hooks (never defined in product builds): extra dummy instructions
-// injected into the fast group, writing temps that are dead at that point.
-#if defined(BSW_EXP_SDWA)
-#define BSW_EXP_EXTRA BSW_X4("v_min_i32_sdwa %[k0], sext(%[pw]), %[v0] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:WORD_0\n\t")
-#elif defined(BSW_EXP_PLAIN)
-#define BSW_EXP_EXTRA BSW_X4("v_min_i32_e32 %[k0], %[pw], %[v0]\n\t")
-#elif defined(BSW_EXP_VOP3)
-#define BSW_EXP_EXTRA BSW_X4("v_max3_i32 %[k0], %[pw], %[v0], 0\n\t")
-#elif defined(BSW_EXP_BRANCH)
-#define BSW_EXP_EXTRA "s_branch 7f\n7:\n\t"
-#elif defined(BSW_EXP_SALU)
-#define BSW_EXP_EXTRA BSW_X4("s_add_u32 %[st], %[st], 1\n\t")
-#else
-#define BSW_EXP_EXTRA
-#endif
-#define BSW_X4(x) x x x x x x x x x x x x x x x x
 
 #ifndef BSW_CELL_FENCE
 #define BSW_CELL_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -148,7 +132,6 @@ __device__ __forceinline__ void lane_group_asm(uint32_t &v0, uint32_t &v1, uint3
         "s_cmp_le_u32 %[st], %[gsp]\n\t"
         "s_cbranch_scc0 3f\n\t"
         "v_perm_b32 %[pw], %[phi], %[plo], %[q]\n\t"
-        BSW_EXP_EXTRA
         "v_sub_u32_sdwa %[x0], %[v0], %[ed] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
         "v_sub_u32_sdwa %[x1], %[v1], %[ed] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
         "v_sub_u32_sdwa %[x2], %[v2], %[ed] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
@@ -483,7 +466,11 @@ __global__ __launch_bounds__(64, 2) void lane_kernel(const KParams kp, const int
     int idr = 0, idq = 0, tlen = 0, qlen = 0, h0 = 0;
     if (valid) {
         idr = sp->idr; idq = sp->idq; tlen = sp->len1; qlen = sp->len2; h0 = sp->h0;
-        if (qlen > QMAX || qlen < 0 || tlen < 0) { atomicOr(err, 1); valid = false; }
+        if (qlen > QMAX || qlen < 0 || tlen < 0 || h0 < 0 ||
+            (int64_t)h0 + (int64_t)kp.maxsc * min(qlen, tlen) >= 32768) {   // int16 cells
+            atomicOr(err, 1);
+            valid = false;
+        }
     }
     // query codes -> perm selectors (4 per VGPR).  Aligned dword loads (a dword holding at
     // least one byte of the query never leaves that byte's page), all issued before use;
@@ -555,12 +542,8 @@ __global__ __launch_bounds__(64, 2) void lane_kernel(const KParams kp, const int
         endc = end;
         // uniform pass bounds: fast = [beg_u, min end) when every live lane shares beg,
         // edge = [fast_hi, max end] (or the whole [min beg, max end] otherwise)
-#ifdef BSW_EXP_NO_REDUCE
-        const int emax = 150, emin = 150;
-#else
         const int emax = wave_max(act ? end : -1);
         const int emin = wave_min(act ? end : INT_MAX);
-#endif
         LaneRow r;
         r.ulo = __builtin_amdgcn_readfirstlane(max(0, i - wl_max));      // min beg (live lanes)
         r.uhi = __builtin_amdgcn_readfirstlane(emax);                    // max end

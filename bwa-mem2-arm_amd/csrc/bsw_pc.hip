@@ -480,15 +480,12 @@ extern "C" int bsw_pc_stats(unsigned long long *out, int reset)
 #endif
 
 template <int QMAX>
-static void launch_pc_q(int wpb, const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order, int32_t n,
+static void launch_pc_q(const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order, int32_t n,
                         const uint8_t *ref, const uint8_t *qer, int32_t *err, hipStream_t s)
 {
-    if (wpb == 4)
-        hipLaunchKernelGGL((pc_kernel<QMAX, 4>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, kp, w, pairs,
-                           order, n, ref, qer, err);
-    else
-        hipLaunchKernelGGL((pc_kernel<QMAX, 1>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, kp, w, pairs, order,
-                           n, ref, qer, err);
+    // one wave per workgroup: a finished wave's slot and LDS are reused at once
+    hipLaunchKernelGGL((pc_kernel<QMAX, 1>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, kp, w, pairs, order,
+                       n, ref, qer, err);
 }
 
 hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
@@ -496,16 +493,12 @@ hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pai
                             const uint8_t *qer, int32_t *err, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
-    static const int wpb = [] {
-        const char *e = getenv("BSW_PC_WPB");
-        return (e && e[0] == '4') ? 4 : 1;
-    }();
     switch (qmax) {
-    case 32: launch_pc_q<32>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
-    case 64: launch_pc_q<64>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
-    case 96: launch_pc_q<96>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
-    case 128: launch_pc_q<128>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
-    case 160: launch_pc_q<160>(wpb, kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 32: launch_pc_q<32>(kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 64: launch_pc_q<64>(kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 96: launch_pc_q<96>(kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 128: launch_pc_q<128>(kp, w, pairs, order, n, ref, qer, err, s); break;
+    case 160: launch_pc_q<160>(kp, w, pairs, order, n, ref, qer, err, s); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -32,7 +32,11 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
                "bswb_write", "bswb_read_header", "bswb_read",
                "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats",
                "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
-               "bsw_set_reference", "bsw_extend_seeds_device")
+               "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option")
+
+# include/bsw.h engine options (bsw_set_option)
+OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK = 1, 2, 3, 4, 5
+OPT_TEST_MISROUTE = 100
 
 # include/bsw_ext.h structs
 SEED_DTYPE = np.dtype([("rbeg", np.int64), ("qbeg", np.int32), ("len", np.int32)])
@@ -115,11 +119,12 @@ def hip_lib():
         L.bsw_global_last_stats.argtypes = [P, P]
         L.bsw_set_reference.argtypes = [P, P, ctypes.c_int64]
         L.bsw_extend_seeds_device.argtypes = [P, P, P, P, P, P, ctypes.c_int32, P, P]
+        L.bsw_set_option.argtypes = [P, ctypes.c_int, ctypes.c_int64]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
                   "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
-                  "bsw_set_reference", "bsw_extend_seeds_device"):
+                  "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -137,11 +142,22 @@ def _ptr(a: np.ndarray):
 class Engine:
     """Python mirror of the C++ shim: one engine = one bsw_ctx_t."""
 
-    def __init__(self, params: Params | None = None, device: int = 0, n_gpus: int = 1):
+    def __init__(self, params: Params | None = None, device: int = 0, n_gpus: int = 1, **options):
         self.params = params if params is not None else default_params()
         self._ctx = ctypes.c_void_p()
         _check(hip_lib().bsw_create(ctypes.byref(self.params), device, n_gpus,
                                     ctypes.byref(self._ctx)))
+        for k, v in options.items():
+            self.set_option(k, v)
+
+    _OPTS = {"kernel8": OPT_KERNEL8, "fork": OPT_FORK, "sortkey": OPT_SORTKEY, "glob_band": OPT_GLOB_BAND,
+             "ext_chunk": OPT_EXT_CHUNK, "test_misroute": OPT_TEST_MISROUTE}
+
+    def set_option(self, name, value: int):
+        """bsw_set_option by name (kernel8, fork, sortkey, glob_band, ext_chunk, test_misroute)
+        or by BSW_OPT_* number."""
+        opt = self._OPTS[name] if isinstance(name, str) else int(name)
+        _check(hip_lib().bsw_set_option(self._ctx, opt, int(value)))
 
     def close(self):
         if self._ctx:

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BSW_ABI_VERSION 2
+#define BSW_ABI_VERSION 3
 
 enum {
     BSW_OK = 0,
@@ -97,6 +97,25 @@ typedef struct bsw_stats_t {
                                    kernels (v_pk_* cells; ABI version 2)                 */
 } bsw_stats_t;
 int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
+
+/* Engine options: tuning and test knobs of one context (no upstream counterpart; upstream
+ * has no such switches, so the defaults are the only production setting).  Set them before
+ * the context is used by concurrent callers.  Returns BSW_E_INVAL for an unknown option or
+ * an out-of-range value. */
+enum {
+    BSW_OPT_KERNEL8 = 1,      /* 8-bit-regime pairs (h0 + min(len1,len2) <= 255, bwa scoring):
+                                 1 = packed-column kernel (default), 0 = int16 lane kernel  */
+    BSW_OPT_FORK = 2,         /* a batch's class launches: 1 = fork over side streams
+                                 (default), 0 = serial on the call's stream                   */
+    BSW_OPT_SORTKEY = 3,      /* plan sort key: 1 = seed identities before h0 (default),
+                                 0 = h0 only (scheduling only; results never change)          */
+    BSW_OPT_GLOB_BAND = 4,    /* bsw_ksw_global2: 0 = column kernel first (default),
+                                 1 = band kernel for every band-eligible job                  */
+    BSW_OPT_EXT_CHUNK = 5,    /* extension calls: reads per chunk (0 = the int32-offset bound) */
+    BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
+                                 any longer query trips the kernels' range guard (BSW_E_RANGE) */
+};
+int  bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value);
 
 const char *bsw_strerror(int code);
 int  bsw_abi_version(void);

@@ -74,7 +74,10 @@ int bsw_set_reference(bsw_ctx_t *ctx, const uint8_t *ref, int64_t ref_len);
  * d_read_len, d_seeds and d_out in HBM of the context's first device, `stream` a hipStream_t
  * or NULL.  Job building, band retries and the local / to-end interpretation run on the GPU
  * (bsw_ext_dev.hip); results equal bsw_extend_seeds's.  BSW_E_INVAL without a resident
- * reference.  Returns when d_out holds the regions. */
+ * reference.  Both forms validate only seeded reads (seeds[i].len > 0) and return BSW_E_RANGE
+ * for the same bad seeds; the device form additionally needs the longest seeded read to
+ * satisfy len + 2w + 1 <= BSW_MAX_LEN (its per-read window stride; the host form checks each
+ * read's actual window instead).  Returns when d_out holds the regions. */
 int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
                             const int64_t *d_read_off, const int32_t *d_read_len, const bsw_seed_t *d_seeds,
                             int32_t n, bsw_alnreg_t *d_out, void *stream);

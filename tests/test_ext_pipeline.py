@@ -232,14 +232,13 @@ def test_gpu_device_pipeline_edges():
 
 
 @pytest.mark.gpu
-def test_gpu_pipelines_chunked(monkeypatch):
+def test_gpu_pipelines_chunked():
     """Calls split into read chunks (the int32 SeqPair-offset guard that applies above ~3.9M reads,
-    forced small by BSW_EXT_CHUNK_READS) give the unsplit results on both pipeline forms."""
+    forced small by BSW_OPT_EXT_CHUNK) give the unsplit results on both pipeline forms."""
     ref, reads, off, lens, seeds, _ = _workload(5_000, seed=5, ref_len=500_000, p_sub=0.03, p_indel=0.005)
     opt = bsw.ext_opt()
     want = oracle.extend_seeds(oracle.make_params(), opt, ref, reads, off, lens, seeds)
-    monkeypatch.setenv("BSW_EXT_CHUNK_READS", "1234")
-    eng = bsw.Engine()
+    eng = bsw.Engine(ext_chunk=1234)
     host = bsw.extend_seeds(eng, ref, reads, off, lens, seeds, opt)
     st = bsw.ext_last_stats(eng)
     assert st.n_pairs[0] > 0 and st.n_pairs[2] > 0                 # aggregated over the chunks
@@ -251,14 +250,13 @@ def test_gpu_pipelines_chunked(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_gpu_pipelines_no_fork(monkeypatch):
-    """Class launches run serially on the caller's stream (BSW_NO_FORK=1) give the forked
+def test_gpu_pipelines_no_fork():
+    """Class launches run serially on the caller's stream (BSW_OPT_FORK = 0) give the forked
     results on both pipeline forms."""
     ref, reads, off, lens, seeds, _ = _workload(3_000, seed=6, ref_len=400_000, p_sub=0.03, p_indel=0.005)
     opt = bsw.ext_opt()
     want = oracle.extend_seeds(oracle.make_params(), opt, ref, reads, off, lens, seeds)
-    monkeypatch.setenv("BSW_NO_FORK", "1")
-    eng = bsw.Engine()
+    eng = bsw.Engine(fork=0)
     host = bsw.extend_seeds(eng, ref, reads, off, lens, seeds, opt)
     bsw.set_reference(eng, ref)
     dev = bsw.extend_seeds_resident(eng, reads, off, lens, seeds, opt)

@@ -170,14 +170,14 @@ def _check(want, got, tag):
 
 
 @pytest.fixture(params=["column", "band"])
-def routing(request, monkeypatch):
-    """Default routing (column kernel first) or BSW_GLOB_BAND=1 (band kernel first); the
-    variable is read on every bsw_ksw_global2 call."""
-    if request.param == "band":
-        monkeypatch.setenv("BSW_GLOB_BAND", "1")
-    else:
-        monkeypatch.delenv("BSW_GLOB_BAND", raising=False)
+def routing(request):
+    """Default routing (column kernel first) or BSW_OPT_GLOB_BAND = 1 (band kernel first), set on
+    every engine the test creates (through _engine)."""
     return request.param
+
+
+def _engine(params, routing):
+    return bsw.Engine(params, glob_band=1 if routing == "band" else 0)
 
 
 @pytest.mark.gpu
@@ -187,7 +187,7 @@ def test_gpu_random_jobs_match_oracle(scoring, routing):
     pairs, ref, qer = _random_batch(4000, seed=a * 100 + od + b)
     p = bsw.default_params(a=a, b=b, o_del=od, e_del=ed, o_ins=oi, e_ins=ei)
     want = oracle.ksw_global2_batch(pairs, ref, qer, list(p.mat), od, ed, oi, ei, stride=96, nthreads=16)
-    eng = bsw.Engine(p)
+    eng = _engine(p, routing)
     got = bsw.ksw_global2(eng, pairs, ref, qer, stride=96)
     _check(want, got, f"random jobs {scoring}")
     assert np.array_equal(pairs["score"], want[0])
@@ -200,7 +200,7 @@ def test_gpu_bwa_shaped_jobs_match_oracle(read_len, routing):
     ref = bsw.synth_reference(4_000_000, seed=13)
     pairs, qer = bsw.synth_globals(ref, 20_000, cfg=bsw.globals_cfg(seed=read_len, read_len=read_len))
     want = oracle.ksw_global2_batch(pairs, ref, qer, bwa_fill_scmat(), stride=64, nthreads=16)
-    eng = bsw.Engine()
+    eng = _engine(None, routing)
     got = bsw.ksw_global2(eng, pairs, ref, qer, stride=64)
     _check(want, got, f"bwa-shaped {read_len}")
     st = bsw.global_last_stats(eng)
@@ -231,7 +231,7 @@ def test_gpu_edges_and_flags(routing):
     ref = np.array(refs + [0], dtype=np.uint8)
     qer = np.array(qers + [0], dtype=np.uint8)
     mat = bwa_fill_scmat()
-    eng = bsw.Engine()
+    eng = _engine(None, routing)
     for stride in (512, 3):
         want = oracle.ksw_global2_batch(pairs, ref, qer, mat, stride=stride)
         got = bsw.ksw_global2(eng, pairs.copy(), ref, qer, stride=stride)
@@ -244,7 +244,7 @@ def test_gpu_edges_and_flags(routing):
     p = bsw.default_params(a=40, b=60, o_del=100, e_del=30, o_ins=100, e_ins=30)
     pr, rf, qr = _random_batch(300, seed=5, qmax=150, tmax=160)
     want = oracle.ksw_global2_batch(pr, rf, qr, list(p.mat), 100, 30, 100, 30, stride=160)
-    eng = bsw.Engine(p)
+    eng = _engine(p, routing)
     got = bsw.ksw_global2(eng, pr, rf, qr, stride=160)
     _check(want, got, "wide scoring")
     st = bsw.global_last_stats(eng)              # the larger jobs exceed the int16 bound

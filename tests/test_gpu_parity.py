@@ -83,14 +83,11 @@ def test_random_mixed_shapes(eng, w):
 
 
 @pytest.mark.parametrize("no_fork", [False, True])
-def test_class_launch_fork(eng, monkeypatch, no_fork):
+def test_class_launch_fork(eng, no_fork):
     """A batch spanning every kernel class (short/long queries up to the wide kernel) gives the
     oracle's results whether its class launches fork over the slot's side streams (default) or
-    run serially on the caller's stream (BSW_NO_FORK=1, read per call)."""
-    if no_fork:
-        monkeypatch.setenv("BSW_NO_FORK", "1")
-    else:
-        monkeypatch.delenv("BSW_NO_FORK", raising=False)
+    run serially on the caller's stream (BSW_OPT_FORK = 0, read per call)."""
+    eng.set_option("fork", 0 if no_fork else 1)
     pairs, ref, qer = bswgen.random_pairs(4000, seed=77, tlen=(0, 700), qlen=(0, 400))
     want, got = pairs.copy(), pairs.copy()
     oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
@@ -99,6 +96,7 @@ def test_class_launch_fork(eng, monkeypatch, no_fork):
         eng.get_scores(got, ref, qer, 100)
         _assert_same(want, got, f"class launches no_fork={no_fork}")
     st = eng.last_stats()
+    eng.set_option("fork", 1)
     assert st.n_launches >= 3 and st.n_wide > 0
     assert st.n_i16 + st.n_u8 + st.n_wide == len(pairs)
 
@@ -233,25 +231,11 @@ def test_multi_gpu_context_shards(c2_full):
     _assert_same(want[:100_000], got, f"n_gpus={n}")
 
 
-def _engine_with(env):
-    import os
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        return bsw.Engine()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k)
-            else:
-                os.environ[k] = v
-
-
 @pytest.fixture(scope="module")
 def eng_lane():
-    """Engine with the packed-column kernel disabled (BSW_PC=0 at create): every 16-bit pair
-    runs on the lane kernel (bsw_kernels.hip)."""
-    e = _engine_with({"BSW_PC": "0"})
+    """Engine with the packed-column kernel disabled (BSW_OPT_KERNEL8 = 0): every pair runs on
+    the int16 lane kernel (bsw_kernels.hip) or the wide kernel."""
+    e = bsw.Engine(kernel8=0)
     yield e
     e.close()
 
@@ -304,41 +288,6 @@ def test_lane_kernel_c2(eng_lane, c2_full):
     assert eng_lane.last_stats().n_packed == 0
 
 
-@pytest.fixture(scope="module")
-def eng_pk():
-    """Engine with the opt-in packed two-pairs-per-lane kernel enabled (BSW_PK=1 at create)."""
-    e = _engine_with({"BSW_PK": "1"})
-    yield e
-    e.close()
-
-
-@pytest.mark.parametrize("w", [0, 1, 7, 40, 100, 200])
-def test_packed_kernel_random(eng_pk, w):
-    """qlen 129..160 with h0 + min(qlen, tlen) <= 255 routes to bsw_pk.hip (1 launch)."""
-    pairs, ref, qer = bswgen.random_pairs(4000, seed=70 + w, qlen=(129, 160), tlen=(0, 330), h0=(0, 95))
-    want, got = pairs.copy(), pairs.copy()
-    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
-    eng_pk.get_scores(got, ref, qer, w)
-    _assert_same(want, got, f"packed w={w}")
-    assert eng_pk.last_stats().n_launches == 1
-
-
-def test_packed_kernel_mixed_routing(eng_pk):
-    """h0 above the 8-bit key bound and short queries fall back to the lane kernels."""
-    pairs, ref, qer = bswgen.random_pairs(4000, seed=5, qlen=(0, 170), tlen=(0, 330), h0=(0, 160))
-    want, got = pairs.copy(), pairs.copy()
-    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
-    eng_pk.get_scores(got, ref, qer, 100)
-    _assert_same(want, got, "packed mixed routing")
-
-
-def test_packed_kernel_c2(eng_pk, c2_full):
-    pairs, ref, qer, want = c2_full
-    got = pairs[:300_000].copy()
-    eng_pk.get_scores(got, ref, qer, 100)
-    _assert_same(want[:300_000], got, "packed C2")
-
-
 def test_argument_errors(eng):
     pairs, ref, qer = bswgen.random_pairs(10, seed=1)
     lib = bsw.hip_lib()
@@ -356,3 +305,38 @@ def test_argument_errors(eng):
                               10, 100, 16) == -34
     # empty batch is a no-op
     eng.get_scores(pairs[:0].copy(), ref, qer, 100)
+
+
+def test_kernel_range_guard_reports_error():
+    """BSW_OPT_TEST_MISROUTE sends every pair to the QMAX=32 lane kernel: pairs with longer
+    queries trip the kernel's range guard, and both call forms must return BSW_E_RANGE (the
+    guard word is read back after the DP launches) instead of BSW_OK with unwritten outputs."""
+    pairs, ref, qer = bswgen.c2_like(500, seed=41)
+    e = bsw.Engine(test_misroute=1)
+    got = pairs.copy()
+    with pytest.raises(bsw.BswError, match="-34"):
+        e.get_scores(got, ref, qer, 100)
+    dp = hiprt.DeviceBuffer.from_array(pairs)
+    dr = hiprt.DeviceBuffer.from_array(ref)
+    dq = hiprt.DeviceBuffer.from_array(qer)
+    with pytest.raises(bsw.BswError, match="-34"):
+        e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, len(pairs), 100)
+    # short queries fit the QMAX=32 class: the same misrouted engine returns the oracle's results
+    sp, sr, sq = bswgen.random_pairs(800, seed=42, qlen=(0, 32), tlen=(0, 90))
+    want, got = sp.copy(), sp.copy()
+    oracle.get_scores(_oparams(), want, sr, sq, 100)
+    e.get_scores(got, sr, sq, 100)
+    _assert_same(want, got, "misrouted short queries")
+    e.set_option("test_misroute", 0)
+    got = pairs.copy()
+    e.get_scores(got, ref, qer, 100)
+    e.close()
+
+
+def test_options_api(eng):
+    lib = bsw.hip_lib()
+    assert lib.bsw_set_option(eng._ctx, 999, 1) == -22
+    assert lib.bsw_set_option(eng._ctx, bsw.OPT_FORK, 2) == -22
+    assert lib.bsw_set_option(eng._ctx, bsw.OPT_EXT_CHUNK, -1) == -22
+    assert lib.bsw_set_option(None, bsw.OPT_FORK, 1) == -22
+    assert lib.bsw_set_option(eng._ctx, bsw.OPT_SORTKEY, 1) == 0
