@@ -312,7 +312,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     }
     // packed-column kernel scoring contract (bsw_pc.hip): match 1, one mismatch value in
     // [-127, -1], every N entry -1, symmetric gap penalties.
-    bool ok = p.o_del == p.o_ins && p.e_del == p.e_ins && p.e_del > 0 && p.o_del + p.e_del < 16384;
+    bool ok = p.o_del == p.o_ins && p.e_del == p.e_ins && p.e_del > 0 && p.o_del + p.e_del < 4096;
     const int mis = p.mat[1];
     ok = ok && mis < 0 && mis >= -127;
     for (int a = 0; a < 5 && ok; ++a)

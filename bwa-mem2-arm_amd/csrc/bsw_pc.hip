@@ -11,12 +11,12 @@
 // value, N -1, symmetric gaps; the host's pk_ok contract):
 //   scores   : Y = v_perm(profile[t], Q[g]) -> {S0, S2, S1, S3} bytes; {S0, S1} and {S2, S3}
 //              sign-extended by packed 16-bit shifts                         (4 instructions)
-//   phase 1  : M = hold + min(S, hold) (the A.5 gate), T = max(M - oe, 0), ME = max(M, E),
-//              E' = max(E - e, T) -- 7 packed instructions per 2 columns      (14)
-//   F chain  : h = max(F, ME_j), F = max(F - e, T_j) per column, 32-bit ops with SDWA
+//   phase 1  : M = hold + min(S, hold) (the A.5 gate), T~ = M - oe, ME = max(M, E),
+//              E' = max(E - e, T~) -- 6 packed instructions per 2 columns     (12)
+//   F chain  : h = max(F, ME_j), F = max(sat(F - e), T~_j) per column, 32-bit ops with SDWA
 //              word selects                                                   (12)
 //   pack/key : HH <- {h_{j-1}, h_j} (v_lshl_or), key = max(HH << 8 | j) by v_pk_max_u16 (6)
-// = 36 VALU per 4 cells, against 47 for the lane kernel's fast group.  ~200 VGPRs at
+// = 34 VALU per 4 cells, against 47 for the lane kernel's fast group.  ~200 VGPRs at
 // QMAX = 160: two waves per SIMD (the occupancy the packed two-pairs-per-lane kernel lacks).
 //
 // Eligibility (planner, bsw_host.cpp): pk_ok scoring, h0 + min(qlen, tlen) <= 255 (H <= 255:
@@ -65,13 +65,18 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
 #define PC_SDWA(op, d, a, b, sel) \
     op "_sdwa " d ", " a ", " b " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" sel "\n\t"
 
-// phase 1 of one packed register X (columns 2k, 2k+1): S in %[sX] -> M -> ME; T in %[tX];
-// E' into EOUT (in place for FAST, %[xX] for MASKED).
+// phase 1 of one packed register X (columns 2k, 2k+1): S in %[sX] -> M -> ME; T~ in %[tX];
+// E~' into EOUT (in place for FAST, %[xX] for MASKED).
+//
+// T and E are kept UNCLAMPED (T~ = M - oe, E~' = max(E~ - e, T~)): only their positive parts
+// matter.  Invariant max(E~, 0) = E: E' = max(E - e, T) = max(max(E~, 0) - e, T~, 0) =
+// max(E~ - e, T~, 0) (as -e < 0).  The F chain clamps instead (f - e saturates at 0, so
+// F >= 0 always) and H = max(ME, F) = max(M, E~, F) equals max(M, E, F) because F >= 0.
+// Bounds: M >= -127, oe < 4096 (pk_ok), so T~, E~ stay far inside int16.
 #define PC_PH1(X, EOUT)                                                                 \
     "v_pk_min_i16 %[s" X "], %[s" X "], %[h" X "]\n\t"                                      \
     "v_pk_add_u16 %[s" X "], %[s" X "], %[h" X "]\n\t"                                      \
     "v_pk_sub_i16 %[t" X "], %[s" X "], %[oe2]\n\t"                                         \
-    "v_pk_max_i16 %[t" X "], %[t" X "], 0\n\t"                                              \
     "v_pk_max_i16 %[s" X "], %[s" X "], %[e" X "]\n\t"                                      \
     "v_pk_sub_i16 " EOUT ", %[e" X "], %[ed2]\n\t"                                          \
     "v_pk_max_i16 " EOUT ", " EOUT ", %[t" X "]\n\t"
@@ -85,7 +90,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
 // one F-chain cell: H -> C, F updated.  X = a|b register, W = WORD_0|WORD_1 half
 #define PC_CELL(C, X, W)                                                                 \
     PC_SDWA("v_max_i32", C, "%[f]", "%[s" X "]", W)                                          \
-    "v_subrev_u32_e32 %[f], %[ed], %[f]\n\t"                                                 \
+    "v_subrev_u32_e64 %[f], %[ed], %[f] clamp\n\t"                                           \
     PC_SDWA("v_max_i32", "%[f]", "%[f]", "%[t" X "]", W)
 
 // masked cell: optional reset entering column J (J == beg: F = 0, H(i, J-1) = 0), then the
@@ -227,34 +232,47 @@ __device__ __forceinline__ void pc_row(std::integer_sequence<int, G...>, uint32_
 }
 
 // Lazy last positive column: when H(i, end-1) == 0 the lanes that need it
-// scan slots right to left (slot j+1 = H(i, j)) from end - 1; groups above every lane's end
-// and groups after all lanes found one are skipped by uniform tests.
-template <int QMAX, int GG>
-__device__ __forceinline__ bool pc_lastpos_group(const uint32_t (&hh)[QMAX / 2], int end, bool pending,
-                                                 int &lp1, int gstart)
+// look for the last slot s <= end (slot s = H(i, s-1)) holding H > 0; lp1 = that slot = 1 + lastH.
+// Packed scan, two slots per instruction, registers from the one holding slot max(end) down:
+//   c = min(H, 1) * s (slot or 0), cleared where s > end, lp = max(lp, c)
+// 6 packed ops per register; a uniform test after each pair of registers stops the scan once
+// every needing lane found its slot.  Slot 0 (the column -1 boundary) contributes 0 = none.
+template <int K>
+__device__ __forceinline__ void pc_lastpos_reg(uint32_t hv, uint32_t endp1w, uint32_t &lp)
 {
-    if (GG > gstart) return pending;                      // uniform
-    if (__ballot(pending) == 0) return false;             // uniform
-#pragma unroll
-    for (int k = 3; k >= 0; --k) {
-        const int j = 4 * GG + k;                         // column; its H sits in slot j + 1
-        if (j + 1 < QMAX) {
-            const uint32_t hv = (hh[(j + 1) >> 1] >> (16 * ((j + 1) & 1))) & 0xffffu;
-            const bool hit = pending & (j < end) & (hv != 0u);
-            lp1 = hit ? j + 1 : lp1;
-            pending = pending & !hit;
-        }
-    }
-    return pending;
+    constexpr uint32_t SC = (uint32_t)(2 * K) | ((uint32_t)(2 * K + 1) << 16);
+    uint32_t c, m;
+    asm volatile(
+        "v_pk_min_u16 %[c], %[h], 1 op_sel_hi:[1,0]\n\t"
+        "v_pk_mul_lo_u16 %[c], %[c], %[sc]\n\t"
+        "v_pk_sub_i16 %[m], %[sc], %[e1]\n\t"               // s - (end + 1) < 0  <=>  s <= end
+        "v_pk_ashrrev_i16 %[m], 15, %[m] op_sel_hi:[0,1]\n\t"
+        "v_and_b32_e32 %[c], %[c], %[m]\n\t"
+        "v_pk_max_u16 %[lp], %[lp], %[c]\n\t"
+        : [lp] "+v"(lp), [c] "=&v"(c), [m] "=&v"(m)
+        : [h] "v"(hv), [sc] "s"(SC), [e1] "v"(endp1w));
+}
+
+template <int QMAX, int GG>
+__device__ __forceinline__ bool pc_lastpos_group(const uint32_t (&hh)[QMAX / 2], uint32_t endp1w, bool pending,
+                                                 uint32_t &lp, int gstart)
+{
+    if (GG > gstart) return pending;                      // uniform: above every lane's end
+    if (__ballot(pending) == 0) return false;             // uniform: all found
+    if constexpr (2 * GG + 1 < QMAX / 2) pc_lastpos_reg<2 * GG + 1>(hh[2 * GG + 1], endp1w, lp);
+    pc_lastpos_reg<2 * GG>(hh[2 * GG], endp1w, lp);
+    return pending & (lp == 0u);
 }
 
 template <int QMAX, int... G>
-__device__ __forceinline__ void pc_lastpos(std::integer_sequence<int, G...>,
-                                           const uint32_t (&hh)[QMAX / 2], int end, bool need,
-                                           int &lp1, int gstart)
+__device__ __forceinline__ int pc_lastpos(std::integer_sequence<int, G...>, const uint32_t (&hh)[QMAX / 2],
+                                          int end, bool need, int gstart)
 {
     bool pending = need;
-    ((pending = pc_lastpos_group<QMAX, QMAX / 4 - 1 - G>(hh, end, pending, lp1, gstart)), ...);
+    uint32_t lp = 0;
+    const uint32_t endp1w = pack2(end + 1);
+    ((pending = pc_lastpos_group<QMAX, QMAX / 4 - 1 - G>(hh, endp1w, pending, lp, gstart)), ...);
+    return (int)max(lp & 0xffffu, lp >> 16);
 }
 
 // WPB waves per workgroup: with 1, a wave's slot (and its LDS) is reused as soon as that wave
@@ -434,9 +452,9 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
 #ifdef BSW_PC_STATS
                     nlast += 1;
 #endif
-                    if (need) lp1 = 0;
-                    pc_lastpos<QMAX>(std::make_integer_sequence<int, NG>{}, hh, end, need, lp1,
-                                     (emax - 1) >> 2);
+                    const int lp = pc_lastpos<QMAX>(std::make_integer_sequence<int, NG>{}, hh, end, need,
+                                                    emax >> 2);
+                    if (need) lp1 = lp;
                 }
                 endc = min(lp1 + 2, qlen);
             }

@@ -18,9 +18,12 @@
  * PARITY UNPINNED by the reference: /root/reference holds no golden vectors, no
  * fixtures and no test for this path, and its source cannot be
  * built here.  This oracle is pinned instead by (1) hand-derived known-answer tests
- * (tests/test_oracle.py), (2) an independent line-by-line Python transcription
- * (oracle/ksw_ext_ref.py) cross-checked on >= 10^5 seeded pairs, and (3) the committed
- * golden fixtures in tests/golden/ generated from it (tests/golden/make_golden.py).
+ * (tests/test_oracle.py), (2) two independent transcriptions: the line-by-line Python one
+ * (oracle/ksw_ext_ref.py, small pairs in tests/test_oracle.py) and the vectorised numpy one
+ * (oracle/ksw_ext_np.py: every committed golden pair in tests/test_oracle.py, and 10^6 C2
+ * pairs + 4 x 10^5 pairs of other classes in tests/oracle_crosscheck.py, recorded output
+ * tests/golden/crosscheck_1e6.json), and (3) the committed golden fixtures in tests/golden/
+ * generated from it (tests/golden/make_golden.py).
  */
 #include <stdint.h>
 #include <stdlib.h>

@@ -131,3 +131,21 @@ def pairs_from_shapes(shapes, seed, p_unrelated=0.2):
             q = mutate(rng, r, Q, rng.uniform(0.0, 0.08), rng.uniform(0.0, 0.03), 0.01)
         items.append((r, q, int(h0)))
     return assemble(items)
+
+
+def repeat_pairs(n, seed, L=(20, 160), h0=(1, 120)):
+    """Tandem repeats (period 1..6 motifs, microsatellites) with light mutation: equal-score
+    paths everywhere, so the last-index tie rules (row max mj, gscore's max_ie) decide."""
+    rng = np.random.default_rng(seed)
+    items = []
+    for _ in range(n):
+        per = int(rng.integers(1, 7))
+        motif = rng.integers(0, 4, per).astype(np.uint8)
+        Q = int(rng.integers(L[0], L[1] + 1))
+        T = Q + int(rng.integers(0, 60))
+        r = np.tile(motif, T // per + 2)[int(rng.integers(0, per)):][:T].copy()
+        q = np.tile(motif, Q // per + 2)[:Q].copy()
+        if rng.random() < 0.5:
+            q = mutate(rng, q, Q, 0.03, 0.01)
+        items.append((r, q, int(rng.integers(h0[0], h0[1] + 1))))
+    return assemble(items)

@@ -18,7 +18,6 @@ for sub in ("oracle", "tests", os.path.join("bwa-mem2-arm_amd", "py")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-GOLDEN = os.path.join(ROOT, "tests", "golden", "golden_v1.npz")
 
 
 def pytest_configure(config):
@@ -26,16 +25,18 @@ def pytest_configure(config):
 
 
 def load_golden():
-    """[(name, pairs, ref, qer, w, scoring), ...] from the committed fixtures."""
+    """[(name, pairs, ref, qer, w, scoring), ...] from the committed fixtures: golden_v1.npz
+    (manifest.json) and golden_v2.npz (manifest_v2.json)."""
     import json
     import bswgen
-    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))
-    z = np.load(GOLDEN)  # allow_pickle=False (default)
     out = []
-    for b in meta["batches"]:
-        nm = b["name"]
-        pairs = np.ascontiguousarray(z[f"{nm}_pairs"]).view(bswgen.SEQPAIR_DTYPE).reshape(-1).copy()
-        out.append((nm, pairs, z[f"{nm}_ref"], z[f"{nm}_qer"], b["w"], b["scoring"]))
+    for mname, fname in (("manifest.json", "golden_v1.npz"), ("manifest_v2.json", "golden_v2.npz")):
+        meta = json.load(open(os.path.join(ROOT, "tests", "golden", mname)))
+        z = np.load(os.path.join(ROOT, "tests", "golden", fname))  # allow_pickle=False (default)
+        for b in meta["batches"]:
+            nm = b["name"]
+            pairs = np.ascontiguousarray(z[f"{nm}_pairs"]).view(bswgen.SEQPAIR_DTYPE).reshape(-1).copy()
+            out.append((nm, pairs, z[f"{nm}_ref"], z[f"{nm}_qer"], b["w"], b["scoring"]))
     return out
 
 

@@ -18,6 +18,14 @@ Batches (each with its own band w and scoring):
   b5  mixed shapes with non-default scoring (-A2 -B3 -O5,7 -E2,1 -d50 -L3), w=40
   b6  partial batches of 1, 15, 31, 32, 33, 50, 64, 100 pairs (the reference's planned
       SVE2 validation sizes, PHASE2_IMPLEMENTATION_SUMMARY.md:194-201), w=100
+
+`python make_golden.py v2` writes golden_v2.npz + manifest_v2.json (round 2: the SURVEY.md
+§8(c) classes v1 lacked -- z-drop off, w = 200, asymmetric gaps, ties):
+  z0_c2 / z0_rand / z0_w5   zdrop = 0 (the `else if (zdrop > 0)` branch never breaks)
+  w200_c2 / w200_long       w = 200 (band wider than the query; 200 bp queries -> wide kernel)
+  asym_ins / asym_del       e_del != e_ins and o_del != o_ins (the non-packed lane kernel)
+  ties                      tandem repeats: equal-score paths, last-index tie rules
+v1 is left as generated in round 1.
 """
 
 import hashlib
@@ -52,31 +60,51 @@ def batches():
     return out
 
 
+ZDROP0 = dict(DEFAULT, zdrop=0)
+ASYM_INS = dict(o_del=6, e_del=1, o_ins=4, e_ins=3, zdrop=100, end_bonus=5, a=1, b=4)
+ASYM_DEL = dict(o_del=3, e_del=3, o_ins=8, e_ins=1, zdrop=80, end_bonus=5, a=1, b=4)
+
+
+def batches_v2():
+    return [
+        ("z0_c2", bswgen.c2_like(400, seed=301), 100, ZDROP0),
+        ("z0_rand", bswgen.random_pairs(400, seed=302), 100, ZDROP0),
+        ("z0_w5", bswgen.random_pairs(300, seed=303, tlen=(0, 200), qlen=(0, 120)), 5, ZDROP0),
+        ("w200_c2", bswgen.c2_like(300, seed=304), 200, DEFAULT),
+        ("w200_long", bswgen.c2_like(200, seed=305, tlen=420, qlen=200, h0=(19, 120)), 200, DEFAULT),
+        ("asym_ins", bswgen.random_pairs(400, seed=306, tlen=(0, 300), qlen=(0, 160)), 100, ASYM_INS),
+        ("asym_del", bswgen.c2_like(300, seed=307), 50, ASYM_DEL),
+        ("ties", bswgen.repeat_pairs(400, seed=308), 100, DEFAULT),
+    ]
+
+
 def params_of(d):
     return oracle.make_params(o_del=d["o_del"], e_del=d["e_del"], o_ins=d["o_ins"], e_ins=d["e_ins"],
                               zdrop=d["zdrop"], end_bonus=d["end_bonus"],
                               mat=bwa_fill_scmat(d["a"], d["b"]))
 
 
-def main():
+def main(version="v1"):
     arrays = {}
     meta = {"generator": "tests/golden/make_golden.py", "oracle": "oracle/ksw_ext_ref.c",
             "parity": "unpinned by the reference (no reference fixtures exist); oracle-generated",
             "batches": []}
-    for name, (pairs, ref, qer), w, sc in batches():
+    for name, (pairs, ref, qer), w, sc in (batches() if version == "v1" else batches_v2()):
         p = pairs.copy()
         oracle.get_scores(params_of(sc), p, ref, qer, w)
         arrays[f"{name}_pairs"] = p.view(np.int32).reshape(len(p), 14)
         arrays[f"{name}_ref"] = ref
         arrays[f"{name}_qer"] = qer
         meta["batches"].append({"name": name, "n": int(len(p)), "w": w, "scoring": sc})
-    path = os.path.join(HERE, "golden_v1.npz")
+    path = os.path.join(HERE, f"golden_{version}.npz")
     np.savez_compressed(path, **arrays)
     meta["sha256"] = hashlib.sha256(open(path, "rb").read()).hexdigest()
-    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+    meta["file"] = os.path.basename(path)
+    mname = "manifest.json" if version == "v1" else f"manifest_{version}.json"
+    with open(os.path.join(HERE, mname), "w") as fh:
         json.dump(meta, fh, indent=1)
     print(f"wrote {path} ({os.path.getsize(path)} B), {sum(b['n'] for b in meta['batches'])} pairs")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "v1")
