@@ -88,10 +88,11 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
     "v_pk_ashrrev_i16 %[sb], 8, %[y] op_sel_hi:[0,1]\n\t"
 
 // one F-chain cell: H -> C, F updated.  X = a|b register, W = WORD_0|WORD_1 half
+// ME and T~ may be negative now: their word selects must sign-extend (sext)
 #define PC_CELL(C, X, W)                                                                 \
-    PC_SDWA("v_max_i32", C, "%[f]", "%[s" X "]", W)                                          \
+    PC_SDWA("v_max_i32", C, "%[f]", "sext(%[s" X "])", W)                                    \
     "v_subrev_u32_e64 %[f], %[ed], %[f] clamp\n\t"                                           \
-    PC_SDWA("v_max_i32", "%[f]", "%[f]", "%[t" X "]", W)
+    PC_SDWA("v_max_i32", "%[f]", "%[f]", "sext(%[t" X "])", W)
 
 // masked cell: optional reset entering column J (J == beg: F = 0, H(i, J-1) = 0), then the
 // cell, then C = (J < end) ? H : HP (H(i, end-1) travels on past end)
