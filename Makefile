@@ -17,7 +17,7 @@ SHIMTEST := $(LIBDIR)/bsw_shim_example
 ORACLE   := oracle/liboracle.so
 
 HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pc.hip $(CSRC)/bsw_mate.hip $(CSRC)/bsw_global.hip $(CSRC)/bsw_ext_dev.hip $(CSRC)/bsw_host.cpp $(CSRC)/bsw_ext.cpp
-HIP_HDRS := $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h
+HIP_HDRS := $(CSRC)/bsw_pool.h $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h
 
 all: product synth oracle
 

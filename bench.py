@@ -18,7 +18,8 @@ Reported beside the metric:
                   launch / HIP-event-timed launch duration, vs the gfx950 packed-int16 VALU
                   peak; traffic = HBM bytes per launch from rocprofv3 PMC (profiles/).
   cpu_baseline -- oracle/bsw_sse41.c (restated upstream SSE4.1 getScores16 design, "port")
-                  on a bounded sample of the same batch, rank 0, N = 1 only.
+                  on a bounded sample of the same batch on every core of the affinity set
+                  (model, core count and cgroup quota recorded), rank 0, N = 1 only.
 """
 
 from __future__ import annotations
@@ -90,24 +91,55 @@ def traffic_per_launch(kernel_name: str):
         return None
 
 
+def host_cpu_info() -> dict:
+    """What the CPU baseline ran on: usable cores (sched affinity), nproc-style count, the
+    lscpu model string and any cgroup CPU quota (the box's real share may be below nproc)."""
+    info = {"affinity_cores": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def _timed(fn, reps):
+    """median wall time of `reps` runs after one warm-up"""
+    fn()
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    return statistics.median(ts)
+
+
 def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
-    """oracle/bsw_sse41.c on a bounded sample (first S pairs), median of 3 after warm-up."""
+    """oracle/bsw_sse41.c (the reference's SSE4.1 getScores16 design restated) on a bounded
+    sample of the same batch: ALL usable host cores (`cores`, default = sched affinity), median
+    of 3 after a warm-up; beside it the 16-thread and 1-thread SSE4.1 rates and the 1-thread
+    scalar ksw_extend2 rate (BASELINE.md / north_star: core count stated)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # CPU baseline leg only (test infrastructure)
     P = oracle.make_params()
-    S = min(len(pairs), 200_000)
+    # ~12.5K pairs per thread (>= 0.1 s per run at ~0.1 M pairs/s/thread), at most the batch
+    S = min(len(pairs), max(200_000, 12_500 * cores))
     sample = pairs[:S]
-    times = []
-    out = None
-    for k in range(4):
-        a = sample.copy()
-        t = time.perf_counter()
-        oracle.sse41_get_scores16(P, a, ref, qer, w, cores)
-        dt = time.perf_counter() - t
-        if k:
-            times.append(dt)
-        out = a
-    sse_mt = S / statistics.median(times) / 1e6
+    out = sample.copy()
+    sse_mt = S / _timed(lambda: oracle.sse41_get_scores16(P, out, ref, qer, w, cores), 3) / 1e6
+    S16 = min(len(pairs), 200_000)
+    a16 = pairs[:S16].copy()
+    sse_16 = S16 / _timed(lambda: oracle.sse41_get_scores16(P, a16, ref, qer, w, 16), 1) / 1e6 \
+        if cores != 16 else sse_mt
     S1 = min(len(pairs), 20_000)
     a = pairs[:S1].copy()
     t = time.perf_counter()
@@ -123,11 +155,75 @@ def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
     return {
         "value": round(sse_mt, 4), "unit": UNIT, "cores": cores, "kind": "port",
         "sample": f"first {S} pairs of the rank-0 C2 batch; oracle/bsw_sse41.c (SSE4.1, 8 x int16 "
-                  f"lanes, restated upstream getScores16 design), {cores} threads, median of 3 after 1 warm-up",
+                  f"lanes, restated upstream getScores16 design, not the upstream binary), {cores} threads "
+                  f"= every core in the process's affinity set, median of 3 after 1 warm-up",
+        "host": host_cpu_info(),
+        "sse41_16threads": round(sse_16, 4),
         "sse41_1thread": round(sse_1t, 4), "scalar_ksw_extend2_1thread": round(scalar_1t, 4),
         "outputs_identical_to_gpu": bool(agree),
         "actual_cells_per_pair": round(cells, 1),
     }
+
+
+def host_path_rates(eng, pairs, ref, qer, w, cell_bits, want):
+    """The drop-in path: bsw_get_scores on HOST buffers (pageable numpy memory, as upstream's
+    getScores16 caller hands them over), PCIe both ways included.  Whole batch (median of 3
+    after a warm-up) and the per-call curve at upstream-like batch sizes (kt_for workers issue
+    thousands of pairs per call): 1 calling thread, and 8 concurrent callers (each call takes
+    its own slot/stream, ctypes releases the GIL).  Whole batch: median of 5 after a warm-up."""
+    import threading
+    n = len(pairs)
+    buf = pairs.copy()
+    ts = []
+    eng.get_scores(buf, ref, qer, w, cell_bits)
+    for _ in range(5):
+        t = time.perf_counter()
+        eng.get_scores(buf, ref, qer, w, cell_bits)
+        ts.append(time.perf_counter() - t)
+    t_all = statistics.median(ts)
+    st = eng.last_stats()
+    same = all(np.array_equal(buf[f], want[f]) for f in bsw.OUT_FIELDS)
+    curve = []
+    for m in (1_000, 10_000, 100_000):
+        if m > n:
+            continue
+        calls = max(4, min(n // m, int(2e6 // m)))
+        lat = []
+        for c in range(calls):
+            a = (c * m) % (n - m + 1)
+            v = buf[a:a + m]
+            t = time.perf_counter()
+            eng.get_scores(v, ref, qer, w, cell_bits)
+            lat.append(time.perf_counter() - t)
+        lat = lat[1:]
+        nthr = 8
+        per = max(2, calls // nthr)
+        go = threading.Barrier(nthr + 1)
+
+        def worker(k):
+            eng.get_scores(buf[:m], ref, qer, w, cell_bits)      # warm: this caller's slots
+            go.wait()
+            go.wait()
+            for c in range(per):
+                a = ((k * per + c) * m) % (n - m + 1)
+                eng.get_scores(buf[a:a + m], ref, qer, w, cell_bits)
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(nthr)]
+        for x in th:
+            x.start()
+        go.wait()
+        t = time.perf_counter()
+        go.wait()
+        for x in th:
+            x.join()
+        dt8 = time.perf_counter() - t
+        curve.append({"pairs_per_call": m, "latency_ms_median": round(statistics.median(lat) * 1e3, 3),
+                      "M_pairs_per_s_1_caller": round(m / statistics.median(lat) / 1e6, 3),
+                      "M_pairs_per_s_8_callers": round(nthr * per * m / dt8 / 1e6, 3)})
+    return {"value": round(n / t_all / 1e6, 3), "ms": round(t_all * 1e3, 3),
+            "ms_all_calls": [round(x * 1e3, 2) for x in ts],
+            "last_call": {"host_ms": round(st.host_ms, 3), "stage_ms": round(st.stage_ms, 3),
+                          "dp_kernel_ms": round(st.kernel_ms, 3), "launches": st.n_launches},
+            "outputs_identical_to_resident": bool(same), "per_call_curve": curve}
 
 
 def main():
@@ -140,6 +236,7 @@ def main():
     ap.add_argument("--cell-bits", type=int, default=16, choices=(8, 16))
     ap.add_argument("--h0-hi", type=int, default=100, help="h0 upper bound (C3 uses 105)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (drop-in ABI) rates")
     ap.add_argument("--workload", default="c2", choices=("c2", "c1", "c4", "mate", "global"),
                     help="c2 (default): resident SeqPair batch; c1: 10K exact SE reads vs 1 Mb (plumbing); "
                          "c4: extension pipeline on synthetic reads; "
@@ -149,6 +246,14 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000, help="c4: reads per GPU per step")
     ap.add_argument("--ref-mb", type=int, default=64, help="c4: random reference size (Mb)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak (default): every rank scores its own resident 1M-pair shard; strong: one "
+                         "fixed batch of --total-pairs split over the ranks by band cells, host buffers "
+                         "in, PCIe both ways inside the timed region (C5)")
+    ap.add_argument("--total-pairs", type=int, default=10_000_000, help="strong: pairs in the whole batch")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share GPUs; rehearsal only)")
+    ap.add_argument("--dump", default="", help="strong: rank 0 writes the gathered outputs here (.npy)")
     args = ap.parse_args()
 
     rank, local, world = dist_init()
@@ -157,8 +262,14 @@ def main():
     ndev = hiprt.device_count()
     if ndev < 1:
         raise SystemExit("bench.py: no HIP device visible")
-    local = local % ndev              # one GPU per rank; more ranks than GPUs share (rehearsal only)
+    if local >= ndev and not args.rehearse:
+        raise SystemExit(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {ndev} GPU(s) are visible; "
+                         f"--rehearse lets ranks share GPUs (never a scaling measurement)")
+    args.distinct_gpus = min(world, ndev)
+    local = local % ndev              # --rehearse: more ranks than GPUs share them
     hiprt.set_device(local)
+    if args.scaling == "strong":
+        return main_strong(args, rank, local, world)
     if args.workload == "c1":          # BASELINE configs[0]: 10K exact 150 bp SE reads vs 1 Mb
         args.reads, args.ref_mb, args.exact = 10_000, 1, True
         return main_c4(args, rank, local, world)
@@ -231,14 +342,22 @@ def main():
                                f"{cfg.tlen} bp ref, band w={args.w}, cell_bits={args.cell_bits}, "
                                f"h0 U[{cfg.h0_lo},{cfg.h0_hi}]",
                    "pairs_per_gpu": args.pairs, "parallelism": f"shard{world} (independent pairs)",
+                   "distinct_gpus": args.distinct_gpus,
                    "routing": {"n_packed": st.n_packed, "n_i16": st.n_i16, "n_u8": st.n_u8, "n_wide": st.n_wide,
                                "int16_fallback_fraction": (round(st.n_i16 / max(1, st.n_i16 + st.n_u8), 4)
                                                            if args.cell_bits == 8 else None)}},
         "roofline": roof,
         "kernel_only_value": round(args.pairs * world / (kms_mean * 1e-3) / 1e6, 3),
     }
+    if args.distinct_gpus < world:
+        out["rehearsal"] = f"{world} ranks on {args.distinct_gpus} GPU(s): not a scaling measurement"
+    if world == 1 and not args.no_host_path:
+        hp = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res)
+        out["abi_inclusive_value"] = hp.pop("value")
+        out["abi_inclusive"] = dict(hp, unit=UNIT, note="bsw_get_scores on pageable host buffers: staging + "
+                                    "H2D + plan/sort/DP + D2H, chunked pipeline over two streams")
     if world == 1 and not args.no_cpu:
-        cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        cores = args.cpu_threads or len(os.sched_getaffinity(0))
         out["cpu_baseline"] = cpu_baseline(pairs, ref, qer, args.w, res, cores)
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
         # achieved rate on the cells the literal loop really visits (10K-pair sample of the batch)
@@ -247,6 +366,82 @@ def main():
         roof["actual_cells_per_s"] = round(args.pairs * acp / (kms_mean * 1e-3) / 1e12, 4)
     out["synth_gen_s"] = round(gen_s, 2)
     print(json.dumps(out), flush=True)
+
+
+def main_strong(args, rank, local, world):
+    """C5-shaped strong scaling: ONE batch of --total-pairs C2 pairs (the whole job), split over
+    the ranks into contiguous ranges of equal static band cells (bsw_split_by_cells, SURVEY.md
+    §8(e)).  Every rank holds its range in host memory, as the process that built the batch
+    would; a step = bsw_get_scores on those HOST buffers (pinned chunked pipeline: H2D over the
+    rank's own PCIe link, plan / sort / DP, D2H of the records) -- the distribution and the
+    gather are inside the timed region.  value = total pairs / max-over-ranks step time."""
+    cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
+    N = args.total_pairs
+    t0 = time.perf_counter()
+    meta = np.zeros(N, dtype=bsw.SEQPAIR_DTYPE)          # lengths of the whole batch (for the cut)
+    step_n = 1_000_000
+    for a in range(0, N, step_n):
+        m = min(step_n, N - a)
+        meta[a:a + m] = bsw.synth_batch(m, pair_base=a, cfg=cfg)[0]
+    cut = bsw.split_by_cells(meta, args.w, world)
+    lo, hi = int(cut[rank]), int(cut[rank + 1])
+    del meta
+    # the rank's range as host batches of <= 2M pairs (SeqPair idr / idq are int32 offsets
+    # into one call's buffers, so one getScores call cannot address more than 2 GB of bases)
+    piece = 2_000_000
+    batches = [bsw.synth_batch(min(piece, hi - a), pair_base=a, cfg=cfg) for a in range(lo, hi, piece)]
+    gen_s = time.perf_counter() - t0
+    eng = bsw.Engine(device=local)
+
+    def step():
+        for p, r, q in batches:
+            eng.get_scores(p, r, q, args.w, args.cell_bits)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier(world)
+    dt = time.perf_counter() - t
+    dt_max = allreduce_max(dt, world)
+    kms = eng.last_stats().kernel_ms
+    kms_max = allreduce_max(kms, world)
+    if args.dump:
+        import torch
+        import torch.distributed as dist
+        work = np.concatenate([b[0] for b in batches]) if batches else np.zeros(0, bsw.SEQPAIR_DTYPE)
+        out = torch.from_numpy(work.view(np.int32).reshape(-1, 14).copy())
+        if world > 1:
+            sizes = [int(cut[r + 1] - cut[r]) for r in range(world)]
+            gathered = [torch.zeros((sz, 14), dtype=torch.int32) for sz in sizes] if rank == 0 else None
+            dist.gather(out, gathered, dst=0)
+        else:
+            gathered = [out]
+        if rank == 0:
+            np.save(args.dump, np.concatenate([g.numpy() for g in gathered]).view(bsw.SEQPAIR_DTYPE).reshape(-1))
+    if rank != 0:
+        return
+    value = N * args.steps / dt_max / 1e6
+    out_j = {
+        "metric": METRIC, "value": round(value, 3), "unit": UNIT, "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int16", "data": "synthetic (bsw_synth.c, seed 42)",
+        "config": {"workload": f"C5 strong scaling: one batch of {N} C2 pairs ({cfg.qlen} bp query / {cfg.tlen} bp "
+                               f"ref, w={args.w}) split over {world} rank(s) by static band cells; host buffers, "
+                               f"PCIe H2D + D2H inside the timed region",
+                   "total_pairs": N, "pairs_rank0": hi - lo, "cut": [int(c) for c in cut],
+                   "parallelism": f"split{world} (bsw_split_by_cells, no data-path collective)",
+                   "distinct_gpus": args.distinct_gpus},
+        "dp_kernel_ms_last_call_max_over_ranks": round(kms_max, 3),
+        "host_batches_rank0": len(batches),
+        "synth_gen_s": round(gen_s, 2),
+    }
+    if args.distinct_gpus < world:
+        out_j["rehearsal"] = f"{world} ranks on {args.distinct_gpus} GPU(s): not a scaling measurement"
+    print(json.dumps(out_j), flush=True)
 
 
 def main_c4(args, rank, local, world):
@@ -408,8 +603,8 @@ def main_mate(args, rank, local, world):
     if world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # CPU baseline leg only (test infrastructure)
-        cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        S = min(args.jobs, 100_000)
+        cores = args.cpu_threads or len(os.sched_getaffinity(0))
+        S = min(args.jobs, max(100_000, 2_000 * cores))
         mat = list(bsw.default_params().mat)
         t = time.perf_counter()
         want = oracle.ksw_align2_batch(pairs[:S], ref, qer, mat, nthreads=cores)
@@ -491,8 +686,8 @@ def main_global(args, rank, local, world):
     if world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # CPU baseline leg only (test infrastructure)
-        cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        S = min(args.jobs, 200_000)
+        cores = args.cpu_threads or len(os.sched_getaffinity(0))
+        S = min(args.jobs, max(200_000, 4_000 * cores))
         mat = list(bsw.default_params().mat)
         t = time.perf_counter()
         ws, wc, wn = oracle.ksw_global2_batch(pairs[:S], ref, qer, mat, stride=stride, nthreads=cores)

@@ -35,6 +35,8 @@
 #include "bsw_ext_k.h"
 #include <chrono>
 #include "bsw_internal.h"
+#include "bsw_pool.h"
+#include <emmintrin.h>
 
 namespace bsw {
 
@@ -140,6 +142,15 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
         atomicAdd(&counts[(blockIdx.x % kMetaSpread) * kMetaCounts + threadIdx.x], s_cnt[threadIdx.x]);
 }
 
+// one device call: run_plan's arguments, kept in the slot for run_dp
+struct PlanCall {
+    SeqPair *d_pairs = nullptr;
+    const uint8_t *d_ref = nullptr, *d_qer = nullptr;
+    int32_t n = 0, w = 0;
+    int cell_bits = 16;
+    hipStream_t stream = nullptr;
+};
+
 struct Slot {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -154,6 +165,9 @@ struct Slot {
     int32_t *d_meta = nullptr;          // counts[kMetaCounts], maxq_wide, err
     int32_t *h_meta = nullptr;          // pinned mirror
     int2 *d_scratch = nullptr; size_t cap_scratch = 0;
+    // host-buffer pipeline: pinned staging of one chunk and its device copy
+    void *h_stage = nullptr; size_t cap_stage = 0;
+    uint8_t *d_stage = nullptr; size_t cap_dstage = 0;
     // mate rescue (bsw_mate.h)
     int32_t *d_mjobs = nullptr; size_t cap_mjobs = 0;
     uint16_t *d_mrows = nullptr; size_t cap_mrows = 0;
@@ -179,6 +193,10 @@ struct Slot {
     bool timed = false;
     hipStream_t run_stream = nullptr;   // stream of the last run_device (finish_stats waits on it)
     bsw_stats_t stats{};
+    hipEvent_t evm = nullptr;           // class-count readback of the last run_plan
+    hipStream_t pstream = nullptr;      // high-priority stream of run_plan
+    hipEvent_t evh = nullptr;           // inputs ready on the call's stream (pstream waits)
+    PlanCall plan;                      // arguments of the last run_plan (run_dp's input)
 };
 
 static int hip_rc(hipError_t e)
@@ -222,6 +240,8 @@ struct DeviceCtx {
         (void)hipFree(s->d_pairs); (void)hipFree(s->d_ref); (void)hipFree(s->d_qer);
         (void)hipFree(s->d_keys); (void)hipFree(s->d_keys2); (void)hipFree(s->d_vals); (void)hipFree(s->d_order);
         (void)hipFree(s->d_tmp); (void)hipFree(s->d_meta); (void)hipFree(s->d_scratch);
+        (void)hipFree(s->d_stage);
+        if (s->h_stage) (void)hipHostFree(s->h_stage);
         (void)hipFree(s->d_mjobs); (void)hipFree(s->d_mrows); (void)hipFree(s->d_mmeta);
         (void)hipFree(s->d_mcells); (void)hipFree(s->d_mpairs); (void)hipFree(s->d_maln);
         if (s->h_mmeta) (void)hipHostFree(s->h_mmeta);
@@ -233,6 +253,9 @@ struct DeviceCtx {
         if (s->ev3) (void)hipEventDestroy(s->ev3);
         if (s->h_meta) (void)hipHostFree(s->h_meta);
         if (s->ev0) (void)hipEventDestroy(s->ev0);
+        if (s->evm) (void)hipEventDestroy(s->evm);
+        if (s->evh) (void)hipEventDestroy(s->evh);
+        if (s->pstream) (void)hipStreamDestroy(s->pstream);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         if (s->stream) (void)hipStreamDestroy(s->stream);
         for (int k = 0; k < Slot::kSide; ++k) {
@@ -284,6 +307,7 @@ struct bsw_ctx {
     struct Pinned { std::mutex mu; void *p = nullptr; size_t cap = 0; } pin[2];
     int glob_band = 0;                  // BSW_OPT_GLOB_BAND
     int64_t ext_chunk = 0;              // BSW_OPT_EXT_CHUNK (0: the int32-offset bound)
+    int32_t host_chunk = 262144;        // BSW_OPT_HOST_CHUNK: pairs per host-buffer pipeline chunk
     ~bsw_ctx()
     {
         for (auto &b : pin)
@@ -344,28 +368,43 @@ static hipError_t grow_sort(Slot &s, int32_t n)
     return hipSuccess;
 }
 
-// The device pipeline on one slot's device; d_* are device pointers valid on `stream`.
-// Enqueues plan -> sort -> (one class-count readback) -> DP kernels -> a readback of the
-// kernels' range-guard word into h_meta[kMetaErr]; finish_stats() waits for it and turns a
-// tripped guard into BSW_E_RANGE.
-static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_t *d_ref,
-                      const uint8_t *d_qer, int32_t n, int32_t w, int cell_bits, hipStream_t stream)
+// The device pipeline on one slot's device; d_* are device pointers valid on `stream`, in two
+// halves so a host pipeline can stage the next chunk between them:
+//   run_plan : enqueue plan -> sort -> the class-count readback (nothing waits)
+//   run_dp   : wait for that readback, enqueue the DP kernels and the readback of their
+//              range-guard word into h_meta[kMetaErr]
+// finish_stats() waits for the rest and turns a tripped guard into BSW_E_RANGE.
+static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
 {
-    (void)cell_bits;      // 8 and 16 route alike: the cell width is the planner's per-pair choice
     s.stats = bsw_stats_t{};
     s.timed = false;
-    s.run_stream = stream;
-    if (n == 0) return BSW_OK;
+    s.run_stream = pc.stream;
+    s.plan = pc;
+    if (pc.n == 0) return BSW_OK;
+    const int32_t n = pc.n;
+    // plan + sort run on the slot's high-priority stream (ordered after the call's stream by an
+    // event): while other chunks' DP kernels fill the GPU, their few blocks are dispatched
+    // first instead of queuing behind thousands of DP workgroups (it delays the next chunk's
+    // DP launch otherwise: 1-3 ms per chunk in the host pipeline's trace)
+    if (!s.pstream) {
+        int lo = 0, hi = 0;
+        BSW_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        BSW_TRY(hipStreamCreateWithPriority(&s.pstream, hipStreamNonBlocking, hi));
+        BSW_TRY(hipEventCreateWithFlags(&s.evh, hipEventDisableTiming));
+    }
+    BSW_TRY(hipEventRecord(s.evh, pc.stream));
+    BSW_TRY(hipStreamWaitEvent(s.pstream, s.evh, 0));
+    hipStream_t stream = s.pstream;
     BSW_TRY(grow_sort(s, n));
     BSW_TRY(hipMemsetAsync(s.d_meta, 0, kMetaWords * sizeof(int32_t), stream));
-    int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaMaxq, *d_err = s.d_meta + kMetaErr;
+    int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaMaxq;
     // pairs in the 8-bit score regime (h0 + min(qlen, tlen) <= 255, bwa-style scoring) take the
     // packed-column kernel on both entry points (getScores8 / getScores16: identical results,
     // fewer instructions per cell), the rest the int16 lane kernel (on cell_bits = 8: the
     // overflow fallback) or the int32 wide kernel
     const int pc_route = (kp.pk_ok && kp.kern8) ? 1 : 0;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       d_pairs, n, kp.maxsc, pc_route, d_ref, d_qer, s.d_keys, s.d_vals, d_counts,
+                       pc.d_pairs, n, kp.maxsc, pc_route, pc.d_ref, pc.d_qer, s.d_keys, s.d_vals, d_counts,
                        d_maxq, (int)kp.keymode, (int)kp.misroute);
     BSW_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
@@ -375,7 +414,23 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     BSW_TRY(hipcub::DeviceRadixSort::SortPairs(s.d_tmp, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals,
                                                s.d_order, n, 0, kKeyBits, stream));
     BSW_TRY(hipMemcpyAsync(s.h_meta, s.d_meta, kMetaWords * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
-    BSW_TRY(hipStreamSynchronize(stream));
+    if (!s.evm) BSW_TRY(hipEventCreateWithFlags(&s.evm, hipEventDisableTiming));
+    BSW_TRY(hipEventRecord(s.evm, stream));
+    return BSW_OK;
+}
+
+static int run_dp(const KParams &kp, Slot &s)
+{
+    const PlanCall &pc = s.plan;
+    if (pc.n == 0) return BSW_OK;
+    hipStream_t stream = pc.stream;
+    const int32_t w = pc.w;
+    const int cell_bits = pc.cell_bits;
+    SeqPair *d_pairs = pc.d_pairs;
+    const uint8_t *d_ref = pc.d_ref, *d_qer = pc.d_qer;
+    int32_t *d_err = s.d_meta + kMetaErr;
+    BSW_TRY(hipEventSynchronize(s.evm));           // the class counts are in h_meta
+    BSW_TRY(hipStreamWaitEvent(stream, s.evm, 0)); // order / meta written on the plan stream
     int32_t counts[kNumClasses] = {};
     for (int sl = 0; sl < kMetaSpread; ++sl)
         for (int c = 0; c < kNumClasses; ++c) counts[c] += s.h_meta[sl * kMetaCounts + c];
@@ -454,6 +509,17 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
     return BSW_OK;
 }
 
+static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_t *d_ref,
+                      const uint8_t *d_qer, int32_t n, int32_t w, int cell_bits, hipStream_t stream)
+{
+    PlanCall pc;
+    pc.d_pairs = d_pairs; pc.d_ref = d_ref; pc.d_qer = d_qer;
+    pc.n = n; pc.w = w; pc.cell_bits = cell_bits; pc.stream = stream;
+    int r = run_plan(kp, s, pc);
+    if (r) return r;
+    return run_dp(kp, s);
+}
+
 // Wait for run_device's work (through the guard readback), record the DP kernel time; a
 // tripped range guard is BSW_E_RANGE (the affected pairs' outputs were not written).
 static int finish_stats(Slot &s)
@@ -469,42 +535,317 @@ static int finish_stats(Slot &s)
     return BSW_OK;
 }
 
-// One device's share of a host-buffer call.
+// 4-bit packing of base codes for the host -> device copy: staged byte k = code[2k] |
+// code[2k+1] << 4 (codes 0..4 in the ABI; the low nibble of any code is kept).  Halves the
+// PCIe bytes of the sequences; unpack_kernel restores the byte-per-base buffers in HBM.
+static void pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes)
+{
+    size_t i = 0;
+    const __m128i m0 = _mm_set1_epi16(0x000f), m1 = _mm_set1_epi16(0x00f0);
+    for (; i + 32 <= nbytes; i += 32) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
+        const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
+        const __m128i ra = _mm_or_si128(_mm_and_si128(a, m0), _mm_and_si128(_mm_srli_epi16(a, 4), m1));
+        const __m128i rb = _mm_or_si128(_mm_and_si128(b, m0), _mm_and_si128(_mm_srli_epi16(b, 4), m1));
+        _mm_storeu_si128((__m128i *)(dst + i / 2), _mm_packus_epi16(ra, rb));
+    }
+    for (; i < nbytes; i += 2)
+        dst[i / 2] = (uint8_t)((src[i] & 15) | (i + 1 < nbytes ? (src[i + 1] & 15) << 4 : 0));
+}
+
+static void par_pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes)
+{
+    constexpr size_t kPiece = (size_t)2 << 20;
+    const int nt = (int)std::min<size_t>(HostPool::kWorkers + 1, nbytes / kPiece);
+    if (nt <= 1) { pack_nibbles(dst, src, nbytes); return; }
+    auto cut = [=](size_t t) { return t == (size_t)nt ? nbytes : (nbytes * t / nt) & ~(size_t)31; };
+    HostPool::get().parallel_for(nt, [=](int t) {
+        const size_t a = cut(t), b = cut(t + 1);
+        pack_nibbles(dst + a / 2, src + a, b - a);
+    });
+}
+
+// bytes out[0, n) from nibbles in[0, (n + 1) / 2): 4 packed bytes -> 8 codes per thread
+__global__ void unpack_kernel(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int64_t n)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t o = t * 8;
+    if (o >= n) return;
+    uint32_t v = 0;
+    const int64_t ib = t * 4, nin = (n + 1) / 2;
+    if (ib + 4 <= nin) v = *(const uint32_t *)(in + ib);
+    else
+        for (int k = 0; k < 4 && ib + k < nin; ++k) v |= (uint32_t)in[ib + k] << (8 * k);
+    const uint32_t lo = (v & 0x0f0f0f0fu), hi = (v >> 4) & 0x0f0f0f0fu;
+    // interleave: byte 2k = lo byte k, byte 2k + 1 = hi byte k
+    const uint32_t w0 = __builtin_amdgcn_perm(hi, lo, 0x05010400u);
+    const uint32_t w1 = __builtin_amdgcn_perm(hi, lo, 0x07030602u);
+    if (o + 8 <= n) {
+        *(uint2 *)(out + o) = make_uint2(w0, w1);
+    } else {
+        const uint8_t b[8] = {(uint8_t)w0, (uint8_t)(w0 >> 8), (uint8_t)(w0 >> 16), (uint8_t)(w0 >> 24),
+                              (uint8_t)w1, (uint8_t)(w1 >> 8), (uint8_t)(w1 >> 16), (uint8_t)(w1 >> 24)};
+        for (int k = 0; o + k < n; ++k) out[o + k] = b[k];
+    }
+}
+
+// Pre-pass of a host-buffer call, one parallel sweep over the records: validation (the ABI's
+// BSW_E_RANGE before any device work) and per-block extents of the byte buffers, from which
+// chunks are cut and staged without another pass.
+constexpr int32_t kStageBlk = 4096;           // pairs per block (a chunk is whole blocks)
+struct BlkStat {
+    int64_t r_lo, r_hi, q_lo, q_hi, r_sum, q_sum;
+    bool bad;
+};
+
+static bool prepass(const SeqPair *pairs, int32_t n, std::vector<BlkStat> &bs)
+{
+    const int32_t nb = (n + kStageBlk - 1) / kStageBlk;
+    bs.assign((size_t)nb, BlkStat{});
+    auto blk = [&](int32_t b) {
+        BlkStat t{INT64_MAX, 0, INT64_MAX, 0, 0, 0, false};
+        const int32_t e = std::min(n, (b + 1) * kStageBlk);
+        for (int32_t i = b * kStageBlk; i < e; ++i) {
+            const SeqPair &p = pairs[i];
+            t.bad |= p.len1 < 0 || p.len2 < 0 || p.len1 > BSW_MAX_LEN || p.len2 > BSW_MAX_LEN || p.idr < 0 ||
+                     p.idq < 0;
+            if (p.len1 > 0) { t.r_lo = std::min<int64_t>(t.r_lo, p.idr); t.r_hi = std::max<int64_t>(t.r_hi, (int64_t)p.idr + p.len1); t.r_sum += p.len1; }
+            if (p.len2 > 0) { t.q_lo = std::min<int64_t>(t.q_lo, p.idq); t.q_hi = std::max<int64_t>(t.q_hi, (int64_t)p.idq + p.len2); t.q_sum += p.len2; }
+        }
+        bs[b] = t;
+    };
+    if (nb < 16) {
+        for (int32_t b = 0; b < nb; ++b) blk(b);
+    } else {
+        const int nt = HostPool::kWorkers + 1;
+        HostPool::get().parallel_for(nt, [&](int t) {
+            for (int32_t b = (int32_t)((int64_t)nb * t / nt); b < (int32_t)((int64_t)nb * (t + 1) / nt); ++b) blk(b);
+        });
+    }
+    for (const auto &t : bs)
+        if (t.bad) return false;
+    return true;
+}
+
+// One chunk of a host-buffer call staged in a slot's pinned buffer: [SeqPair x n | ref | qer].
+// Contiguous chunks (the upstream layout: each batch's windows concatenated in pair order) pack
+// their byte extents into nibbles (unpacked in HBM by unpack_kernel); scattered ones are
+// gathered pair by pair as bytes and the staged records' idr / idq rewritten (only outputs
+// ever go back to the caller).
+struct StagedChunk {
+    int32_t n = 0;
+    bool packed = false;
+    size_t pair_off = 0, ref_off = 0, qer_off = 0, bytes = 0;
+    size_t rb = 0, qb = 0;              // ref / qer bytes after unpacking
+    int64_t r_base = 0, q_base = 0;     // staged ref byte 0 = caller byte r_base (bulk mode)
+};
+
+// blocks [b0, b1) = pairs [a, a + n)
+static int stage_chunk(Slot &s, const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t n,
+                       const BlkStat *bs, int32_t nblk, StagedChunk &c)
+{
+    int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
+    for (int32_t b = 0; b < nblk; ++b) {
+        r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi); r_sum += bs[b].r_sum;
+        q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi); q_sum += bs[b].q_sum;
+    }
+    if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+    if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+    // bulk when the extents hold little besides the chunk's own bytes; else gather
+    const bool bulk = (r_hi - r_lo) <= r_sum + r_sum / 4 + 4096 && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096;
+    c.rb = (size_t)(bulk ? r_hi - r_lo : r_sum);
+    c.qb = (size_t)(bulk ? q_hi - q_lo : q_sum);
+    c.packed = bulk;
+    const size_t rs = bulk ? (c.rb + 1) / 2 : c.rb, qs = bulk ? (c.qb + 1) / 2 : c.qb;   // staged sizes
+    c.n = n;
+    c.pair_off = 0;
+    c.ref_off = ((size_t)n * sizeof(SeqPair) + 255) & ~(size_t)255;
+    c.qer_off = (c.ref_off + rs + 4 + 255) & ~(size_t)255;     // +4: kernels' aligned dword loads
+    c.bytes = c.qer_off + qs + 4;
+    if (c.bytes > s.cap_stage) {
+        const size_t cap = std::max(c.bytes, s.cap_stage * 3 / 2);
+        if (s.h_stage) (void)hipHostFree(s.h_stage);
+        s.h_stage = nullptr; s.cap_stage = 0;
+        BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));
+        s.cap_stage = cap;
+    }
+    uint8_t *h = (uint8_t *)s.h_stage;
+    SeqPair *sp = (SeqPair *)(h + c.pair_off);
+    if (bulk) {
+        c.r_base = r_lo; c.q_base = q_lo;
+        // records + both packs as one pool job list (pieces of ~2 MB)
+        const size_t pb = (size_t)n * sizeof(SeqPair);
+        const int np = (int)std::max<size_t>(1, pb >> 21), nr = (int)std::max<size_t>(1, c.rb >> 22),
+                  nq = (int)std::max<size_t>(1, c.qb >> 22);
+        auto even = [](size_t total, int k, int parts) {
+            return k == parts ? total : (total * (size_t)k / (size_t)parts) & ~(size_t)31;
+        };
+        HostPool::get().parallel_for(np + nr + nq, [&](int t) {
+            if (t < np) {
+                const size_t a0 = pb * t / np, a1 = pb * (t + 1) / np;
+                memcpy((char *)sp + a0, (const char *)pairs + a0, a1 - a0);
+            } else if (t < np + nr) {
+                const size_t a0 = even(c.rb, t - np, nr), a1 = even(c.rb, t - np + 1, nr);
+                pack_nibbles(h + c.ref_off + a0 / 2, ref + r_lo + a0, a1 - a0);
+            } else {
+                const size_t a0 = even(c.qb, t - np - nr, nq), a1 = even(c.qb, t - np - nr + 1, nq);
+                pack_nibbles(h + c.qer_off + a0 / 2, qer + q_lo + a0, a1 - a0);
+            }
+        });
+    } else {
+        par_memcpy(sp, pairs, (size_t)n * sizeof(SeqPair));
+        c.r_base = c.q_base = 0;
+        int64_t ro = 0, qo = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            SeqPair &p = sp[i];
+            if (p.len1 > 0) { memcpy(h + c.ref_off + ro, ref + p.idr, (size_t)p.len1); p.idr = (int32_t)ro; ro += p.len1; }
+            else p.idr = 0;
+            if (p.len2 > 0) { memcpy(h + c.qer_off + qo, qer + p.idq, (size_t)p.len2); p.idq = (int32_t)qo; qo += p.len2; }
+            else p.idq = 0;
+        }
+    }
+    memset(h + c.ref_off + rs, 0, 4);
+    memset(h + c.qer_off + qs, 0, 4);
+    return BSW_OK;
+}
+
+// outputs of a finished chunk (staged records) -> the caller's records.  Bulk-staged records
+// carry the caller's own input fields, so whole records copy back; gathered ones had their
+// offsets rewritten and copy field by field.
+static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, bool whole)
+{
+    const SeqPair *sp = (const SeqPair *)s.h_stage;
+    if (whole) {
+        par_memcpy(pairs, sp, (size_t)n * sizeof(SeqPair));
+        return;
+    }
+    for (int32_t i = 0; i < n; ++i) {
+        pairs[i].score = sp[i].score; pairs[i].tle = sp[i].tle; pairs[i].gtle = sp[i].gtle;
+        pairs[i].qle = sp[i].qle; pairs[i].gscore = sp[i].gscore; pairs[i].max_off = sp[i].max_off;
+    }
+}
+
+// One device's share of a host-buffer call: a pipeline of chunks over up to three slots.
+// Per chunk: stage into the slot's pinned buffer (records + nibble-packed sequences, host
+// pool) -> one H2D -> unpack -> plan / sort -> DP kernels -> D2H of the records.  The host
+// stages chunk k + 1 while chunk k's copy and plan run and chunk k - 1's kernels compute;
+// chunks ramp from ~n/32 pairs up to `chunk` so the first kernels start early.  Outputs are
+// identical to one unchunked call (pairs are independent).
 static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref,
-                      const uint8_t *qer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *st)
+                      const uint8_t *qer, int32_t n, int32_t w, int cell_bits, int32_t chunk,
+                      bsw_stats_t *st)
 {
     if (n == 0) return BSW_OK;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t_start = now();
+    std::vector<BlkStat> bs;
+    if (!prepass(pairs, n, bs)) return BSW_E_RANGE;
+    if (chunk <= 0) chunk = n;
+    constexpr int nslots = 3;  // slots are taken as chunks start (a one-chunk call takes one)
     int rc = BSW_OK;
-    auto slot = dc.acquire(rc);
-    if (!slot) return rc;
-    Slot &s = *slot;
+    std::unique_ptr<Slot> slots[nslots];
+    slots[0] = dc.acquire(rc);
+    if (rc) return rc;
+    int32_t pend_at[nslots] = {}, pend_n[nslots] = {};  // chunk in flight per slot
+    bool pend_whole[nslots] = {};
+    bsw_stats_t agg{};
+    auto finish = [&](int k) -> int {                   // wait for slot k's chunk, outputs back
+        if (pend_n[k] == 0) return BSW_OK;
+        Slot &s = *slots[k];
+        const int r = finish_stats(s);                  // also BSW_E_RANGE: kernel guard tripped
+        if (r) return r;
+        unstage_outputs(s, pairs + pend_at[k], pend_n[k], pend_whole[k]);
+        agg.kernel_ms += s.stats.kernel_ms;
+        agg.n_i16 += s.stats.n_i16; agg.n_u8 += s.stats.n_u8; agg.n_wide += s.stats.n_wide;
+        agg.n_packed += s.stats.n_packed; agg.n_launches += s.stats.n_launches;
+        pend_n[k] = 0;
+        return BSW_OK;
+    };
+    double stage_ms = 0;
     rc = [&]() -> int {
         BSW_TRY(hipSetDevice(dc.device));
-        // extents of the byte buffers this shard touches
-        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
-        for (int32_t i = 0; i < n; ++i) {
-            const SeqPair &p = pairs[i];
-            if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
-            if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
+        int k = 0, prev = -1;
+        // the previous chunk's DP launches + record readback, enqueued once the next chunk is
+        // staged and its H2D / plan are queued behind them
+        auto launch_prev = [&]() -> int {
+            if (prev < 0) return BSW_OK;
+            Slot &p = *slots[prev];
+            const int r = run_dp(kp, p);
+            if (r) return r;
+            BSW_TRY(hipMemcpyAsync(p.h_stage, p.plan.d_pairs, (size_t)p.plan.n * sizeof(SeqPair),
+                                   hipMemcpyDeviceToHost, p.stream));
+            prev = -1;
+            return BSW_OK;
+        };
+        const int32_t nblk = (int32_t)bs.size();
+        const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
+        // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
+        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
+        for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, cur = std::min(cap_blk, cur * 2)) {
+            // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
+            int64_t bytes = 0;
+            for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
+                const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
+                if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
+                bytes += x;
+            }
+            const int32_t a = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a;
+            int r = prev == k ? launch_prev() : BSW_OK;
+            if (r) return r;
+            if ((r = finish(k))) return r;              // slot k's last chunk
+            if (!slots[k]) {
+                slots[k] = dc.acquire(r);
+                if (r) return r;
+            }
+            Slot &s = *slots[k];
+            StagedChunk c;
+            const auto t0 = now();
+            if ((r = stage_chunk(s, pairs + a, ref, qer, m, bs.data() + b, nb, c))) return r;
+            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
+            BSW_TRY(grow(s.d_stage, s.cap_dstage, c.bytes));
+            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.bytes, hipMemcpyHostToDevice, s.stream));
+            const uint8_t *d_r = s.d_stage + c.ref_off, *d_q = s.d_stage + c.qer_off;
+            if (c.packed) {                 // nibbles -> one byte per base in the slot's buffers
+                BSW_TRY(grow(s.d_ref, s.cap_ref, c.rb + 4));
+                BSW_TRY(grow(s.d_qer, s.cap_qer, c.qb + 4));
+                BSW_TRY(hipMemsetAsync(s.d_ref + c.rb, 0, 4, s.stream));
+                BSW_TRY(hipMemsetAsync(s.d_qer + c.qb, 0, 4, s.stream));
+                const int64_t tr = ((int64_t)c.rb + 7) / 8, tq = ((int64_t)c.qb + 7) / 8;
+                if (tr > 0)
+                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, s.stream,
+                                       d_r, s.d_ref, (int64_t)c.rb);
+                if (tq > 0)
+                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, s.stream,
+                                       d_q, s.d_qer, (int64_t)c.qb);
+                BSW_TRY(hipGetLastError());
+                d_r = s.d_ref;
+                d_q = s.d_qer;
+            }
+            PlanCall pc;
+            pc.d_pairs = (SeqPair *)(s.d_stage + c.pair_off);
+            // kernels index ref / qer by idr / idq: shift the bases so staged byte 0 is r_base / q_base
+            pc.d_ref = d_r - c.r_base;
+            pc.d_qer = d_q - c.q_base;
+            pc.n = m; pc.w = w; pc.cell_bits = cell_bits; pc.stream = s.stream;
+            if ((r = run_plan(kp, s, pc))) return r;
+            if ((r = launch_prev())) return r;
+            pend_at[k] = a; pend_n[k] = m; pend_whole[k] = c.packed;
+            prev = k;
         }
-        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
-        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
-        const size_t rbytes = (size_t)(r_hi - r_lo) + 1, qbytes = (size_t)(q_hi - q_lo) + 1;
-        BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)n));
-        BSW_TRY(grow(s.d_ref, s.cap_ref, rbytes));
-        BSW_TRY(grow(s.d_qer, s.cap_qer, qbytes));
-        BSW_TRY(hipMemcpyAsync(s.d_pairs, pairs, (size_t)n * sizeof(SeqPair), hipMemcpyHostToDevice, s.stream));
-        if (r_hi > r_lo) BSW_TRY(hipMemcpyAsync(s.d_ref, ref + r_lo, (size_t)(r_hi - r_lo), hipMemcpyHostToDevice, s.stream));
-        if (q_hi > q_lo) BSW_TRY(hipMemcpyAsync(s.d_qer, qer + q_lo, (size_t)(q_hi - q_lo), hipMemcpyHostToDevice, s.stream));
-        // kernels index ref/qer by idr/idq: shift the base so d_ref[idr - r_lo] is byte idr
-        int r = run_device(kp, s, s.d_pairs, s.d_ref - r_lo, s.d_qer - q_lo, n, w, cell_bits, s.stream);
+        int r = launch_prev();
         if (r) return r;
-        BSW_TRY(hipMemcpyAsync(pairs, s.d_pairs, (size_t)n * sizeof(SeqPair), hipMemcpyDeviceToHost, s.stream));
-        if ((r = finish_stats(s))) return r;             // also BSW_E_RANGE: kernel guard tripped
-        if (st) *st = s.stats;
+        for (int j = 0; j < nslots; ++j)
+            if ((r = finish(j))) return r;
         return BSW_OK;
     }();
-    dc.give_back(std::move(slot));
+    agg.stage_ms = (float)stage_ms;
+    agg.host_ms = (float)std::chrono::duration<double, std::milli>(now() - t_start).count();
+    for (int k = 0; k < nslots; ++k) {
+        if (!slots[k]) continue;
+        if (rc) (void)hipStreamSynchronize(slots[k]->stream);   // nothing in flight on a returned slot
+        dc.give_back(std::move(slots[k]));
+    }
+    if (rc == BSW_OK && st) *st = agg;
     return rc;
 }
 
@@ -769,6 +1110,38 @@ static int validate(const SeqPair *pairs, int32_t n, int32_t w, int cell_bits)
 
 namespace bsw {
 
+// Static band cells of one pair (rows i < tlen, columns [max(0, i - w), min(qlen, i + w + 1))):
+// the work estimate behind the multi-device split.
+static int64_t band_cells_est(int64_t qlen, int64_t tlen, int64_t w)
+{
+    if (qlen <= 0 || tlen <= 0) return 0;
+    const int64_t T = std::min(tlen, qlen + w);                  // rows with a non-empty band
+    auto ssum = [](int64_t a, int64_t b, int64_t c) {            // sum_{i=a}^{b-1} (i + c)
+        return b > a ? (b - a) * (a + b - 1) / 2 + c * (b - a) : (int64_t)0;
+    };
+    const int64_t k = std::min(T, std::max<int64_t>(qlen - w, 0));   // rows with i + w + 1 <= qlen
+    const int64_t hi = ssum(0, k, w + 1) + qlen * (T - k);
+    const int64_t lo = ssum(std::min(T, w + 1), T, -w);              // rows with i > w
+    return std::max<int64_t>(hi - lo, 0);
+}
+
+// nd + 1 cut points: device d takes pairs [cut[d], cut[d+1]), each range ~1/nd of the cells
+// (plus a per-pair constant for the plan / sort / launch share)
+static std::vector<int32_t> split_by_cells(const SeqPair *pairs, int32_t n, int32_t w, int nd)
+{
+    std::vector<int64_t> pre((size_t)n + 1, 0);
+    for (int32_t i = 0; i < n; ++i)
+        pre[i + 1] = pre[i] + 64 + band_cells_est(pairs[i].len2, pairs[i].len1, w);
+    std::vector<int32_t> cut((size_t)nd + 1, n);
+    cut[0] = 0;
+    for (int d = 1; d < nd; ++d) {
+        const int64_t target = pre[n] * d / nd;
+        cut[d] = (int32_t)(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
+        cut[d] = std::max(cut[d], cut[d - 1]);
+    }
+    return cut;
+}
+
 int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *seqBufRef,
               const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *out)
 {
@@ -778,24 +1151,29 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
     *out = bsw_stats_t{};
     if (n == 0) return BSW_OK;
     if (!seqBufRef || !seqBufQer) return BSW_E_INVAL;
-    for (int32_t i = 0; i < n; ++i)
-        if (pairs[i].len1 < 0 || pairs[i].len2 < 0 || pairs[i].len1 > BSW_MAX_LEN ||
-            pairs[i].len2 > BSW_MAX_LEN || pairs[i].idr < 0 || pairs[i].idq < 0)
-            return BSW_E_RANGE;
     KParams kp = ctx->kp;
     kp.end_bonus = end_bonus;
     const int nd = (int)ctx->devs.size();
+    // one device: host_shard's parallel pre-pass validates; several: validate the whole batch
+    // before any device starts
+    if (nd > 1)
+        for (int32_t i = 0; i < n; ++i)
+            if (pairs[i].len1 < 0 || pairs[i].len2 < 0 || pairs[i].len1 > BSW_MAX_LEN ||
+                pairs[i].len2 > BSW_MAX_LEN || pairs[i].idr < 0 || pairs[i].idq < 0)
+                return BSW_E_RANGE;
     std::vector<int> rcs(nd, BSW_OK);
     std::vector<bsw_stats_t> st(nd);
     if (nd == 1) {
-        rcs[0] = host_shard(kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, cell_bits, &st[0]);
+        rcs[0] = host_shard(kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, cell_bits, ctx->host_chunk, &st[0]);
     } else {
+        // contiguous pair ranges of equal estimated work (static band cells)
+        const std::vector<int32_t> cut = split_by_cells(pairs, n, w, nd);
         std::vector<std::thread> th;
         for (int d = 0; d < nd; ++d) {
-            const int32_t a = (int32_t)((int64_t)n * d / nd), b = (int32_t)((int64_t)n * (d + 1) / nd);
+            const int32_t a = cut[d], b = cut[d + 1];
             th.emplace_back([&, d, a, b] {
                 rcs[d] = host_shard(kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a, w,
-                                    cell_bits, &st[d]);
+                                    cell_bits, ctx->host_chunk, &st[d]);
             });
         }
         for (auto &t : th) t.join();
@@ -806,6 +1184,8 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
         agg.kernel_ms = std::max(agg.kernel_ms, st[d].kernel_ms);
         agg.n_i16 += st[d].n_i16; agg.n_u8 += st[d].n_u8; agg.n_wide += st[d].n_wide; agg.n_packed += st[d].n_packed;
         agg.n_launches += st[d].n_launches;
+        agg.stage_ms = std::max(agg.stage_ms, st[d].stage_ms);
+        agg.host_ms = std::max(agg.host_ms, st[d].host_ms);
     }
     *out = agg;
     return BSW_OK;
@@ -1222,6 +1602,14 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
     return BSW_OK;
 }
 
+int bsw_split_by_cells(const SeqPair *pairs, int32_t n, int32_t w, int32_t parts, int32_t *cut)
+{
+    if (n < 0 || w < 0 || parts < 1 || !cut || (n > 0 && !pairs)) return BSW_E_INVAL;
+    const std::vector<int32_t> c = bsw::split_by_cells(pairs, n, w, parts);
+    std::copy(c.begin(), c.end(), cut);
+    return BSW_OK;
+}
+
 int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
 {
     if (!ctx) return BSW_E_INVAL;
@@ -1232,6 +1620,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     case BSW_OPT_SORTKEY: if (!b01) return BSW_E_INVAL; ctx->kp.keymode = value ? 2 : 0; return BSW_OK;
     case BSW_OPT_GLOB_BAND: if (!b01) return BSW_E_INVAL; ctx->glob_band = (int)value; return BSW_OK;
     case BSW_OPT_EXT_CHUNK: if (value < 0) return BSW_E_INVAL; ctx->ext_chunk = value; return BSW_OK;
+    case BSW_OPT_HOST_CHUNK: if (value < 1 || value > INT32_MAX) return BSW_E_INVAL; ctx->host_chunk = (int32_t)value; return BSW_OK;
     case BSW_OPT_TEST_MISROUTE: if (!b01) return BSW_E_INVAL; ctx->kp.misroute = (int8_t)value; return BSW_OK;
     default: return BSW_E_INVAL;
     }

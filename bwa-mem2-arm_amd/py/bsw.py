@@ -32,10 +32,11 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
                "bswb_write", "bswb_read_header", "bswb_read",
                "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats",
                "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
-               "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option")
+               "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option",
+               "bsw_split_by_cells")
 
 # include/bsw.h engine options (bsw_set_option)
-OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK = 1, 2, 3, 4, 5
+OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK = 1, 2, 3, 4, 5, 6
 OPT_TEST_MISROUTE = 100
 
 # include/bsw_ext.h structs
@@ -63,7 +64,8 @@ class Params(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_float), ("n_i16", ctypes.c_int32),
                 ("n_u8", ctypes.c_int32), ("n_wide", ctypes.c_int32),
-                ("n_launches", ctypes.c_int32), ("n_packed", ctypes.c_int32)]
+                ("n_launches", ctypes.c_int32), ("n_packed", ctypes.c_int32),
+                ("stage_ms", ctypes.c_float), ("host_ms", ctypes.c_float)]
 
 
 def default_params(a=1, b=4, o_del=6, e_del=1, o_ins=6, e_ins=1, zdrop=100, end_bonus=5,
@@ -120,11 +122,13 @@ def hip_lib():
         L.bsw_set_reference.argtypes = [P, P, ctypes.c_int64]
         L.bsw_extend_seeds_device.argtypes = [P, P, P, P, P, P, ctypes.c_int32, P, P]
         L.bsw_set_option.argtypes = [P, ctypes.c_int, ctypes.c_int64]
+        L.bsw_split_by_cells.argtypes = [P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
                   "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
-                  "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option"):
+                  "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option",
+               "bsw_split_by_cells"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -151,10 +155,10 @@ class Engine:
             self.set_option(k, v)
 
     _OPTS = {"kernel8": OPT_KERNEL8, "fork": OPT_FORK, "sortkey": OPT_SORTKEY, "glob_band": OPT_GLOB_BAND,
-             "ext_chunk": OPT_EXT_CHUNK, "test_misroute": OPT_TEST_MISROUTE}
+             "ext_chunk": OPT_EXT_CHUNK, "host_chunk": OPT_HOST_CHUNK, "test_misroute": OPT_TEST_MISROUTE}
 
     def set_option(self, name, value: int):
-        """bsw_set_option by name (kernel8, fork, sortkey, glob_band, ext_chunk, test_misroute)
+        """bsw_set_option by name (kernel8, fork, sortkey, glob_band, ext_chunk, host_chunk, test_misroute)
         or by BSW_OPT_* number."""
         opt = self._OPTS[name] if isinstance(name, str) else int(name)
         _check(hip_lib().bsw_set_option(self._ctx, opt, int(value)))
@@ -190,6 +194,14 @@ class Engine:
         s = Stats()
         _check(hip_lib().bsw_last_stats(self._ctx, ctypes.byref(s)))
         return s
+
+
+def split_by_cells(pairs: np.ndarray, w: int, parts: int) -> np.ndarray:
+    """bsw_split_by_cells: parts + 1 cut points of equal static band cells (host-only)."""
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    cut = np.zeros(parts + 1, dtype=np.int32)
+    _check(hip_lib().bsw_split_by_cells(_ptr(pairs), len(pairs), w, parts, _ptr(cut)))
+    return cut
 
 
 # ---------------------------------------------------------------- .bswb batch files

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BSW_ABI_VERSION 3
+#define BSW_ABI_VERSION 4
 
 enum {
     BSW_OK = 0,
@@ -95,6 +95,10 @@ typedef struct bsw_stats_t {
     int32_t n_launches;         /* DP-kernel launches                                    */
     int32_t n_packed;           /* of n_i16 + n_u8: pairs run on the 8-bit-regime packed
                                    kernels (v_pk_* cells; ABI version 2)                 */
+    float   stage_ms;           /* host-buffer calls: host time staging chunks into pinned
+                                   memory (ABI version 4; 0 for device calls)            */
+    float   host_ms;            /* host-buffer calls: wall time of the call on the device's
+                                   host thread (staging + H2D + kernels + D2H)           */
 } bsw_stats_t;
 int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
 
@@ -112,10 +116,22 @@ enum {
     BSW_OPT_GLOB_BAND = 4,    /* bsw_ksw_global2: 0 = column kernel first (default),
                                  1 = band kernel for every band-eligible job                  */
     BSW_OPT_EXT_CHUNK = 5,    /* extension calls: reads per chunk (0 = the int32-offset bound) */
+    BSW_OPT_HOST_CHUNK = 6,   /* bsw_get_scores: largest pipeline chunk in pairs (default
+                                 262144, rounded down to whole 4096-pair blocks, at least one):
+                                 a host-buffer call is staged, copied and computed chunk by
+                                 chunk over up to three streams so copies overlap the DP
+                                 kernels; calls of <= 128K pairs run as one chunk            */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };
 int  bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value);
+
+/* Work-balanced split of one batch into `parts` contiguous pair ranges (what an n_gpus
+ * context does inside bsw_get_scores, and what a one-process-per-GPU caller uses to shard a
+ * batch across ranks): part k = pairs [cut[k], cut[k+1]), cut[0] = 0, cut[parts] = n, each
+ * holding ~1/parts of the static band cells.  cut has parts + 1 entries.
+ * Host-only arithmetic; needs no device. */
+int  bsw_split_by_cells(const SeqPair *pairs, int32_t n, int32_t w, int32_t parts, int32_t *cut);
 
 const char *bsw_strerror(int code);
 int  bsw_abi_version(void);

@@ -283,8 +283,8 @@ int sse41_get_scores16(const sse_params_t *p, SeqPair *pairs, const uint8_t *ref
     if (nthreads <= 1) {
         sse_worker(&jb);
     } else {
-        pthread_t th[256];
-        if (nthreads > 256) nthreads = 256;
+        pthread_t th[512];
+        if (nthreads > 512) nthreads = 512;
         for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, sse_worker, &jb);
         for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
     }

@@ -251,9 +251,9 @@ void oracle_ksw_align2_batch(const void *pairs, const uint8_t *ref, const uint8_
                              int nthreads)
 {
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > 64) nthreads = 64;
-    pthread_t th[64];
-    ojob_t jb[64];
+    if (nthreads > 512) nthreads = 512;
+    pthread_t th[512];
+    ojob_t jb[512];
     for (int t = 0; t < nthreads; ++t) {
         jb[t] = (ojob_t){(const oseqpair_t *)pairs, ref, qer, (okswr_t *)aln, n, nthreads, t, mat, o_del,
                          e_del, o_ins, e_ins};

@@ -192,9 +192,9 @@ void oracle_get_scores_mt(const oracle_params_t *p, SeqPair *pairs, const uint8_
         oracle_get_scores(p, pairs, r, q, n, w);
         return;
     }
-    pthread_t th[256];
-    oracle_job_t jobs[256];
-    if (nthreads > 256) nthreads = 256;
+    pthread_t th[512];
+    oracle_job_t jobs[512];
+    if (nthreads > 512) nthreads = 512;
     for (int t = 0; t < nthreads; ++t) {
         int32_t a = (int32_t)((int64_t)n * t / nthreads), b = (int32_t)((int64_t)n * (t + 1) / nthreads);
         jobs[t] = (oracle_job_t){p, pairs + a, r, q, b - a, w};

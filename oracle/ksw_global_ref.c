@@ -168,9 +168,9 @@ void oracle_ksw_global2_batch(const void *pairs, const uint8_t *ref, const uint8
                               int32_t *score, uint32_t *cigar, int stride, int32_t *n_cigar, int nthreads)
 {
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > 64) nthreads = 64;
-    pthread_t th[64];
-    og_job_t J[64];
+    if (nthreads > 512) nthreads = 512;
+    pthread_t th[512];
+    og_job_t J[512];
     for (int t = 0; t < nthreads; ++t) {
         J[t] = (og_job_t){(const og_pair_t *)pairs, ref, qer, n, mat, o_del, e_del, o_ins, e_ins,
                           score, cigar, stride, n_cigar, (int)((int64_t)n * t / nthreads),

@@ -69,7 +69,7 @@ def test_params_default_and_abi_version():
     assert (p.o_del, p.e_del, p.o_ins, p.e_ins, p.zdrop, p.end_bonus) == (6, 1, 6, 1, 100, 5)
     mat = np.frombuffer(bytes(p.mat), np.int8).reshape(5, 5)
     assert mat[0, 0] == 1 and mat[0, 1] == -4 and mat[4, 4] == -1 and mat[2, 4] == -1
-    assert lib.bsw_abi_version() == 3
+    assert lib.bsw_abi_version() == 4
     ref = bsw.default_params()
     assert bytes(ref.mat) == bytes(p.mat)
 
@@ -129,3 +129,31 @@ def test_ext_header_layouts_compile(tmp_path):
     assert r.returncode == 0, r.stderr
     assert bsw.SEED_DTYPE.itemsize == 16 and bsw.ALNREG_DTYPE.itemsize == 40
     assert ctypes.sizeof(bsw.ExtOpt) == 16
+
+
+def _static_cells(q, t, w):
+    return sum(max(0, min(q, i + w + 1) - max(0, i - w)) for i in range(t))
+
+
+def test_split_by_cells_balances_static_band_cells():
+    """bsw_split_by_cells (host-only): contiguous parts of ~equal static band cells; the split
+    the n_gpus engine and bench.py's strong-scaling ranks use."""
+    rng = np.random.default_rng(5)
+    n, w = 3000, 40
+    pairs = np.zeros(n, dtype=bsw.SEQPAIR_DTYPE)
+    pairs["len2"] = rng.integers(0, 200, n)
+    pairs["len1"] = rng.integers(0, 400, n)
+    pairs["len2"][:1000] = 20                     # a cheap head: a count split would be unbalanced
+    cost = np.array([64 + _static_cells(int(q), int(t), w) for q, t in zip(pairs["len2"], pairs["len1"])])
+    for parts in (1, 2, 3, 8):
+        cut = bsw.split_by_cells(pairs, w, parts)
+        assert cut[0] == 0 and cut[-1] == n and np.all(np.diff(cut) >= 0)
+        shares = [cost[cut[k]:cut[k + 1]].sum() for k in range(parts)]
+        assert max(shares) - min(shares) <= 2 * cost.max(), (parts, shares)
+    # closed form == the row sum on the C2 shape (25,100 cells: SURVEY.md §8(d))
+    one = np.zeros(2, dtype=bsw.SEQPAIR_DTYPE)
+    one["len2"], one["len1"] = 150, 300
+    assert _static_cells(150, 300, 100) == 25_100
+    assert list(bsw.split_by_cells(one, 100, 2)) == [0, 1, 2]
+    with pytest.raises(bsw.BswError):
+        bsw.split_by_cells(one, 100, 0)

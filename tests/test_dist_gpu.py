@@ -1,0 +1,53 @@
+"""Multi-rank runs of the HIP engine (the N > 1 path of bench.py) on the GPU box.
+
+Two ranks (torchrun, one process per rank, gloo for the control plane) share the box's one
+GPU under --rehearse: bench.py --scaling strong splits ONE batch by static band cells
+(bsw_split_by_cells), each rank scores its range through the host-buffer C ABI, rank 0
+gathers the records.  The gathered outputs must equal the CPU oracle on the whole batch,
+and the split must tile the batch.  (the 8-GPU curve is the driver's.)"""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import bsw
+import oracle
+from conftest import ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2])
+def test_ranks_strong_split_equal_oracle(tmp_path, world):
+    n = 120_000
+    dump = str(tmp_path / "out.npy")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--scaling", "strong", "--total-pairs", str(n),
+           "--steps", "1", "--warmup", "1", "--rehearse", "--dump", dump]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["scaling"] == "strong" and line["n_gpus"] == world and "rehearsal" in line
+    cut = line["config"]["cut"]
+    assert cut[0] == 0 and cut[-1] == n and len(cut) == world + 1
+    got = np.load(dump)
+    assert got.dtype == bsw.SEQPAIR_DTYPE and len(got) == n
+    full, ref, qer = bsw.synth_batch(n)
+    want = full.copy()
+    oracle.get_scores(oracle.make_params(), want, ref, qer, 100, nthreads=16)
+    for f in ("len1", "len2", "h0") + bsw.OUT_FIELDS:
+        assert np.array_equal(got[f], want[f]), f

@@ -222,6 +222,26 @@ def test_concurrent_callers(eng):
         _assert_same(wants[k], gots[k], f"thread {k}")
 
 
+@pytest.mark.parametrize("chunk", [1, 8192, 1 << 20])
+def test_host_pipeline_chunks(chunk):
+    """Host-buffer pipeline (bsw_get_scores): the batch is staged / copied / computed chunk by
+    chunk over two slots (BSW_OPT_HOST_CHUNK); contiguous batches stage byte extents in bulk,
+    permuted ones are gathered pair by pair with rewritten offsets.  Chunks are whole 4096-pair
+    blocks: chunk 1 and 8192 give 3 and 3 chunks, 1 << 20 one.  Outputs equal the oracle and
+    only the six output fields of the caller's records change."""
+    e = bsw.Engine(host_chunk=chunk)
+    pairs, ref, qer = bswgen.random_pairs(20000 if chunk > 1 else 9000, seed=chunk % 1000, qlen=(0, 190), tlen=(0, 330))
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    for order in (np.arange(len(pairs)), np.random.default_rng(chunk).permutation(len(pairs))):
+        got = pairs[order].copy()
+        e.get_scores(got, ref, qer, 100)
+        _assert_same(want[order], got, f"chunk {chunk}")
+        for f in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid"):
+            assert np.array_equal(got[f], pairs[order][f])
+    e.close()
+
+
 def test_multi_gpu_context_shards(c2_full):
     pairs, ref, qer, want = c2_full
     n = hiprt.device_count()
