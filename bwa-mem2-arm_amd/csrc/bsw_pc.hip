@@ -142,15 +142,16 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
 #define PC_CNT_OPS
 #endif
 
+// Layout: the FAST body is the fall-through path (one bit test, a not-taken branch, no taken
+// branch); skipped and masked groups branch to code in subsection 1 of the kernel's section
+// (out of line, after the kernel's main body) and back.  Branch targets stay inside the
+// kernel's own section (built with -ffunction-sections), well within s_cbranch's +-128 KB.
 #define PC_GROUP_ASM(KEYA_FAST, KEYA_MASK)                                                \
     asm volatile(                                                                            \
-        "s_bitcmp1_b64 %[men], %[g]\n\t"             /* outside [min beg, max end]: skip */ \
-        "s_cbranch_scc0 3f\n\t"                                                              \
-        PC_CNT(0)                                                                            \
-        PC_SCORES                                                                            \
         "s_bitcmp1_b64 %[mfa], %[g]\n\t"             /* every live lane in band: FAST */    \
-        "s_cbranch_scc0 2f\n\t"                                                              \
-        PC_CNT(1)                                                                            \
+        "s_cbranch_scc0 5f\n\t"                                                              \
+        PC_CNT(0) PC_CNT(1)                                                                  \
+        PC_SCORES                                                                            \
         PC_PH1("a", "%[ea]") PC_PH1("b", "%[eb]")                                            \
         PC_CELL("%[c0]", "a", "WORD_0")                                                      \
         PC_CELL("%[c1]", "a", "WORD_1")                                                      \
@@ -161,9 +162,14 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
         KEYA_FAST                                                                            \
         "v_pk_max_u16 %[key], %[key], %[pa]\n\t"                                             \
         "v_lshl_or_b32 %[pb], %[hb], 8, %[jjb]\n\t"                                          \
-        "v_pk_max_u16 %[key], %[key], %[pb]\n\t"                                             \
-        "s_branch 3f\n"                                                                      \
-        "2:\n\t"                                                                             \
+        "v_pk_max_u16 %[key], %[key], %[pb]\n"                                               \
+        "3:\n"                                                                               \
+        ".subsection 1\n"                                                                    \
+        "5:\n\t"                                                                             \
+        "s_bitcmp1_b64 %[men], %[g]\n\t"             /* outside [min beg, max end]: skip */ \
+        "s_cbranch_scc0 3b\n\t"                                                              \
+        PC_CNT(0)                                                                            \
+        PC_SCORES                                                                            \
         "s_bitcmp1_b64 %[mle], %[g]\n\t"             /* some lane's beg in this group: L */ \
         "s_cbranch_scc1 4f\n\t"                                                              \
         PC_CNT(2)                                                                            \
@@ -172,7 +178,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
                   PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"),                        \
                   PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"),                        \
                   KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t", "", "")           \
-        "s_branch 3f\n"                                                                      \
+        "s_branch 3b\n"                                                                      \
         "4:\n\t"                                                                             \
         PC_CNT(3)                                                                            \
         PC_MASKED(PC_RESET("%[h1]", "%[r0]") PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"), \
@@ -181,7 +187,8 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
                   PC_RESET("%[c2]", "%[j3]") PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"), \
                   KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t",                    \
                   PC_LEFTMASK("a"), PC_LEFTMASK("b"))                                        \
-        "3:"                                                                                 \
+        "s_branch 3b\n"                                                                      \
+        ".subsection 0\n"                                                                    \
         : [ha] "+v"(ha), [hb] "+v"(hb), [ea] "+v"(ea), [eb] "+v"(eb), [f] "+v"(f),           \
           [h1] "+v"(h1), [key] "+v"(key), [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb),     \
           [ta] "=&v"(ta), [tb] "=&v"(tb), [xa] "=&v"(xa), [xb] "=&v"(xb), [c0] "=&v"(c0),    \
