@@ -385,6 +385,28 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
         const bool act = alive && i < tlen;
         alive = act;
         if (__ballot(act) == 0) break;
+        // the row's target base and score profile first: their LDS reads then overlap the band
+        // bookkeeping below instead of stalling the first group (lgkmcnt wait)
+        uint2 pr = make_uint2(0u, 0u);
+        if (act) {
+            if ((i & 3) == 0) {            // new 4-row block: 4 target bases from LDS
+                if ((i & 63) == 0) {          // chunk boundary: its DMA was issued 64 rows ago
+                    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                const int k = (i >> 2) & 15;
+                const uint32_t *src = &s_tgt[wv][(i >> 6) & 1][k][ln];
+                tcur = __builtin_amdgcn_alignbyte(src[64], src[0], tsh);
+                if ((i & 63) == 0) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (i > 0) issue_chunk((i >> 6) + 1);   // refill the buffer just drained
+                }
+            }
+            // per-row score profile of target base t (8 bytes: mat[t][q], q = 0..7)
+            const uint32_t t = (tcur >> (8 * (i & 3))) & 0xffu;
+            pr = s_prof[min(t, 7u)];                     // one ds_read_b64 (codes > 4 score as N)
+        }
+        __builtin_amdgcn_sched_barrier(0);
         const int beg = max(0, i - wl);
         const int end = min(min(endc, i + wl + 1), qlen);
         endc = end;
@@ -408,22 +430,6 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             r.left = gbits(glo, gln + 1);
         }
         if (act) {
-            if ((i & 3) == 0) {            // new 4-row block: 4 target bases from LDS
-                if ((i & 63) == 0) {          // chunk boundary: its DMA was issued 64 rows ago
-                    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                const int k = (i >> 2) & 15;
-                const uint32_t *src = &s_tgt[wv][(i >> 6) & 1][k][ln];
-                tcur = __builtin_amdgcn_alignbyte(src[64], src[0], tsh);
-                if ((i & 63) == 0) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (i > 0) issue_chunk((i >> 6) + 1);   // refill the buffer just drained
-                }
-            }
-            // per-row score profile of target base t (8 bytes: mat[t][q], q = 0..7)
-            const uint32_t t = (tcur >> (8 * (i & 3))) & 0xffu;
-            const uint2 pr = s_prof[min(t, 7u)];         // one ds_read_b64 (codes > 4 score as N)
             int h1 = (beg == 0) ? max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) : 0;
             int f = 0;
             uint32_t key = 0;
