@@ -52,6 +52,12 @@ def static_band_cells(qlen: int, tlen: int, w: int, maxsc=1, end_bonus=5, o=6, e
     return sum(max(0, min(qlen, i + wl + 1) - max(0, i - wl)) for i in range(tlen))
 
 
+def wave_cols(qlen: int, w: int, maxsc=1, end_bonus=5, o=6, e=1) -> int:
+    """columns per lane of the wave kernel for this shape (bsw_host.cpp wv_class)"""
+    wl = min(w, max((qlen * maxsc + end_bonus - o + e) // e, 1))
+    return next(c for c in (4, 8, 16) if 2 * wl + c + 2 <= 64 * c)
+
+
 def dist_init():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -235,6 +241,8 @@ def main():
     ap.add_argument("--w", type=int, default=100)
     ap.add_argument("--cell-bits", type=int, default=16, choices=(8, 16))
     ap.add_argument("--h0-hi", type=int, default=100, help="h0 upper bound (C3 uses 105)")
+    ap.add_argument("--qlen", type=int, default=150, help="query length (C2: 150; long reads: 250 / 500 / 1000)")
+    ap.add_argument("--tlen", type=int, default=300, help="target window length (C2: 300)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (drop-in ABI) rates")
     ap.add_argument("--workload", default="c2", choices=("c2", "c1", "c4", "mate", "global"),
@@ -280,7 +288,7 @@ def main():
     if args.workload == "global":
         return main_global(args, rank, local, world)
 
-    cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
+    cfg = bsw.synth_cfg(h0_hi=args.h0_hi, qlen=args.qlen, tlen=args.tlen)
     t0 = time.perf_counter()
     pairs, ref, qer = bsw.synth_batch(args.pairs, pair_base=rank * args.pairs, cfg=cfg)
     gen_s = time.perf_counter() - t0
@@ -320,15 +328,16 @@ def main():
     # regime (C2: every pair; C3: most, the rest on the int16 lane kernel), else the lane
     # kernel; BSW_PK=1 selects the two-pairs-per-lane kernel for those pairs instead
     packed = 2 * st.n_packed > args.pairs
-    kname = ("pk_kernel<160>" if os.environ.get("BSW_PK") == "1" else "pc_kernel<160>") if packed \
-        else "lane_kernel<160>"
+    wave = 2 * st.n_wave > args.pairs
+    kname = "pc_kernel<160>" if packed else (f"wv_kernel<{wave_cols(cfg.qlen, args.w)}>" if wave
+                                             else "lane_kernel<160>")
     roof = {
         "bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
         "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
         "traffic": traffic_per_launch(kname),
         "kernel": kname, "launch_ms": round(kms_mean, 4),
         "cells_per_s": round(args.pairs * cells / (kms_mean * 1e-3) / 1e12, 4),
-        "cells_unit": "T band cells/s (25,100 static cells/pair)",
+        "cells_unit": f"T band cells/s ({cells:,} static cells/pair)",
         "algorithmic": f"{OPS_PER_CELL} int ops x {cells} band cells x {args.pairs} pairs per launch",
         "pairs_per_launch": per_launch_pairs,
     }
@@ -338,17 +347,30 @@ def main():
         "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int16" if args.cell_bits == 16 else "u8+int16",
         "data": "synthetic (bsw_synth.c, seed 42)",
-        "config": {"workload": f"{'C3' if args.cell_bits == 8 else 'C2'}: {args.pairs} SeqPairs/GPU resident in HBM, {cfg.qlen} bp query / "
+        "config": {"workload": f"{'C3' if args.cell_bits == 8 else 'C2' if cfg.qlen <= 160 else 'long reads'}: {args.pairs} SeqPairs/GPU resident in HBM, {cfg.qlen} bp query / "
                                f"{cfg.tlen} bp ref, band w={args.w}, cell_bits={args.cell_bits}, "
                                f"h0 U[{cfg.h0_lo},{cfg.h0_hi}]",
                    "pairs_per_gpu": args.pairs, "parallelism": f"shard{world} (independent pairs)",
                    "distinct_gpus": args.distinct_gpus,
                    "routing": {"n_packed": st.n_packed, "n_i16": st.n_i16, "n_u8": st.n_u8, "n_wide": st.n_wide,
+                               "n_wave": st.n_wave,
                                "int16_fallback_fraction": (round(st.n_i16 / max(1, st.n_i16 + st.n_u8), 4)
                                                            if args.cell_bits == 8 else None)}},
         "roofline": roof,
         "kernel_only_value": round(args.pairs * world / (kms_mean * 1e-3) / 1e6, 3),
     }
+    if wave and world == 1:
+        # the same resident batch on the int32 wide kernel (BSW_OPT_LONG 0): what long queries
+        # ran on before the wave kernel
+        e0 = bsw.Engine(device=local, long=0)
+        e0.get_scores_device(d_pairs.ptr, d_ref.ptr, d_qer.ptr, args.pairs, args.w, args.cell_bits)
+        t = time.perf_counter()
+        e0.get_scores_device(d_pairs.ptr, d_ref.ptr, d_qer.ptr, args.pairs, args.w, args.cell_bits)
+        wide_s = time.perf_counter() - t
+        out["wide_kernel_comparison"] = {"M_pairs_per_s": round(args.pairs / wide_s / 1e6, 3),
+                                         "dp_kernel_ms": round(e0.last_stats().kernel_ms, 3),
+                                         "n_wide": e0.last_stats().n_wide}
+        e0.close()
     if args.distinct_gpus < world:
         out["rehearsal"] = f"{world} ranks on {args.distinct_gpus} GPU(s): not a scaling measurement"
     if world == 1 and not args.no_host_path:

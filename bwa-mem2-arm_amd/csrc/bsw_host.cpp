@@ -43,7 +43,10 @@ namespace bsw {
 constexpr int kNumLaneClasses = 5;          // QMAX 32, 64, 96, 128, 160
 constexpr int kPkClass0 = kNumLaneClasses;  // packed kernel, same QMAX buckets (classes 5..9)
 constexpr int kWideClass = kPkClass0 + kNumLaneClasses;   // index of the wide-kernel class
-constexpr int kNumClasses = kWideClass + 1;
+constexpr int kWvClass0 = kWideClass + 1;   // wave-per-alignment kernel, 4 / 8 / 16 columns per lane
+constexpr int kNumWvClasses = 3;
+constexpr int kWvCols[kNumWvClasses] = {4, 8, 16};
+constexpr int kNumClasses = kWvClass0 + kNumWvClasses;
 constexpr int kMetaCounts = 16;             // class counters per slot (one 64-B line per slot)
 constexpr int kMetaSpread = 32;             // slots: block b adds into slot b % 32 (no hot line)
 constexpr int kMetaMaxq = kMetaCounts * kMetaSpread;   // d_meta: counts[32][16], maxq_wide, err
@@ -80,12 +83,29 @@ __device__ __forceinline__ int seed_matches(const uint8_t *__restrict__ q, int q
 }
 
 // Per pair: class + sort key.  Lane classes need qlen <= QMAX and int16-safe scores.
-__global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_t maxsc,
-                            int32_t pc_route, const uint8_t *__restrict__ ref,
+// Wave-kernel class for a pair (bsw_wv.hip contract), -1 if it does not qualify.
+__device__ __forceinline__ int wv_class(const KParams &kp, int32_t w, int qlen, int tlen, int h0)
+{
+    if (kp.maxsc != 1 || qlen > kWvQmax || h0 < 0) return -1;
+    if ((int64_t)kp.e_ins * qlen >= 2700) return -1;
+    if ((int64_t)h0 + min(qlen, tlen) + (int64_t)kp.e_ins * (qlen + 1) >= 30000) return -1;
+    int wl = w;
+    const int ni = qlen * kp.maxsc + kp.end_bonus - kp.o_ins;
+    const int nd = qlen * kp.maxsc + kp.end_bonus - kp.o_del;
+    wl = min(wl, max((ni + kp.e_ins) / kp.e_ins, 1));
+    wl = min(wl, max((nd + kp.e_del) / kp.e_del, 1));
+    for (int k = 0; k < kNumWvClasses; ++k)
+        if (2 * wl + kWvCols[k] + 2 <= 64 * kWvCols[k]) return kWvClass0 + k;
+    return -1;
+}
+
+__global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, const KParams kp, int32_t w,
+                            int32_t pc_route, int32_t wv_route, const uint8_t *__restrict__ ref,
                             const uint8_t *__restrict__ qer, uint32_t *__restrict__ keys,
                             int32_t *__restrict__ vals, int32_t *__restrict__ counts,
                             int32_t *__restrict__ maxq_wide, int keymode, int misroute)
 {
+    const int maxsc = kp.maxsc;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < n;
     SeqPair p{};
@@ -93,7 +113,11 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
     const int qlen = max(p.len2, 0), tlen = max(p.len1, 0);
     const int64_t hi = (int64_t)max(p.h0, 0) + (int64_t)max(maxsc, 0) * min(qlen, tlen);
     int c = kWideClass;
-    if (hi < 32768 && p.h0 >= 0) {
+    // queries past the register kernels' 160 columns: the wave-per-alignment kernel
+    // (BSW_OPT_LONG 1, default); BSW_OPT_LONG 2 sends every qualifying pair there (tests)
+    const int wvc = wv_route ? wv_class(kp, w, qlen, tlen, p.h0) : -1;
+    if (wv_route == 2 && wvc >= 0) c = wvc;
+    else if (hi < 32768 && p.h0 >= 0) {
         if (qlen <= 32) c = 0;
         else if (qlen <= 64) c = 1;
         else if (qlen <= 96) c = 2;
@@ -104,6 +128,7 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, int32_
         if (pc_route && c < kNumLaneClasses && p.h0 + min(qlen, tlen) <= 255 && qlen + 1 <= 160)
             c = kPkClass0 + (qlen + 1 <= 32 ? 0 : qlen + 1 <= 64 ? 1 : qlen + 1 <= 96 ? 2 : qlen + 1 <= 128 ? 3 : 4);
     }
+    if (c == kWideClass && wvc >= 0) c = wvc;
     if (misroute) c = 0;          // BSW_OPT_TEST_MISROUTE: the QMAX=32 lane kernel's guard must trip
     if (valid) {
         if (c == kWideClass) atomicMax(maxq_wide, qlen);
@@ -350,6 +375,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.keymode = 2;
     kp.misroute = 0;
     kp.fork = 1;
+    kp.long_route = 1;
 }
 
 // keys / keys2 / vals / order (radix-sort buffers) grow together
@@ -404,8 +430,8 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     // overflow fallback) or the int32 wide kernel
     const int pc_route = (kp.pk_ok && kp.kern8) ? 1 : 0;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       pc.d_pairs, n, kp.maxsc, pc_route, pc.d_ref, pc.d_qer, s.d_keys, s.d_vals, d_counts,
-                       d_maxq, (int)kp.keymode, (int)kp.misroute);
+                       pc.d_pairs, n, kp, pc.w, pc_route, (int32_t)kp.long_route, pc.d_ref, pc.d_qer, s.d_keys,
+                       s.d_vals, d_counts, d_maxq, (int)kp.keymode, (int)kp.misroute);
     BSW_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
     BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals,
@@ -489,6 +515,18 @@ static int run_dp(const KParams &kp, Slot &s)
                                        nw, next_stream()));
             s.stats.n_launches++;
             s.stats.n_wide += nw;
+        }
+        off += counts[kWideClass];
+        for (int c = 0; c < kNumWvClasses; ++c) {
+            const int32_t nv = counts[kWvClass0 + c];
+            if (nv > 0) {
+                BSW_TRY(launch_wv_kernel(kWvCols[c], kp, w, d_pairs, s.d_order + off, nv, d_ref, d_qer, d_err,
+                                         next_stream()));
+                s.stats.n_launches++;
+                s.stats.n_i16 += nv;
+                s.stats.n_wave += nv;
+            }
+            off += nv;
         }
         return BSW_OK;
     }();
@@ -757,7 +795,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         unstage_outputs(s, pairs + pend_at[k], pend_n[k], pend_whole[k]);
         agg.kernel_ms += s.stats.kernel_ms;
         agg.n_i16 += s.stats.n_i16; agg.n_u8 += s.stats.n_u8; agg.n_wide += s.stats.n_wide;
-        agg.n_packed += s.stats.n_packed; agg.n_launches += s.stats.n_launches;
+        agg.n_packed += s.stats.n_packed; agg.n_launches += s.stats.n_launches; agg.n_wave += s.stats.n_wave;
         pend_n[k] = 0;
         return BSW_OK;
     };
@@ -1184,6 +1222,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
         agg.kernel_ms = std::max(agg.kernel_ms, st[d].kernel_ms);
         agg.n_i16 += st[d].n_i16; agg.n_u8 += st[d].n_u8; agg.n_wide += st[d].n_wide; agg.n_packed += st[d].n_packed;
         agg.n_launches += st[d].n_launches;
+        agg.n_wave += st[d].n_wave;
         agg.stage_ms = std::max(agg.stage_ms, st[d].stage_ms);
         agg.host_ms = std::max(agg.host_ms, st[d].host_ms);
     }
@@ -1620,6 +1659,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     case BSW_OPT_SORTKEY: if (!b01) return BSW_E_INVAL; ctx->kp.keymode = value ? 2 : 0; return BSW_OK;
     case BSW_OPT_GLOB_BAND: if (!b01) return BSW_E_INVAL; ctx->glob_band = (int)value; return BSW_OK;
     case BSW_OPT_EXT_CHUNK: if (value < 0) return BSW_E_INVAL; ctx->ext_chunk = value; return BSW_OK;
+    case BSW_OPT_LONG: if (value < 0 || value > 2) return BSW_E_INVAL; ctx->kp.long_route = (int8_t)value; return BSW_OK;
     case BSW_OPT_HOST_CHUNK: if (value < 1 || value > INT32_MAX) return BSW_E_INVAL; ctx->host_chunk = (int32_t)value; return BSW_OK;
     case BSW_OPT_TEST_MISROUTE: if (!b01) return BSW_E_INVAL; ctx->kp.misroute = (int8_t)value; return BSW_OK;
     default: return BSW_E_INVAL;

@@ -31,6 +31,9 @@ struct KParams {
     int8_t fork;                // host: class launches fork over side streams (BSW_OPT_FORK)
     int8_t misroute;            // host, tests only: every pair to the QMAX=32 lane class
                                 //   (BSW_OPT_TEST_MISROUTE: trips the kernels' range guard)
+    int8_t long_route;          // host: queries past 160 columns -> 1 wave kernel (default),
+                                //   0 wide kernel, 2 every qualifying pair to the wave kernel
+                                //   (BSW_OPT_LONG)
 };
 
 // qlen limit of the register-resident kernel instantiations.
@@ -48,6 +51,14 @@ hipError_t launch_lane_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *p
 hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
                             const int32_t *order, int32_t n, const uint8_t *ref,
                             const uint8_t *qer, int32_t *err, hipStream_t s);
+
+// Wave-per-alignment band kernel (bsw_wv.hip): one SeqPair per wavefront, the row spread over
+// the 64 lanes as a sliding window of 64 * cols absolute columns (cols = 4, 8 or 16).  Needs
+// max(mat) == 1, qlen <= kWvQmax, 2 * wl + cols + 2 <= 64 * cols (wl = the pair's band cap) and
+// int16-safe values (h0 + min(qlen, tlen) + e_ins * (qlen + 1) < 30000, e_ins * qlen < 2700).
+constexpr int kWvQmax = 4096;
+hipError_t launch_wv_kernel(int cols, const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order,
+                            int32_t n, const uint8_t *ref, const uint8_t *qer, int32_t *err, hipStream_t s);
 
 // Wide kernel: any qlen/tlen, int32 cells, eh scratch of n * (max_qlen + 2) int2 in HBM.
 hipError_t launch_wide_kernel(const KParams &kp, int32_t w, SeqPair *pairs,

@@ -36,7 +36,7 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
                "bsw_split_by_cells")
 
 # include/bsw.h engine options (bsw_set_option)
-OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK = 1, 2, 3, 4, 5, 6
+OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK, OPT_LONG = 1, 2, 3, 4, 5, 6, 7
 OPT_TEST_MISROUTE = 100
 
 # include/bsw_ext.h structs
@@ -65,7 +65,7 @@ class Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_float), ("n_i16", ctypes.c_int32),
                 ("n_u8", ctypes.c_int32), ("n_wide", ctypes.c_int32),
                 ("n_launches", ctypes.c_int32), ("n_packed", ctypes.c_int32),
-                ("stage_ms", ctypes.c_float), ("host_ms", ctypes.c_float)]
+                ("stage_ms", ctypes.c_float), ("host_ms", ctypes.c_float), ("n_wave", ctypes.c_int32)]
 
 
 def default_params(a=1, b=4, o_del=6, e_del=1, o_ins=6, e_ins=1, zdrop=100, end_bonus=5,
@@ -155,7 +155,7 @@ class Engine:
             self.set_option(k, v)
 
     _OPTS = {"kernel8": OPT_KERNEL8, "fork": OPT_FORK, "sortkey": OPT_SORTKEY, "glob_band": OPT_GLOB_BAND,
-             "ext_chunk": OPT_EXT_CHUNK, "host_chunk": OPT_HOST_CHUNK, "test_misroute": OPT_TEST_MISROUTE}
+             "ext_chunk": OPT_EXT_CHUNK, "host_chunk": OPT_HOST_CHUNK, "long": OPT_LONG, "test_misroute": OPT_TEST_MISROUTE}
 
     def set_option(self, name, value: int):
         """bsw_set_option by name (kernel8, fork, sortkey, glob_band, ext_chunk, host_chunk, test_misroute)

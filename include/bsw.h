@@ -99,6 +99,8 @@ typedef struct bsw_stats_t {
                                    memory (ABI version 4; 0 for device calls)            */
     float   host_ms;            /* host-buffer calls: wall time of the call on the device's
                                    host thread (staging + H2D + kernels + D2H)           */
+    int32_t n_wave;             /* of n_i16: pairs run on the wave-per-alignment kernel
+                                   (queries past 160 columns; ABI version 4)             */
 } bsw_stats_t;
 int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
 
@@ -116,6 +118,9 @@ enum {
     BSW_OPT_GLOB_BAND = 4,    /* bsw_ksw_global2: 0 = column kernel first (default),
                                  1 = band kernel for every band-eligible job                  */
     BSW_OPT_EXT_CHUNK = 5,    /* extension calls: reads per chunk (0 = the int32-offset bound) */
+    BSW_OPT_LONG = 7,         /* queries past the 160-column register kernels: 1 = one wavefront
+                                 per alignment (bsw_wv.hip, default), 0 = the int32 wide kernel,
+                                 2 = every pair the wave kernel can run goes there (tests)   */
     BSW_OPT_HOST_CHUNK = 6,   /* bsw_get_scores: largest pipeline chunk in pairs (default
                                  262144, rounded down to whole 4096-pair blocks, at least one):
                                  a host-buffer call is staged, copied and computed chunk by

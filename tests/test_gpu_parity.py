@@ -97,17 +97,69 @@ def test_class_launch_fork(eng, no_fork):
         _assert_same(want, got, f"class launches no_fork={no_fork}")
     st = eng.last_stats()
     eng.set_option("fork", 1)
-    assert st.n_launches >= 3 and st.n_wide > 0
+    assert st.n_launches >= 3 and st.n_wave > 0
     assert st.n_i16 + st.n_u8 + st.n_wide == len(pairs)
 
 
-def test_long_queries_wide_kernel(eng):
+@pytest.mark.parametrize("route", [1, 0])
+def test_long_queries(eng, route):
+    """Queries past the register kernels' 160 columns: the wave-per-alignment kernel
+    (BSW_OPT_LONG 1, default) or the int32 wide kernel (0) -- both equal the oracle."""
+    eng.set_option("long", route)
     pairs, ref, qer = bswgen.random_pairs(300, seed=9, tlen=(100, 700), qlen=(161, 600))
     want, got = pairs.copy(), pairs.copy()
     oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
     eng.get_scores(got, ref, qer, 100)
-    _assert_same(want, got, "wide")
-    assert eng.last_stats().n_wide == len(pairs)
+    st = eng.last_stats()
+    eng.set_option("long", 1)
+    _assert_same(want, got, f"long queries route {route}")
+    assert (st.n_wave if route else st.n_wide) == len(pairs)
+
+
+@pytest.mark.parametrize("L", [250, 500, 1000])
+def test_wave_kernel_long_reads(eng, L):
+    """bwa-shaped extensions of L-bp reads (query = the target's prefix with substitutions and
+    short indels, target window L + 100) on the wave kernel, w = 100 and the w << 1 retry band."""
+    n = 400 if L < 1000 else 160
+    pairs, ref, qer = bswgen.random_pairs(n, seed=L, tlen=(L + 50, L + 150), qlen=(L, L), h0=(1, 200),
+                                          p_sub=(0.0, 0.05), p_indel=(0.0, 0.01))
+    for w in (100, 200):
+        want, got = pairs.copy(), pairs.copy()
+        oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+        eng.get_scores(got, ref, qer, w)
+        _assert_same(want, got, f"long reads L={L} w={w}")
+        assert eng.last_stats().n_wave == n
+
+
+def test_wave_kernel_forced_golden(golden):
+    """Every golden batch whose scoring the wave kernel takes (max(mat) == 1), with every pair
+    routed to it (BSW_OPT_LONG 2) -- short queries, empty sequences, w = 0 .. 200, z-drop off."""
+    engines, ran = {}, 0
+    for name, pairs, ref, qer, w, sc in golden:
+        if sc.get("a", 1) != 1:
+            continue
+        key = tuple(sorted(sc.items()))
+        if key not in engines:
+            engines[key] = bsw.Engine(_gparams(sc), long=2)
+        got = pairs.copy()
+        for f in bsw.OUT_FIELDS:
+            got[f] = -9
+        engines[key].get_scores(got, ref, qer, w)
+        _assert_same(pairs, got, f"golden {name} on the wave kernel")
+        ran += engines[key].last_stats().n_wave
+    assert ran > 0
+
+
+@pytest.mark.parametrize("w", [0, 1, 7, 100, 200])
+def test_wave_kernel_forced_random(w):
+    e = bsw.Engine(long=2)
+    pairs, ref, qer = bswgen.random_pairs(2000, seed=700 + w, tlen=(0, 400), qlen=(0, 300))
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+    e.get_scores(got, ref, qer, w)
+    _assert_same(want, got, f"wave kernel random w={w}")
+    assert e.last_stats().n_wave == len(pairs)
+    e.close()
 
 
 def test_edge_cases(eng):

@@ -3,6 +3,9 @@
 //   V0: no scalar tests            V1: 2 not-taken test+branch pairs (skip / fast tests)
 //   V2: V1 + the taken s_branch over the masked bodies (the product layout)
 //   V3: V1 + a taken branch every 2nd group
+//   V4: V0 + the 6 byte-unpack/repack v_perm of a narrow (8-bit stored H and E) row, the C3
+//       "int8 cells" variant: 4 columns per VGPR for H and E halves the row's registers (3-4
+//       waves per SIMD instead of 2) but adds these instructions to every group
 // at 1, 2 and 3 waves per SIMD (grid = 1024 * k one-wave blocks).
 // build: hipcc -O3 --offload-arch=gfx950 -o tools/pc_branch_bench tools/pc_branch_bench.hip
 #include <hip/hip_runtime.h>
@@ -48,7 +51,25 @@ __device__ __forceinline__ void grp(uint32_t &ha, uint32_t &hb, uint32_t &ea, ui
                                     uint64_t men, uint64_t mfa, int G)
 {
     uint32_t y, sa, sb, ta, tb, c0, c1, c2, pa, pb;
-    if constexpr (V == 0) {
+    if constexpr (V == 4) {
+        uint32_t u0, u1;
+        asm volatile("v_perm_b32 %[u0], 0, %[ha], %[s0]\n\t"     /* bytes -> int16 pairs */
+                     "v_perm_b32 %[u1], 0, %[ha], %[s1]\n\t"
+                     "v_perm_b32 %[ea], 0, %[eb], %[s0]\n\t"
+                     "v_perm_b32 %[eb], 0, %[eb], %[s1]\n\t"
+                     : [u0] "=&v"(u0), [u1] "=&v"(u1), [ea] "+v"(ea), [eb] "+v"(eb)
+                     : [ha] "v"(ha), [s0] "s"(0x0c010c00u), [s1] "s"(0x0c030c02u));
+        ha = u0; hb = u1;
+        asm volatile(PC_SCORES FAST_BODY
+            : [ha] "+v"(ha), [hb] "+v"(hb), [ea] "+v"(ea), [eb] "+v"(eb), [f] "+v"(f), [h1] "+v"(h1), [key] "+v"(key),
+              [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb), [ta] "=&v"(ta), [tb] "=&v"(tb), [c0] "=&v"(c0),
+              [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb)
+            : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe2] "s"(0x70007u), [ed2] "s"(0x10001u), [ed] "s"(1),
+              [jja] "s"(0x40003u), [jjb] "s"(0x60005u));
+        asm volatile("v_perm_b32 %[ha], %[hb], %[ha], %[s2]\n\t"   /* int16 pairs -> bytes */
+                     "v_perm_b32 %[ea], %[eb], %[ea], %[s2]\n\t"
+                     : [ha] "+v"(ha), [ea] "+v"(ea) : [hb] "v"(hb), [eb] "v"(eb), [s2] "s"(0x06040200u));
+    } else if constexpr (V == 0) {
         asm volatile(PC_SCORES FAST_BODY
             : [ha] "+v"(ha), [hb] "+v"(hb), [ea] "+v"(ea), [eb] "+v"(eb), [f] "+v"(f), [h1] "+v"(h1), [key] "+v"(key),
               [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb), [ta] "=&v"(ta), [tb] "=&v"(tb), [c0] "=&v"(c0),
@@ -111,7 +132,7 @@ __global__ __launch_bounds__(64) void kern(unsigned long long *out, int seed)
 }
 
 static const char *kNames[] = {"V0 no tests", "V1 2 not-taken tests", "V2 + taken branch/group",
-                               "V3 + taken branch/2 groups"};
+                               "V3 + taken branch/2 groups", "V4 V0 + narrow-row unpack/repack"};
 template <int V> static void run(int k, unsigned long long *d, std::vector<unsigned long long> &h)
 {
     const int blocks = 1024 * k;
@@ -133,6 +154,6 @@ int main()
 {
     unsigned long long *d; (void)hipMalloc(&d, 1024 * 4 * 8);
     std::vector<unsigned long long> h(1024 * 4);
-    for (int k = 1; k <= 3; ++k) { run<0>(k, d, h); run<1>(k, d, h); run<2>(k, d, h); run<3>(k, d, h); }
+    for (int k = 1; k <= 4; ++k) { run<0>(k, d, h); run<1>(k, d, h); run<2>(k, d, h); run<3>(k, d, h); run<4>(k, d, h); }
     return 0;
 }
