@@ -245,9 +245,10 @@ def main():
     ap.add_argument("--tlen", type=int, default=300, help="target window length (C2: 300)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (drop-in ABI) rates")
-    ap.add_argument("--workload", default="c2", choices=("c2", "c1", "c4", "mate", "global"),
+    ap.add_argument("--workload", default="c2", choices=("c2", "c1", "c4", "c4seed", "mate", "global"),
                     help="c2 (default): resident SeqPair batch; c1: 10K exact SE reads vs 1 Mb (plumbing); "
-                         "c4: extension pipeline on synthetic reads; "
+                         "c4: paired-end reads with several seeds / chains each through mem_chain2aln "
+                         "(bsw_chain2aln_device); c4seed: one seed per read through the extension pipeline; "
                          "mate: resident mate-rescue batch (ksw_align2 jobs, SURVEY.md §8(f) row 2); "
                          "global: resident ksw_global2 + CIGAR batch (SURVEY.md §8(f) row 4)")
     ap.add_argument("--jobs", type=int, default=1_000_000, help="mate: jobs per GPU")
@@ -282,6 +283,8 @@ def main():
         args.reads, args.ref_mb, args.exact = 10_000, 1, True
         return main_c4(args, rank, local, world)
     if args.workload == "c4":
+        return main_c4pe(args, rank, local, world)
+    if args.workload == "c4seed":
         return main_c4(args, rank, local, world)
     if args.workload == "mate":
         return main_mate(args, rank, local, world)
@@ -562,6 +565,94 @@ def main_c4(args, rank, local, world):
                       f"scalar ksw_extend2), 1 thread; first-try extensions counted",
             "outputs_identical_to_gpu": bool(all(np.array_equal(ref_reg[f], out[:S][f])
                                                  for f in bsw.ALNREG_DTYPE.names)),
+        }
+    out_j["synth_gen_s"] = round(gen_s, 2)
+    print(json.dumps(out_j), flush=True)
+
+
+def main_c4pe(args, rank, local, world):
+    """C4/C5: `--reads` paired-end 150 bp reads per GPU (reads/2 fragments, insert 400-600) from a
+    `--ref-mb` random reference RESIDENT in HBM, with every maximal exact run >= 19 bp along each
+    read's true path as a seed (one chain, longest first) plus a planted spurious chain on 10%
+    of the reads (bsw_synth_pe_seeds).  A step = bsw_chain2aln_device over all of them: upstream's
+    per-read chain / seed order with contained-seed skipping (mem_chain2aln), batched across reads
+    in rounds; each round's LEFT / RIGHT extensions (+ band retries) run on the GPU against the
+    resident reads and reference.  Reported: extensions/s (SeqPairs through the engine) and
+    reads/s; seeds per read, extended fraction and rounds beside it.  FM-index seeding is out of
+    scope (the north star keeps it on the host)."""
+    t0 = time.perf_counter()
+    ref = bsw.synth_reference(args.ref_mb * 1_000_000, seed=7)
+    npairs = max(1, args.reads // 2)
+    reads, off, lens, seeds, sr, sc = bsw.synth_pe_seeds(ref, npairs, pair_base=rank * npairs)
+    gen_s = time.perf_counter() - t0
+    eng = bsw.Engine(device=local)
+    opt = bsw.ext_opt(w=args.w)
+    bsw.set_reference(eng, ref)
+    d_reads = hiprt.DeviceBuffer.from_array(reads)
+
+    out_buf = np.zeros(len(seeds), dtype=bsw.ALNREG_DTYPE)
+    ext_buf = np.zeros(len(seeds), dtype=np.int32)
+
+    def step():
+        out, ext = bsw.chain2aln_device(eng, d_reads.ptr, off, lens, seeds, sr, sc, opt, out=out_buf, ext=ext_buf)
+        st = bsw.chain_last_stats(eng)
+        return out, ext, st
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    t = time.perf_counter()
+    n_ext, sts = 0, []
+    for _ in range(args.steps):
+        out, ext, st = step()
+        n_ext += sum(st.n_pairs)
+        sts.append(st)
+    barrier(world)
+    dt = time.perf_counter() - t
+    dt_max = allreduce_max(dt, world)
+    n_ext_all = allreduce_sum(n_ext, world)
+    if rank != 0:
+        return
+    st = sts[-1]
+    value = n_ext_all / dt_max / 1e6
+    nreads = 2 * npairs
+    out_j = {
+        "metric": METRIC, "value": round(value, 3), "unit": UNIT, "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int16", "data": "synthetic (bsw_synth.c PE reads, seed 42)",
+        "config": {"workload": f"C4: {nreads} paired-end 150 bp reads/GPU ({npairs} fragments, insert 400-600) from a "
+                               f"{args.ref_mb} Mb random reference resident in HBM, {len(seeds)} seeds "
+                               f"({len(seeds) / nreads:.2f}/read, chains of every exact run >= 19 bp + 10% spurious "
+                               f"chains), mem_chain2aln with contained-seed skipping, w={args.w}, band retry",
+                   "reads_per_gpu": nreads, "parallelism": f"shard{world} (independent reads)",
+                   "distinct_gpus": args.distinct_gpus},
+        "reads_per_s_M": round(nreads * world * args.steps / dt_max / 1e6, 3),
+        "seeds_per_read": round(len(seeds) / nreads, 3),
+        "extended_fraction": round(st.n_extended / max(1, len(seeds)), 4),
+        "rounds": st.rounds,
+        "extensions_per_step_rank0": list(st.n_pairs),
+        "dp_kernel_ms_per_step": round(float(np.mean([x.kernel_ms for x in sts])), 3),
+        "host_containment_ms_per_step": round(float(np.mean([x.check_ms for x in sts])), 3),
+        "host_prep_ms_per_step": round(float(np.mean([x.prep_ms for x in sts])), 3),
+        "extension_calls_ms_per_step": round(float(np.mean([x.ext_ms for x in sts])), 3),
+    }
+    if world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # CPU baseline leg only (test infrastructure)
+        S = int(np.searchsorted(sr, min(nreads, 20_000)))     # seeds of the first 20K reads
+        t = time.perf_counter()
+        want, wext = oracle.chain2aln(oracle.make_params(), opt, ref, reads, off, lens, seeds[:S], sr[:S], sc[:S])
+        dt_cpu = time.perf_counter() - t
+        # the extensions the CPU ran: LEFT / RIGHT of every extended seed (+ retries not counted)
+        n_cpu = int(np.sum(wext * ((seeds[:S]["qbeg"] > 0).astype(int) +
+                                   ((seeds[:S]["qbeg"] + seeds[:S]["len"]) < lens[sr[:S]]).astype(int))))
+        out_j["cpu_baseline"] = {
+            "value": round(n_cpu / dt_cpu / 1e6, 4), "unit": UNIT, "cores": 1, "kind": "port",
+            "sample": f"seeds of the first 20K reads ({S}); oracle/ext_ref.c oracle_chain2aln (literal per-read "
+                      f"mem_chain2aln, scalar ksw_extend2), 1 thread; first-try extensions counted",
+            "outputs_identical_to_gpu": bool(np.array_equal(wext, ext[:S]) and
+                                             all(np.array_equal(want[f], out[:S][f]) for f in bsw.ALNREG_DTYPE.names)),
         }
     out_j["synth_gen_s"] = round(gen_s, 2)
     print(json.dumps(out_j), flush=True)

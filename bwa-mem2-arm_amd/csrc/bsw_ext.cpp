@@ -19,6 +19,7 @@
 #include <vector>
 #include "../../include/bsw_ext.h"
 #include "bsw_internal.h"
+#include "bsw_pool.h"
 
 namespace {
 
@@ -43,20 +44,18 @@ int cal_max_gap(const bsw_params_t &p, int a, int w, int qlen)
     return std::min(l, w << 1);
 }
 
+// f(a, b) over [0, n) in pieces on the engine's host pool (bsw_pool.h)
 template <class F>
 void parallel_for(int32_t n, F f)
 {
-    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (n < 4096 || nt == 1) {
+    const int nt = bsw::HostPool::kWorkers + 1;
+    if (n < 4096) {
         f(0, n);
         return;
     }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) {
-        const int32_t a = (int32_t)((int64_t)n * t / nt), b = (int32_t)((int64_t)n * (t + 1) / nt);
-        th.emplace_back([=] { f(a, b); });
-    }
-    for (auto &x : th) x.join();
+    bsw::HostPool::get().parallel_for(nt, [&](int t) {
+        f((int32_t)((int64_t)n * t / nt), (int32_t)((int64_t)n * (t + 1) / nt));
+    });
 }
 
 struct Buf {                       // code buffer: pinned per-context staging when free, else heap
@@ -292,4 +291,197 @@ extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const 
         if (seeds[i].len > 0) out[i].w = std::max(lw[i], rw[i]);
     bsw::set_ext_stats(ctx, es);
     return BSW_OK;
+}
+
+// ---------------------------------------------------------------- mem_chain2aln over chains
+// The per-read order of upstream's mem_chain2aln (chains in order, each chain's seeds by score
+// descending; a seed contained "around" an earlier region of the read is skipped unless an
+// extended, >= 95%-as-long seed of its chain overlaps it off-diagonal; SURVEY.md §8(f) row 1,
+// oracle/ext_ref.c oracle_chain2aln) run ACROSS reads in rounds: round r extends, for every
+// read, the next seed its containment test keeps -- one LEFT + RIGHT batch set per round
+// (mem_chain2aln_across_reads_V2's batching), so only the skip decisions are sequential per
+// read.  Rounds <= seeds per read; most reads finish in round 1 (their later seeds fall
+// inside the first region).
+namespace {
+
+bool ext_contained(const bsw_params_t &p, int a, const bsw_ext_opt_t &opt, const bsw_seed_t &s, int l_query,
+                   const bsw_alnreg_t *out, const int32_t *av, int32_t nav)
+{
+    for (int32_t k = 0; k < nav; ++k) {
+        const bsw_alnreg_t &q = out[av[k]];
+        if (s.rbeg < q.rb || s.rbeg + s.len > q.re || s.qbeg < q.qb || s.qbeg + s.len > q.qe) continue;
+        if (s.len - q.seedlen0 > .1 * l_query) continue;
+        int qd = s.qbeg - q.qb;
+        int64_t rd = s.rbeg - q.rb;
+        int max_gap = cal_max_gap(p, a, opt.w, qd < rd ? qd : (int)rd);
+        int w = std::min(max_gap, q.w);
+        if (qd - rd < w && rd - qd < w) return true;
+        qd = q.qe - (s.qbeg + s.len);
+        rd = q.re - (s.rbeg + s.len);
+        max_gap = cal_max_gap(p, a, opt.w, qd < rd ? qd : (int)rd);
+        w = std::min(max_gap, q.w);
+        if (qd - rd < w && rd - qd < w) return true;
+    }
+    return false;
+}
+
+// extend(nj, job read offsets / lengths / seeds, regions out) runs one round's extensions
+template <class Extend>
+int chain_rounds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const int64_t *read_off, const int32_t *read_len,
+                 int32_t n_reads, const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain,
+                 int32_t ns, bsw_alnreg_t *out, int32_t *extended, bsw_chain_stats_t *cs, Extend extend)
+{
+    bsw_params_t p;
+    bsw::ctx_params(ctx, &p);
+    const int a = p.mat[0];
+    *cs = bsw_chain_stats_t{};
+    auto tp = Clock::now();
+    // read runs (seeds grouped by read)
+    std::vector<int32_t> rstart;
+    rstart.reserve((size_t)std::max(1, n_reads) + 1);
+    for (int32_t k = 0; k < ns; ++k) {
+        if (seed_read[k] < 0 || seed_read[k] >= n_reads || (k > 0 && seed_read[k] < seed_read[k - 1]))
+            return BSW_E_INVAL;
+        if (k == 0 || seed_read[k] != seed_read[k - 1]) rstart.push_back(k);
+    }
+    const int32_t nrun = (int32_t)rstart.size();
+    rstart.push_back(ns);
+    // processing order per read: chains in order, each chain's seeds by (score, index) desc;
+    // order[] positions of a chain coincide with its seed-index range
+    std::vector<int32_t> order((size_t)ns), chain_of((size_t)ns);
+    parallel_for(nrun, [&](int32_t r0, int32_t r1) {
+        for (int32_t r = r0; r < r1; ++r) {
+            for (int32_t k = rstart[r]; k < rstart[r + 1]; ++k) { memset(&out[k], 0, sizeof(out[k])); extended[k] = 0; }
+            for (int32_t c0 = rstart[r]; c0 < rstart[r + 1];) {
+                int32_t c1 = c0;
+                while (c1 < rstart[r + 1] && seed_chain[c1] == seed_chain[c0]) ++c1;
+                for (int32_t i = c0; i < c1; ++i) { order[i] = i; chain_of[i] = c0; }
+                std::sort(order.begin() + c0, order.begin() + c1, [&](int32_t x, int32_t y) {
+                    const int64_t kx = (int64_t)seeds[x].len * a, ky = (int64_t)seeds[y].len * a;
+                    return kx != ky ? kx > ky : x > y;
+                });
+                c0 = c1;
+            }
+        }
+    });
+    // per read: next position in order[], regions so far (flat: av[rstart[r] ..], nav[r])
+    std::vector<int32_t> pos(rstart.begin(), rstart.end() - 1), av((size_t)ns), nav((size_t)nrun, 0);
+    std::vector<int32_t> pick((size_t)nrun), jobs, job_run, jcnt;
+    std::vector<int64_t> joff;
+    std::vector<int32_t> jlen;
+    std::vector<bsw_seed_t> jseed;
+    std::vector<bsw_alnreg_t> jout;
+    cs->prep_ms = ms_since(tp);
+    for (;;) {
+        auto tc = Clock::now();
+        parallel_for(nrun, [&](int32_t b0, int32_t b1) {
+            for (int32_t r = b0; r < b1; ++r) {
+                pick[r] = -1;
+                while (pos[r] < rstart[r + 1]) {
+                    const int32_t si = order[pos[r]++];
+                    const bsw_seed_t &s = seeds[si];
+                    const int l_query = read_len[seed_read[si]];
+                    if (s.len > 0 && ext_contained(p, a, *opt, s, l_query, out, av.data() + rstart[r], nav[r])) {
+                        // overlapping extended seeds of the same chain processed earlier
+                        bool keep = false;
+                        const int32_t c0 = chain_of[si];
+                        for (int32_t q = c0; q < pos[r] - 1 && !keep; ++q) {
+                            const int32_t ti = order[q];
+                            if (!extended[ti]) continue;
+                            const bsw_seed_t &t = seeds[ti];
+                            if (t.len < s.len * .95) continue;
+                            if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 &&
+                                t.qbeg - s.qbeg != t.rbeg - s.rbeg) keep = true;
+                            if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 &&
+                                s.qbeg - t.qbeg != s.rbeg - t.rbeg) keep = true;
+                        }
+                        if (!keep) continue;           // skipped, next seed of this read
+                    }
+                    pick[r] = si;
+                    break;
+                }
+            }
+        });
+        jobs.clear(); job_run.clear();
+        for (int32_t r = 0; r < nrun; ++r)
+            if (pick[r] >= 0) { jobs.push_back(pick[r]); job_run.push_back(r); }
+        cs->check_ms += ms_since(tc);
+        if (jobs.empty()) break;
+        const int32_t nj = (int32_t)jobs.size();
+        joff.resize(nj); jlen.resize(nj); jseed.resize(nj); jout.resize(nj);
+        parallel_for(nj, [&](int32_t k0, int32_t k1) {
+            for (int32_t k = k0; k < k1; ++k) {
+                const int32_t si = jobs[k], rid = seed_read[si];
+                joff[k] = read_off[rid]; jlen[k] = read_len[rid]; jseed[k] = seeds[si];
+            }
+        });
+        auto te = Clock::now();
+        const int rc = extend(nj, joff.data(), jlen.data(), jseed.data(), jout.data());
+        if (rc) return rc;
+        cs->ext_ms += ms_since(te);
+        bsw_ext_stats_t es{};
+        bsw::get_ext_stats(ctx, &es);
+        for (int q = 0; q < 4; ++q) cs->n_pairs[q] += es.n_pairs[q];
+        cs->kernel_ms += es.kernel_ms;
+        parallel_for(nj, [&](int32_t k0, int32_t k1) {
+            for (int32_t k = k0; k < k1; ++k) {
+                const int32_t si = jobs[k], r = job_run[k];
+                out[si] = jout[k];
+                extended[si] = 1;
+                av[rstart[r] + nav[r]++] = si;
+            }
+        });
+        cs->rounds++;
+        cs->n_extended += nj;
+    }
+    cs->n_skipped = ns - cs->n_extended;
+    return BSW_OK;
+}
+
+}  // namespace
+
+extern "C" int bsw_chain2aln(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *ref, int64_t ref_len,
+                             const uint8_t *reads, const int64_t *read_off, const int32_t *read_len, int32_t n_reads,
+                             const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain,
+                             int32_t n_seeds, bsw_alnreg_t *out, int32_t *extended)
+{
+    if (!ctx || !opt || n_seeds < 0 || n_reads < 0 ||
+        (n_seeds > 0 && (!ref || !reads || !read_off || !read_len || !seeds || !seed_read || !seed_chain || !out ||
+                         !extended)))
+        return BSW_E_INVAL;
+    bsw_chain_stats_t cs{};
+    const int rc = chain_rounds(ctx, opt, read_off, read_len, n_reads, seeds, seed_read, seed_chain, n_seeds, out,
+                                extended, &cs,
+                                [&](int32_t nj, const int64_t *jo, const int32_t *jl, const bsw_seed_t *js,
+                                    bsw_alnreg_t *jr) {
+                                    return bsw_extend_seeds(ctx, opt, ref, ref_len, reads, jo, jl, js, nj, jr);
+                                });
+    bsw::set_chain_stats(ctx, cs);
+    return rc;
+}
+
+extern "C" int bsw_chain2aln_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
+                                    const int64_t *read_off, const int32_t *read_len, int32_t n_reads,
+                                    const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain,
+                                    int32_t n_seeds, bsw_alnreg_t *out, int32_t *extended)
+{
+    if (!ctx || !opt || n_seeds < 0 || n_reads < 0 ||
+        (n_seeds > 0 && (!d_reads || !read_off || !read_len || !seeds || !seed_read || !seed_chain || !out ||
+                         !extended)))
+        return BSW_E_INVAL;
+    bsw::DevJobs dj;
+    bsw_chain_stats_t cs{};
+    const int rc = chain_rounds(ctx, opt, read_off, read_len, n_reads, seeds, seed_read, seed_chain, n_seeds, out,
+                                extended, &cs,
+                                [&](int32_t nj, const int64_t *jo, const int32_t *jl, const bsw_seed_t *js,
+                                    bsw_alnreg_t *jr) {
+                                    return bsw::ext_device_jobs(ctx, opt, d_reads, dj, nj, jo, jl, js, jr);
+                                });
+    bsw::set_chain_stats(ctx, cs);
+    return rc;
+}
+
+extern "C" int bsw_chain_last_stats(bsw_ctx_t *ctx, bsw_chain_stats_t *out)
+{
+    return bsw::get_chain_stats(ctx, out);
 }

@@ -327,6 +327,7 @@ struct bsw_ctx {
     std::mutex stats_mu;
     bsw_stats_t last{};
     bsw_ext_stats_t ext_last{};
+    bsw_chain_stats_t chain_last{};
     bsw_mate_stats_t mate_last{};
     bsw_global_stats_t glob_last{};
     struct Pinned { std::mutex mu; void *p = nullptr; size_t cap = 0; } pin[2];
@@ -1253,6 +1254,56 @@ void pinned_release(bsw_ctx_t *ctx, int which) { ctx->pin[which & 1].mu.unlock()
 int64_t ext_chunk_cap(const bsw_ctx_t *ctx)
 {
     return ctx->ext_chunk > 0 ? ctx->ext_chunk : (int64_t)INT32_MAX;
+}
+
+void set_chain_stats(bsw_ctx_t *ctx, const bsw_chain_stats_t &s)
+{
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    ctx->chain_last = s;
+}
+
+int get_chain_stats(bsw_ctx_t *ctx, bsw_chain_stats_t *out)
+{
+    if (!ctx || !out) return BSW_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->stats_mu);
+    *out = ctx->chain_last;
+    return BSW_OK;
+}
+
+DevJobs::~DevJobs()
+{
+    if (device < 0) return;
+    (void)hipSetDevice(device);
+    (void)hipFree(d_off); (void)hipFree(d_len); (void)hipFree(d_seed); (void)hipFree(d_out);
+}
+
+int ext_device_jobs(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads, DevJobs &dj, int32_t nj,
+                    const int64_t *off, const int32_t *len, const bsw_seed_t *seeds, bsw_alnreg_t *out)
+{
+    if (nj <= 0) return BSW_OK;
+    BSW_TRY(hipSetDevice(ctx->devs[0]->device));
+    if ((size_t)nj > dj.cap) {
+        if (dj.device >= 0) {
+            (void)hipFree(dj.d_off); (void)hipFree(dj.d_len); (void)hipFree(dj.d_seed); (void)hipFree(dj.d_out);
+        }
+        dj.device = ctx->devs[0]->device;
+        dj.d_off = dj.d_len = dj.d_seed = dj.d_out = nullptr;
+        dj.cap = 0;
+        const size_t cap = std::max((size_t)nj, (size_t)4096);
+        BSW_TRY(hipMalloc(&dj.d_off, cap * sizeof(int64_t)));
+        BSW_TRY(hipMalloc(&dj.d_len, cap * sizeof(int32_t)));
+        BSW_TRY(hipMalloc(&dj.d_seed, cap * sizeof(bsw_seed_t)));
+        BSW_TRY(hipMalloc(&dj.d_out, cap * sizeof(bsw_alnreg_t)));
+        dj.cap = cap;
+    }
+    BSW_TRY(hipMemcpy(dj.d_off, off, (size_t)nj * sizeof(int64_t), hipMemcpyHostToDevice));
+    BSW_TRY(hipMemcpy(dj.d_len, len, (size_t)nj * sizeof(int32_t), hipMemcpyHostToDevice));
+    BSW_TRY(hipMemcpy(dj.d_seed, seeds, (size_t)nj * sizeof(bsw_seed_t), hipMemcpyHostToDevice));
+    const int rc = bsw_extend_seeds_device(ctx, opt, d_reads, (const int64_t *)dj.d_off, (const int32_t *)dj.d_len,
+                                           (const bsw_seed_t *)dj.d_seed, nj, (bsw_alnreg_t *)dj.d_out, nullptr);
+    if (rc) return rc;
+    BSW_TRY(hipMemcpy(out, dj.d_out, (size_t)nj * sizeof(bsw_alnreg_t), hipMemcpyDeviceToHost));
+    return BSW_OK;
 }
 
 void set_ext_stats(bsw_ctx_t *ctx, const bsw_ext_stats_t &s)

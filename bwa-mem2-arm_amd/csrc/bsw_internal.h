@@ -17,4 +17,16 @@ void pinned_release(bsw_ctx_t *ctx, int which);
 void set_ext_stats(bsw_ctx_t *ctx, const bsw_ext_stats_t &s);
 int64_t ext_chunk_cap(const bsw_ctx_t *ctx);   // reads per extension chunk (BSW_OPT_EXT_CHUNK)
 int get_ext_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out);
+void set_chain_stats(bsw_ctx_t *ctx, const bsw_chain_stats_t &s);
+int get_chain_stats(bsw_ctx_t *ctx, bsw_chain_stats_t *out);
+// Device buffers of one round of bsw_chain2aln_device (job arrays up, regions down).
+struct DevJobs {
+    void *d_off = nullptr, *d_len = nullptr, *d_seed = nullptr, *d_out = nullptr;
+    size_t cap = 0;
+    int device = -1;
+    ~DevJobs();
+};
+// bsw_extend_seeds_device over nj jobs given on the host (reads resident at d_reads)
+int ext_device_jobs(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads, DevJobs &dj, int32_t nj,
+                    const int64_t *off, const int32_t *len, const bsw_seed_t *seeds, bsw_alnreg_t *out);
 }  // namespace bsw

@@ -199,6 +199,105 @@ int32_t bsw_synth_reads(const bsw_reads_cfg *c, const uint8_t *ref, int64_t ref_
     return nseeded;
 }
 
+/* Paired-end reads with SEVERAL seeds per read (C4/C5, closer to what upstream's SMEM
+ * seeding + chaining hand to mem_chain2aln_across_reads_V2).  Read pair k covers fragment
+ * [p, p + I) of the reference, I uniform in [ins_lo, ins_hi]: read 2k = the fragment's first
+ * read_len bases, read 2k+1 its last read_len bases in forward-strand orientation (the
+ * reverse-complemented mate as the extension sees it; the extension math is strand-free).
+ * Each read gets its own substitution / indel script.  Seeds: EVERY maximal exact run of
+ * >= min_seed bases along the read's true alignment path (one chain of up to 8 seeds, longest
+ * first, as chaining orders them); with probability p_spurious an extra 19..30 bp exact copy
+ * of a random reference position is planted in the read (a second, spurious chain); a
+ * fraction p_unrelated of reads are random sequence with only such a planted seed.
+ * Output: reads[r * read_len ..] for r in [0, 2 n_pairs), seeds[0..ns) with seed_read[k] =
+ * the read (relative to this call) of seed k, grouped by read, and seed_chain[k] = 0 for the
+ * read's true chain, 1 for a planted spurious seed on a true read (chains in bwa's order: the
+ * heavier one first); returns ns (<= 9 per read), -1 if the reference is too short. */
+int32_t bsw_synth_pe_seeds(const bsw_reads_cfg *c, const uint8_t *ref, int64_t ref_len, int64_t pair_base,
+                           int32_t n_pairs, int32_t ins_lo, int32_t ins_hi, double p_spurious,
+                           uint8_t *reads, bsw_seed_s *seeds, int32_t *seed_read, int32_t *seed_chain)
+{
+    const int32_t L = c->read_len;
+    int64_t rp[4096];
+    int32_t ns = 0;
+    if (L > 4096 || ins_hi < L || ref_len < (int64_t)ins_hi + 2 * (int64_t)L + 64) return -1;
+    for (int32_t k = 0; k < n_pairs; ++k) {
+        const int64_t gi = pair_base + k;
+        uint64_t s = c->seed * 0x9E3779B97F4A7C15ull ^ ((uint64_t)gi * 0x94D049BB133111EBull) ^ 0xA5A5;
+        splitmix64(&s);
+        const int32_t ins = ins_lo + (int32_t)below(&s, (uint32_t)(ins_hi - ins_lo + 1));
+        const int64_t frag = (int64_t)(u01(&s) * (double)(ref_len - ins - 64));
+        for (int m = 0; m < 2; ++m) {
+            const int32_t rid = 2 * k + m;
+            uint8_t *q = reads + (int64_t)rid * L;
+            const int64_t org = m == 0 ? frag : frag + ins - L;
+            int32_t first = ns;
+            if (u01(&s) < c->p_unrelated) {          /* random read, one planted spurious seed */
+                for (int32_t j = 0; j < L; ++j) q[j] = (uint8_t)below(&s, 4);
+            } else {
+                int64_t i = org;
+                int32_t j = 0;
+                while (j < L) {
+                    const double u = u01(&s);
+                    if (u < c->p_indel) {
+                        const int32_t l = 1 + (int32_t)below(&s, 3);
+                        if (splitmix64(&s) & 1) {
+                            for (int32_t t = 0; t < l && j < L; ++t) { rp[j] = -1; q[j++] = (uint8_t)below(&s, 4); }
+                        } else {
+                            i += l;
+                        }
+                        continue;
+                    }
+                    uint8_t b = ref[i];
+                    if (u01(&s) < c->p_sub) b = (uint8_t)((b < 4 ? b : 0) + 1 + below(&s, 3)) & 3;
+                    rp[j] = i;
+                    q[j++] = b;
+                    ++i;
+                }
+                /* maximal runs of consecutive matching reference positions (non-N) */
+                int32_t run = 0;
+                for (int32_t t = 0; t <= L; ++t) {
+                    const int ok = t < L && rp[t] >= 0 && ref[rp[t]] < 4 && q[t] == ref[rp[t]] &&
+                                   (run == 0 || rp[t] == rp[t - 1] + 1);
+                    if (ok) { ++run; continue; }
+                    if (run >= c->min_seed && ns - first < 8) {
+                        seeds[ns].qbeg = t - run; seeds[ns].rbeg = rp[t - run]; seeds[ns].len = run;
+                        seed_chain[ns] = 0;
+                        seed_read[ns++] = rid;
+                    }
+                    run = (t < L && rp[t] >= 0 && ref[rp[t]] < 4 && q[t] == ref[rp[t]]) ? 1 : 0;
+                }
+                /* longest first (chaining's order) */
+                for (int32_t a = first + 1; a < ns; ++a)
+                    for (int32_t b2 = a; b2 > first && seeds[b2].len > seeds[b2 - 1].len; --b2) {
+                        bsw_seed_s t2 = seeds[b2]; seeds[b2] = seeds[b2 - 1]; seeds[b2 - 1] = t2;
+                        /* seed_read / seed_chain are equal within the run */
+                    }
+                if (!(u01(&s) < p_spurious)) continue;
+            }
+            /* planted spurious seed: exact copy of a random reference position */
+            const int32_t sl = 19 + (int32_t)below(&s, 12);
+            const int32_t qb = (int32_t)below(&s, (uint32_t)(L - sl + 1));
+            const int64_t rb = (int64_t)(u01(&s) * (double)(ref_len - sl));
+            int ok = 1;
+            for (int32_t t = 0; t < sl; ++t) { q[qb + t] = ref[rb + t]; if (ref[rb + t] > 3) ok = 0; }
+            /* true seeds overlapping the planted bases are no longer exact: drop them */
+            int32_t w2 = first;
+            for (int32_t a = first; a < ns; ++a)
+                if (seeds[a].qbeg + seeds[a].len <= qb || seeds[a].qbeg >= qb + sl) {
+                    seeds[w2] = seeds[a]; seed_chain[w2] = seed_chain[a]; seed_read[w2++] = seed_read[a];
+                }
+            ns = w2;
+            if (ok) {
+                seeds[ns].rbeg = rb; seeds[ns].qbeg = qb; seeds[ns].len = sl;
+                seed_chain[ns] = ns > first ? 1 : 0;
+                seed_read[ns++] = rid;
+            }
+        }
+    }
+    return ns;
+}
+
 /* ---------------------------------------------------------------- mate-rescue jobs
  * Jobs shaped like mem_matesw's (bwamem_pair.cpp; include/bsw_mate.h): the mate read
  * (read_len bases sampled from the reference with substitutions / short indels) against a

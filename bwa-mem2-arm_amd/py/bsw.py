@@ -33,7 +33,7 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
                "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats",
                "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
                "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option",
-               "bsw_split_by_cells")
+               "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats")
 
 # include/bsw.h engine options (bsw_set_option)
 OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK, OPT_LONG = 1, 2, 3, 4, 5, 6, 7
@@ -123,12 +123,15 @@ def hip_lib():
         L.bsw_extend_seeds_device.argtypes = [P, P, P, P, P, P, ctypes.c_int32, P, P]
         L.bsw_set_option.argtypes = [P, ctypes.c_int, ctypes.c_int64]
         L.bsw_split_by_cells.argtypes = [P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P]
+        L.bsw_chain2aln.argtypes = [P, P, P, ctypes.c_int64, P, P, P, ctypes.c_int32, P, P, P, ctypes.c_int32, P, P]
+        L.bsw_chain2aln_device.argtypes = [P, P, P, P, P, ctypes.c_int32, P, P, P, ctypes.c_int32, P, P]
+        L.bsw_chain_last_stats.argtypes = [P, P]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
                   "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
                   "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option",
-               "bsw_split_by_cells"):
+               "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -392,6 +395,10 @@ def synth_lib():
         L.bsw_synth_reads.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.bsw_synth_reads.restype = ctypes.c_int32
+        L.bsw_synth_pe_seeds.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.bsw_synth_pe_seeds.restype = ctypes.c_int32
         L.bsw_mates_default.argtypes = [ctypes.c_void_p]
         L.bsw_synth_mates.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
@@ -457,6 +464,78 @@ def synth_reads(ref: np.ndarray, n: int, read_base: int = 0, cfg: ReadsCfg | Non
     read_off = np.arange(n, dtype=np.int64) * L
     read_len = np.full(n, L, dtype=np.int32)
     return reads, read_off, read_len, seeds, origin
+
+
+def synth_pe_seeds(ref: np.ndarray, n_pairs: int, pair_base: int = 0, cfg: ReadsCfg | None = None,
+                   ins=(400, 600), p_spurious: float = 0.1):
+    """Paired-end reads with several seeds each (bsw_synth_pe_seeds): (reads, read_off, read_len,
+    seeds, seed_read, seed_chain); read_off / read_len are PER READ (2 n_pairs reads; reads 2k /
+    2k+1 are the mates of fragment k), seed_read / seed_chain map each seed to its read and chain
+    (bsw_chain2aln's input layout; for bsw_extend_seeds index read_off by seed_read)."""
+    cfg = cfg if cfg is not None else reads_cfg()
+    L = cfg.read_len
+    n_reads = 2 * n_pairs
+    reads = np.zeros(max(1, n_reads * L), dtype=np.uint8)
+    seeds = np.zeros(max(1, n_reads * 9), dtype=SEED_DTYPE)
+    seed_read = np.zeros(max(1, n_reads * 9), dtype=np.int32)
+    seed_chain = np.zeros(max(1, n_reads * 9), dtype=np.int32)
+    ns = synth_lib().bsw_synth_pe_seeds(ctypes.byref(cfg), _ptr(ref), len(ref), pair_base, n_pairs, ins[0], ins[1],
+                                        ctypes.c_double(p_spurious), _ptr(reads), _ptr(seeds), _ptr(seed_read),
+                                        _ptr(seed_chain))
+    if ns < 0:
+        raise BswError("bsw_synth_pe_seeds: reference too short")
+    read_off = np.arange(n_reads, dtype=np.int64) * L
+    read_len = np.full(n_reads, L, dtype=np.int32)
+    return reads, read_off, read_len, seeds[:ns].copy(), seed_read[:ns].copy(), seed_chain[:ns].copy()
+
+
+class ChainStats(ctypes.Structure):
+    _fields_ = [("rounds", ctypes.c_int32), ("n_extended", ctypes.c_int32), ("n_skipped", ctypes.c_int32),
+                ("n_pairs", ctypes.c_int32 * 4), ("kernel_ms", ctypes.c_float), ("ext_ms", ctypes.c_float),
+                ("check_ms", ctypes.c_float), ("prep_ms", ctypes.c_float)]
+
+
+def chain2aln(engine, ref, reads, read_off, read_len, seeds, seed_read, seed_chain, opt: ExtOpt | None = None):
+    """bsw_chain2aln: (regions per seed, extended flags)."""
+    opt = opt if opt is not None else ext_opt()
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    reads = np.ascontiguousarray(reads, dtype=np.uint8)
+    read_off = np.ascontiguousarray(read_off, dtype=np.int64)
+    read_len = np.ascontiguousarray(read_len, dtype=np.int32)
+    seeds = np.ascontiguousarray(seeds, dtype=SEED_DTYPE)
+    seed_read = np.ascontiguousarray(seed_read, dtype=np.int32)
+    seed_chain = np.ascontiguousarray(seed_chain, dtype=np.int32)
+    out = np.zeros(len(seeds), dtype=ALNREG_DTYPE)
+    ext = np.zeros(len(seeds), dtype=np.int32)
+    _check(hip_lib().bsw_chain2aln(engine._ctx, ctypes.byref(opt), _ptr(ref), len(ref), _ptr(reads), _ptr(read_off),
+                                   _ptr(read_len), len(read_len), _ptr(seeds), _ptr(seed_read), _ptr(seed_chain),
+                                   len(seeds), _ptr(out), _ptr(ext)))
+    return out, ext
+
+
+def chain2aln_device(engine, d_reads: int, read_off, read_len, seeds, seed_read, seed_chain,
+                     opt: ExtOpt | None = None, out=None, ext=None):
+    """bsw_chain2aln_device: reads resident at d_reads (device pointer), reference resident;
+    `out` / `ext` may be preallocated (ALNREG_DTYPE / int32, len(seeds))."""
+    opt = opt if opt is not None else ext_opt()
+    read_off = np.ascontiguousarray(read_off, dtype=np.int64)
+    read_len = np.ascontiguousarray(read_len, dtype=np.int32)
+    seeds = np.ascontiguousarray(seeds, dtype=SEED_DTYPE)
+    seed_read = np.ascontiguousarray(seed_read, dtype=np.int32)
+    seed_chain = np.ascontiguousarray(seed_chain, dtype=np.int32)
+    out = np.zeros(len(seeds), dtype=ALNREG_DTYPE) if out is None else out
+    ext = np.zeros(len(seeds), dtype=np.int32) if ext is None else ext
+    assert out.dtype == ALNREG_DTYPE and len(out) == len(seeds) and ext.dtype == np.int32 and len(ext) == len(seeds)
+    _check(hip_lib().bsw_chain2aln_device(engine._ctx, ctypes.byref(opt), ctypes.c_void_p(d_reads), _ptr(read_off),
+                                          _ptr(read_len), len(read_len), _ptr(seeds), _ptr(seed_read),
+                                          _ptr(seed_chain), len(seeds), _ptr(out), _ptr(ext)))
+    return out, ext
+
+
+def chain_last_stats(engine) -> ChainStats:
+    st = ChainStats()
+    _check(hip_lib().bsw_chain_last_stats(engine._ctx, ctypes.byref(st)))
+    return st
 
 
 class MatesCfg(ctypes.Structure):

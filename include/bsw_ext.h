@@ -24,7 +24,9 @@
  *
  * All LEFT extensions of a call form one batch (then one retry batch), then all RIGHT
  * extensions (their h0 depends on LEFT's result) -- the across-reads batching of
- * mem_chain2aln_across_reads_V2.  One seed per read in this interface.
+ * mem_chain2aln_across_reads_V2.  bsw_extend_seeds takes one seed per job (jobs of the same
+ * read repeat its read_off / read_len); bsw_chain2aln below adds upstream's per-read chain /
+ * seed order and contained-seed skipping on top.
  */
 #ifndef BSW_EXT_H
 #define BSW_EXT_H
@@ -93,6 +95,42 @@ typedef struct bsw_ext_stats_t {
     float   interp_ms;               /* host: local / to-end interpretation (device form: 0)     */
 } bsw_ext_stats_t;
 int bsw_ext_last_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out);
+
+/* mem_chain2aln over the chains of many reads (upstream's per-read order, batched across reads
+ * as mem_chain2aln_across_reads_V2 does).  Seeds are grouped by read
+ * (seed_read[k] non-decreasing, indexing read_off / read_len of n_reads reads); within a read,
+ * runs of equal seed_chain[k] are its chains, in the order bwa processes them.  Per read: each
+ * chain's seeds by score (len * a) descending, ties the later seed first; a seed lying
+ * "around" the diagonal of an earlier region of the read (any chain; upstream's containment
+ * test with cal_max_gap and the region's band) is SKIPPED unless an extended seed of its own
+ * chain, at least 95% as long, overlaps it by >= 1/4 of its length on another diagonal;
+ * every other seed is extended exactly as bsw_extend_seeds does.  out[k] = seed k's region
+ * (zeroed if skipped), extended[k] = 1 / 0.  Work runs in rounds: round r extends, for every
+ * read, the next seed its containment test keeps -- one batch set (LEFT, retries, RIGHT,
+ * retries) per round across all reads.  Blocking; 0 or a BSW_E* code. */
+int bsw_chain2aln(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *ref, int64_t ref_len,
+                  const uint8_t *reads, const int64_t *read_off, const int32_t *read_len, int32_t n_reads,
+                  const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain, int32_t n_seeds,
+                  bsw_alnreg_t *out, int32_t *extended);
+
+/* The same with the reads RESIDENT in HBM (d_reads on the context's first device, read_off /
+ * read_len and the seeds on the host) and the resident reference of bsw_set_reference: each
+ * round's extensions run through bsw_extend_seeds_device (job arrays up, regions down). */
+int bsw_chain2aln_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
+                         const int64_t *read_off, const int32_t *read_len, int32_t n_reads,
+                         const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain,
+                         int32_t n_seeds, bsw_alnreg_t *out, int32_t *extended);
+
+typedef struct bsw_chain_stats_t {
+    int32_t rounds;                  /* batch rounds of the last bsw_chain2aln(_device)        */
+    int32_t n_extended, n_skipped;   /* seeds extended / skipped as contained                  */
+    int32_t n_pairs[4];              /* SeqPairs per phase summed over rounds (as ext stats)   */
+    float   kernel_ms;               /* DP kernels (HIP events)                                */
+    float   ext_ms;                  /* wall time in the rounds' extension calls               */
+    float   check_ms;                /* host: containment tests between rounds                 */
+    float   prep_ms;                 /* host: per-read chain / seed order                      */
+} bsw_chain_stats_t;
+int bsw_chain_last_stats(bsw_ctx_t *ctx, bsw_chain_stats_t *out);
 
 #ifdef __cplusplus
 }

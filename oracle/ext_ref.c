@@ -33,20 +33,16 @@ static int cal_max_gap(const oracle_params_t *p, int a, int w, int qlen)
     return l < w << 1 ? l : w << 1;
 }
 
-void oracle_extend_seeds(const oracle_params_t *p, const bsw_ext_opt_t *opt, const uint8_t *ref,
-                         int64_t ref_len, const uint8_t *reads, const int64_t *read_off,
-                         const int32_t *read_len, const bsw_seed_t *seeds, int32_t n,
-                         bsw_alnreg_t *out)
+/* one seed's extension (the body of mem_chain2aln's per-seed step) */
+static void oracle_extend_one(const oracle_params_t *p, const bsw_ext_opt_t *opt, const uint8_t *ref,
+                              int64_t ref_len, const uint8_t *query, int l_query, const bsw_seed_t *s,
+                              bsw_alnreg_t *r)
 {
     const int a = p->mat[0];
-    for (int32_t i = 0; i < n; ++i) {
-        bsw_alnreg_t *r = &out[i];
-        const bsw_seed_t *s = &seeds[i];
-        const uint8_t *query = reads + read_off[i];
-        const int l_query = read_len[i];
+    {
         int qle, tle, gtle, gscore, max_off[2] = {0, 0}, aw[2];
         memset(r, 0, sizeof(*r));
-        if (s->len <= 0) continue;
+        if (s->len <= 0) return;
         int64_t rmax0 = s->rbeg - (s->qbeg + cal_max_gap(p, a, opt->w, s->qbeg));
         int64_t rmax1 = s->rbeg + s->len + ((l_query - s->qbeg - s->len) +
                                             cal_max_gap(p, a, opt->w, l_query - s->qbeg - s->len));
@@ -102,4 +98,101 @@ void oracle_extend_seeds(const oracle_params_t *p, const bsw_ext_opt_t *opt, con
         }
         r->w = aw[0] > aw[1] ? aw[0] : aw[1];
     }
+}
+
+void oracle_extend_seeds(const oracle_params_t *p, const bsw_ext_opt_t *opt, const uint8_t *ref,
+                         int64_t ref_len, const uint8_t *reads, const int64_t *read_off,
+                         const int32_t *read_len, const bsw_seed_t *seeds, int32_t n,
+                         bsw_alnreg_t *out)
+{
+    for (int32_t i = 0; i < n; ++i)
+        oracle_extend_one(p, opt, ref, ref_len, reads + read_off[i], read_len[i], &seeds[i], &out[i]);
+}
+
+/* mem_chain2aln over the chains of every read, literal per-read order (bwa 0.7.x src/bwamem.c,
+ * kept by bwa-mem2's src/bwamem.cpp; [UPSTREAM-RECALL]): the read's
+ * chains in the given order, each chain's seeds by score descending (ties: the later seed
+ * first, bwa's srt[] = score << 32 | index sorted ascending and walked down); a seed is
+ * skipped when an earlier region of the READ (any chain) contains it "around" the same
+ * diagonal -- unless an extended, at least 95%-as-long seed of its own chain overlaps it on a
+ * different diagonal; otherwise it is extended (oracle_extend_one) and its region appended.
+ * Seeds are grouped by read (seed_read non-decreasing), chains are runs of equal seed_chain. */
+static int oracle_contained(const oracle_params_t *p, const bsw_ext_opt_t *opt, const bsw_seed_t *s,
+                            int l_query, const bsw_alnreg_t *out, const int32_t *av, int nav)
+{
+    const int a = p->mat[0];
+    for (int i = 0; i < nav; ++i) {
+        const bsw_alnreg_t *q = &out[av[i]];
+        int64_t rd;
+        int qd, w, max_gap;
+        if (s->rbeg < q->rb || s->rbeg + s->len > q->re || s->qbeg < q->qb || s->qbeg + s->len > q->qe) continue;
+        if (s->len - q->seedlen0 > .1 * l_query) continue;
+        qd = s->qbeg - q->qb; rd = s->rbeg - q->rb;
+        max_gap = cal_max_gap(p, a, opt->w, qd < rd ? qd : (int)rd);
+        w = max_gap < q->w ? max_gap : q->w;
+        if (qd - rd < w && rd - qd < w) return 1;
+        qd = q->qe - (s->qbeg + s->len); rd = q->re - (s->rbeg + s->len);
+        max_gap = cal_max_gap(p, a, opt->w, qd < rd ? qd : (int)rd);
+        w = max_gap < q->w ? max_gap : q->w;
+        if (qd - rd < w && rd - qd < w) return 1;
+    }
+    return 0;
+}
+
+void oracle_chain2aln(const oracle_params_t *p, const bsw_ext_opt_t *opt, const uint8_t *ref, int64_t ref_len,
+                      const uint8_t *reads, const int64_t *read_off, const int32_t *read_len,
+                      const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain, int32_t ns,
+                      bsw_alnreg_t *out, int32_t *extended)
+{
+    const int a = p->mat[0];
+    int32_t *av = (int32_t *)malloc(sizeof(int32_t) * (size_t)(ns > 0 ? ns : 1));
+    int32_t *srt = (int32_t *)malloc(sizeof(int32_t) * (size_t)(ns > 0 ? ns : 1));
+    for (int32_t k = 0; k < ns; ++k) { memset(&out[k], 0, sizeof(out[k])); extended[k] = 0; }
+    for (int32_t r0 = 0; r0 < ns;) {
+        int32_t r1 = r0;
+        while (r1 < ns && seed_read[r1] == seed_read[r0]) ++r1;
+        const int rid = seed_read[r0];
+        const uint8_t *query = reads + read_off[rid];
+        const int l_query = read_len[rid];
+        int nav = 0;
+        for (int32_t c0 = r0; c0 < r1;) {
+            int32_t c1 = c0;
+            while (c1 < r1 && seed_chain[c1] == seed_chain[c0]) ++c1;
+            const int n = c1 - c0;
+            /* srt ascending by (score, index); processed from the top down */
+            for (int i = 0; i < n; ++i) srt[i] = c0 + i;
+            for (int i = 1; i < n; ++i)
+                for (int j = i; j > 0; --j) {
+                    const int32_t x = srt[j - 1], y = srt[j];
+                    const int64_t kx = ((int64_t)(seeds[x].len * a) << 32) | (x - c0);
+                    const int64_t ky = ((int64_t)(seeds[y].len * a) << 32) | (y - c0);
+                    if (kx > ky) { srt[j - 1] = y; srt[j] = x; } else break;
+                }
+            for (int k = n - 1; k >= 0; --k) {
+                const int32_t si = srt[k];
+                const bsw_seed_t *s = &seeds[si];
+                if (oracle_contained(p, opt, s, l_query, out, av, nav)) {
+                    int i;
+                    for (i = k + 1; i < n; ++i) {          /* overlapping extended seeds of the chain */
+                        const bsw_seed_t *t;
+                        if (!extended[srt[i]]) continue;
+                        t = &seeds[srt[i]];
+                        if (t->len < s->len * .95) continue;
+                        if (s->qbeg <= t->qbeg && s->qbeg + s->len - t->qbeg >= s->len >> 2 &&
+                            t->qbeg - s->qbeg != t->rbeg - s->rbeg) break;
+                        if (t->qbeg <= s->qbeg && t->qbeg + t->len - s->qbeg >= s->len >> 2 &&
+                            s->qbeg - t->qbeg != s->rbeg - t->rbeg) break;
+                    }
+                    if (i == n) continue;                   /* skipped: not extended */
+                }
+                oracle_extend_one(p, opt, ref, ref_len, query, l_query, s, &out[si]);
+                extended[si] = 1;
+                av[nav++] = si;
+            }
+            c0 = c1;
+        }
+        r0 = r1;
+    }
+    free(av);
+    free(srt);
 }

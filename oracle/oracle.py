@@ -107,6 +107,24 @@ def sse41_get_scores16(params: OracleParams, pairs: np.ndarray, ref: np.ndarray,
                                     len(pairs), w, nthreads)
 
 
+def chain2aln(params, opt, ref, reads, read_off, read_len, seeds, seed_read, seed_chain):
+    """oracle_chain2aln (oracle/ext_ref.c): literal per-read mem_chain2aln -> (regions, extended)."""
+    import bsw  # dtypes of the product binding (ALNREG_DTYPE)
+    L = lib()
+    P = ctypes.c_void_p
+    L.oracle_chain2aln.argtypes = [P, P, P, ctypes.c_int64, P, P, P, P, P, P, ctypes.c_int32, P, P]
+    ptr = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    arrs = [np.ascontiguousarray(x, dtype=d) for x, d in ((ref, np.uint8), (reads, np.uint8), (read_off, np.int64),
+                                                           (read_len, np.int32), (seed_read, np.int32),
+                                                           (seed_chain, np.int32))]
+    seeds = np.ascontiguousarray(seeds)
+    out = np.zeros(len(seeds), dtype=bsw.ALNREG_DTYPE)
+    ext = np.zeros(len(seeds), dtype=np.int32)
+    L.oracle_chain2aln(ctypes.byref(params), ctypes.byref(opt), ptr(arrs[0]), len(arrs[0]), ptr(arrs[1]), ptr(arrs[2]),
+                       ptr(arrs[3]), ptr(seeds), ptr(arrs[4]), ptr(arrs[5]), len(seeds), ptr(out), ptr(ext))
+    return out, ext
+
+
 def extend_seeds(params, opt, ref, reads, read_off, read_len, seeds):
     """oracle/ext_ref.c: per-read CPU restatement of the extension consumer (test checker)."""
     import sys as _sys
