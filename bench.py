@@ -129,6 +129,24 @@ def _timed(fn, reps):
     return statistics.median(ts)
 
 
+def traffic_dominant(prefix: str):
+    """(kernel, HBM bytes per launch) of the longest-running kernel whose short name starts with
+    `prefix` in profiles/pmc_latest.json (rocprofv3 PMC passes of tools/profile.sh), else
+    (None, None)."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    c = [(v.get("total_ns", 0), k, v.get("hbm_bytes_per_launch")) for k, v in d.items()
+         if k.startswith(prefix) and v.get("hbm_bytes_per_launch") is not None]
+    if not c:
+        return None, None
+    _, k, b = max(c)
+    return k, b
+
+
 def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
     """oracle/bsw_sse41.c (the reference's SSE4.1 getScores16 design restated) on a bounded
     sample of the same batch: ALL usable host cores (`cores`, default = sched affinity), median
@@ -707,7 +725,9 @@ def main_mate(args, rank, local, world):
                    "jobs_per_gpu": args.jobs, "parallelism": f"shard{world} (independent jobs)",
                    "n_fwd": st.n_fwd, "n_rev": st.n_rev},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
-                     "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+                     "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                     "traffic": traffic_dominant("mate_kernel")[1],
+                     "traffic_kernel": traffic_dominant("mate_kernel")[0],
                      "kernel": "mate forward pass", "launch_ms": round(fwd_ms, 4),
                      "cells_per_s": round(st.cells_fwd / (fwd_ms * 1e-3) / 1e12, 4),
                      "algorithmic": f"{OPS_PER_CELL} int ops x {st.cells_fwd} forward cells per launch"},
@@ -789,7 +809,9 @@ def main_global(args, rank, local, world):
         "roofline": {"bound": "valu", "achieved": round(st.cells * OPS_PER_CELL / (kms * 1e-3) / 1e12, 3),
                      "peak": round(VALU_PEAK_TOPS, 1), "unit": "TOP/s",
                      "frac": round(st.cells * OPS_PER_CELL / (kms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
-                     "traffic": None, "kernel": "glob_lane_kernel<160> (DP + traceback)", "launch_ms": round(kms, 4),
+                     "traffic": traffic_dominant("glob_lane_kernel")[1],
+                     "traffic_kernel": traffic_dominant("glob_lane_kernel")[0],
+                     "kernel": "glob_lane_kernel<160> (DP + traceback)", "launch_ms": round(kms, 4),
                      "cells_per_s": round(st.cells / (kms * 1e-3) / 1e12, 4),
                      "traceback_matrix_GBps": round(st.z_bytes / (kms * 1e-3) / 1e9, 1),
                      "algorithmic": f"{OPS_PER_CELL} int ops x {st.cells} band cells per step"},

@@ -221,6 +221,9 @@ __device__ __forceinline__ void glob_group_at(uint32_t (&R)[QMAX], const uint32_
     if (8 * G >= r.fb && 8 * G + 8 <= r.fe) word = glob_group<G, QMAX, false>(R, q8, pr, h1, f, c, beg, end);
     else word = glob_group<G, QMAX, true>(R, q8, pr, h1, f, c, beg, end);
     if (zrow && G - r.dlo < r.cap_dw) zrow[(G - r.dlo) * 64 + lane] = word;
+    // keep the scheduler from interleaving groups: each group's temporaries die here, so the
+    // row (QMAX packed {h, e} registers) plus one group's working set fits 2 waves per SIMD
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int QMAX, int... G>
@@ -254,17 +257,30 @@ __global__ __launch_bounds__(64, 2) void glob_lane_kernel(
 
     // query codes, 8 per VGPR as nibbles in order {c0, c2, c4, c6 | c1, c3, c5, c7} by byte
     // (glob_group splits them into two v_perm selectors)
+    // Aligned dword loads (a dword holding a byte of the query never leaves that byte's page),
+    // realigned by v_alignbyte; positions >= qlen read as code 4; codes kept to 3 bits.
     uint32_t q8[NG];
+    {
+        const uintptr_t qa = (uintptr_t)(qer + (live ? p.idq : 0));
+        const uint32_t *wp = (const uint32_t *)(qa & ~(uintptr_t)3);
+        const int sh = (int)(qa & 3);
+        const int nw = (live && qlen > 0) ? (sh + qlen + 3) >> 2 : 0;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        uint32_t w8 = 0;
+        for (int g = 0; g < NG; ++g) {
+            uint32_t wv[3];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int j = 8 * g + k;
-            const uint32_t code = (live && j < qlen) ? qer[p.idq + j] : 4u;
-            w8 |= min(code, 7u) << (8 * (k >> 1) + 4 * (k & 1));
+            for (int k = 0; k < 3; ++k) wv[k] = nw > 0 ? wp[min(2 * g + k, nw - 1)] : 0u;
+            uint32_t c0 = __builtin_amdgcn_alignbyte(wv[1], wv[0], sh);
+            uint32_t c1 = __builtin_amdgcn_alignbyte(wv[2], wv[1], sh);
+            // bytes k >= qlen - 8g -> 4
+            const int lim = min(max(qlen - 8 * g, 0), 8);
+            const uint64_t m = lim >= 8 ? ~0ull : ((1ull << (8 * lim)) - 1);
+            const uint32_t m0 = (uint32_t)m, m1 = (uint32_t)(m >> 32);
+            c0 = ((c0 & 0x07070707u) & m0) | (0x04040404u & ~m0);
+            c1 = ((c1 & 0x07070707u) & m1) | (0x04040404u & ~m1);
+            const uint32_t y0 = (c0 | (c0 >> 4)) & 0x00ff00ffu, y1 = (c1 | (c1 >> 4)) & 0x00ff00ffu;
+            q8[g] = __builtin_amdgcn_perm(y1, y0, 0x06040200u);      // {k0|k1<<4, k2|k3<<4, k4|k5<<4, k6|k7<<4}
         }
-        q8[g] = w8;
     }
     // first row: eh[0] = {0, -inf}, eh[j] = {-(o_ins + e_ins j), -inf} for 1 <= j <= min(qlen, w)
     uint32_t R[QMAX];

@@ -29,9 +29,10 @@ def rows(pattern):
     return out
 
 def short(name):
-    for kern in ('pc_kernel', 'pk_kernel', 'lane_kernel', 'mate_kernel'):
+    for kern in ('glob_lane_kernel', 'glob_band_kernel', 'glob_wide_kernel', 'wv_kernel', 'pc_kernel',
+                 'pk_kernel', 'lane_kernel', 'mate_kernel'):
         if kern in name:
-            for q in ('160', '128', '96', '64', '32'):
+            for q in ('160', '128', '96', '80', '64', '48', '32', '16', '8', '4'):
                 if f'ILi{q}E' in name or f'<{q},' in name or f'<{q}>' in name:
                     return f'{kern}<{q}>'
             return kern
@@ -75,5 +76,12 @@ if dest:
         shutil.copy(f, os.path.join(dest, 'kernel_stats.csv'))
     with open(os.path.join(dest, 'pmc_summary.json'), 'w') as fh:
         json.dump(summary, fh, indent=1)
-    with open(os.path.join(os.path.dirname(dest.rstrip('/')), 'pmc_latest.json'), 'w') as fh:
-        json.dump(summary, fh, indent=1)
+    # profiles/pmc_latest.json: merged over workloads (bench.py reads each kernel's traffic)
+    latest = os.path.join(os.path.dirname(dest.rstrip('/')), 'pmc_latest.json')
+    merged = {}
+    if os.path.exists(latest):
+        with open(latest) as fh:
+            merged = json.load(fh)
+    merged.update({k: v for k, v in summary.items() if 'hbm_bytes_per_launch' in v or k not in merged})
+    with open(latest, 'w') as fh:
+        json.dump(merged, fh, indent=1)
