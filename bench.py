@@ -18,14 +18,15 @@ Reported beside the metric:
                   launch / HIP-event-timed launch duration, vs the gfx950 packed-int16 VALU
                   peak; traffic = HBM bytes per launch from rocprofv3 PMC (profiles/).
   cpu_baseline -- oracle/bsw_sse41.c (restated upstream SSE4.1 getScores16 design, "port")
-                  on a bounded sample of the same batch on every core of the affinity set
-                  (model, core count and cgroup quota recorded), rank 0, N = 1 only.
+                  on a bounded sample of the same batch; best of {affinity set, cgroup quota,
+                  16} threads (model, core count and quota recorded), rank 0, N = 1 only.
 """
 
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -149,21 +150,32 @@ def traffic_dominant(prefix: str):
 
 def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
     """oracle/bsw_sse41.c (the reference's SSE4.1 getScores16 design restated) on a bounded
-    sample of the same batch: ALL usable host cores (`cores`, default = sched affinity), median
-    of 3 after a warm-up; beside it the 16-thread and 1-thread SSE4.1 rates and the 1-thread
-    scalar ksw_extend2 rate (BASELINE.md / north_star: core count stated)."""
+    sample of the same batch, median of 3 after a warm-up.  Thread counts tried: every core of
+    the affinity set (`cores`), the cgroup CPU quota (the box's real CPU share, which can be far
+    below the affinity set) and 16; `value` is the BEST of them with `cores` = the count that
+    gave it, the others beside it, plus the 1-thread SSE4.1 and scalar ksw_extend2 rates
+    (BASELINE.md / north_star: core count stated)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # CPU baseline leg only (test infrastructure)
     P = oracle.make_params()
-    # ~12.5K pairs per thread (>= 0.1 s per run at ~0.1 M pairs/s/thread), at most the batch
-    S = min(len(pairs), max(200_000, 12_500 * cores))
-    sample = pairs[:S]
-    out = sample.copy()
-    sse_mt = S / _timed(lambda: oracle.sse41_get_scores16(P, out, ref, qer, w, cores), 3) / 1e6
-    S16 = min(len(pairs), 200_000)
-    a16 = pairs[:S16].copy()
-    sse_16 = S16 / _timed(lambda: oracle.sse41_get_scores16(P, a16, ref, qer, w, 16), 1) / 1e6 \
-        if cores != 16 else sse_mt
+    host = host_cpu_info()
+    quota = host.get("cgroup_cpu_quota")
+    counts = [cores]
+    if quota and int(math.ceil(quota)) < cores:
+        counts.append(int(math.ceil(quota)))
+    if 16 < cores and 16 not in counts:
+        counts.append(16)
+    rates = {}
+    best = None
+    for c in counts:
+        # ~12.5K pairs per thread (>= 0.1 s per run at ~0.1 M pairs/s/thread), at most the batch
+        S = min(len(pairs), max(200_000, 12_500 * c))
+        out = pairs[:S].copy()
+        r = S / _timed(lambda: oracle.sse41_get_scores16(P, out, ref, qer, w, c), 3) / 1e6
+        rates[c] = r
+        if best is None or r > best[1]:
+            best = (c, r, S, out)
+    bc, bval, S, out = best
     S1 = min(len(pairs), 20_000)
     a = pairs[:S1].copy()
     t = time.perf_counter()
@@ -177,12 +189,13 @@ def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
     agree = all(np.array_equal(out[f], gpu_pairs[:S][f]) for f in bsw.OUT_FIELDS)
     cells = oracle.band_cells(P, pairs[:S2], ref, qer, w) / S2     # actual (narrowed) band cells per pair
     return {
-        "value": round(sse_mt, 4), "unit": UNIT, "cores": cores, "kind": "port",
+        "value": round(bval, 4), "unit": UNIT, "cores": bc, "kind": "port",
         "sample": f"first {S} pairs of the rank-0 C2 batch; oracle/bsw_sse41.c (SSE4.1, 8 x int16 "
-                  f"lanes, restated upstream getScores16 design, not the upstream binary), {cores} threads "
-                  f"= every core in the process's affinity set, median of 3 after 1 warm-up",
-        "host": host_cpu_info(),
-        "sse41_16threads": round(sse_16, 4),
+                  f"lanes, restated upstream getScores16 design, not the upstream binary), {bc} threads "
+                  f"(best of {sorted(counts)} threads: affinity set {cores}, cgroup quota {quota}), "
+                  f"median of 3 after 1 warm-up",
+        "host": host,
+        "sse41_by_threads": {str(c): round(r, 4) for c, r in sorted(rates.items())},
         "sse41_1thread": round(sse_1t, 4), "scalar_ksw_extend2_1thread": round(scalar_1t, 4),
         "outputs_identical_to_gpu": bool(agree),
         "actual_cells_per_pair": round(cells, 1),

@@ -142,6 +142,34 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
 #define PC_CNT_OPS
 #endif
 
+// FAST F chain, packed (two columns per instruction where the recurrence allows it).
+// F(j+1) = max(sat(F(j) - e), T~(j)); H(j) = max(ME(j), F(j)).  Per register X (columns 2k, 2k+1)
+// with Fp = {F(2k), sat(F(2k) - e)} entering:
+//   Fp <- max(Fp, {T~(2k), T~(2k)})          = {max(F(2k), T~(2k)), F(2k+1)}  (the low half may
+//                                              absorb T~(2k): ME >= M > T~, so H(2k) is unchanged)
+//   Hp  = max(Fp, ME)                        = {H(2k), H(2k+1)}
+//   Fp <- max(sat({F(2k+1) - e, F(2k+1) - 2e}), {T~(2k+1), T~(2k+1) - e})
+//                                            = {F(2k+2), sat(F(2k+2) - e)}
+// (sat(max(a, b) - e) = max(sat(a - e), sat(b - e)); the second half is >= 0 through its first
+// operand, so T~ needs no clamp).  The group enters with a clean f = F(4G) and leaves with a clean
+// f = F(4G+4) (32-bit ops for the last step, so masked bodies read it unchanged), and leaves
+// h1 = {H(4G+2), H(4G+3)}: h1 travels in its HIGH half between groups, so the new row
+// registers are two byte-aligns, HH[2G] = {H(4G-1), H(4G)}, HH[2G+1] = {H(4G+1), H(4G+2)}.
+// 10 VALU per 4 cells for the chain (12 before) and 2 for the packing.
+#define PC_FAST_CHAIN                                                                    \
+    "v_pk_sub_u16 %[fp], %[f], %[e0e] op_sel_hi:[0,1] clamp\n\t"                            \
+    "v_pk_max_i16 %[fp], %[fp], %[ta] op_sel_hi:[1,0]\n\t"                                  \
+    "v_pk_max_i16 %[pa], %[fp], %[sa]\n\t"                                                  \
+    "v_pk_sub_u16 %[fp], %[fp], %[ee2] op_sel:[1,0] clamp\n\t"                              \
+    "v_pk_sub_i16 %[y], %[ta], %[e0e] op_sel:[1,0]\n\t"                                     \
+    "v_pk_max_i16 %[fp], %[fp], %[y]\n\t"                                                   \
+    "v_alignbyte_b32 %[ha], %[pa], %[h1], 2\n\t"                                            \
+    "v_pk_max_i16 %[fp], %[fp], %[tb] op_sel_hi:[1,0]\n\t"                                  \
+    "v_pk_max_i16 %[h1], %[fp], %[sb]\n\t"                                                  \
+    "v_sub_u32_sdwa %[f], %[fp], %[ed] clamp dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t" \
+    "v_alignbyte_b32 %[hb], %[h1], %[pa], 2\n\t"                                            \
+    PC_SDWA("v_max_i32", "%[f]", "%[f]", "sext(%[tb])", "WORD_1")
+
 // Layout: the FAST body is the fall-through path (one bit test, a not-taken branch, no taken
 // branch); skipped and masked groups branch to code in subsection 1 of the kernel's section
 // (out of line, after the kernel's main body) and back.  Branch targets stay inside the
@@ -153,12 +181,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
         PC_CNT(0) PC_CNT(1)                                                                  \
         PC_SCORES                                                                            \
         PC_PH1("a", "%[ea]") PC_PH1("b", "%[eb]")                                            \
-        PC_CELL("%[c0]", "a", "WORD_0")                                                      \
-        PC_CELL("%[c1]", "a", "WORD_1")                                                      \
-        "v_lshl_or_b32 %[ha], %[c0], 16, %[h1]\n\t"                                          \
-        PC_CELL("%[c2]", "b", "WORD_0")                                                      \
-        PC_CELL("%[h1]", "b", "WORD_1")                                                      \
-        "v_lshl_or_b32 %[hb], %[c2], 16, %[c1]\n\t"                                          \
+        PC_FAST_CHAIN                                                                        \
         KEYA_FAST                                                                            \
         "v_pk_max_u16 %[key], %[key], %[pa]\n\t"                                             \
         "v_lshl_or_b32 %[pb], %[hb], 8, %[jjb]\n\t"                                          \
@@ -169,6 +192,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
         "s_bitcmp1_b64 %[men], %[g]\n\t"             /* outside [min beg, max end]: skip */ \
         "s_cbranch_scc0 3b\n\t"                                                              \
         PC_CNT(0)                                                                            \
+        "v_lshrrev_b32_e32 %[h1], 16, %[h1]\n\t"     /* masked bodies: h1 as a clean int */ \
         PC_SCORES                                                                            \
         "s_bitcmp1_b64 %[mle], %[g]\n\t"             /* some lane's beg in this group: L */ \
         "s_cbranch_scc1 4f\n\t"                                                              \
@@ -178,6 +202,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
                   PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"),                        \
                   PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"),                        \
                   KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t", "", "")           \
+        "v_lshlrev_b32_e32 %[h1], 16, %[h1]\n\t"                                              \
         "s_branch 3b\n"                                                                      \
         "4:\n\t"                                                                             \
         PC_CNT(3)                                                                            \
@@ -187,15 +212,16 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
                   PC_RESET("%[c2]", "%[j3]") PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"), \
                   KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t",                    \
                   PC_LEFTMASK("a"), PC_LEFTMASK("b"))                                        \
+        "v_lshlrev_b32_e32 %[h1], 16, %[h1]\n\t"                                              \
         "s_branch 3b\n"                                                                      \
         ".subsection 0\n"                                                                    \
         : [ha] "+v"(ha), [hb] "+v"(hb), [ea] "+v"(ea), [eb] "+v"(eb), [f] "+v"(f),           \
           [h1] "+v"(h1), [key] "+v"(key), [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb),     \
           [ta] "=&v"(ta), [tb] "=&v"(tb), [xa] "=&v"(xa), [xb] "=&v"(xb), [c0] "=&v"(c0),    \
-          [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb)                     \
+          [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb), [fp] "=&v"(fp)    \
           PC_CNT_OPS                                                                         \
         : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe2] "s"(oe2), [ed2] "s"(ed2),        \
-          [ed] "s"(ed), [men] "s"(r.enter), [mfa] "s"(r.fast), [mle] "s"(r.left),           \
+          [ed] "s"(ed), [e0e] "s"(e0e), [ee2] "s"(ee2), [men] "s"(r.enter), [mfa] "s"(r.fast), [mle] "s"(r.left),           \
           [endw] "v"(endw), [endm1w] "v"(endm1w),                                            \
           [begm2w] "v"(begm2w), [endv] "v"(endv), [begv] "v"(begv), [g] "i"(G),             \
           [jja] "s"(JJA), [jjb] "s"(JJB), [j0] "i"(4 * G), [j1] "i"(4 * G + 1),              \
@@ -216,10 +242,12 @@ __device__ __forceinline__ void pc_group(uint32_t &ha, uint32_t &hb, uint32_t &e
     constexpr uint32_t JJA = ((uint32_t)(4 * G - 1) & 0xffffu) | ((uint32_t)(4 * G) << 16);
     constexpr uint32_t JJB = (uint32_t)(4 * G + 1) | ((uint32_t)(4 * G + 2) << 16);
     constexpr int R0 = (G == 0) ? -1 : 4 * G;   // no reset entering column 0 (the boundary)
-    uint32_t y, sa, sb, ta, tb, xa, xb, c0, c1, c2, pa, pb;
+    uint32_t y, sa, sb, ta, tb, xa, xb, c0, c1, c2, pa, pb, fp;
+    const uint32_t e0e = (uint32_t)ed << 16;                          // {0, e}
+    const uint32_t ee2 = (uint32_t)ed | ((uint32_t)(2 * ed) << 16);   // {e, 2e}
     if constexpr (G == 0) {
         // slot 0 holds the column-0 boundary, not a cell: its key half is 0 (c0 << 24 | 0)
-        PC_GROUP_ASM("v_lshl_or_b32 %[pa], %[c0], 24, 0\n\t",
+        PC_GROUP_ASM("v_lshlrev_b32_e32 %[pa], 24, %[pa]\n\t",        /* pa = {H(0), H(1)} here */
                      "v_lshl_or_b32 %[pa], %[c0], 24, 0\n\t");
     } else {
         PC_GROUP_ASM("v_lshl_or_b32 %[pa], %[ha], 8, %[jja]\n\t",
@@ -395,8 +423,14 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 const int k = (i >> 2) & 15;
-                const uint32_t *src = &s_tgt[wv][(i >> 6) & 1][k][ln];
-                tcur = __builtin_amdgcn_alignbyte(src[64], src[0], tsh);
+                // the two dwords by inline asm: the compiler would otherwise put a vmcnt(0) before
+                // every LDS read (it cannot tell this buffer from the one the in-flight LDS-DMA
+                // refill writes) -- this chunk's DMA was waited for at its first row above
+                const uint32_t la = (uint32_t)(uintptr_t)(lptr_t)&s_tgt[wv][(i >> 6) & 1][k][ln];
+                uint2 d;
+                asm volatile("ds_read2st64_b32 %0, %1 offset1:1\n\ts_waitcnt lgkmcnt(0)"
+                             : "=v"(d) : "v"(la) : "memory");
+                tcur = __builtin_amdgcn_alignbyte(d.y, d.x, tsh);
                 if ((i & 63) == 0) {
                     __builtin_amdgcn_sched_barrier(0);
                     if (i > 0) issue_chunk((i >> 6) + 1);   // refill the buffer just drained
@@ -410,8 +444,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
         const int beg = max(0, i - wl);
         const int end = min(min(endc, i + wl + 1), qlen);
         endc = end;
-        const int emax = wave_max_bc(act ? end : -1);
-        const int emin = wave_min_bc(act ? end : INT_MAX);
+        int emax, emin;
+        wave_maxmin_bc(act ? end : -1, act ? end : INT_MAX, emax, emin);
         PcRow r;
         {
             const int ulo = __builtin_amdgcn_readfirstlane(max(0, i - wl_max));  // min beg
@@ -430,7 +464,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             r.left = gbits(glo, gln + 1);
         }
         if (act) {
-            int h1 = (beg == 0) ? max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) : 0;
+            // h1 = H(i, j-1) entering each group, in the HIGH half (PC_FAST_CHAIN)
+            int h1 = (beg == 0) ? (int)((uint32_t)max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) << 16) : 0;
             int f = 0;
             uint32_t key = 0;
             const uint32_t endw = pack2(end);
@@ -438,6 +473,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             const uint32_t begm2w = pack2(beg - 2);
             pc_row<QMAX>(std::make_integer_sequence<int, NG>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
                          oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg, ctr);
+            h1 = (int)((uint32_t)h1 >> 16);               // H(i, end-1)
             const uint32_t k32 = max(key & 0xffffu, key >> 16);
             const int m = (int)(k32 >> 8), mj = (int)(k32 & 0xffu);
             if (end == qlen) {                    // A.4: j == qlen; h1 = H(i, qlen - 1)

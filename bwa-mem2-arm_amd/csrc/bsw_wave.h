@@ -51,6 +51,20 @@ __device__ __forceinline__ int wave_min_bc(int x)
     return __builtin_amdgcn_readlane(x, 63);
 }
 
+// wave_max_bc(xmax) and wave_min_bc(xmin) in one interleaved chain: each DPP step of one
+// reduction covers the other's data hazard, so no s_nop sits between dependent DPP ops.
+__device__ __forceinline__ void wave_maxmin_bc(int xmax, int xmin, int &omax, int &omin)
+{
+#define BSW_MM_STEP(ctl, rm)                                                                 \
+    xmax = max(xmax, __builtin_amdgcn_update_dpp(INT_MIN, xmax, ctl, rm, 0xf, false));      \
+    xmin = min(xmin, __builtin_amdgcn_update_dpp(INT_MAX, xmin, ctl, rm, 0xf, false));
+    BSW_MM_STEP(0x111, 0xf) BSW_MM_STEP(0x112, 0xf) BSW_MM_STEP(0x114, 0xf)
+    BSW_MM_STEP(0x118, 0xf) BSW_MM_STEP(0x142, 0xa) BSW_MM_STEP(0x143, 0xc)
+#undef BSW_MM_STEP
+    omax = __builtin_amdgcn_readlane(xmax, 63);
+    omin = __builtin_amdgcn_readlane(xmin, 63);
+}
+
 typedef const __attribute__((address_space(1))) void *gptr_t;
 typedef __attribute__((address_space(3))) void *lptr_t;
 

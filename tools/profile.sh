@@ -10,7 +10,7 @@
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 OUT=${OUT:-gpurun_out/prof}
-ARGS=${ARGS:---steps 5 --warmup 1 --no-cpu}
+ARGS=${ARGS:---steps 5 --warmup 1 --no-cpu --no-host-path}
 rm -rf "$OUT"; mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -- python3 bench.py $ARGS > "$OUT/pmc_fetch.log" 2>&1
