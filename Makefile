@@ -16,8 +16,8 @@ SYNTH    := $(LIBDIR)/libbsw_synth.so
 SHIMTEST := $(LIBDIR)/bsw_shim_example
 ORACLE   := oracle/liboracle.so
 
-HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pc.hip $(CSRC)/bsw_wv.hip $(CSRC)/bsw_mate.hip $(CSRC)/bsw_global.hip $(CSRC)/bsw_ext_dev.hip $(CSRC)/bsw_host.cpp $(CSRC)/bsw_ext.cpp
-HIP_HDRS := $(CSRC)/bsw_pool.h $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h
+HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pc.hip $(CSRC)/bsw_wv.hip $(CSRC)/bsw_mate.hip $(CSRC)/bsw_global.hip $(CSRC)/bsw_ext_dev.hip $(CSRC)/bsw_fmi.hip $(CSRC)/bsw_host.cpp $(CSRC)/bsw_ext.cpp
+HIP_HDRS := $(CSRC)/bsw_pool.h $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h include/bsw_fmi.h
 
 all: product synth oracle
 
@@ -46,6 +46,9 @@ $(LIBDIR)/bsw_global.o: $(CSRC)/bsw_global.hip $(HIP_HDRS) | $(LIBDIR)
 $(LIBDIR)/bsw_ext_dev.o: $(CSRC)/bsw_ext_dev.hip $(HIP_HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(LIBDIR)/bsw_fmi.o: $(CSRC)/bsw_fmi.hip $(HIP_HDRS) | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/bsw_host.o: $(CSRC)/bsw_host.cpp $(HIP_HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
@@ -55,14 +58,14 @@ $(LIBDIR)/bsw_ext.o: $(CSRC)/bsw_ext.cpp $(HIP_HDRS) | $(LIBDIR)
 $(LIBDIR)/bsw_batch.o: $(CSRC)/bsw_batch.c include/bsw_batch.h include/bsw.h | $(LIBDIR)
 	gcc $(CFLAGS) -std=c11 -c $< -o $@
 
-$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_batch.o
+$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_batch.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 $(SYNTH): $(CSRC)/bsw_synth.c include/bsw_seqpair.h | $(LIBDIR)
 	gcc $(CFLAGS) -shared -o $@ $<
 
-$(ORACLE): oracle/ksw_ext_ref.c oracle/bsw_sse41.c oracle/ext_ref.c oracle/ksw_align_ref.c oracle/ksw_global_ref.c include/bsw_seqpair.h include/bsw_ext.h
-	gcc $(CFLAGS) -msse4.1 -shared -o $@ oracle/ksw_ext_ref.c oracle/bsw_sse41.c oracle/ext_ref.c oracle/ksw_align_ref.c oracle/ksw_global_ref.c -lpthread
+$(ORACLE): oracle/ksw_ext_ref.c oracle/bsw_sse41.c oracle/ext_ref.c oracle/ksw_align_ref.c oracle/ksw_global_ref.c oracle/fmi_ref.c include/bsw_seqpair.h include/bsw_ext.h
+	gcc $(CFLAGS) -msse4.1 -shared -o $@ oracle/ksw_ext_ref.c oracle/bsw_sse41.c oracle/ext_ref.c oracle/ksw_align_ref.c oracle/ksw_global_ref.c oracle/fmi_ref.c -lpthread
 
 clean:
 	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so $(ORACLE)
@@ -72,7 +75,7 @@ STATSLIB := $(LIBDIR)/libbsw_hip_stats.so
 stats: $(STATSLIB)
 $(LIBDIR)/bsw_pc_stats.o: $(CSRC)/bsw_pc.hip $(HIP_HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DBSW_PC_STATS -c $< -o $@
-$(STATSLIB): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_stats.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_batch.o
+$(STATSLIB): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_stats.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_batch.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 .PHONY: all product synth oracle clean stats

@@ -1,0 +1,677 @@
+// bsw_fmi.hip -- FM-index SMEM seeding on gfx950 (include/bsw_fmi.h).
+//
+// Index (host build, resident in HBM):
+//   T = ref + revcomp(ref), n = |T|; rows r = 0..n of the sorted suffixes of T$ (row 0 = '$').
+//   Suffix array by prefix doubling: one 64-bit LSD radix sort of 27-base keys (base 5 with
+//   '$'/past-the-end = 0, so suffixes that reach '$' inside the key are already unique), then
+//   only the remaining tie groups are re-sorted by rank[i + h], h = 27, 54, 108, ... (ranks =
+//   group starts, refined in place).
+//   Occ blocks: one 64-byte block per 64 BWT rows -- cnt[c] = #c in rows [0, 64b) (uint32) and
+//   bits[c] = one-hot mask of rows 64b + y holding c (bit y) -- so Occ(c, r) = cnt[c] +
+//   popcount(bits[c] & ((1 << (r & 63)) - 1)) is ONE 64-byte load (bwa-mem2's CP_OCC layout with
+//   32-bit counts).  The '$' row has no bit set.
+//
+// Kernel (one lane per read; the FM-index walk is a serial chain of dependent, data-dependent
+// HBM loads, so the GPU's job is to keep ~10^5 such chains in flight, not to vectorise one):
+//   backward extension of (k, l, s) by base a (FMI_search::backwardExt):
+//     k' = count[a] + Occ(a, k), s' = Occ(a, k + s) - Occ(a, k),
+//     l' = l + [k <= sentinel < k + s] + sum_{b > a} (Occ(b, k + s) - Occ(b, k))
+//   forward extension by read base q = backward extension of the swapped interval (l, k, s) by
+//   3 - q, swapped back.  Rows k and k + s share one block whenever s is small (the common
+//   case after a few bases), and then one load serves both.
+//   bwt_smem1a / bwt_seed_strategy1 / mem_collect_intv control flow as in oracle/fmi_ref.c;
+//   the per-read interval vectors (prev / curr) live in HBM scratch laid out [slot][read] (16 B
+//   per entry: k, l, s, end), the output intervals at mems[read * cap + t], sorted in place
+//   by an insertion sort at the end.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <algorithm>
+#include <chrono>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include "../../include/bsw_fmi.h"
+
+namespace {
+
+struct alignas(64) FmiBlock {
+    uint32_t cnt[4];
+    uint32_t pad[4];
+    uint64_t bits[4];
+};
+static_assert(sizeof(FmiBlock) == 64, "one 64-byte block per 64 rows");
+
+struct FmiDev {                      // kernel view of the resident index
+    const FmiBlock *blk;
+    uint32_t count[5];
+    uint32_t sentinel;
+    uint32_t n;                      // |T|
+};
+
+struct MemOpt {
+    int32_t min_seed_len, split_width, max_mem_intv, split_len;
+};
+
+// ---------------------------------------------------------------- device: index queries
+
+__device__ __forceinline__ void load_block(const FmiBlock *b, uint4 &cnt, ulonglong2 &b01, ulonglong2 &b23)
+{
+    const uint4 *p = reinterpret_cast<const uint4 *>(b);
+    cnt = p[0];
+    b01 = reinterpret_cast<const ulonglong2 *>(b)[2];
+    b23 = reinterpret_cast<const ulonglong2 *>(b)[3];
+}
+
+__device__ __forceinline__ uint32_t occ_of(const uint4 &cnt, const ulonglong2 &b01, const ulonglong2 &b23,
+                                           int c, uint64_t mask)
+{
+    const uint32_t cc = c == 0 ? cnt.x : c == 1 ? cnt.y : c == 2 ? cnt.z : cnt.w;
+    const uint64_t bb = c == 0 ? b01.x : c == 1 ? b01.y : c == 2 ? b23.x : b23.y;
+    return cc + (uint32_t)__popcll(bb & mask);
+}
+
+struct Iv {
+    uint32_t k, l, s;
+};
+
+// FMI_search::backwardExt restricted to the one base the caller keeps
+__device__ __forceinline__ Iv backward_ext(const FmiDev &f, Iv in, int a)
+{
+    const uint32_t sp = in.k, ep = in.k + in.s;
+    uint4 c0, c1;
+    ulonglong2 a01, a23, e01, e23;
+    load_block(f.blk + (sp >> 6), c0, a01, a23);
+    if ((ep >> 6) == (sp >> 6)) {
+        c1 = c0; e01 = a01; e23 = a23;
+    } else {
+        load_block(f.blk + (ep >> 6), c1, e01, e23);
+    }
+    const uint64_t ms = (sp & 63) ? (~0ull >> (64 - (sp & 63))) : 0ull;
+    const uint64_t me = (ep & 63) ? (~0ull >> (64 - (ep & 63))) : 0ull;
+    uint32_t osp[4], oep[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        osp[b] = occ_of(c0, a01, a23, b, ms);
+        oep[b] = occ_of(c1, e01, e23, b, me);
+    }
+    uint32_t l = in.l + ((sp <= f.sentinel && ep > f.sentinel) ? 1u : 0u);
+    // l[3] = l + sent; l[b] = l[b + 1] + s[b + 1]
+#pragma unroll
+    for (int b = 3; b > 0; --b)
+        if (b > a) l += oep[b] - osp[b];
+    Iv o;
+    const uint32_t ca = a == 0 ? f.count[0] : a == 1 ? f.count[1] : a == 2 ? f.count[2] : f.count[3];
+    const uint32_t oa = a == 0 ? osp[0] : a == 1 ? osp[1] : a == 2 ? osp[2] : osp[3];
+    const uint32_t ea = a == 0 ? oep[0] : a == 1 ? oep[1] : a == 2 ? oep[2] : oep[3];
+    o.k = ca + oa;
+    o.s = ea - oa;
+    o.l = l;
+    return o;
+}
+
+__device__ __forceinline__ Iv forward_ext(const FmiDev &f, Iv in, int q)   // q = read base 0..3
+{
+    Iv sw = {in.l, in.k, in.s};
+    Iv o = backward_ext(f, sw, 3 - q);
+    return Iv{o.l, o.k, o.s};
+}
+
+__device__ __forceinline__ Iv set_intv(const FmiDev &f, int c)
+{
+    const uint32_t k = f.count[c], k1 = f.count[c + 1], l = f.count[3 - c];
+    return Iv{k, l, k1 - k};
+}
+
+// ---------------------------------------------------------------- device: per-read passes
+
+struct Lane {
+    const uint8_t *q;
+    int len;
+    uint4 *sa, *sb;          // scratch vectors, element j at [j * stride]
+    size_t stride;
+    int scap;                // scratch entries per vector
+    bsw_bwtintv_t *out;      // this read's output slots
+    int cap;
+    int nout;                // intervals produced (may exceed cap)
+    int overflow;            // scratch overflow (cannot happen for scap >= len + 1)
+};
+
+__device__ __forceinline__ void push_out(Lane &L, Iv v, uint32_t start, uint32_t end)
+{
+    if (L.nout < L.cap) {
+        bsw_bwtintv_t o;
+        o.x[0] = v.k; o.x[1] = v.l; o.x[2] = v.s;
+        o.info = ((uint64_t)start << 32) | end;
+        L.out[L.nout] = o;
+    }
+    ++L.nout;
+}
+
+// bwt_smem1a with max_intv = 0 (bwt_smem1): SMEMs overlapping x with occurrence >= min_intv;
+// those of length >= keep_len go to the output.  Returns the next x.
+__device__ int smem1(const FmiDev &f, Lane &L, int x, uint32_t min_intv, int keep_len)
+{
+    const uint8_t *q = L.q;
+    const int len = L.len;
+    const int qx = q[x];
+    if (qx > 3) return x + 1;
+    if (min_intv < 1) min_intv = 1;
+    uint4 *curr = L.sa, *prev = L.sb;
+    const size_t st = L.stride;
+    Iv ik = set_intv(f, qx);
+    uint32_t ikend = (uint32_t)(x + 1);
+    int nc = 0, i;
+    for (i = x + 1; i < len; ++i) {                      // forward search
+        const int qi = q[i];
+        if (qi < 4) {
+            const Iv ok = forward_ext(f, ik, qi);
+            if (ok.s != ik.s) {
+                if (nc < L.scap) curr[(size_t)nc * st] = make_uint4(ik.k, ik.l, ik.s, ikend);
+                else L.overflow = 1;
+                ++nc;
+                if (ok.s < min_intv) break;
+            }
+            ik = ok; ikend = (uint32_t)(i + 1);
+        } else {
+            if (nc < L.scap) curr[(size_t)nc * st] = make_uint4(ik.k, ik.l, ik.s, ikend);
+            else L.overflow = 1;
+            ++nc;
+            break;
+        }
+    }
+    if (i == len) {
+        if (nc < L.scap) curr[(size_t)nc * st] = make_uint4(ik.k, ik.l, ik.s, ikend);
+        else L.overflow = 1;
+        ++nc;
+    }
+    nc = min(nc, L.scap);
+    // upstream reverses curr (longest matches first); here prev is read back to front once
+    const int ret = (int)curr[(size_t)(nc - 1) * st].w;
+    { uint4 *t = curr; curr = prev; prev = t; }
+    int np = nc;
+    bool rev = true;
+    int nmem = 0;
+    uint32_t last_start = 0;
+    for (i = x - 1; i >= -1; --i) {                      // backward search
+        const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+        nc = 0;
+        uint32_t last_cs = 0;
+        for (int j = 0; j < np; ++j) {
+            const uint4 pv = prev[(size_t)(rev ? np - 1 - j : j) * st];
+            const Iv p = {pv.x, pv.y, pv.z};
+            Iv ok = {0, 0, 0};
+            if (c >= 0) ok = backward_ext(f, p, c);
+            if (c < 0 || ok.s < min_intv) {
+                if (nc == 0) {
+                    if (nmem == 0 || (uint32_t)(i + 1) < last_start) {
+                        last_start = (uint32_t)(i + 1);
+                        ++nmem;
+                        if ((int)(pv.w - last_start) >= keep_len) push_out(L, p, last_start, pv.w);
+                    }
+                }
+            } else if (nc == 0 || ok.s != last_cs) {
+                if (nc < L.scap) curr[(size_t)nc * st] = make_uint4(ok.k, ok.l, ok.s, pv.w);
+                else L.overflow = 1;
+                ++nc;
+                last_cs = ok.s;
+            }
+        }
+        if (nc == 0) break;
+        np = min(nc, L.scap);
+        rev = false;
+        { uint4 *t = curr; curr = prev; prev = t; }
+    }
+    return ret;
+}
+
+// bwt_seed_strategy1
+__device__ int seed_strategy1(const FmiDev &f, Lane &L, int x, int min_len, uint32_t max_intv)
+{
+    const uint8_t *q = L.q;
+    const int qx = q[x];
+    if (qx > 3) return x + 1;
+    Iv ik = set_intv(f, qx);
+    for (int i = x + 1; i < L.len; ++i) {
+        const int qi = q[i];
+        if (qi < 4) {
+            const Iv ok = forward_ext(f, ik, qi);
+            if (ok.s < max_intv && i - x >= min_len) {
+                if (ok.s > 0) push_out(L, ok, (uint32_t)x, (uint32_t)(i + 1));
+                return i + 1;
+            }
+            ik = ok;
+        } else {
+            return i + 1;
+        }
+    }
+    return L.len;
+}
+
+__device__ __forceinline__ bool iv_less(const bsw_bwtintv_t &a, const bsw_bwtintv_t &b)
+{
+    if (a.info != b.info) return a.info < b.info;
+    if (a.x[0] != b.x[0]) return a.x[0] < b.x[0];
+    if (a.x[2] != b.x[2]) return a.x[2] < b.x[2];
+    return a.x[1] < b.x[1];
+}
+
+__global__ __launch_bounds__(64) void smem_kernel(const FmiDev f, const MemOpt opt, const uint8_t *__restrict__ reads,
+                                                  const int64_t *__restrict__ read_off,
+                                                  const int32_t *__restrict__ read_len, int32_t n0, int32_t n,
+                                                  uint4 *__restrict__ scratch, int32_t scap,
+                                                  bsw_bwtintv_t *__restrict__ mems, int32_t cap,
+                                                  int32_t *__restrict__ n_mems, int32_t *__restrict__ err)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;    // lane within this chunk
+    if (t >= n) return;
+    const int r = n0 + t;                                    // read index
+    Lane L;
+    L.q = reads + read_off[r];
+    L.len = read_len[r];
+    L.stride = (size_t)n;
+    L.sa = scratch + t;
+    L.sb = scratch + (size_t)scap * n + t;
+    L.scap = scap;
+    L.out = mems + (size_t)r * cap;
+    L.cap = cap;
+    L.nout = 0;
+    L.overflow = 0;
+    if (L.len < 0 || L.len > scap - 1) {
+        atomicOr(err, 2);
+        n_mems[r] = 0;
+        return;
+    }
+    // pass 1: SMEMs
+    int x = 0;
+    while (x < L.len) {
+        if (L.q[x] < 4) x = smem1(f, L, x, 1, opt.min_seed_len);
+        else ++x;
+    }
+    // pass 2: re-seeding inside long SMEMs of few occurrences
+    const int old_n = min(L.nout, cap);
+    for (int k = 0; k < old_n; ++k) {
+        const bsw_bwtintv_t p = L.out[k];
+        const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
+        if (end - start < opt.split_len || p.x[2] > (uint64_t)opt.split_width) continue;
+        smem1(f, L, (start + end) >> 1, (uint32_t)p.x[2] + 1, opt.min_seed_len);
+    }
+    // pass 3: LAST-like seeds
+    if (opt.max_mem_intv > 0) {
+        x = 0;
+        while (x < L.len) {
+            if (L.q[x] < 4) x = seed_strategy1(f, L, x, opt.min_seed_len, (uint32_t)opt.max_mem_intv);
+            else ++x;
+        }
+    }
+    // sort by (info, k, s, l)
+    const int m = min(L.nout, cap);
+    for (int a = 1; a < m; ++a) {
+        const bsw_bwtintv_t v = L.out[a];
+        int b = a - 1;
+        while (b >= 0 && iv_less(v, L.out[b])) {
+            L.out[b + 1] = L.out[b];
+            --b;
+        }
+        L.out[b + 1] = v;
+    }
+    n_mems[r] = L.nout;
+    if (L.nout > cap) atomicOr(err, 1);
+    if (L.overflow) atomicOr(err, 2);
+}
+
+__global__ void sa_kernel(const uint32_t *__restrict__ sa, uint32_t nrows, const uint64_t *__restrict__ k,
+                          int64_t n, int64_t *__restrict__ pos)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t r = k[i];
+    pos[i] = r < nrows ? (int64_t)sa[r] : -1;
+}
+
+// ---------------------------------------------------------------- host: suffix array
+
+// LSD radix sort of (key, idx) by key, 16-bit digits over the bits that can be set
+void radix_sort64(std::vector<uint64_t> &key, std::vector<uint32_t> &idx, int bits)
+{
+    const size_t n = key.size();
+    std::vector<uint64_t> k2(n);
+    std::vector<uint32_t> i2(n);
+    std::vector<size_t> cnt(1 << 16);
+    for (int sh = 0; sh < bits; sh += 16) {
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (size_t i = 0; i < n; ++i) cnt[(key[i] >> sh) & 0xffff]++;
+        size_t acc = 0;
+        for (auto &c : cnt) { const size_t t = c; c = acc; acc += t; }
+        for (size_t i = 0; i < n; ++i) {
+            const size_t d = cnt[(key[i] >> sh) & 0xffff]++;
+            k2[d] = key[i];
+            i2[d] = idx[i];
+        }
+        key.swap(k2);
+        idx.swap(i2);
+    }
+}
+
+// suffix array of T$ (t = codes 0..3, length n); sa has n + 1 entries
+void build_sa(const uint8_t *t, uint32_t n, std::vector<uint32_t> &sa)
+{
+    const uint32_t N = n + 1;
+    constexpr int H0 = 27;                                   // 5^27 < 2^63
+    std::vector<uint64_t> key(N);
+    {
+        uint64_t p26 = 1;
+        for (int d = 0; d < H0 - 1; ++d) p26 *= 5;
+        uint64_t k = 0;
+        for (int64_t i = (int64_t)N - 1; i >= 0; --i) {      // key[i] = c(i) 5^26 + key[i + 1] / 5
+            const uint64_t c = (uint64_t)i < n ? (uint64_t)t[i] + 1 : 0;
+            k = c * p26 + k / 5;
+            key[i] = k;
+        }
+    }
+    sa.resize(N);
+    for (uint32_t i = 0; i < N; ++i) sa[i] = i;
+    radix_sort64(key, sa, 64);
+    std::vector<uint32_t> rank(N);
+    std::vector<std::pair<uint32_t, uint32_t>> groups;       // [start, end) tie groups
+    for (uint32_t j = 0; j < N;) {
+        uint32_t e = j + 1;
+        while (e < N && key[e] == key[j]) ++e;
+        for (uint32_t u = j; u < e; ++u) rank[sa[u]] = j;
+        if (e - j > 1) groups.emplace_back(j, e);
+        j = e;
+    }
+    std::vector<uint64_t>().swap(key);
+    std::vector<std::pair<uint32_t, uint32_t>> tmp, next;
+    for (uint64_t h = H0; !groups.empty(); h *= 2) {
+        next.clear();
+        for (const auto &g : groups) {
+            tmp.clear();
+            for (uint32_t u = g.first; u < g.second; ++u) {
+                const uint64_t p = (uint64_t)sa[u] + h;     // < N inside a tie group ('$' is unique)
+                tmp.emplace_back(p < N ? rank[p] : 0u, sa[u]);
+            }
+            std::sort(tmp.begin(), tmp.end());
+            for (uint32_t u = 0; u < tmp.size(); ++u) sa[g.first + u] = tmp[u].second;
+            for (uint32_t u = 0; u < tmp.size();) {
+                uint32_t e = u + 1;
+                while (e < tmp.size() && tmp[e].first == tmp[u].first) ++e;
+                for (uint32_t v = u; v < e; ++v) rank[tmp[v].second] = g.first + u;
+                if (e - u > 1) next.emplace_back(g.first + u, g.first + e);
+                u = e;
+            }
+        }
+        groups.swap(next);
+    }
+}
+
+}  // namespace
+
+struct bsw_fmi {
+    int device = 0;
+    uint32_t n = 0;
+    FmiDev dv{};
+    FmiBlock *d_blk = nullptr;
+    uint32_t *d_sa = nullptr;
+    std::vector<uint32_t> sa;                 // host copies (tests, bwt_sa on the host side)
+    std::vector<uint8_t> bwt;
+    int64_t count[5] = {0, 0, 0, 0, 0};
+    int64_t dev_bytes = 0;
+    float build_s = 0, kernel_ms = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint4 *d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+    int32_t *d_err = nullptr;
+    void *h_stage = nullptr;                  // host-buffer calls: device copies
+    std::mutex mu;                            // one seeding call at a time per index
+};
+
+namespace {
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? BSW_OK : (e == hipErrorOutOfMemory ? BSW_E_NOMEM : BSW_E_HIP); }
+
+int run_collect(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads, const int64_t *d_off,
+                const int32_t *d_len, int32_t n, int32_t max_len, bsw_bwtintv_t *d_mems, int32_t cap,
+                int32_t *d_cnt, hipStream_t s)
+{
+    MemOpt mo;
+    mo.min_seed_len = opt->min_seed_len;
+    mo.split_width = opt->split_width;
+    mo.max_mem_intv = opt->max_mem_intv;
+    mo.split_len = (int)(opt->min_seed_len * opt->split_factor + .499);
+    const int32_t scap = max_len + 1;
+    // chunk so the two scratch vectors stay within ~4 GB
+    const size_t per_read = (size_t)2 * scap * sizeof(uint4);
+    const int32_t chunk = (int32_t)std::max<size_t>(64, std::min<size_t>((size_t)n, ((size_t)4 << 30) / per_read));
+    const size_t need = per_read * (size_t)std::min(chunk, n);
+    if (need > f->scratch_bytes) {
+        if (f->d_scratch) (void)hipFree(f->d_scratch);
+        f->d_scratch = nullptr;
+        f->scratch_bytes = 0;
+        if (hipMalloc(&f->d_scratch, need) != hipSuccess) return BSW_E_NOMEM;
+        f->scratch_bytes = need;
+    }
+    if (hipMemsetAsync(f->d_err, 0, sizeof(int32_t), s) != hipSuccess) return BSW_E_HIP;
+    (void)hipEventRecord(f->ev0, s);
+    for (int32_t n0 = 0; n0 < n; n0 += chunk) {
+        const int32_t m = std::min(chunk, n - n0);
+        hipLaunchKernelGGL(smem_kernel, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, f->dv, mo, d_reads, d_off,
+                           d_len, n0, m, f->d_scratch, scap, d_mems, cap, d_cnt, f->d_err);
+        if (hipGetLastError() != hipSuccess) return BSW_E_HIP;
+    }
+    (void)hipEventRecord(f->ev1, s);
+    int32_t herr = 0;
+    if (hipMemcpyAsync(&herr, f->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess) return BSW_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return BSW_E_HIP;
+    (void)hipEventElapsedTime(&f->kernel_ms, f->ev0, f->ev1);
+    return herr ? BSW_E_RANGE : BSW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void bsw_mem_opt_default(bsw_mem_opt_t *opt)
+{
+    opt->min_seed_len = 19;
+    opt->split_width = 10;
+    opt->max_mem_intv = 20;
+    opt->split_factor = 1.5f;
+}
+
+int bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **out)
+{
+    if (!out || (!ref && ref_len > 0) || ref_len < 0) return BSW_E_INVAL;
+    *out = nullptr;
+    if (2 * ref_len + 2 >= (int64_t)UINT32_MAX) return BSW_E_RANGE;
+    for (int64_t i = 0; i < ref_len; ++i)
+        if (ref[i] > 3) return BSW_E_INVAL;
+    int ndev = 0;
+    if (device >= 0 && (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev)) return BSW_E_NODEV;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t n = (uint32_t)(2 * ref_len), N = n + 1;
+    std::vector<uint8_t> t(n);
+    for (int64_t i = 0; i < ref_len; ++i) {
+        t[i] = ref[i];
+        t[n - 1 - i] = (uint8_t)(3 - ref[i]);
+    }
+    bsw_fmi_t *f = new bsw_fmi_t;
+    f->device = device;
+    f->n = n;
+    build_sa(t.data(), n, f->sa);
+    f->bwt.resize(N);
+    uint32_t sentinel = 0;
+    for (uint32_t r = 0; r < N; ++r) {
+        const uint32_t p = f->sa[r];
+        f->bwt[r] = p == 0 ? 4 : t[p - 1];
+        if (p == 0) sentinel = r;
+    }
+    const size_t nb = (size_t)(N >> 6) + 1;                  // covers row N (= k + s at most)
+    std::vector<FmiBlock> blk(nb);
+    uint32_t run[4] = {0, 0, 0, 0};
+    for (size_t b = 0; b < nb; ++b) {
+        FmiBlock &B = blk[b];
+        memset(&B, 0, sizeof(B));
+        for (int c = 0; c < 4; ++c) B.cnt[c] = run[c];
+        for (uint32_t y = 0; y < 64; ++y) {
+            const size_t r = b * 64 + y;
+            if (r >= N) break;
+            const uint8_t c = f->bwt[r];
+            if (c < 4) { B.bits[c] |= 1ull << y; run[c]++; }
+        }
+    }
+    f->count[0] = 1;
+    for (int c = 0; c < 4; ++c) f->count[c + 1] = f->count[c] + run[c];
+    f->build_s = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
+    f->dv.sentinel = sentinel;
+    f->dv.n = n;
+    if (device < 0) {                        // host-only index (tests of the builder): no HBM copy
+        *out = f;
+        return BSW_OK;
+    }
+    int rc = BSW_OK;
+    if ((rc = hip_rc(hipSetDevice(device))) == BSW_OK &&
+        (rc = hip_rc(hipMalloc(&f->d_blk, nb * sizeof(FmiBlock)))) == BSW_OK &&
+        (rc = hip_rc(hipMalloc(&f->d_sa, (size_t)N * sizeof(uint32_t)))) == BSW_OK &&
+        (rc = hip_rc(hipMalloc(&f->d_err, sizeof(int32_t)))) == BSW_OK &&
+        (rc = hip_rc(hipMemcpy(f->d_blk, blk.data(), nb * sizeof(FmiBlock), hipMemcpyHostToDevice))) == BSW_OK &&
+        (rc = hip_rc(hipMemcpy(f->d_sa, f->sa.data(), (size_t)N * sizeof(uint32_t), hipMemcpyHostToDevice))) == BSW_OK &&
+        (rc = hip_rc(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking))) == BSW_OK &&
+        (rc = hip_rc(hipEventCreate(&f->ev0))) == BSW_OK && (rc = hip_rc(hipEventCreate(&f->ev1))) == BSW_OK) {
+        f->dev_bytes = (int64_t)(nb * sizeof(FmiBlock) + (size_t)N * sizeof(uint32_t));
+        f->dv.blk = f->d_blk;
+        for (int c = 0; c < 5; ++c) f->dv.count[c] = (uint32_t)f->count[c];
+        *out = f;
+        return BSW_OK;
+    }
+    bsw_fmi_destroy(f);
+    return rc;
+}
+
+void bsw_fmi_destroy(bsw_fmi_t *f)
+{
+    if (!f) return;
+    (void)hipSetDevice(f->device);
+    if (f->d_blk) (void)hipFree(f->d_blk);
+    if (f->d_sa) (void)hipFree(f->d_sa);
+    if (f->d_err) (void)hipFree(f->d_err);
+    if (f->d_scratch) (void)hipFree(f->d_scratch);
+    if (f->ev0) (void)hipEventDestroy(f->ev0);
+    if (f->ev1) (void)hipEventDestroy(f->ev1);
+    if (f->stream) (void)hipStreamDestroy(f->stream);
+    delete f;
+}
+
+int bsw_fmi_get_info(const bsw_fmi_t *f, bsw_fmi_info_t *out)
+{
+    if (!f || !out) return BSW_E_INVAL;
+    out->n = f->n;
+    out->sentinel = f->dv.sentinel;
+    for (int c = 0; c < 5; ++c) out->count[c] = f->count[c];
+    out->device_bytes = f->dev_bytes;
+    out->build_s = f->build_s;
+    return BSW_OK;
+}
+
+int bsw_fmi_copy_sa(const bsw_fmi_t *f, int64_t *sa)
+{
+    if (!f || !sa) return BSW_E_INVAL;
+    for (size_t r = 0; r < f->sa.size(); ++r) sa[r] = f->sa[r];
+    return BSW_OK;
+}
+
+int bsw_fmi_copy_bwt(const bsw_fmi_t *f, uint8_t *bwt)
+{
+    if (!f || !bwt) return BSW_E_INVAL;
+    memcpy(bwt, f->bwt.data(), f->bwt.size());
+    return BSW_OK;
+}
+
+int bsw_mem_collect_intv_device(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads,
+                                const int64_t *d_read_off, const int32_t *d_read_len, int32_t n, int32_t max_len,
+                                bsw_bwtintv_t *d_mems, int32_t cap, int32_t *d_n_mems, void *stream)
+{
+    if (!f || !opt || n < 0 || cap < 0 || max_len < 0 || max_len > BSW_MAX_LEN) return BSW_E_INVAL;
+    if (f->device < 0) return BSW_E_NODEV;
+    if (n == 0) return BSW_OK;
+    if (!d_reads || !d_read_off || !d_read_len || !d_n_mems || (!d_mems && cap > 0)) return BSW_E_INVAL;
+    if (opt->min_seed_len < 1 || opt->split_width < 0 || opt->max_mem_intv < 0) return BSW_E_INVAL;
+    std::lock_guard<std::mutex> lk(f->mu);
+    if (hipSetDevice(f->device) != hipSuccess) return BSW_E_HIP;
+    hipStream_t s = stream ? (hipStream_t)stream : f->stream;
+    return run_collect(f, opt, d_reads, d_read_off, d_read_len, n, max_len, d_mems, cap, d_n_mems, s);
+}
+
+int bsw_mem_collect_intv(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *reads, const int64_t *read_off,
+                         const int32_t *read_len, int32_t n, bsw_bwtintv_t *mems, int32_t cap, int32_t *n_mems)
+{
+    if (!f || !opt || n < 0 || cap < 0) return BSW_E_INVAL;
+    if (f->device < 0) return BSW_E_NODEV;
+    if (n == 0) return BSW_OK;
+    if (!reads || !read_off || !read_len || !n_mems || (!mems && cap > 0)) return BSW_E_INVAL;
+    // pack the reads the calls address into one contiguous device buffer
+    std::vector<int64_t> off(n);
+    int64_t tot = 0;
+    int32_t max_len = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        if (read_len[i] < 0 || read_len[i] > BSW_MAX_LEN || read_off[i] < 0) return BSW_E_RANGE;
+        off[i] = tot;
+        tot += read_len[i];
+        max_len = std::max(max_len, read_len[i]);
+    }
+    std::vector<uint8_t> buf((size_t)std::max<int64_t>(tot, 1));
+    for (int32_t i = 0; i < n; ++i) memcpy(buf.data() + off[i], reads + read_off[i], (size_t)read_len[i]);
+    std::lock_guard<std::mutex> lk(f->mu);
+    if (hipSetDevice(f->device) != hipSuccess) return BSW_E_HIP;
+    uint8_t *d_reads = nullptr;
+    int64_t *d_off = nullptr;
+    int32_t *d_len = nullptr, *d_cnt = nullptr;
+    bsw_bwtintv_t *d_mems = nullptr;
+    int rc = BSW_OK;
+    hipStream_t s = f->stream;
+    if ((rc = hip_rc(hipMalloc(&d_reads, buf.size()))) == BSW_OK &&
+        (rc = hip_rc(hipMalloc(&d_off, sizeof(int64_t) * n))) == BSW_OK &&
+        (rc = hip_rc(hipMalloc(&d_len, sizeof(int32_t) * n))) == BSW_OK &&
+        (rc = hip_rc(hipMalloc(&d_cnt, sizeof(int32_t) * n))) == BSW_OK &&
+        (rc = hip_rc(hipMalloc(&d_mems, sizeof(bsw_bwtintv_t) * ((size_t)n * cap + 1)))) == BSW_OK &&
+        (rc = hip_rc(hipMemcpyAsync(d_reads, buf.data(), buf.size(), hipMemcpyHostToDevice, s))) == BSW_OK &&
+        (rc = hip_rc(hipMemcpyAsync(d_off, off.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, s))) == BSW_OK &&
+        (rc = hip_rc(hipMemcpyAsync(d_len, read_len, sizeof(int32_t) * n, hipMemcpyHostToDevice, s))) == BSW_OK) {
+        const int krc = run_collect(f, opt, d_reads, d_off, d_len, n, max_len, d_mems, cap, d_cnt, s);
+        if (krc == BSW_OK || krc == BSW_E_RANGE) {
+            if ((rc = hip_rc(hipMemcpyAsync(n_mems, d_cnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s))) == BSW_OK &&
+                (cap == 0 || (rc = hip_rc(hipMemcpyAsync(mems, d_mems, sizeof(bsw_bwtintv_t) * (size_t)n * cap,
+                                                         hipMemcpyDeviceToHost, s))) == BSW_OK) &&
+                (rc = hip_rc(hipStreamSynchronize(s))) == BSW_OK)
+                rc = krc;
+        } else {
+            rc = krc;
+        }
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(d_reads); (void)hipFree(d_off); (void)hipFree(d_len); (void)hipFree(d_cnt); (void)hipFree(d_mems);
+    return rc;
+}
+
+int bsw_fmi_sa_device(bsw_fmi_t *f, const uint64_t *d_k, int64_t n, int64_t *d_pos, void *stream)
+{
+    if (!f || n < 0 || (n > 0 && (!d_k || !d_pos))) return BSW_E_INVAL;
+    if (f->device < 0) return BSW_E_NODEV;
+    if (n == 0) return BSW_OK;
+    if (hipSetDevice(f->device) != hipSuccess) return BSW_E_HIP;
+    hipStream_t s = stream ? (hipStream_t)stream : f->stream;
+    hipLaunchKernelGGL(sa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, f->d_sa, f->n + 1, d_k, n, d_pos);
+    if (hipGetLastError() != hipSuccess) return BSW_E_HIP;
+    return hipStreamSynchronize(s) == hipSuccess ? BSW_OK : BSW_E_HIP;
+}
+
+int bsw_fmi_last_kernel_ms(const bsw_fmi_t *f, float *ms)
+{
+    if (!f || !ms) return BSW_E_INVAL;
+    *ms = f->kernel_ms;
+    return BSW_OK;
+}
+
+}  // extern "C"
+

@@ -33,7 +33,10 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
                "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats",
                "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
                "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option",
-               "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats")
+               "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats",
+               "bsw_mem_opt_default", "bsw_fmi_build", "bsw_fmi_destroy", "bsw_fmi_get_info", "bsw_fmi_copy_sa",
+               "bsw_fmi_copy_bwt", "bsw_mem_collect_intv", "bsw_mem_collect_intv_device", "bsw_fmi_sa_device",
+               "bsw_fmi_last_kernel_ms")
 
 # include/bsw.h engine options (bsw_set_option)
 OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK, OPT_LONG = 1, 2, 3, 4, 5, 6, 7
@@ -126,12 +129,25 @@ def hip_lib():
         L.bsw_chain2aln.argtypes = [P, P, P, ctypes.c_int64, P, P, P, ctypes.c_int32, P, P, P, ctypes.c_int32, P, P]
         L.bsw_chain2aln_device.argtypes = [P, P, P, P, P, ctypes.c_int32, P, P, P, ctypes.c_int32, P, P]
         L.bsw_chain_last_stats.argtypes = [P, P]
+        L.bsw_mem_opt_default.argtypes = [P]
+        L.bsw_fmi_build.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(P)]
+        L.bsw_fmi_destroy.argtypes = [P]
+        L.bsw_fmi_get_info.argtypes = [P, P]
+        L.bsw_fmi_copy_sa.argtypes = [P, P]
+        L.bsw_fmi_copy_bwt.argtypes = [P, P]
+        L.bsw_mem_collect_intv.argtypes = [P, P, P, P, P, ctypes.c_int32, P, ctypes.c_int32, P]
+        L.bsw_mem_collect_intv_device.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int32, P, ctypes.c_int32,
+                                                  P, P]
+        L.bsw_fmi_sa_device.argtypes = [P, P, ctypes.c_int64, P, P]
+        L.bsw_fmi_last_kernel_ms.argtypes = [P, P]
         for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
                   "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
                   "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option",
-               "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats"):
+               "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats",
+                  "bsw_fmi_build", "bsw_fmi_get_info", "bsw_fmi_copy_sa", "bsw_fmi_copy_bwt", "bsw_mem_collect_intv",
+                  "bsw_mem_collect_intv_device", "bsw_fmi_sa_device", "bsw_fmi_last_kernel_ms"):
             getattr(L, f).restype = ctypes.c_int
         _hip = L
     return _hip
@@ -588,3 +604,94 @@ def synth_globals(ref: np.ndarray, n: int, base: int = 0, cfg: GlobalsCfg | None
     if r < 0:
         raise BswError("bsw_synth_globals: reference too short for the read length")
     return pairs, qer
+
+
+# ---- include/bsw_fmi.h: FM-index SMEM seeding
+
+BWTINTV_DTYPE = np.dtype([("k", "<u8"), ("l", "<u8"), ("s", "<u8"), ("info", "<u8")])   # bsw_bwtintv_t
+assert BWTINTV_DTYPE.itemsize == 32
+
+
+class MemOpt(ctypes.Structure):
+    _fields_ = [("min_seed_len", ctypes.c_int32), ("split_width", ctypes.c_int32),
+                ("max_mem_intv", ctypes.c_int32), ("split_factor", ctypes.c_float)]
+
+
+class FmiInfo(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("sentinel", ctypes.c_int64), ("count", ctypes.c_int64 * 5),
+                ("device_bytes", ctypes.c_int64), ("build_s", ctypes.c_float)]
+
+
+def mem_opt(**kw) -> MemOpt:
+    o = MemOpt()
+    hip_lib().bsw_mem_opt_default(ctypes.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+class Fmi:
+    """One resident FM-index (bsw_fmi_t) of ref + reverse-complement(ref) on `device`."""
+
+    def __init__(self, ref: np.ndarray, device: int = 0):
+        self.ref = np.ascontiguousarray(ref, dtype=np.uint8)
+        self._f = ctypes.c_void_p()
+        _check(hip_lib().bsw_fmi_build(_ptr(self.ref), len(self.ref), device, ctypes.byref(self._f)))
+
+    def close(self):
+        if self._f:
+            hip_lib().bsw_fmi_destroy(self._f)
+            self._f = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> FmiInfo:
+        i = FmiInfo()
+        _check(hip_lib().bsw_fmi_get_info(self._f, ctypes.byref(i)))
+        return i
+
+    def sa(self) -> np.ndarray:
+        a = np.zeros(self.info().n + 1, dtype=np.int64)
+        _check(hip_lib().bsw_fmi_copy_sa(self._f, _ptr(a)))
+        return a
+
+    def bwt(self) -> np.ndarray:
+        a = np.zeros(self.info().n + 1, dtype=np.uint8)
+        _check(hip_lib().bsw_fmi_copy_bwt(self._f, _ptr(a)))
+        return a
+
+    def collect_intv(self, reads, read_off, read_len, cap: int = 256, opt: MemOpt | None = None, strict=True):
+        """bsw_mem_collect_intv (host buffers) -> (intervals [n, cap], counts [n])"""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        read_off = np.ascontiguousarray(read_off, dtype=np.int64)
+        read_len = np.ascontiguousarray(read_len, dtype=np.int32)
+        n = len(read_len)
+        out = np.zeros((n, cap), dtype=BWTINTV_DTYPE)
+        cnt = np.zeros(n, dtype=np.int32)
+        o = opt if opt is not None else mem_opt()
+        rc = hip_lib().bsw_mem_collect_intv(self._f, ctypes.byref(o), _ptr(reads), _ptr(read_off), _ptr(read_len),
+                                            n, _ptr(out), cap, _ptr(cnt))
+        if strict or rc != -34:
+            _check(rc)
+        return out, cnt
+
+    def collect_intv_device(self, d_reads: int, d_off: int, d_len: int, n: int, max_len: int, d_mems: int, cap: int,
+                            d_cnt: int, opt: MemOpt | None = None, stream: int = 0) -> int:
+        o = opt if opt is not None else mem_opt()
+        return hip_lib().bsw_mem_collect_intv_device(self._f, ctypes.byref(o), ctypes.c_void_p(d_reads),
+                                                     ctypes.c_void_p(d_off), ctypes.c_void_p(d_len), n, max_len,
+                                                     ctypes.c_void_p(d_mems), cap, ctypes.c_void_p(d_cnt),
+                                                     ctypes.c_void_p(stream or None))
+
+    def sa_device(self, d_k: int, n: int, d_pos: int, stream: int = 0):
+        _check(hip_lib().bsw_fmi_sa_device(self._f, ctypes.c_void_p(d_k), n, ctypes.c_void_p(d_pos),
+                                           ctypes.c_void_p(stream or None)))
+
+    def last_kernel_ms(self) -> float:
+        v = ctypes.c_float()
+        _check(hip_lib().bsw_fmi_last_kernel_ms(self._f, ctypes.byref(v)))
+        return v.value

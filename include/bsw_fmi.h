@@ -1,0 +1,101 @@
+/*
+ * bsw_fmi.h -- FM-index SMEM seeding on the GPU (second half).
+ *
+ * Replaces the seeding half of upstream bwa-mem2's per-read pipeline (the reference names it
+ * as 80% of runtime, PHASE4_SEEDING_ANALYSIS.md:32-66): FMI_search::backwardExt /
+ * getSMEMsOnePosOneThread / getSMEMsAllPosOneThread / bwtSeedStrategyAllPosOneThread in
+ * src/FMI_search.cpp and mem_collect_intv in src/bwamem.cpp [UPSTREAM-RECALL; the reference
+ * holds no source of them].  Semantics = lh3/bwa's bwt_smem1a + bwt_seed_strategy1 +
+ * mem_collect_intv, which bwa-mem2 documents as output-identical:
+ *
+ *   pass 1  x = 0; while x < len: x = smem1(x, min_intv = 1) keeping SMEMs of >= min_seed_len
+ *   pass 2  for every pass-1 SMEM of length >= min_seed_len * split_factor (+.499, truncated)
+ *           and occurrence s <= split_width: smem1((start + end) >> 1, min_intv = s + 1)
+ *   pass 3  (max_mem_intv > 0) LAST-like seeds: from x, the shortest forward match of length
+ *           >= min_seed_len + 1 with fewer than max_mem_intv occurrences
+ *   then sorted by info (qbeg << 32 | qend); ties (upstream's introsort leaves them unordered)
+ *   by k, s, l.
+ *
+ * Index (built on the host, resident in HBM): T = ref + reverse-complement(ref), the BWT of T$
+ * with the sentinel kept, count[c] = 1 + #{bases < c}, occurrence counts in 64-base blocks of
+ * 64 bytes (4 x uint32 counts + 4 x uint64 one-hot masks: one block load per Occ query), the
+ * full suffix array as uint32 (|T| < 2^32 - 1; 4 B per text position -- a 3 Gb genome's 6 G
+ * positions would need the 64-bit form, not built here).  Intervals are bwa-mem2's:
+ * [k, k + s) 0-based over the n + 1 rows of T$, l = k of the reverse-complement string.
+ * Reference bases must be 0..3 (ambiguous bases replaced beforehand, as bwa's .pac does);
+ * read bases 0..4 (4 = N ends every match).
+ */
+#ifndef BSW_FMI_H
+#define BSW_FMI_H
+
+#include <stdint.h>
+#include "bsw.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bsw_fmi bsw_fmi_t;
+
+/* bwa's bwtintv_t: x[0] = k, x[1] = l, x[2] = s (occurrences), info = qbeg << 32 | qend */
+typedef struct bsw_bwtintv_t {
+    uint64_t x[3];
+    uint64_t info;
+} bsw_bwtintv_t;
+
+typedef struct bsw_mem_opt_t {       /* the mem_opt_t fields seeding reads                        */
+    int32_t min_seed_len;            /* bwa -k (19)                                               */
+    int32_t split_width;             /* re-seed SMEMs with at most this many occurrences (10)     */
+    int32_t max_mem_intv;            /* pass-3 occurrence bound; 0 disables pass 3 (20)           */
+    float   split_factor;            /* bwa -r (1.5)                                              */
+} bsw_mem_opt_t;
+
+typedef struct bsw_fmi_info_t {
+    int64_t n;                       /* |T| = 2 * ref_len (the BWT has n + 1 rows)                */
+    int64_t sentinel;                /* BWT row holding '$' (SA = 0)                              */
+    int64_t count[5];                /* count[c] = 1 + #{T[i] < c}                                */
+    int64_t device_bytes;            /* HBM held by the resident index                            */
+    float   build_s;                 /* host build time (suffix array + BWT + blocks)             */
+} bsw_fmi_info_t;
+
+void bsw_mem_opt_default(bsw_mem_opt_t *opt);
+
+/* Build the FM-index of ref[0, ref_len) on the host (prefix-doubling suffix array over 27-base
+ * keys) and keep it resident on HIP device `device` (device < 0: host-only index -- suffix array,
+ * BWT and counts for inspection; seeding calls on it return BSW_E_NODEV).  Blocking.
+ * BSW_E_INVAL for a base > 3, BSW_E_RANGE if 2 * ref_len + 2 >= 2^32. */
+int  bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **out);
+void bsw_fmi_destroy(bsw_fmi_t *fmi);
+int  bsw_fmi_get_info(const bsw_fmi_t *fmi, bsw_fmi_info_t *out);
+/* Host copies of the suffix array (n + 1 entries) and the BWT (n + 1 codes, 4 = '$'). */
+int  bsw_fmi_copy_sa(const bsw_fmi_t *fmi, int64_t *sa);
+int  bsw_fmi_copy_bwt(const bsw_fmi_t *fmi, uint8_t *bwt);
+
+/* mem_collect_intv for n reads (read i = reads[read_off[i], read_off[i] + read_len[i]), codes
+ * 0..4): up to `cap` intervals of read i at mems[i * cap], their number in n_mems[i].  If some
+ * read has more than cap, its n_mems is > cap (a lower bound of the true count: re-seeding only
+ * sees the SMEMs that were stored), its intervals are incomplete, and the call returns
+ * BSW_E_RANGE; reads with n_mems <= cap are exact.  Host buffers; blocking. */
+int  bsw_mem_collect_intv(bsw_fmi_t *fmi, const bsw_mem_opt_t *opt, const uint8_t *reads,
+                          const int64_t *read_off, const int32_t *read_len, int32_t n,
+                          bsw_bwtintv_t *mems, int32_t cap, int32_t *n_mems);
+
+/* Device-resident form (all pointers in HBM of the index's device; max_len >= every read
+ * length bounds the per-read scratch).  `stream` a hipStream_t or NULL.  Returns when the
+ * results are in HBM; BSW_E_RANGE as above (the overflow flag is read back). */
+int  bsw_mem_collect_intv_device(bsw_fmi_t *fmi, const bsw_mem_opt_t *opt, const uint8_t *d_reads,
+                                 const int64_t *d_read_off, const int32_t *d_read_len, int32_t n,
+                                 int32_t max_len, bsw_bwtintv_t *d_mems, int32_t cap,
+                                 int32_t *d_n_mems, void *stream);
+
+/* bwt_sa over device arrays: d_pos[i] = SA[d_k[i]] (text position of BWT row k; positions
+ * >= ref_len lie on the reverse strand, as bns_depos reads them).  Rows > n give -1. */
+int  bsw_fmi_sa_device(bsw_fmi_t *fmi, const uint64_t *d_k, int64_t n, int64_t *d_pos, void *stream);
+
+/* The last seeding call's SMEM kernel time (HIP events). */
+int  bsw_fmi_last_kernel_ms(const bsw_fmi_t *fmi, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSW_FMI_H */

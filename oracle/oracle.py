@@ -218,3 +218,83 @@ def ksw_global2_batch(pairs, ref, qer, mat, o_del=6, e_del=1, o_ins=6, e_ins=1, 
                                _ptr(score), _ptr(cig) if cig is not None else None, stride, _ptr(ncig),
                                nthreads)
     return score, cig, ncig
+
+
+# ---- FM-index SMEM seeding (oracle/fmi_ref.c: bwt_smem1a / bwt_seed_strategy1 / mem_collect_intv)
+
+BWTINTV_DTYPE = np.dtype([("k", "<u8"), ("l", "<u8"), ("s", "<u8"), ("info", "<u8")])   # bwa's bwtintv_t
+
+
+class _MemOpt(ctypes.Structure):
+    _fields_ = [("min_seed_len", ctypes.c_int32), ("split_width", ctypes.c_int32),
+                ("max_mem_intv", ctypes.c_int32), ("split_factor", ctypes.c_float)]
+
+
+def mem_opt(min_seed_len=19, split_width=10, max_mem_intv=20, split_factor=1.5):
+    """bwa mem defaults: -k 19, split_width 10, max_mem_intv 20, -r 1.5"""
+    return _MemOpt(min_seed_len, split_width, max_mem_intv, split_factor)
+
+
+class FmiRef:
+    """The oracle's FM-index of ref + reverse-complement(ref) (comparison-sorted suffix array,
+    prefix-count occurrence table) and its SMEM passes."""
+
+    def __init__(self, ref):
+        L = lib()
+        P = ctypes.c_void_p
+        L.oracle_fmi_sizeof.restype = ctypes.c_size_t
+        L.oracle_fmi_build.argtypes = [P, ctypes.c_int64, P]
+        L.oracle_fmi_build.restype = ctypes.c_int
+        for f in ("oracle_fmi_n", "oracle_fmi_sentinel"):
+            getattr(L, f).restype = ctypes.c_int64
+            getattr(L, f).argtypes = [P]
+        L.oracle_fmi_count.argtypes = [P, P]
+        L.oracle_fmi_sa.argtypes = [P, P]
+        L.oracle_fmi_bwt.argtypes = [P, P]
+        L.oracle_fmi_free.argtypes = [P]
+        L.oracle_collect_intv_mt.argtypes = [P, P, P, P, P, ctypes.c_int32, P, ctypes.c_int32, P, ctypes.c_int]
+        self._buf = ctypes.create_string_buffer(L.oracle_fmi_sizeof())
+        self.ref = np.ascontiguousarray(ref, dtype=np.uint8)
+        if L.oracle_fmi_build(_ptr(self.ref), len(self.ref), self._buf) != 0:
+            raise ValueError("oracle_fmi_build failed (codes must be 0..3)")
+        self.n = L.oracle_fmi_n(self._buf)
+        self.sentinel = L.oracle_fmi_sentinel(self._buf)
+        self.count = np.zeros(5, dtype=np.int64)
+        L.oracle_fmi_count(self._buf, _ptr(self.count))
+
+    def sa(self):
+        a = np.zeros(self.n + 1, dtype=np.int64)
+        lib().oracle_fmi_sa(self._buf, _ptr(a))
+        return a
+
+    def bwt(self):
+        a = np.zeros(self.n + 1, dtype=np.uint8)
+        lib().oracle_fmi_bwt(self._buf, _ptr(a))
+        return a
+
+    def collect_intv(self, reads, off, lens, cap=256, opt=None, nthreads=1):
+        """mem_collect_intv per read -> (intervals [n, cap] BWTINTV_DTYPE, counts [n])"""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        n = len(lens)
+        out = np.zeros((n, cap), dtype=BWTINTV_DTYPE)
+        cnt = np.zeros(n, dtype=np.int32)
+        o = opt if opt is not None else mem_opt()
+        lib().oracle_collect_intv_mt(self._buf, ctypes.byref(o), _ptr(reads), _ptr(off), _ptr(lens), n,
+                                     _ptr(out), cap, _ptr(cnt), nthreads)
+        return out, cnt
+
+    @staticmethod
+    def counters(reset=False):
+        """(backward extensions, 64-row blocks they touched) since the last reset"""
+        c = np.zeros(2, dtype=np.uint64)
+        lib().oracle_fmi_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib().oracle_fmi_counters(_ptr(c), int(reset))
+        return int(c[0]), int(c[1])
+
+    def __del__(self):
+        try:
+            lib().oracle_fmi_free(self._buf)
+        except Exception:
+            pass

@@ -13,7 +13,7 @@ import pytest
 import bsw
 from conftest import ROOT
 
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("bsw.h", "bsw_ext.h", "bsw_batch.h", "bsw_mate.h", "bsw_global.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("bsw.h", "bsw_ext.h", "bsw_batch.h", "bsw_mate.h", "bsw_global.h", "bsw_fmi.h")]
 
 
 def declared_functions():

@@ -1,0 +1,269 @@
+"""FM-index SMEM seeding (include/bsw_fmi.h).
+
+CPU: the oracle (oracle/fmi_ref.c: bwt_smem1a / bwt_seed_strategy1 / mem_collect_intv restated)
+is pinned by brute force -- every interval's occurrence count, SA row and reverse-complement row
+against naive string search over T = ref + revcomp(ref); the pass-1 SMEMs are exactly the
+super-maximal exact matches of the read (computed naively); the product's host-built suffix
+array / BWT / counts equal the oracle's.  Parity vs upstream itself is unpinned (the reference
+holds no source or fixtures for this path).
+GPU: bsw_mem_collect_intv(_device) == oracle on random, repetitive and edge-case inputs.
+"""
+import bisect
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "bwa-mem2-arm_amd", "py"))
+import oracle  # noqa: E402
+import bsw  # noqa: E402
+
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def repetitive_ref(n, seed):
+    """random reference with segment duplications, an inverted copy and tandem repeats"""
+    rng = np.random.default_rng(seed)
+    ref = rng.integers(0, 4, n, dtype=np.uint8)
+    seg = n // 10
+    ref[2 * seg:3 * seg] = ref[seg // 2:seg // 2 + seg]                          # duplication
+    ref[4 * seg:4 * seg + seg // 2] = 3 - ref[seg:seg + seg // 2][::-1]          # inverted copy
+    ref[6 * seg:6 * seg + 120] = np.tile(np.array([0, 1, 1], np.uint8), 40)      # tandem repeat
+    ref[7 * seg:7 * seg + 60] = 2                                                # homopolymer
+    for k in range(8):                                                           # 8 near copies
+        a = 8 * seg + k * (seg // 8)
+        ref[a:a + 40] = ref[5 * seg:5 * seg + 40]
+        ref[a + 20] = (ref[a + 20] + 1 + k % 3) % 4
+    return ref
+
+
+def sample_reads(ref, n, L, seed, p_sub=0.02, p_n=0.002, p_rand=0.1, p_rc=0.5):
+    """reads from either strand with substitutions / N, plus random reads: (reads, off, len)"""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        if rng.random() < p_rand:
+            r = rng.integers(0, 4, L, dtype=np.uint8)
+        else:
+            p = int(rng.integers(0, len(ref) - L))
+            r = ref[p:p + L].copy()
+            if rng.random() < p_rc:
+                r = (3 - r[::-1]).astype(np.uint8)
+            m = rng.random(L) < p_sub
+            r[m] = (r[m] + rng.integers(1, 4, int(m.sum()))) % 4
+        r[rng.random(L) < p_n] = 4
+        out.append(r.astype(np.uint8))
+    lens = np.array([len(r) for r in out], dtype=np.int32)
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    return np.concatenate(out) if out else np.zeros(1, np.uint8), off, lens
+
+
+class Naive:
+    """brute-force string view of T$ = ref + revcomp(ref) + '$'"""
+
+    def __init__(self, ref):
+        t = np.concatenate([ref, 3 - ref[::-1]]).astype(np.uint8)
+        self.T = ACGT[t].tobytes().decode()
+        self.n = len(self.T)
+        # '$' sorts before every base: suffix strings with '#' (< 'A') appended
+        self.sorted = sorted(self.T[i:] + "#" for i in range(self.n + 1))
+
+    def count(self, p):
+        c, i = 0, self.T.find(p)
+        while i >= 0:
+            c += 1
+            i = self.T.find(p, i + 1)
+        return c
+
+    def first_row(self, p):
+        return bisect.bisect_left(self.sorted, p)
+
+
+def s_of(read):
+    return ACGT[np.minimum(read, 3)].tobytes().decode()
+
+
+def revcomp(p):
+    return p[::-1].translate(str.maketrans("ACGT", "TGCA"))
+
+
+@pytest.fixture(scope="module")
+def small_world():
+    ref = repetitive_ref(3000, 5)
+    return ref, oracle.FmiRef(ref), Naive(ref)
+
+
+def test_oracle_index_matches_naive(small_world):
+    ref, o, nv = small_world
+    sa = o.sa()
+    assert [nv.T[i:] + "#" for i in sa] == nv.sorted
+    bwt = o.bwt()
+    assert bwt[o.sentinel] == 4 and sa[o.sentinel] == 0
+    assert list(o.count) == [1] + list(1 + np.cumsum([nv.T.count(c) for c in "ACGT"]))
+
+
+def test_oracle_intervals_pinned_by_brute_force(small_world):
+    ref, o, nv = small_world
+    reads, off, lens = sample_reads(ref, 60, 100, 11)
+    out, cnt = o.collect_intv(reads, off, lens, cap=256, opt=oracle.mem_opt(min_seed_len=12))
+    checked = 0
+    for i in range(len(lens)):
+        rd = reads[off[i]:off[i] + lens[i]]
+        prev = None
+        for v in out[i, :cnt[i]]:
+            m, e = int(v["info"] >> 32), int(v["info"] & 0xffffffff)
+            assert 0 <= m < e <= lens[i] and (rd[m:e] < 4).all()
+            p = s_of(rd[m:e])
+            assert int(v["s"]) == nv.count(p), (i, m, e)
+            assert int(v["k"]) == nv.first_row(p)
+            assert int(v["l"]) == nv.first_row(revcomp(p))
+            key = (int(v["info"]), int(v["k"]), int(v["s"]), int(v["l"]))
+            assert prev is None or prev <= key                     # sorted by info, then k, s, l
+            prev = key
+            checked += 1
+    assert checked > 200
+
+
+def naive_smems(nv, rd):
+    """super-maximal exact matches of the read: [m, e) occurring in T, not extendable left or
+    right, not contained in another such match (bases 4 never match)"""
+    L = len(rd)
+    ends = []
+    for m in range(L):
+        e = m
+        while e < L and rd[e] < 4 and nv.count(s_of(rd[m:e + 1])) > 0:
+            e += 1
+        ends.append(e)
+    mems = {(m, ends[m]) for m in range(L) if ends[m] > m and (m == 0 or ends[m - 1] < ends[m])}
+    return {(m, e) for (m, e) in mems if not any(a <= m and e <= b and (a, b) != (m, e) for (a, b) in mems)}
+
+
+def test_oracle_pass1_is_the_smem_set(small_world):
+    ref, o, nv = small_world
+    reads, off, lens = sample_reads(ref, 40, 60, 12, p_sub=0.04)
+    only_pass1 = oracle.mem_opt(min_seed_len=1, max_mem_intv=0, split_factor=1000.0)
+    out, cnt = o.collect_intv(reads, off, lens, cap=256, opt=only_pass1)
+    for i in range(len(lens)):
+        rd = reads[off[i]:off[i] + lens[i]]
+        got = {(int(v["info"] >> 32), int(v["info"] & 0xffffffff)) for v in out[i, :cnt[i]]}
+        assert got == naive_smems(nv, rd), i
+
+
+def test_oracle_passes_2_and_3_fire(small_world):
+    """the repetitive reference makes re-seeding (pass 2) and LAST-like seeds (pass 3) add
+    intervals that pass 1 alone does not produce"""
+    ref, o, nv = small_world
+    seg = len(ref) // 10
+    reads = np.concatenate([ref[seg // 2 + 10:seg // 2 + 110], ref[8 * seg:8 * seg + 100], ref[5 * seg:5 * seg + 100]])
+    off = np.array([0, 100, 200], dtype=np.int64)
+    lens = np.array([100, 100, 100], dtype=np.int32)
+    _, c_all = o.collect_intv(reads, off, lens, opt=oracle.mem_opt())
+    _, c_1 = o.collect_intv(reads, off, lens, opt=oracle.mem_opt(max_mem_intv=0, split_factor=1000.0))
+    _, c_12 = o.collect_intv(reads, off, lens, opt=oracle.mem_opt(max_mem_intv=0))
+    assert (c_12 >= c_1).all() and (c_all >= c_12).all()
+    assert c_12.sum() > c_1.sum() and c_all.sum() > c_12.sum()
+
+
+@pytest.mark.parametrize("seed,n", [(1, 5000), (3, 40000)])
+def test_host_builder_equals_oracle(seed, n):
+    """the product's prefix-doubling suffix array / BWT / counts (host-only index, no GPU) ==
+    the oracle's comparison-sorted ones"""
+    ref = repetitive_ref(n, seed)
+    o = oracle.FmiRef(ref)
+    f = bsw.Fmi(ref, device=-1)
+    info = f.info()
+    assert info.n == o.n and info.sentinel == o.sentinel and list(info.count) == list(o.count)
+    assert np.array_equal(f.sa(), o.sa())
+    assert np.array_equal(f.bwt(), o.bwt())
+    f.close()
+
+
+def test_host_builder_rejects_bad_input():
+    with pytest.raises(bsw.BswError):
+        bsw.Fmi(np.array([0, 1, 4, 2], dtype=np.uint8), device=-1)
+    f = bsw.Fmi(np.array([0], dtype=np.uint8), device=-1)          # tiny reference
+    assert list(f.sa()) == [2, 0, 1] and f.info().count[4] == 3
+    f.close()
+
+
+# ------------------------------------------------------------------------------------- GPU
+
+def _compare(o_out, o_cnt, g_out, g_cnt):
+    assert np.array_equal(o_cnt, g_cnt)
+    for i in range(len(o_cnt)):
+        c = min(int(o_cnt[i]), o_out.shape[1])
+        assert np.array_equal(o_out[i, :c], g_out[i, :c]), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n_ref,n_reads,L", [("random", 200_000, 4000, 151), ("repetitive", 100_000, 3000, 151),
+                                                  ("repetitive", 50_000, 500, 250)])
+def test_gpu_collect_intv_equals_oracle(kind, n_ref, n_reads, L):
+    ref = repetitive_ref(n_ref, 9) if kind == "repetitive" else np.random.default_rng(9).integers(0, 4, n_ref, dtype=np.uint8)
+    reads, off, lens = sample_reads(ref, n_reads, L, 21)
+    o = oracle.FmiRef(ref)
+    f = bsw.Fmi(ref)
+    for opt in (dict(), dict(min_seed_len=15), dict(max_mem_intv=0), dict(split_width=50, min_seed_len=11)):
+        o_out, o_cnt = o.collect_intv(reads, off, lens, cap=320, opt=oracle.mem_opt(**opt), nthreads=8)
+        g_out, g_cnt = f.collect_intv(reads, off, lens, cap=320, opt=bsw.mem_opt(**opt))
+        _compare(o_out, o_cnt, g_out, g_cnt)
+    f.close()
+
+
+@pytest.mark.gpu
+def test_gpu_collect_intv_edges():
+    ref = repetitive_ref(20_000, 4)
+    o = oracle.FmiRef(ref)
+    f = bsw.Fmi(ref)
+    seg = len(ref) // 10
+    rd = [np.zeros(0, np.uint8), np.array([2], np.uint8), np.full(30, 4, np.uint8),
+          np.concatenate([[4], ref[100:160], [4]]).astype(np.uint8), ref[7 * seg - 10:7 * seg + 90].copy(),
+          ref[6 * seg:6 * seg + 150].copy(), (3 - ref[200:350][::-1]).astype(np.uint8), ref[:80].copy(),
+          ref[-80:].copy(), np.full(100, 2, np.uint8)]
+    lens = np.array([len(r) for r in rd], dtype=np.int32)
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    reads = np.concatenate(rd).astype(np.uint8)
+    o_out, o_cnt = o.collect_intv(reads, off, lens, cap=2048)
+    g_out, g_cnt = f.collect_intv(reads, off, lens, cap=2048)
+    _compare(o_out, o_cnt, g_out, g_cnt)
+    assert g_cnt[0] == 0 and g_cnt[2] == 0 and g_cnt[-1] > 1000      # 100 G vs a 60-G run: 1572
+    # too small a cap: the call reports BSW_E_RANGE, reads that fit are exact, the others are
+    # flagged with a count > cap (a lower bound: re-seeding only sees the stored SMEMs)
+    with pytest.raises(bsw.BswError):
+        f.collect_intv(reads, off, lens, cap=2)
+    g2, c2 = f.collect_intv(reads, off, lens, cap=2, strict=False)
+    fit = o_cnt <= 2
+    assert np.array_equal(c2[fit], o_cnt[fit]) and (c2[~fit] > 2).all() and (c2[~fit] <= o_cnt[~fit]).all()
+    for i in np.nonzero(fit)[0]:
+        assert np.array_equal(g2[i, :o_cnt[i]], o_out[i, :o_cnt[i]])
+    f.close()
+
+
+@pytest.mark.gpu
+def test_gpu_device_api_and_sa_lookup():
+    import hiprt
+    ref = np.random.default_rng(6).integers(0, 4, 100_000, dtype=np.uint8)
+    reads, off, lens = sample_reads(ref, 2000, 151, 8)
+    o = oracle.FmiRef(ref)
+    f = bsw.Fmi(ref)
+    cap = 128
+    d_reads, d_off, d_len = (hiprt.DeviceBuffer.from_array(a) for a in (reads, off, lens))
+    d_mems = hiprt.DeviceBuffer(len(lens) * cap * 32)
+    d_cnt = hiprt.DeviceBuffer(len(lens) * 4)
+    assert f.collect_intv_device(d_reads.ptr, d_off.ptr, d_len.ptr, len(lens), 151, d_mems.ptr, cap, d_cnt.ptr) == 0
+    g_out = d_mems.download(np.zeros((len(lens), cap), dtype=bsw.BWTINTV_DTYPE))
+    g_cnt = d_cnt.download(np.zeros(len(lens), dtype=np.int32))
+    o_out, o_cnt = o.collect_intv(reads, off, lens, cap=cap, nthreads=8)
+    _compare(o_out, o_cnt, g_out, g_cnt)
+    # bwt_sa over every row an interval starts at, plus out-of-range rows
+    ks = np.concatenate([o_out[i, :o_cnt[i]]["k"] for i in range(len(lens))] + [np.array([o.n + 1, 2**40], np.uint64)])
+    d_k = hiprt.DeviceBuffer.from_array(ks.astype(np.uint64))
+    d_pos = hiprt.DeviceBuffer(len(ks) * 8)
+    f.sa_device(d_k.ptr, len(ks), d_pos.ptr)
+    pos = d_pos.download(np.zeros(len(ks), dtype=np.int64))
+    sa = o.sa()
+    assert np.array_equal(pos[:-2], sa[ks[:-2].astype(np.int64)]) and (pos[-2:] == -1).all()
+    f.close()
