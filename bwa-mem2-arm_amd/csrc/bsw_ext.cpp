@@ -48,7 +48,7 @@ int cal_max_gap(const bsw_params_t &p, int a, int w, int qlen)
 template <class F>
 void parallel_for(int32_t n, F f)
 {
-    const int nt = bsw::HostPool::kWorkers + 1;
+    const int nt = bsw::HostPool::workers() + 1;
     if (n < 4096) {
         f(0, n);
         return;

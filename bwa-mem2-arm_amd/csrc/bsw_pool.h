@@ -1,12 +1,16 @@
 // bsw_pool.h -- the engine's host worker pool (host-buffer staging, packing, scans).
 //
-// One process-wide pool of kWorkers threads, created on first use.  parallel_for(n, fn) runs
+// One process-wide pool of workers() threads, created on first use (the process's CPU share
+// minus the caller: the cgroup CPU quota when one is set, else the affinity set; 2..32 lanes).  parallel_for(n, fn) runs
 // fn(0..n-1), the caller taking part; several callers (upstream calls getScores* from kt_for
 // workers) may submit at once -- tasks interleave in one queue and each call waits only for its
 // own.  Spawning threads per call instead cost ~30 us each, several ms per 1M-pair call.
 #pragma once
 #include <algorithm>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <sched.h>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -18,7 +22,27 @@ namespace bsw {
 
 class HostPool {
 public:
-    static constexpr int kWorkers = 7;          // + the calling thread = 8 lanes of host work
+    static int workers()                        // + the calling thread = lanes of host work
+    {
+        static const int w = [] {
+            int n = (int)std::thread::hardware_concurrency();
+            if (n <= 0) n = 8;
+#ifdef __linux__
+            cpu_set_t cs;
+            if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = std::min(n, (int)CPU_COUNT(&cs));
+            if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+                char q[32] = {0};
+                long per = 0;
+                if (fscanf(f, "%31s %ld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+                    n = std::min(n, (int)((atol(q) + per - 1) / per));
+                fclose(f);
+            }
+#endif
+            if (const char *e = getenv("BSW_HOST_THREADS")) n = atoi(e);   // tuning override
+            return std::max(2, std::min(n, 32)) - 1;
+        }();
+        return w;
+    }
     static HostPool &get()
     {
         static HostPool p;
@@ -71,7 +95,7 @@ public:
 private:
     HostPool()
     {
-        for (int k = 0; k < kWorkers; ++k)
+        for (int k = 0; k < workers(); ++k)
             th_.emplace_back([this] {
                 for (;;) {
                     std::function<void()> t;
@@ -97,7 +121,7 @@ private:
 inline void par_memcpy(void *dst, const void *src, size_t bytes)
 {
     constexpr size_t kPiece = (size_t)2 << 20;
-    const int nt = (int)std::min<size_t>(HostPool::kWorkers + 1, bytes / kPiece);
+    const int nt = (int)std::min<size_t>(HostPool::workers() + 1, bytes / kPiece);
     if (nt <= 1) { memcpy(dst, src, bytes); return; }
     HostPool::get().parallel_for(nt, [=](int t) {
         const size_t a = bytes * t / nt, b = bytes * (t + 1) / nt;

@@ -6,7 +6,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+// zero-copy "pull": a kernel streams pinned host memory over PCIe into HBM (16-B loads, many in flight)
+__global__ void pull_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, size_t n16)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
 int main()
 {
     const size_t B = (size_t)512 << 20;
@@ -35,6 +42,26 @@ int main()
     run("pinned_h2d", 1, true, h); run("pinned_h2d", 2, true, h); run("pinned_h2d", 4, true, h);
     run("pinned_d2h", 1, false, h); run("pinned_d2h", 2, false, h);
     run("pageable_h2d", 1, true, pg);
+    {
+        void *hd = nullptr;
+        CK(hipHostGetDevicePointer(&hd, h, 0));
+        for (int grid : {512, 1024, 2048, 4096}) {
+            double best = 0;
+            for (int rep = 0; rep < 4; ++rep) {
+                CK(hipDeviceSynchronize());
+                auto t0 = std::chrono::steady_clock::now();
+                hipLaunchKernelGGL(pull_kernel, dim3(grid), dim3(256), 0, st[0], (const uint4 *)hd, (uint4 *)d, B / 16);
+                CK(hipStreamSynchronize(st[0]));
+                const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                best = std::max(best, B / s / 1e9);
+            }
+            printf("{\"case\": \"pull_kernel_h2d\", \"grid\": %d, \"GBps\": %.2f}\n", grid, best);
+        }
+        if (((unsigned char *)d)[0] == 0) {}   // keep d
+        std::vector<unsigned char> chk(64);
+        CK(hipMemcpy(chk.data(), d, 64, hipMemcpyDeviceToHost));
+        printf("{\"case\": \"pull_check\", \"ok\": %d}\n", chk[0] == 1 && chk[63] == 1);
+    }
     // host memcpy into pinned memory (the staging step), 1 thread
     auto t0 = std::chrono::steady_clock::now();
     memcpy(h, pg, B);
