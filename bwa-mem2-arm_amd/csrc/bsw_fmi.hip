@@ -68,7 +68,7 @@ __device__ __forceinline__ uint32_t occ_of(const uint4 &cnt, const ulonglong2 &b
 {
     const uint32_t cc = c == 0 ? cnt.x : c == 1 ? cnt.y : c == 2 ? cnt.z : cnt.w;
     const uint64_t bb = c == 0 ? b01.x : c == 1 ? b01.y : c == 2 ? b23.x : b23.y;
-    return cc + (uint32_t)__popcll(bb & mask);
+    return cc + (uint32_t)__builtin_popcountll(bb & mask);
 }
 
 struct Iv {
@@ -256,15 +256,16 @@ __device__ __forceinline__ bool iv_less(const bsw_bwtintv_t &a, const bsw_bwtint
     return a.x[1] < b.x[1];
 }
 
-__global__ __launch_bounds__(64) void smem_kernel(const FmiDev f, const MemOpt opt, const uint8_t *__restrict__ reads,
-                                                  const int64_t *__restrict__ read_off,
-                                                  const int32_t *__restrict__ read_len, int32_t n0, int32_t n,
-                                                  uint4 *__restrict__ scratch, int32_t scap,
-                                                  bsw_bwtintv_t *__restrict__ mems, int32_t cap,
-                                                  int32_t *__restrict__ n_mems, int32_t *__restrict__ err)
+// one read's mem_collect_intv (lane t of a launch over reads n0 .. n0 + n - 1): returns error
+// bits (1: more than cap intervals, 2: bad length / scratch overflow).  Plain loops, as upstream
+// writes them: a per-lane state machine doing one extension per iteration (so that a wave's time
+// is its busiest lane's work instead of the sum of per-phase maxima) measured 1.4x SLOWER (31.9
+// vs 22.1 ms on 1M reads x 16 Mb) -- the bookkeeping transitions cost whole iterations.
+__device__ int smem_read(const FmiDev &f, const MemOpt &opt, const uint8_t *__restrict__ reads,
+                         const int64_t *__restrict__ read_off, const int32_t *__restrict__ read_len, int32_t n0,
+                         int32_t n, int t, uint4 *__restrict__ scratch, int32_t scap, bsw_bwtintv_t *__restrict__ mems,
+                         int32_t cap, int32_t *__restrict__ n_mems)
 {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;    // lane within this chunk
-    if (t >= n) return;
     const int r = n0 + t;                                    // read index
     Lane L;
     L.q = reads + read_off[r];
@@ -278,9 +279,8 @@ __global__ __launch_bounds__(64) void smem_kernel(const FmiDev f, const MemOpt o
     L.nout = 0;
     L.overflow = 0;
     if (L.len < 0 || L.len > scap - 1) {
-        atomicOr(err, 2);
         n_mems[r] = 0;
-        return;
+        return 2;
     }
     // pass 1: SMEMs
     int x = 0;
@@ -316,8 +316,20 @@ __global__ __launch_bounds__(64) void smem_kernel(const FmiDev f, const MemOpt o
         L.out[b + 1] = v;
     }
     n_mems[r] = L.nout;
-    if (L.nout > cap) atomicOr(err, 1);
-    if (L.overflow) atomicOr(err, 2);
+    return (L.nout > cap ? 1 : 0) | (L.overflow ? 2 : 0);
+}
+
+__global__ __launch_bounds__(64) void smem_kernel(const FmiDev f, const MemOpt opt, const uint8_t *__restrict__ reads,
+                                                  const int64_t *__restrict__ read_off,
+                                                  const int32_t *__restrict__ read_len, int32_t n0, int32_t n,
+                                                  uint4 *__restrict__ scratch, int32_t scap,
+                                                  bsw_bwtintv_t *__restrict__ mems, int32_t cap,
+                                                  int32_t *__restrict__ n_mems, int32_t *__restrict__ err)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;    // lane within this chunk
+    if (t >= n) return;
+    const int e = smem_read(f, opt, reads, read_off, read_len, n0, n, t, scratch, scap, mems, cap, n_mems);
+    if (e) atomicOr(err, e);
 }
 
 __global__ void sa_kernel(const uint32_t *__restrict__ sa, uint32_t nrows, const uint64_t *__restrict__ k,
@@ -414,6 +426,7 @@ struct bsw_fmi {
     FmiBlock *d_blk = nullptr;
     uint32_t *d_sa = nullptr;
     std::vector<uint32_t> sa;                 // host copies (tests, bwt_sa on the host side)
+    std::vector<FmiBlock> h_blk;              // host-only index (device < 0): the occurrence blocks
     std::vector<uint8_t> bwt;
     int64_t count[5] = {0, 0, 0, 0, 0};
     int64_t dev_bytes = 0;
@@ -527,6 +540,9 @@ int bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **o
     f->dv.sentinel = sentinel;
     f->dv.n = n;
     if (device < 0) {                        // host-only index (tests of the builder): no HBM copy
+        f->h_blk.swap(blk);
+        f->dv.blk = f->h_blk.data();
+        for (int c = 0; c < 5; ++c) f->dv.count[c] = (uint32_t)f->count[c];
         *out = f;
         return BSW_OK;
     }
