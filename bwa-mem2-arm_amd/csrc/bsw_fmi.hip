@@ -454,9 +454,10 @@ int run_collect(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads, 
     mo.max_mem_intv = opt->max_mem_intv;
     mo.split_len = (int)(opt->min_seed_len * opt->split_factor + .499);
     const int32_t scap = max_len + 1;
-    // chunk so the two scratch vectors stay within ~4 GB
+    // chunk so the two scratch vectors stay within 16 GB (of 288 GB: one launch for up to ~3M
+    // 151-bp reads)
     const size_t per_read = (size_t)2 * scap * sizeof(uint4);
-    const int32_t chunk = (int32_t)std::max<size_t>(64, std::min<size_t>((size_t)n, ((size_t)4 << 30) / per_read));
+    const int32_t chunk = (int32_t)std::max<size_t>(64, std::min<size_t>((size_t)n, ((size_t)16 << 30) / per_read));
     const size_t need = per_read * (size_t)std::min(chunk, n);
     if (need > f->scratch_bytes) {
         if (f->d_scratch) (void)hipFree(f->d_scratch);
