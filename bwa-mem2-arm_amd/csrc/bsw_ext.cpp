@@ -460,26 +460,7 @@ extern "C" int bsw_chain2aln(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uin
     return rc;
 }
 
-extern "C" int bsw_chain2aln_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
-                                    const int64_t *read_off, const int32_t *read_len, int32_t n_reads,
-                                    const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain,
-                                    int32_t n_seeds, bsw_alnreg_t *out, int32_t *extended)
-{
-    if (!ctx || !opt || n_seeds < 0 || n_reads < 0 ||
-        (n_seeds > 0 && (!d_reads || !read_off || !read_len || !seeds || !seed_read || !seed_chain || !out ||
-                         !extended)))
-        return BSW_E_INVAL;
-    bsw::DevJobs dj;
-    bsw_chain_stats_t cs{};
-    const int rc = chain_rounds(ctx, opt, read_off, read_len, n_reads, seeds, seed_read, seed_chain, n_seeds, out,
-                                extended, &cs,
-                                [&](int32_t nj, const int64_t *jo, const int32_t *jl, const bsw_seed_t *js,
-                                    bsw_alnreg_t *jr) {
-                                    return bsw::ext_device_jobs(ctx, opt, d_reads, dj, nj, jo, jl, js, jr);
-                                });
-    bsw::set_chain_stats(ctx, cs);
-    return rc;
-}
+// bsw_chain2aln_device / bsw_chain2aln_resident: csrc/bsw_chain.hip (GPU rounds)
 
 extern "C" int bsw_chain_last_stats(bsw_ctx_t *ctx, bsw_chain_stats_t *out)
 {

@@ -1284,6 +1284,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
 }
 
 void ctx_params(const bsw_ctx_t *ctx, bsw_params_t *out) { *out = ctx->params; }
+int ctx_device(const bsw_ctx_t *ctx) { return ctx->devs[0]->device; }
 
 void *pinned_acquire(bsw_ctx_t *ctx, int which, size_t bytes)
 {

@@ -9,6 +9,7 @@ namespace bsw {
 int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *ref,
               const uint8_t *qer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *st);
 void ctx_params(const bsw_ctx_t *ctx, bsw_params_t *out);
+int ctx_device(const bsw_ctx_t *ctx);          // HIP device of the context's first device slot pool
 // Per-context pinned host staging buffer `which` (0, 1) of at least `bytes`: DMA-speed H2D for
 // the extension pipeline's code buffers.  Returns nullptr when another call holds it (the
 // caller then uses pageable memory); release with pinned_release.
@@ -29,4 +30,10 @@ struct DevJobs {
 // bsw_extend_seeds_device over nj jobs given on the host (reads resident at d_reads)
 int ext_device_jobs(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads, DevJobs &dj, int32_t nj,
                     const int64_t *off, const int32_t *len, const bsw_seed_t *seeds, bsw_alnreg_t *out);
+// mem_chain2aln rounds with every per-read decision on the GPU (bsw_chain.hip): inputs and
+// outputs device-resident on the context's first device
+int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads, const int64_t *d_read_off,
+                        const int32_t *d_read_len, int32_t n_reads, const bsw_seed_t *d_seeds,
+                        const int32_t *d_sr, const int32_t *d_sc, int32_t ns, bsw_alnreg_t *d_out, int32_t *d_ext,
+                        bsw_chain_stats_t *cs);
 }  // namespace bsw

@@ -34,7 +34,7 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
                "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
                "bsw_set_reference", "bsw_extend_seeds_device", "bsw_set_option",
                "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats",
-               "bsw_mem_opt_default", "bsw_fmi_build", "bsw_fmi_destroy", "bsw_fmi_get_info", "bsw_fmi_copy_sa",
+               "bsw_chain2aln_resident", "bsw_mem_opt_default", "bsw_fmi_build", "bsw_fmi_destroy", "bsw_fmi_get_info", "bsw_fmi_copy_sa",
                "bsw_fmi_copy_bwt", "bsw_mem_collect_intv", "bsw_mem_collect_intv_device", "bsw_fmi_sa_device",
                "bsw_fmi_last_kernel_ms")
 
@@ -129,6 +129,8 @@ def hip_lib():
         L.bsw_chain2aln.argtypes = [P, P, P, ctypes.c_int64, P, P, P, ctypes.c_int32, P, P, P, ctypes.c_int32, P, P]
         L.bsw_chain2aln_device.argtypes = [P, P, P, P, P, ctypes.c_int32, P, P, P, ctypes.c_int32, P, P]
         L.bsw_chain_last_stats.argtypes = [P, P]
+        L.bsw_chain2aln_resident.argtypes = [P, P, P, P, P, ctypes.c_int32, P, P, P, ctypes.c_int32, P, P]
+        L.bsw_chain2aln_resident.restype = ctypes.c_int
         L.bsw_mem_opt_default.argtypes = [P]
         L.bsw_fmi_build.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(P)]
         L.bsw_fmi_destroy.argtypes = [P]
@@ -546,6 +548,15 @@ def chain2aln_device(engine, d_reads: int, read_off, read_len, seeds, seed_read,
                                           _ptr(read_len), len(read_len), _ptr(seeds), _ptr(seed_read),
                                           _ptr(seed_chain), len(seeds), _ptr(out), _ptr(ext)))
     return out, ext
+
+
+def chain2aln_resident(engine, d_reads: int, d_off: int, d_len: int, n_reads: int, d_seeds: int, d_sr: int,
+                       d_sc: int, n_seeds: int, d_out: int, d_ext: int, opt: ExtOpt | None = None):
+    """bsw_chain2aln_resident: every array a device pointer (regions / flags into d_out / d_ext)."""
+    opt = opt if opt is not None else ext_opt()
+    V = ctypes.c_void_p
+    _check(hip_lib().bsw_chain2aln_resident(engine._ctx, ctypes.byref(opt), V(d_reads), V(d_off), V(d_len), n_reads,
+                                            V(d_seeds), V(d_sr), V(d_sc), n_seeds, V(d_out), V(d_ext)))
 
 
 def chain_last_stats(engine) -> ChainStats:

@@ -114,12 +114,22 @@ int bsw_chain2aln(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *ref, 
                   bsw_alnreg_t *out, int32_t *extended);
 
 /* The same with the reads RESIDENT in HBM (d_reads on the context's first device, read_off /
- * read_len and the seeds on the host) and the resident reference of bsw_set_reference: each
- * round's extensions run through bsw_extend_seeds_device (job arrays up, regions down). */
+ * read_len and the seeds on the host) and the resident reference of bsw_set_reference: the
+ * inputs go up once, every per-read step (chain order, containment tests, picks, job arrays)
+ * runs on the GPU (csrc/bsw_chain.hip) around the device extension pipeline, one job count per
+ * round comes back, the regions come down at the end. */
 int bsw_chain2aln_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
                          const int64_t *read_off, const int32_t *read_len, int32_t n_reads,
                          const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain,
                          int32_t n_seeds, bsw_alnreg_t *out, int32_t *extended);
+
+/* Fully device-resident form: every array on the context's first device (d_seed_read sorted,
+ * as above); regions and flags are written to d_out / d_extended.  No host copies at all --
+ * the form a GPU seeding stage (bsw_fmi.h) feeds. */
+int bsw_chain2aln_resident(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
+                           const int64_t *d_read_off, const int32_t *d_read_len, int32_t n_reads,
+                           const bsw_seed_t *d_seeds, const int32_t *d_seed_read, const int32_t *d_seed_chain,
+                           int32_t n_seeds, bsw_alnreg_t *d_out, int32_t *d_extended);
 
 typedef struct bsw_chain_stats_t {
     int32_t rounds;                  /* batch rounds of the last bsw_chain2aln(_device)        */

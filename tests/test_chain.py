@@ -91,3 +91,31 @@ def test_chain2aln_device_200k_reads_equal_oracle(ref):
     assert np.array_equal(wext, gext)
     _same(want, got, "chain2aln device 200K reads")
     eng.close()
+
+
+@pytest.mark.gpu
+def test_chain2aln_resident_equals_oracle(ref):
+    """every array device-resident (bsw_chain2aln_resident: chain order, containment and picks on
+    the GPU) == the oracle; an unsorted seed_read is rejected"""
+    reads, off, lens, seeds, sr, sc = bsw.synth_pe_seeds(ref, 30_000, pair_base=9000)
+    opt = bsw.ext_opt()
+    want, wext = oracle.chain2aln(oracle.make_params(), opt, ref, reads, off, lens, seeds, sr, sc)
+    eng = bsw.Engine()
+    bsw.set_reference(eng, ref)
+    d = {k: hiprt.DeviceBuffer.from_array(v) for k, v in
+         dict(reads=reads, off=off, lens=lens, seeds=seeds, sr=sr, sc=sc).items()}
+    d_out = hiprt.DeviceBuffer(len(seeds) * bsw.ALNREG_DTYPE.itemsize)
+    d_ext = hiprt.DeviceBuffer(len(seeds) * 4)
+    bsw.chain2aln_resident(eng, d["reads"].ptr, d["off"].ptr, d["lens"].ptr, len(lens), d["seeds"].ptr, d["sr"].ptr,
+                           d["sc"].ptr, len(seeds), d_out.ptr, d_ext.ptr, opt)
+    got = d_out.download(np.zeros(len(seeds), dtype=bsw.ALNREG_DTYPE))
+    gext = d_ext.download(np.zeros(len(seeds), dtype=np.int32))
+    assert np.array_equal(wext, gext)
+    _same(want, got, "chain2aln resident")
+    st = bsw.chain_last_stats(eng)
+    assert st.rounds >= 2 and st.n_extended == int(gext.sum())
+    bad = hiprt.DeviceBuffer.from_array(sr[::-1].copy())
+    with pytest.raises(bsw.BswError):
+        bsw.chain2aln_resident(eng, d["reads"].ptr, d["off"].ptr, d["lens"].ptr, len(lens), d["seeds"].ptr, bad.ptr,
+                               d["sc"].ptr, len(seeds), d_out.ptr, d_ext.ptr, opt)
+    eng.close()
