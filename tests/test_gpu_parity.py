@@ -399,9 +399,22 @@ def test_kernel_range_guard_reports_error():
     oracle.get_scores(_oparams(), want, sr, sq, 100)
     e.get_scores(got, sr, sq, 100)
     _assert_same(want, got, "misrouted short queries")
+    # a multi-chunk host call (launcher-thread pipeline): the guard trips inside the pipeline,
+    # the call returns BSW_E_RANGE without hanging, and the engine keeps working afterwards
+    big, bref, bqer = bswgen.c2_like(40_000, seed=43)
+    e.set_option("host_chunk", 4096)
+    with pytest.raises(bsw.BswError, match="-34"):
+        e.get_scores(big.copy(), bref, bqer, 100)
     e.set_option("test_misroute", 0)
     got = pairs.copy()
     e.get_scores(got, ref, qer, 100)
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100)
+    _assert_same(want, got, "after a tripped guard")
+    gb, wb = big.copy(), big.copy()
+    e.get_scores(gb, bref, bqer, 100)
+    oracle.get_scores(_oparams(), wb, bref, bqer, 100)
+    _assert_same(wb, gb, "chunked call after a tripped guard")
     e.close()
 
 
