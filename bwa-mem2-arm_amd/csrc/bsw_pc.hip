@@ -552,8 +552,11 @@ static void launch_pc_q(const KParams &kp, int32_t w, SeqPair *pairs, const int3
                         const uint8_t *ref, const uint8_t *qer, int32_t *err, hipStream_t s)
 {
     // one wave per workgroup: a finished wave's slot and LDS are reused at once
-    hipLaunchKernelGGL((pc_kernel<QMAX, 1>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, kp, w, pairs, order,
-                       n, ref, qer, err);
+#ifndef BSW_PC_LDS_PAD          // experiment builds only: dynamic LDS per workgroup caps waves per CU
+#define BSW_PC_LDS_PAD 0
+#endif
+    hipLaunchKernelGGL((pc_kernel<QMAX, 1>), dim3((unsigned)((n + 63) / 64)), dim3(64), BSW_PC_LDS_PAD, s, kp, w, pairs,
+                       order, n, ref, qer, err);
 }
 
 hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
