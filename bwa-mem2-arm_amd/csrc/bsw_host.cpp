@@ -583,6 +583,18 @@ static void pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes)
 {
     size_t i = 0;
     const __m128i m0 = _mm_set1_epi16(0x000f), m1 = _mm_set1_epi16(0x00f0);
+    // streaming (non-temporal) stores into the pinned staging buffer when it is 16-B aligned: no
+    // read-for-ownership of destination lines the CPU never reads again (the DMA engine does)
+    if (((uintptr_t)dst & 15) == 0) {
+        for (; i + 32 <= nbytes; i += 32) {
+            const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
+            const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
+            const __m128i ra = _mm_or_si128(_mm_and_si128(a, m0), _mm_and_si128(_mm_srli_epi16(a, 4), m1));
+            const __m128i rb = _mm_or_si128(_mm_and_si128(b, m0), _mm_and_si128(_mm_srli_epi16(b, 4), m1));
+            _mm_stream_si128((__m128i *)(dst + i / 2), _mm_packus_epi16(ra, rb));
+        }
+        _mm_sfence();
+    }
     for (; i + 32 <= nbytes; i += 32) {
         const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
         const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
