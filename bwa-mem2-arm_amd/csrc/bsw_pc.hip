@@ -255,16 +255,44 @@ __device__ __forceinline__ void pc_group(uint32_t &ha, uint32_t &hb, uint32_t &e
     }
 }
 
-template <int QMAX, int... G>
-__device__ __forceinline__ void pc_row(std::integer_sequence<int, G...>, uint32_t (&hh)[QMAX / 2],
+template <int QMAX, int G>
+__device__ __forceinline__ void pc_group_if(uint32_t (&hh)[QMAX / 2], uint32_t (&ee)[QMAX / 2],
+                                            const uint32_t (&qs)[QMAX / 4], uint32_t plo, uint32_t phi, int &f,
+                                            int &h1, uint32_t &key, uint32_t oe2, uint32_t ed2, int ed,
+                                            const PcRow &r, uint32_t endw, uint32_t endm1w, uint32_t begm2w, int endv,
+                                            int begv, uint32_t (&ctr)[4])
+{
+    if constexpr (G < QMAX / 4)
+        pc_group<G>(hh[2 * G], hh[2 * G + 1], ee[2 * G], ee[2 * G + 1], qs[G], plo, phi, f, h1, key, oe2, ed2, ed,
+                    r, endw, endm1w, begm2w, endv, begv, ctr);
+}
+
+// Segments of 8 groups behind one uniform test of the row's entered set: a segment no lane's
+// band touches costs one s_and + branch instead of 8 x (FAST test + skip test + 2 branches)
+constexpr int kPcSeg = 8;
+template <int QMAX, int S, int... K>
+__device__ __forceinline__ void pc_seg(std::integer_sequence<int, K...>, uint32_t (&hh)[QMAX / 2],
+                                       uint32_t (&ee)[QMAX / 2], const uint32_t (&qs)[QMAX / 4], uint32_t plo,
+                                       uint32_t phi, int &f, int &h1, uint32_t &key, uint32_t oe2, uint32_t ed2,
+                                       int ed, const PcRow &r, uint32_t endw, uint32_t endm1w, uint32_t begm2w,
+                                       int endv, int begv, uint32_t (&ctr)[4])
+{
+    constexpr uint64_t kSegMask = ((1ull << kPcSeg) - 1) << (kPcSeg * S);
+    if (r.enter & kSegMask)
+        (pc_group_if<QMAX, kPcSeg * S + K>(hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r, endw, endm1w, begm2w,
+                                           endv, begv, ctr), ...);
+}
+
+template <int QMAX, int... S>
+__device__ __forceinline__ void pc_row(std::integer_sequence<int, S...>, uint32_t (&hh)[QMAX / 2],
                                        uint32_t (&ee)[QMAX / 2], const uint32_t (&qs)[QMAX / 4],
                                        uint32_t plo, uint32_t phi, int &f, int &h1, uint32_t &key,
                                        uint32_t oe2, uint32_t ed2, int ed, const PcRow &r,
                                        uint32_t endw, uint32_t endm1w, uint32_t begm2w, int endv,
                                        int begv, uint32_t (&ctr)[4])
 {
-    (pc_group<G>(hh[2 * G], hh[2 * G + 1], ee[2 * G], ee[2 * G + 1], qs[G], plo, phi, f, h1, key,
-                 oe2, ed2, ed, r, endw, endm1w, begm2w, endv, begv, ctr), ...);
+    (pc_seg<QMAX, S>(std::make_integer_sequence<int, kPcSeg>{}, hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r,
+                     endw, endm1w, begm2w, endv, begv, ctr), ...);
 }
 
 // Lazy last positive column: when H(i, end-1) == 0 the lanes that need it
@@ -471,7 +499,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             const uint32_t endw = pack2(end);
             const uint32_t endm1w = pack2(end - 1);                         // end = 0: {-1, -1}
             const uint32_t begm2w = pack2(beg - 2);
-            pc_row<QMAX>(std::make_integer_sequence<int, NG>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
+            pc_row<QMAX>(std::make_integer_sequence<int, (NG + kPcSeg - 1) / kPcSeg>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
                          oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg, ctr);
             h1 = (int)((uint32_t)h1 >> 16);               // H(i, end-1)
             const uint32_t k32 = max(key & 0xffffu, key >> 16);
