@@ -81,4 +81,11 @@ $(LIBDIR)/bsw_pc_stats.o: $(CSRC)/bsw_pc.hip $(HIP_HDRS) | $(LIBDIR)
 $(STATSLIB): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_stats.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_batch.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
-.PHONY: all product synth oracle clean stats
+# experiment build: the product with bsw_pc.hip compiled under AB_FLAGS (tools/gpu_ab.sh A/B runs)
+ABLIB := $(LIBDIR)/libbsw_hip_ab.so
+AB_FLAGS ?=
+ab:
+	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/bsw_pc.hip -o $(LIBDIR)/bsw_pc_ab.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(ABLIB) $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_ab.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_batch.o -lpthread
+
+.PHONY: all product synth oracle clean stats ab

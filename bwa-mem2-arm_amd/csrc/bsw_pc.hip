@@ -269,7 +269,13 @@ __device__ __forceinline__ void pc_group_if(uint32_t (&hh)[QMAX / 2], uint32_t (
 
 // Segments of 8 groups behind one uniform test of the row's entered set: a segment no lane's
 // band touches costs one s_and + branch instead of 8 x (FAST test + skip test + 2 branches)
-constexpr int kPcSeg = 8;
+// (one segment, no test, for QMAX <= 64: the tests' registers would cost the 64 class its
+// fourth wave per SIMD, 127 -> 137 VGPRs)
+#ifndef BSW_PC_SEG             // experiment builds (make ab AB_FLAGS=-DBSW_PC_SEG=4) only
+#define BSW_PC_SEG 8
+#endif
+constexpr int kPcSeg = BSW_PC_SEG;
+template <int QMAX> constexpr int pc_seg_len() { return QMAX <= 64 ? QMAX / 4 : kPcSeg; }
 template <int QMAX, int S, int... K>
 __device__ __forceinline__ void pc_seg(std::integer_sequence<int, K...>, uint32_t (&hh)[QMAX / 2],
                                        uint32_t (&ee)[QMAX / 2], const uint32_t (&qs)[QMAX / 4], uint32_t plo,
@@ -277,9 +283,10 @@ __device__ __forceinline__ void pc_seg(std::integer_sequence<int, K...>, uint32_
                                        int ed, const PcRow &r, uint32_t endw, uint32_t endm1w, uint32_t begm2w,
                                        int endv, int begv, uint32_t (&ctr)[4])
 {
-    constexpr uint64_t kSegMask = ((1ull << kPcSeg) - 1) << (kPcSeg * S);
-    if (r.enter & kSegMask)
-        (pc_group_if<QMAX, kPcSeg * S + K>(hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r, endw, endm1w, begm2w,
+    constexpr int kSeg = sizeof...(K);
+    constexpr uint64_t kSegMask = ((1ull << kSeg) - 1) << (kSeg * S);
+    if (kSeg == QMAX / 4 || (r.enter & kSegMask))
+        (pc_group_if<QMAX, kSeg * S + K>(hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r, endw, endm1w, begm2w,
                                            endv, begv, ctr), ...);
 }
 
@@ -291,7 +298,7 @@ __device__ __forceinline__ void pc_row(std::integer_sequence<int, S...>, uint32_
                                        uint32_t endw, uint32_t endm1w, uint32_t begm2w, int endv,
                                        int begv, uint32_t (&ctr)[4])
 {
-    (pc_seg<QMAX, S>(std::make_integer_sequence<int, kPcSeg>{}, hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r,
+    (pc_seg<QMAX, S>(std::make_integer_sequence<int, pc_seg_len<QMAX>()>{}, hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r,
                      endw, endm1w, begm2w, endv, begv, ctr), ...);
 }
 
@@ -499,7 +506,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             const uint32_t endw = pack2(end);
             const uint32_t endm1w = pack2(end - 1);                         // end = 0: {-1, -1}
             const uint32_t begm2w = pack2(beg - 2);
-            pc_row<QMAX>(std::make_integer_sequence<int, (NG + kPcSeg - 1) / kPcSeg>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
+            pc_row<QMAX>(std::make_integer_sequence<int, (NG + pc_seg_len<QMAX>() - 1) / pc_seg_len<QMAX>()>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
                          oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg, ctr);
             h1 = (int)((uint32_t)h1 >> 16);               // H(i, end-1)
             const uint32_t k32 = max(key & 0xffffu, key >> 16);
