@@ -336,6 +336,7 @@ struct bsw_ctx {
     int glob_band = 0;                  // BSW_OPT_GLOB_BAND
     int64_t ext_chunk = 0;              // BSW_OPT_EXT_CHUNK (0: the int32-offset bound)
     int32_t host_chunk = 262144;        // BSW_OPT_HOST_CHUNK: pairs per host-buffer pipeline chunk
+    int host_pack = 2;                  // BSW_OPT_HOST_PACK: 2-bit (2) or nibble (4) staging
     ~bsw_ctx()
     {
         for (auto &b : pin)
@@ -576,36 +577,6 @@ static int finish_stats(Slot &s)
     return BSW_OK;
 }
 
-// 4-bit packing of base codes for the host -> device copy: staged byte k = code[2k] |
-// code[2k+1] << 4 (codes 0..4 in the ABI; the low nibble of any code is kept).  Halves the
-// PCIe bytes of the sequences; unpack_kernel restores the byte-per-base buffers in HBM.
-static void pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes)
-{
-    size_t i = 0;
-    const __m128i m0 = _mm_set1_epi16(0x000f), m1 = _mm_set1_epi16(0x00f0);
-    // streaming (non-temporal) stores into the pinned staging buffer when it is 16-B aligned: no
-    // read-for-ownership of destination lines the CPU never reads again (the DMA engine does)
-    if (((uintptr_t)dst & 15) == 0) {
-        for (; i + 32 <= nbytes; i += 32) {
-            const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
-            const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
-            const __m128i ra = _mm_or_si128(_mm_and_si128(a, m0), _mm_and_si128(_mm_srli_epi16(a, 4), m1));
-            const __m128i rb = _mm_or_si128(_mm_and_si128(b, m0), _mm_and_si128(_mm_srli_epi16(b, 4), m1));
-            _mm_stream_si128((__m128i *)(dst + i / 2), _mm_packus_epi16(ra, rb));
-        }
-        _mm_sfence();
-    }
-    for (; i + 32 <= nbytes; i += 32) {
-        const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
-        const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
-        const __m128i ra = _mm_or_si128(_mm_and_si128(a, m0), _mm_and_si128(_mm_srli_epi16(a, 4), m1));
-        const __m128i rb = _mm_or_si128(_mm_and_si128(b, m0), _mm_and_si128(_mm_srli_epi16(b, 4), m1));
-        _mm_storeu_si128((__m128i *)(dst + i / 2), _mm_packus_epi16(ra, rb));
-    }
-    for (; i < nbytes; i += 2)
-        dst[i / 2] = (uint8_t)((src[i] & 15) | (i + 1 < nbytes ? (src[i + 1] & 15) << 4 : 0));
-}
-
 static void par_pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes)
 {
     constexpr size_t kPiece = (size_t)2 << 20;
@@ -640,6 +611,69 @@ __global__ void unpack_kernel(const uint8_t *__restrict__ in, uint8_t *__restric
                               (uint8_t)w1, (uint8_t)(w1 >> 8), (uint8_t)(w1 >> 16), (uint8_t)(w1 >> 24)};
         for (int k = 0; o + k < n; ++k) out[o + k] = b[k];
     }
+}
+
+// bytes out[0, n) from 2-bit codes in[0, (n + 3) / 4): 4 packed bytes -> 16 codes per thread
+__global__ void unpack2_kernel(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int64_t n)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t o = t * 16;
+    if (o >= n) return;
+    uint32_t v = 0;
+    const int64_t ib = t * 4, nin = (n + 3) / 4;
+    if (ib + 4 <= nin) v = *(const uint32_t *)(in + ib);
+    else
+        for (int k = 0; k < 4 && ib + k < nin; ++k) v |= (uint32_t)in[ib + k] << (8 * k);
+    // plane p holds code 4m + p in byte m; output dword m = byte m of planes 0..3
+    const uint32_t p0 = v & 0x03030303u, p1 = (v >> 2) & 0x03030303u;
+    const uint32_t p2 = (v >> 4) & 0x03030303u, p3 = (v >> 6) & 0x03030303u;
+    const uint32_t a01 = __builtin_amdgcn_perm(p1, p0, 0x05010400u), b01 = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
+    const uint32_t a23 = __builtin_amdgcn_perm(p3, p2, 0x05010400u), b23 = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
+    const uint4 r = make_uint4(__builtin_amdgcn_perm(a23, a01, 0x05040100u), __builtin_amdgcn_perm(a23, a01, 0x07060302u),
+                               __builtin_amdgcn_perm(b23, b01, 0x05040100u), __builtin_amdgcn_perm(b23, b01, 0x07060302u));
+    if (o + 16 <= n) {
+        *(uint4 *)(out + o) = r;
+    } else {
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+        for (int k = 0; o + k < n; ++k) out[o + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+}
+
+// exception words of a 2-bit chunk: the first n_r patch ref, the rest qer
+__global__ void patch_codes_kernel(const uint32_t *__restrict__ exc, int32_t n_r, int32_t n_all,
+                                   uint8_t *__restrict__ ref, uint8_t *__restrict__ qer)
+{
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_all) return;
+    const uint32_t e = exc[t];
+    (t < n_r ? ref : qer)[e >> 4] = (uint8_t)(e & 15u);
+}
+
+// the kernels' input fields of a SeqPair, staged without the caller bookkeeping and outputs
+struct PairIn {
+    int32_t idr, idq, len1, len2, h0;
+};
+static_assert(sizeof(PairIn) == 20, "PairIn");
+
+__global__ void expand_pairs_kernel(const PairIn *__restrict__ in, SeqPair *__restrict__ out, int32_t n)
+{
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const PairIn p = in[i];
+    SeqPair sp;
+    memset(&sp, 0, sizeof(sp));
+    sp.idr = p.idr; sp.idq = p.idq; sp.len1 = p.len1; sp.len2 = p.len2; sp.h0 = p.h0;
+    out[i] = sp;
+}
+
+// the six outputs of each pair (SeqPair bytes 32..55) -> 24 B per pair for the D2H
+__global__ void gather_outputs_kernel(const SeqPair *__restrict__ in, int32_t *__restrict__ out, int32_t n)
+{
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SeqPair &p = in[i];
+    int32_t *o = out + 6 * (int64_t)i;
+    o[0] = p.score; o[1] = p.tle; o[2] = p.gtle; o[3] = p.qle; o[4] = p.gscore; o[5] = p.max_off;
 }
 
 // Pre-pass of a host-buffer call, one parallel sweep over the records: validation (the ABI's
@@ -682,20 +716,85 @@ static bool prepass(const SeqPair *pairs, int32_t n, std::vector<BlkStat> &bs)
 
 // One chunk of a host-buffer call staged in a slot's pinned buffer: [SeqPair x n | ref | qer].
 // Contiguous chunks (the upstream layout: each batch's windows concatenated in pair order) pack
-// their byte extents into nibbles (unpacked in HBM by unpack_kernel); scattered ones are
+// their byte extents into 2-bit codes + exception words, with the records cut to their five
+// input fields (20 of 56 B) and only the 24 output bytes coming back -- or into nibbles with
+// whole records when the chunk holds too many non-ACGT bytes; scattered ones are
 // gathered pair by pair as bytes and the staged records' idr / idq rewritten (only outputs
 // ever go back to the caller).
+enum StageMode { kStageGather = 0, kStageNibble = 1, kStage2bit = 2 };
 struct StagedChunk {
     int32_t n = 0;
-    bool packed = false;
-    size_t pair_off = 0, ref_off = 0, qer_off = 0, bytes = 0;
+    int mode = kStageGather;
+    bool packed = false;                // bulk extents (nibble or 2-bit)
+    size_t pair_off = 0, ref_off = 0, qer_off = 0, exc_off = 0, bytes = 0;
+    int32_t n_exr = 0, n_exq = 0;       // 2-bit: exception words for ref / qer
     size_t rb = 0, qb = 0;              // ref / qer bytes after unpacking
     int64_t r_base = 0, q_base = 0;     // staged ref byte 0 = caller byte r_base (bulk mode)
 };
 
 // blocks [b0, b1) = pairs [a, a + n)
+// 2-bit staging of a bulk chunk: [PairIn x n | ref codes | qer codes | exception words], sized
+// for at least the 24 B per pair of outputs that come back through the same buffers.  Returns 1
+// (nothing staged) when the exception words would pass 1/32 of the bytes.
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+static int stage_2bit(Slot &s, const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t n,
+                      StagedChunk &c)
+{
+    const size_t rs = (c.rb + 3) / 4, qs = (c.qb + 3) / 4;
+    const size_t exc_cap = (c.rb + c.qb) / 32 + 1024;
+    c.pair_off = 0;
+    c.ref_off = align256((size_t)n * sizeof(PairIn));
+    c.qer_off = align256(c.ref_off + rs + 4);          // +4: the unpack's dword loads
+    c.exc_off = align256(c.qer_off + qs + 4);
+    c.bytes = std::max(c.exc_off + exc_cap * 4, (size_t)n * 24);
+    if (c.bytes > s.cap_stage) {
+        const size_t cap = std::max(c.bytes, s.cap_stage * 3 / 2);
+        if (s.h_stage) (void)hipHostFree(s.h_stage);
+        s.h_stage = nullptr; s.cap_stage = 0;
+        BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));
+        s.cap_stage = cap;
+    }
+    uint8_t *h = (uint8_t *)s.h_stage;
+    PairIn *pin = (PairIn *)(h + c.pair_off);
+    const int np = (int)std::max<size_t>(1, ((size_t)n * sizeof(SeqPair)) >> 21);
+    const int nr = (int)std::max<size_t>(1, c.rb >> 22), nq = (int)std::max<size_t>(1, c.qb >> 22);
+    auto even = [](size_t total, int k, int parts) {     // piece bounds: multiples of 64 codes
+        return k == parts ? total : (total * (size_t)k / (size_t)parts) & ~(size_t)63;
+    };
+    std::vector<std::vector<uint32_t>> ex((size_t)(nr + nq));
+    HostPool::get().parallel_for(np + nr + nq, [&](int t) {
+        if (t < np) {
+            const int32_t a0 = (int32_t)((int64_t)n * t / np), a1 = (int32_t)((int64_t)n * (t + 1) / np);
+            for (int32_t i = a0; i < a1; ++i)
+                pin[i] = PairIn{pairs[i].idr, pairs[i].idq, pairs[i].len1, pairs[i].len2, pairs[i].h0};
+        } else if (t < np + nr) {
+            const size_t a0 = even(c.rb, t - np, nr), a1 = even(c.rb, t - np + 1, nr);
+            pack_2bit(h + c.ref_off + a0 / 4, ref + a0, a1 - a0, (uint32_t)a0, ex[(size_t)(t - np)]);
+        } else {
+            const size_t a0 = even(c.qb, t - np - nr, nq), a1 = even(c.qb, t - np - nr + 1, nq);
+            pack_2bit(h + c.qer_off + a0 / 4, qer + a0, a1 - a0, (uint32_t)a0, ex[(size_t)(t - np)]);
+        }
+    });
+    size_t tot = 0, tr = 0;
+    for (size_t k = 0; k < ex.size(); ++k) {
+        tot += ex[k].size();
+        if (k < (size_t)nr) tr += ex[k].size();
+    }
+    if (tot > exc_cap) return 1;
+    uint32_t *exw = (uint32_t *)(h + c.exc_off);
+    for (size_t k = 0, o = 0; k < ex.size(); o += ex[k].size(), ++k)
+        if (!ex[k].empty()) memcpy(exw + o, ex[k].data(), ex[k].size() * 4);
+    c.n_exr = (int32_t)tr;
+    c.n_exq = (int32_t)(tot - tr);
+    c.mode = kStage2bit;
+    c.bytes = std::max(c.exc_off + tot * 4, (size_t)n * 24);
+    memset(h + c.ref_off + rs, 0, 4);
+    memset(h + c.qer_off + qs, 0, 4);
+    return BSW_OK;
+}
+
 static int stage_chunk(Slot &s, const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t n,
-                       const BlkStat *bs, int32_t nblk, StagedChunk &c)
+                       const BlkStat *bs, int32_t nblk, bool two_bit, StagedChunk &c)
 {
     int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
     for (int32_t b = 0; b < nblk; ++b) {
@@ -709,6 +808,15 @@ static int stage_chunk(Slot &s, const SeqPair *pairs, const uint8_t *ref, const 
     c.rb = (size_t)(bulk ? r_hi - r_lo : r_sum);
     c.qb = (size_t)(bulk ? q_hi - q_lo : q_sum);
     c.packed = bulk;
+    c.n = n;
+    if (bulk && two_bit && c.rb < ((size_t)1 << 28) && c.qb < ((size_t)1 << 28)) {
+        const int r = stage_2bit(s, pairs, ref + r_lo, qer + q_lo, n, c);
+        if (r != 1) {                       // 1: too many exception bytes -> nibbles below
+            c.r_base = r_lo; c.q_base = q_lo;
+            return r;
+        }
+    }
+    c.mode = bulk ? kStageNibble : kStageGather;
     const size_t rs = bulk ? (c.rb + 1) / 2 : c.rb, qs = bulk ? (c.qb + 1) / 2 : c.qb;   // staged sizes
     c.n = n;
     c.pair_off = 0;
@@ -765,10 +873,22 @@ static int stage_chunk(Slot &s, const SeqPair *pairs, const uint8_t *ref, const 
 // outputs of a finished chunk (staged records) -> the caller's records.  Bulk-staged records
 // carry the caller's own input fields, so whole records copy back; gathered ones had their
 // offsets rewritten and copy field by field.
-static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, bool whole)
+static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, int mode)
 {
+    if (mode == kStage2bit) {                           // 24 B of outputs per pair
+        const int32_t *o = (const int32_t *)s.h_stage;
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(HostPool::workers() + 1, n >> 15));
+        HostPool::get().parallel_for(nt, [&](int t) {
+            for (int32_t i = (int32_t)((int64_t)n * t / nt); i < (int32_t)((int64_t)n * (t + 1) / nt); ++i) {
+                const int32_t *q = o + 6 * (int64_t)i;
+                pairs[i].score = q[0]; pairs[i].tle = q[1]; pairs[i].gtle = q[2];
+                pairs[i].qle = q[3]; pairs[i].gscore = q[4]; pairs[i].max_off = q[5];
+            }
+        });
+        return;
+    }
     const SeqPair *sp = (const SeqPair *)s.h_stage;
-    if (whole) {
+    if (mode == kStageNibble) {
         par_memcpy(pairs, sp, (size_t)n * sizeof(SeqPair));
         return;
     }
@@ -788,7 +908,7 @@ static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, bool whole
 // rocprofv3 timeline).  Chunks ramp from ~n/32 pairs up to `chunk` so the first kernels start
 // early.  Outputs are identical to one unchunked call (pairs are independent).
 static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref,
-                      const uint8_t *qer, int32_t n, int32_t w, int cell_bits, int32_t chunk,
+                      const uint8_t *qer, int32_t n, int32_t w, int cell_bits, int32_t chunk, bool two_bit,
                       bsw_stats_t *st)
 {
     if (n == 0) return BSW_OK;
@@ -804,13 +924,14 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     if (rc) return rc;
     int32_t pend_at[nslots] = {}, pend_n[nslots] = {};  // chunk in flight per slot
     int32_t pend_seq[nslots] = {-1, -1, -1};
-    bool pend_whole[nslots] = {};
+    int pend_mode[nslots] = {};
     bsw_stats_t agg{};
     // launcher thread: chunk seq numbers in order; launched[k] = last seq whose DP is enqueued
     struct Launcher {
         std::mutex mu;
         std::condition_variable cv;
-        std::deque<std::pair<int, int32_t>> q;    // (slot, seq)
+        struct Job { int first; int32_t second; int mode; };
+        std::deque<Job> q;                        // (slot, seq, staging mode)
         int32_t launched[nslots] = {-1, -1, -1};
         bool stop = false;
         int rc = BSW_OK;
@@ -818,7 +939,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     std::thread launcher([&] {
         const bool dev_ok = hipSetDevice(dc.device) == hipSuccess;
         for (;;) {
-            std::pair<int, int32_t> job;
+            Launcher::Job job;
             {
                 std::unique_lock<std::mutex> lk(L.mu);
                 L.cv.wait(lk, [&] { return L.stop || !L.q.empty(); });
@@ -833,9 +954,17 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
             }
             Slot &p = *slots[job.first];
             if (!r) r = run_dp(kp, p);
-            if (!r && hipMemcpyAsync(p.h_stage, p.plan.d_pairs, (size_t)p.plan.n * sizeof(SeqPair),
-                                     hipMemcpyDeviceToHost, p.stream) != hipSuccess)
+            if (!r && job.mode == kStage2bit) {        // outputs only: 24 B per pair
+                const int32_t m = p.plan.n;
+                hipLaunchKernelGGL(gather_outputs_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, p.stream,
+                                   p.plan.d_pairs, (int32_t *)p.d_stage, m);
+                if (hipGetLastError() != hipSuccess ||
+                    hipMemcpyAsync(p.h_stage, p.d_stage, (size_t)m * 24, hipMemcpyDeviceToHost, p.stream) != hipSuccess)
+                    r = BSW_E_HIP;
+            } else if (!r && hipMemcpyAsync(p.h_stage, p.plan.d_pairs, (size_t)p.plan.n * sizeof(SeqPair),
+                                            hipMemcpyDeviceToHost, p.stream) != hipSuccess) {
                 r = BSW_E_HIP;
+            }
             {
                 std::lock_guard<std::mutex> g(L.mu);
                 if (r && !L.rc) L.rc = r;
@@ -862,7 +991,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         Slot &s = *slots[k];
         const int r = finish_stats(s);                  // also BSW_E_RANGE: kernel guard tripped
         if (r) return r;
-        unstage_outputs(s, pairs + pend_at[k], pend_n[k], pend_whole[k]);
+        unstage_outputs(s, pairs + pend_at[k], pend_n[k], pend_mode[k]);
         agg.kernel_ms += s.stats.kernel_ms;
         agg.n_i16 += s.stats.n_i16; agg.n_u8 += s.stats.n_u8; agg.n_wide += s.stats.n_wide;
         agg.n_packed += s.stats.n_packed; agg.n_launches += s.stats.n_launches; agg.n_wave += s.stats.n_wave;
@@ -896,12 +1025,36 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
             Slot &s = *slots[k];
             StagedChunk c;
             const auto t0 = now();
-            if ((r = stage_chunk(s, pairs + a, ref, qer, m, bs.data() + b, nb, c))) return r;
+            if ((r = stage_chunk(s, pairs + a, ref, qer, m, bs.data() + b, nb, two_bit, c))) return r;
             stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
             BSW_TRY(grow(s.d_stage, s.cap_dstage, c.bytes));
             BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.bytes, hipMemcpyHostToDevice, s.stream));
             const uint8_t *d_r = s.d_stage + c.ref_off, *d_q = s.d_stage + c.qer_off;
-            if (c.packed) {                 // nibbles -> one byte per base in the slot's buffers
+            SeqPair *d_p = (SeqPair *)(s.d_stage + c.pair_off);
+            if (c.mode == kStage2bit) {     // 2-bit codes -> bytes, exceptions patched, records expanded
+                BSW_TRY(grow(s.d_ref, s.cap_ref, c.rb + 4));
+                BSW_TRY(grow(s.d_qer, s.cap_qer, c.qb + 4));
+                BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)m));
+                BSW_TRY(hipMemsetAsync(s.d_ref + c.rb, 0, 4, s.stream));
+                BSW_TRY(hipMemsetAsync(s.d_qer + c.qb, 0, 4, s.stream));
+                const int64_t tr = ((int64_t)c.rb + 15) / 16, tq = ((int64_t)c.qb + 15) / 16;
+                if (tr > 0)
+                    hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, s.stream,
+                                       d_r, s.d_ref, (int64_t)c.rb);
+                if (tq > 0)
+                    hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, s.stream,
+                                       d_q, s.d_qer, (int64_t)c.qb);
+                const int32_t ne = c.n_exr + c.n_exq;
+                if (ne > 0)
+                    hipLaunchKernelGGL(patch_codes_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s.stream,
+                                       (const uint32_t *)(s.d_stage + c.exc_off), c.n_exr, ne, s.d_ref, s.d_qer);
+                hipLaunchKernelGGL(expand_pairs_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s.stream,
+                                   (const PairIn *)(s.d_stage + c.pair_off), s.d_pairs, m);
+                BSW_TRY(hipGetLastError());
+                d_r = s.d_ref;
+                d_q = s.d_qer;
+                d_p = s.d_pairs;
+            } else if (c.packed) {          // nibbles -> one byte per base in the slot's buffers
                 BSW_TRY(grow(s.d_ref, s.cap_ref, c.rb + 4));
                 BSW_TRY(grow(s.d_qer, s.cap_qer, c.qb + 4));
                 BSW_TRY(hipMemsetAsync(s.d_ref + c.rb, 0, 4, s.stream));
@@ -918,16 +1071,16 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
                 d_q = s.d_qer;
             }
             PlanCall pc;
-            pc.d_pairs = (SeqPair *)(s.d_stage + c.pair_off);
+            pc.d_pairs = d_p;
             // kernels index ref / qer by idr / idq: shift the bases so staged byte 0 is r_base / q_base
             pc.d_ref = d_r - c.r_base;
             pc.d_qer = d_q - c.q_base;
             pc.n = m; pc.w = w; pc.cell_bits = cell_bits; pc.stream = s.stream;
             if ((r = run_plan(kp, s, pc))) return r;
-            pend_at[k] = a; pend_n[k] = m; pend_whole[k] = c.packed; pend_seq[k] = seq;
+            pend_at[k] = a; pend_n[k] = m; pend_mode[k] = c.mode; pend_seq[k] = seq;
             {
                 std::lock_guard<std::mutex> g(L.mu);
-                L.q.emplace_back(k, seq);
+                L.q.push_back(Launcher::Job{k, seq, c.mode});
             }
             L.cv.notify_all();
         }
@@ -1267,7 +1420,8 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
     std::vector<int> rcs(nd, BSW_OK);
     std::vector<bsw_stats_t> st(nd);
     if (nd == 1) {
-        rcs[0] = host_shard(kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, cell_bits, ctx->host_chunk, &st[0]);
+        rcs[0] = host_shard(kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, cell_bits, ctx->host_chunk,
+                            ctx->host_pack == 2, &st[0]);
     } else {
         // contiguous pair ranges of equal estimated work (static band cells)
         const std::vector<int32_t> cut = split_by_cells(pairs, n, w, nd);
@@ -1276,7 +1430,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
             const int32_t a = cut[d], b = cut[d + 1];
             th.emplace_back([&, d, a, b] {
                 rcs[d] = host_shard(kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a, w,
-                                    cell_bits, ctx->host_chunk, &st[d]);
+                                    cell_bits, ctx->host_chunk, ctx->host_pack == 2, &st[d]);
             });
         }
         for (auto &t : th) t.join();
@@ -1777,6 +1931,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     case BSW_OPT_EXT_CHUNK: if (value < 0) return BSW_E_INVAL; ctx->ext_chunk = value; return BSW_OK;
     case BSW_OPT_LONG: if (value < 0 || value > 2) return BSW_E_INVAL; ctx->kp.long_route = (int8_t)value; return BSW_OK;
     case BSW_OPT_HOST_CHUNK: if (value < 1 || value > INT32_MAX) return BSW_E_INVAL; ctx->host_chunk = (int32_t)value; return BSW_OK;
+    case BSW_OPT_HOST_PACK: if (value != 2 && value != 4) return BSW_E_INVAL; ctx->host_pack = (int)value; return BSW_OK;
     case BSW_OPT_TEST_MISROUTE: if (!b01) return BSW_E_INVAL; ctx->kp.misroute = (int8_t)value; return BSW_OK;
     default: return BSW_E_INVAL;
     }

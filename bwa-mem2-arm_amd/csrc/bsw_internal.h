@@ -2,6 +2,8 @@
 #pragma once
 #include "../../include/bsw.h"
 #include "../../include/bsw_ext.h"
+#include <cstdint>
+#include <vector>
 
 namespace bsw {
 // bsw_get_scores with a per-call end_bonus (LEFT uses pen_clip5, RIGHT pen_clip3) and the
@@ -36,4 +38,8 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
                         const int32_t *d_read_len, int32_t n_reads, const bsw_seed_t *d_seeds,
                         const int32_t *d_sr, const int32_t *d_sc, int32_t ns, bsw_alnreg_t *d_out, int32_t *d_ext,
                         bsw_chain_stats_t *cs);
+// staging packers (bsw_pack.cpp): nibbles (dst[k] = src[2k] & 15 | (src[2k+1] & 15) << 4) and
+// 2-bit codes + exception words (pos0 + k) << 4 | (src[k] & 15) for bytes outside 0..3
+void pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes);
+void pack_2bit(uint8_t *dst, const uint8_t *src, size_t nbytes, uint32_t pos0, std::vector<uint32_t> &exc);
 }  // namespace bsw

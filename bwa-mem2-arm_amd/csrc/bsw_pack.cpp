@@ -1,0 +1,142 @@
+// bsw_pack.cpp -- host-side code packing of the bsw_get_scores staging pipeline (bsw_host.cpp):
+// nibbles and 2-bit codes + exception words, written into the pinned staging buffer with
+// streaming stores.  Plain C++ (g++), so the AVX2 form can be selected at run time without the
+// HIP device pass seeing x86 target attributes.
+#include <emmintrin.h>
+#include <immintrin.h>
+#include <cstdint>
+#include <cstddef>
+#include <vector>
+#include "bsw_internal.h"
+
+namespace bsw {
+
+// 4-bit packing of base codes for the host -> device copy: staged byte k = code[2k] |
+// code[2k+1] << 4 (codes 0..4 in the ABI; the low nibble of any code is kept).  Halves the
+// PCIe bytes of the sequences; unpack_kernel restores the byte-per-base buffers in HBM.
+void pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes)
+{
+    size_t i = 0;
+    const __m128i m0 = _mm_set1_epi16(0x000f), m1 = _mm_set1_epi16(0x00f0);
+    // streaming (non-temporal) stores into the pinned staging buffer when it is 16-B aligned: no
+    // read-for-ownership of destination lines the CPU never reads again (the DMA engine does)
+    if (((uintptr_t)dst & 15) == 0) {
+        for (; i + 32 <= nbytes; i += 32) {
+            const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
+            const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
+            const __m128i ra = _mm_or_si128(_mm_and_si128(a, m0), _mm_and_si128(_mm_srli_epi16(a, 4), m1));
+            const __m128i rb = _mm_or_si128(_mm_and_si128(b, m0), _mm_and_si128(_mm_srli_epi16(b, 4), m1));
+            _mm_stream_si128((__m128i *)(dst + i / 2), _mm_packus_epi16(ra, rb));
+        }
+        _mm_sfence();
+    }
+    for (; i + 32 <= nbytes; i += 32) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
+        const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
+        const __m128i ra = _mm_or_si128(_mm_and_si128(a, m0), _mm_and_si128(_mm_srli_epi16(a, 4), m1));
+        const __m128i rb = _mm_or_si128(_mm_and_si128(b, m0), _mm_and_si128(_mm_srli_epi16(b, 4), m1));
+        _mm_storeu_si128((__m128i *)(dst + i / 2), _mm_packus_epi16(ra, rb));
+    }
+    for (; i < nbytes; i += 2)
+        dst[i / 2] = (uint8_t)((src[i] & 15) | (i + 1 < nbytes ? (src[i + 1] & 15) << 4 : 0));
+}
+
+// 2-bit packing (round 2): staged byte k = code[4k] | code[4k+1] << 2 | code[4k+2] << 4 |
+// code[4k+3] << 6 (low two bits), plus an exception word (pos << 4 | low nibble) for every
+// byte outside 0..3 (N bases: 0.1% on C2), patched in HBM after the 2-bit unpack -- the same
+// bytes in HBM as the nibble path, at a quarter of the byte-per-base PCIe traffic.
+static inline __m128i pack2_lanes(__m128i x)      // 4 codes per dword -> one byte (low byte)
+{
+    x = _mm_and_si128(x, _mm_set1_epi8(3));
+    x = _mm_or_si128(x, _mm_srli_epi32(x, 6));     // bits 0-3: c0 | c1 << 2; bits 16-19: c2 | c3 << 2
+    x = _mm_or_si128(x, _mm_srli_epi32(x, 12));    // bits 4-7: c2 | c3 << 2
+    return _mm_and_si128(x, _mm_set1_epi32(0xff));
+}
+
+static void pack_2bit_sse2(uint8_t *dst, const uint8_t *src, size_t nbytes, uint32_t pos0, std::vector<uint32_t> &exc)
+{
+    auto scan = [&](size_t a, size_t b) {
+        for (size_t k = a; k < b; ++k)
+            if (src[k] & 0xfc) exc.push_back(((pos0 + (uint32_t)k) << 4) | (src[k] & 15u));
+    };
+    const __m128i hi = _mm_set1_epi8((char)0xfc), z = _mm_setzero_si128();
+    const bool nt = ((uintptr_t)dst & 15) == 0;      // streaming stores (see pack_nibbles)
+    size_t i = 0;
+    for (; i + 64 <= nbytes; i += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
+        const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i *)(src + i + 32));
+        const __m128i d = _mm_loadu_si128((const __m128i *)(src + i + 48));
+        const __m128i o = _mm_or_si128(_mm_or_si128(a, b), _mm_or_si128(c, d));
+        if (_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_and_si128(o, hi), z)) != 0xffff) scan(i, i + 64);
+        const __m128i r = _mm_packus_epi16(_mm_packs_epi32(pack2_lanes(a), pack2_lanes(b)),
+                                           _mm_packs_epi32(pack2_lanes(c), pack2_lanes(d)));
+        if (nt) _mm_stream_si128((__m128i *)(dst + i / 4), r);
+        else _mm_storeu_si128((__m128i *)(dst + i / 4), r);
+    }
+    if (nt) _mm_sfence();
+    scan(i, nbytes);
+    for (; i < nbytes; i += 4) {
+        uint32_t v = 0;
+        for (size_t k = 0; k < 4 && i + k < nbytes; ++k) v |= (uint32_t)(src[i + k] & 3u) << (2 * k);
+        dst[i / 4] = (uint8_t)v;
+    }
+}
+
+
+// AVX2 form: 128 codes -> 32 bytes per step.  Codes are masked to 2 bits and each dword's four
+// codes multiplied into its top byte: x * (2^24 + 2^18 + 2^12 + 2^6) puts c0 | c1 << 2 |
+// c2 << 4 | c3 << 6 in bits 24..31 (the cross terms stay below 2^24, no carry).  Exceptions come
+// from a per-vector byte mask (one bit per non-ACGT byte), visited bit by bit.
+__attribute__((target("avx2"))) static inline void exc_avx2(__m256i v, const uint8_t *src, size_t at, uint32_t pos0,
+                                                           std::vector<uint32_t> &exc)
+{
+    uint32_t m = ~(uint32_t)_mm256_movemask_epi8(
+        _mm256_cmpeq_epi8(_mm256_and_si256(v, _mm256_set1_epi8((char)0xfc)), _mm256_setzero_si256()));
+    while (m) {
+        const size_t k = at + (size_t)__builtin_ctz(m);
+        exc.push_back(((pos0 + (uint32_t)k) << 4) | (src[k] & 15u));
+        m &= m - 1;
+    }
+}
+
+__attribute__((target("avx2"))) static void pack_2bit_avx2(uint8_t *dst, const uint8_t *src, size_t nbytes,
+                                                          uint32_t pos0, std::vector<uint32_t> &exc)
+{
+    const __m256i m3 = _mm256_set1_epi8(3), hi = _mm256_set1_epi8((char)0xfc);
+    const __m256i mul = _mm256_set1_epi32(0x01041040);
+    const __m256i perm = _mm256_setr_epi32(0, 4, 1, 5, 2, 6, 3, 7);
+    const bool nt = ((uintptr_t)dst & 31) == 0;
+    size_t i = 0;
+    for (; i + 128 <= nbytes; i += 128) {
+        __m256i a = _mm256_loadu_si256((const __m256i *)(src + i));
+        __m256i b = _mm256_loadu_si256((const __m256i *)(src + i + 32));
+        __m256i c = _mm256_loadu_si256((const __m256i *)(src + i + 64));
+        __m256i d = _mm256_loadu_si256((const __m256i *)(src + i + 96));
+        const __m256i o = _mm256_or_si256(_mm256_or_si256(a, b), _mm256_or_si256(c, d));
+        if (!_mm256_testz_si256(o, hi)) {
+            exc_avx2(a, src, i, pos0, exc); exc_avx2(b, src, i + 32, pos0, exc);
+            exc_avx2(c, src, i + 64, pos0, exc); exc_avx2(d, src, i + 96, pos0, exc);
+        }
+        a = _mm256_srli_epi32(_mm256_mullo_epi32(_mm256_and_si256(a, m3), mul), 24);
+        b = _mm256_srli_epi32(_mm256_mullo_epi32(_mm256_and_si256(b, m3), mul), 24);
+        c = _mm256_srli_epi32(_mm256_mullo_epi32(_mm256_and_si256(c, m3), mul), 24);
+        d = _mm256_srli_epi32(_mm256_mullo_epi32(_mm256_and_si256(d, m3), mul), 24);
+        // per 128-bit half: [a b c d] dwords of half 0, then of half 1 -> a0 a1 b0 b1 c0 c1 d0 d1
+        const __m256i r = _mm256_permutevar8x32_epi32(
+            _mm256_packus_epi16(_mm256_packus_epi32(a, b), _mm256_packus_epi32(c, d)), perm);
+        if (nt) _mm256_stream_si256((__m256i *)(dst + i / 4), r);
+        else _mm256_storeu_si256((__m256i *)(dst + i / 4), r);
+    }
+    if (nt) _mm_sfence();
+    if (i < nbytes) pack_2bit_sse2(dst + i / 4, src + i, nbytes - i, pos0 + (uint32_t)i, exc);
+}
+
+void pack_2bit(uint8_t *dst, const uint8_t *src, size_t nbytes, uint32_t pos0, std::vector<uint32_t> &exc)
+{
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) pack_2bit_avx2(dst, src, nbytes, pos0, exc);
+    else pack_2bit_sse2(dst, src, nbytes, pos0, exc);
+}
+
+}  // namespace bsw

@@ -126,6 +126,11 @@ enum {
                                  a host-buffer call is staged, copied and computed chunk by
                                  chunk over up to three streams so copies overlap the DP
                                  kernels; calls of <= 128K pairs run as one chunk            */
+    BSW_OPT_HOST_PACK = 8,    /* bsw_get_scores staging of contiguous sequence buffers: 2 = 2-bit
+                                 codes + exception words for bytes outside 0..3, 20-B input
+                                 records, 24-B outputs back (default); 4 = nibbles + whole
+                                 records (also the automatic fallback for chunks with > 1/32
+                                 non-ACGT bytes); outputs are identical                      */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };

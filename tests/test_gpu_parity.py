@@ -294,6 +294,25 @@ def test_host_pipeline_chunks(chunk):
     e.close()
 
 
+@pytest.mark.parametrize("pack,p_n", [(2, 0.0), (2, 0.02), (2, 0.1), (4, 0.02)])
+def test_host_pipeline_packing(pack, p_n):
+    """Staging of contiguous sequence buffers (BSW_OPT_HOST_PACK): 2-bit codes + exception words
+    for N bytes, 20-B input records and 24-B outputs back (default), or nibbles + whole records.
+    p_n = 0.1 puts more than 1/32 of the bytes outside 0..3, so those chunks fall back to nibbles.
+    Odd extents (lengths 0..331) exercise the unpack tails; outputs equal the oracle either way and
+    the caller's input fields are untouched."""
+    e = bsw.Engine(host_chunk=8192, host_pack=pack)
+    pairs, ref, qer = bswgen.random_pairs(20000, seed=int(p_n * 1000) + pack, qlen=(0, 190), tlen=(0, 331), p_n=p_n)
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    got = pairs.copy()
+    e.get_scores(got, ref, qer, 100)
+    _assert_same(want, got, f"pack {pack} p_n {p_n}")
+    for f in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid"):
+        assert np.array_equal(got[f], pairs[f])
+    e.close()
+
+
 def test_multi_gpu_context_shards(c2_full):
     pairs, ref, qer, want = c2_full
     n = hiprt.device_count()
