@@ -380,6 +380,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.misroute = 0;
     kp.fork = 1;
     kp.long_route = 1;
+    kp.small_batch = 16384;
 }
 
 // keys / keys2 / vals / order (radix-sort buffers) grow together
@@ -433,8 +434,13 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     // fewer instructions per cell), the rest the int16 lane kernel (on cell_bits = 8: the
     // overflow fallback) or the int32 wide kernel
     const int pc_route = (kp.pk_ok && kp.kern8) ? 1 : 0;
+    // small batches (upstream's kt_for workers hand over a few thousand pairs per call): one
+    // lane-per-pair wave lives ~1.2 ms whatever the batch size, so they are latency-bound; the
+    // wave-per-alignment kernel spreads each pair over 64 lanes -- 0.35 vs 1.39 ms per call at
+    // 1K C2 pairs, 1.05 vs 1.58 at 10K, slower past ~20K
+    const int32_t long_route = (kp.long_route == 1 && n <= kp.small_batch) ? 2 : kp.long_route;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       pc.d_pairs, n, kp, pc.w, pc_route, (int32_t)kp.long_route, pc.d_ref, pc.d_qer, s.d_keys,
+                       pc.d_pairs, n, kp, pc.w, pc_route, long_route, pc.d_ref, pc.d_qer, s.d_keys,
                        s.d_vals, d_counts, d_maxq, (int)kp.keymode, (int)kp.misroute);
     BSW_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
@@ -1932,6 +1938,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     case BSW_OPT_LONG: if (value < 0 || value > 2) return BSW_E_INVAL; ctx->kp.long_route = (int8_t)value; return BSW_OK;
     case BSW_OPT_HOST_CHUNK: if (value < 1 || value > INT32_MAX) return BSW_E_INVAL; ctx->host_chunk = (int32_t)value; return BSW_OK;
     case BSW_OPT_HOST_PACK: if (value != 2 && value != 4) return BSW_E_INVAL; ctx->host_pack = (int)value; return BSW_OK;
+    case BSW_OPT_SMALL_BATCH: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.small_batch = (int32_t)value; return BSW_OK;
     case BSW_OPT_TEST_MISROUTE: if (!b01) return BSW_E_INVAL; ctx->kp.misroute = (int8_t)value; return BSW_OK;
     default: return BSW_E_INVAL;
     }

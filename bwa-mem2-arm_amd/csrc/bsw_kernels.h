@@ -34,6 +34,9 @@ struct KParams {
     int8_t long_route;          // host: queries past 160 columns -> 1 wave kernel (default),
                                 //   0 wide kernel, 2 every qualifying pair to the wave kernel
                                 //   (BSW_OPT_LONG)
+    int32_t small_batch;        // host: calls / chunks of at most this many pairs run every
+                                //   qualifying pair on the wave kernel (latency, not
+                                //   throughput, bounds them; BSW_OPT_SMALL_BATCH, 0 = off)
 };
 
 // qlen limit of the register-resident kernel instantiations.

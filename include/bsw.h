@@ -131,6 +131,12 @@ enum {
                                  records, 24-B outputs back (default); 4 = nibbles + whole
                                  records (also the automatic fallback for chunks with > 1/32
                                  non-ACGT bytes); outputs are identical                      */
+    BSW_OPT_SMALL_BATCH = 9,  /* calls (device calls, or host-buffer pipeline chunks) of at most
+                                 this many pairs run every pair the wave-per-alignment kernel
+                                 can take there (default 16384; 0 = off): a lane-per-pair wave
+                                 lives ~1.2 ms at any batch size, a wave per alignment spreads
+                                 the pair over 64 lanes -- kt_for-sized calls are latency-bound.
+                                 Outputs are identical either way                              */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };

@@ -52,7 +52,7 @@ def _assert_same(want, got, tag=""):
 
 @pytest.fixture(scope="module")
 def eng():
-    e = bsw.Engine()
+    e = bsw.Engine(small_batch=0)   # kernel-class tests: small batches stay on their classes
     yield e
     e.close()
 
@@ -63,7 +63,7 @@ def test_golden_fixtures(golden, cell_bits):
     for name, pairs, ref, qer, w, sc in golden:
         key = tuple(sorted(sc.items()))
         if key not in engines:
-            engines[key] = bsw.Engine(_gparams(sc))
+            engines[key] = bsw.Engine(_gparams(sc), small_batch=0)
         got = pairs.copy()
         for f in bsw.OUT_FIELDS:
             got[f] = -9
@@ -182,7 +182,7 @@ def test_partial_batches(eng, m):
 
 def test_nondefault_scoring_generic_kernel():
     sc = dict(o_del=5, e_del=2, o_ins=7, e_ins=1, zdrop=50, end_bonus=3, a=2, b=3)
-    e = bsw.Engine(_gparams(sc))
+    e = bsw.Engine(_gparams(sc), small_batch=0)
     pairs, ref, qer = bswgen.random_pairs(2000, seed=31, tlen=(0, 300), qlen=(0, 160))
     want, got = pairs.copy(), pairs.copy()
     oracle.get_scores(_oparams(sc), want, ref, qer, 60, nthreads=8)
@@ -281,7 +281,7 @@ def test_host_pipeline_chunks(chunk):
     permuted ones are gathered pair by pair with rewritten offsets.  Chunks are whole 4096-pair
     blocks: chunk 1 and 8192 give 3 and 3 chunks, 1 << 20 one.  Outputs equal the oracle and
     only the six output fields of the caller's records change."""
-    e = bsw.Engine(host_chunk=chunk)
+    e = bsw.Engine(host_chunk=chunk, small_batch=0)
     pairs, ref, qer = bswgen.random_pairs(20000 if chunk > 1 else 9000, seed=chunk % 1000, qlen=(0, 190), tlen=(0, 330))
     want = pairs.copy()
     oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
@@ -301,7 +301,7 @@ def test_host_pipeline_packing(pack, p_n):
     p_n = 0.1 puts more than 1/32 of the bytes outside 0..3, so those chunks fall back to nibbles.
     Odd extents (lengths 0..331) exercise the unpack tails; outputs equal the oracle either way and
     the caller's input fields are untouched."""
-    e = bsw.Engine(host_chunk=8192, host_pack=pack)
+    e = bsw.Engine(host_chunk=8192, host_pack=pack, small_batch=0)
     pairs, ref, qer = bswgen.random_pairs(20000, seed=int(p_n * 1000) + pack, qlen=(0, 190), tlen=(0, 331), p_n=p_n)
     want = pairs.copy()
     oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
@@ -313,10 +313,47 @@ def test_host_pipeline_packing(pack, p_n):
     e.close()
 
 
+@pytest.mark.parametrize("n", [1, 63, 1000, 16384, 16385])
+def test_small_batch_route(n, c2_full):
+    """Default routing (BSW_OPT_SMALL_BATCH = 16384): calls of at most 16384 pairs run every
+    int16-safe pair on the wave-per-alignment kernel (latency-bound regime), larger ones on the
+    lane / packed-column classes; both entry points (host buffers, resident) and both cell widths
+    give the oracle's outputs."""
+    pairs, ref, qer, want = c2_full
+    e = bsw.Engine()
+    for cell_bits in (16, 8):
+        got = pairs[:n].copy()
+        e.get_scores(got, ref, qer, 100, cell_bits)
+        _assert_same(want[:n], got, f"n {n} cell_bits {cell_bits}")
+        st = e.last_stats()
+        assert st.n_wave == (n if n <= 16384 else 0)
+        assert st.n_i16 + st.n_u8 + st.n_wide == n
+    dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (pairs[:n].copy(), ref, qer))
+    e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, n, 100, 16)
+    _assert_same(want[:n], dp.download(np.empty_like(pairs[:n])), f"device n {n}")
+    e.close()
+
+
+def test_small_batch_mixed():
+    """A small batch holding int16-unsafe pairs (h0 large) and queries past 160 columns: the
+    unsafe ones stay on the int32 wide kernel, most of the rest go to the wave kernel (empty
+    pairs keep their lane class)."""
+    pairs, ref, qer = bswgen.random_pairs(3000, seed=91, qlen=(0, 400), tlen=(0, 500), h0=(0, 32700))
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    e = bsw.Engine()
+    got = pairs.copy()
+    e.get_scores(got, ref, qer, 100)
+    _assert_same(want, got, "mixed small batch")
+    st = e.last_stats()
+    assert st.n_wide > 0 and st.n_wave > 0 and st.n_i16 + st.n_u8 + st.n_wide == len(pairs)
+    e.close()
+
+
 def test_multi_gpu_context_shards(c2_full):
     pairs, ref, qer, want = c2_full
     n = hiprt.device_count()
-    e = bsw.Engine(n_gpus=n)
+    e = bsw.Engine(n_gpus=n, small_batch=0)
     got = pairs[:100_000].copy()
     e.get_scores(got, ref, qer, 100)
     _assert_same(want[:100_000], got, f"n_gpus={n}")
@@ -326,7 +363,7 @@ def test_multi_gpu_context_shards(c2_full):
 def eng_lane():
     """Engine with the packed-column kernel disabled (BSW_OPT_KERNEL8 = 0): every pair runs on
     the int16 lane kernel (bsw_kernels.hip) or the wide kernel."""
-    e = bsw.Engine(kernel8=0)
+    e = bsw.Engine(kernel8=0, small_batch=0)
     yield e
     e.close()
 
@@ -403,7 +440,7 @@ def test_kernel_range_guard_reports_error():
     queries trip the kernel's range guard, and both call forms must return BSW_E_RANGE (the
     guard word is read back after the DP launches) instead of BSW_OK with unwritten outputs."""
     pairs, ref, qer = bswgen.c2_like(500, seed=41)
-    e = bsw.Engine(test_misroute=1)
+    e = bsw.Engine(test_misroute=1, small_batch=0)
     got = pairs.copy()
     with pytest.raises(bsw.BswError, match="-34"):
         e.get_scores(got, ref, qer, 100)
