@@ -5,6 +5,7 @@ argument validation / error strings behave (no compute call is made here)."""
 import ctypes
 import os
 import re
+import shutil
 import subprocess
 
 import numpy as np
@@ -45,9 +46,12 @@ def test_library_links_hip_runtime_not_torch():
     assert "torch" not in out and "python" not in out
 
 
-def test_kernels_are_gfx950_code_objects():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", bsw.HIP_LIB],
-                         capture_output=True, text=True)
+def test_kernels_are_gfx950_code_objects(tmp_path):
+    # on a copy: --offloading extracts the code objects next to the file it reads
+    lib = tmp_path / "lib.so"
+    shutil.copyfile(bsw.HIP_LIB, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     text = out.stdout + out.stderr
     assert "gfx950" in text
 
