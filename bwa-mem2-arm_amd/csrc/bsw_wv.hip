@@ -275,34 +275,29 @@ __global__ __launch_bounds__(64) void wv_kernel(const KParams kp, const int32_t 
                 hh[r] = (hnew[r] & le) | (hh[r] & ~le);
                 ee[r] = (enew[r] & lt) | (ee[r] & ~le);
             }
-            // row max (last column on ties) and the last positive column, over [beg, end)
-            uint32_t key = 0, lp = 0;
+            // row max (last column on ties) over [beg, end)
+            uint32_t key = 0, hm[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t in = plt(jj[r], endw) & ~plt(jj[r], begw);
-                const uint32_t hm = hcur[r] & in;
-                key = max(key, __builtin_amdgcn_perm(hm, jj[r], 0x05040100u));   // H.lo << 16 | j
-                key = max(key, __builtin_amdgcn_perm(hm, jj[r], 0x07060302u));   // H.hi << 16 | j+1
-                // last positive column: (j + 1) where H > 0
-                const uint32_t plo = (hm & 0xffffu) ? (jj[r] & 0xffffu) + 1u : 0u;
-                const uint32_t phi = (hm >> 16) ? (jj[r] >> 16) + 1u : 0u;
-                lp = max(lp, max(plo, phi));
+                hm[r] = hcur[r] & in;
+                key = max(key, __builtin_amdgcn_perm(hm[r], jj[r], 0x05040100u));   // H.lo << 16 | j
+                key = max(key, __builtin_amdgcn_perm(hm[r], jj[r], 0x07060302u));   // H.hi << 16 | j+1
             }
             const uint32_t kmax = wave_max_u32(key);
             const int m = (int)(kmax >> 16), mj = (int)(kmax & 0xffffu);
-            if (end == qlen) {                       // A.4: j == qlen; h1 = H(i, qlen - 1)
-                const int jl = qlen - 1;             // = end - 1; an empty row leaves h1 = h1b
-                int hq;
-                if (jl < beg) hq = h1b;
-                else {
-                    const int rel = jl - wb, lane = rel / C, col = rel % C;
-                    uint32_t hv = 0;
+            // h1 at row end = H(i, end - 1) (an empty row leaves h1 = h1b): one v_readlane
+            int hq = h1b;
+            if (end - 1 >= beg) {
+                const int rel = end - 1 - wb, lane = rel / C, col = rel % C;
+                uint32_t hv = 0;
 #pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        if (col >> 1 == r) hv = hcur[r];
-                    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)hv, lane);
-                    hq = (int)(int16_t)((col & 1) ? (x >> 16) : (x & 0xffffu));
-                }
+                for (int r = 0; r < R; ++r)
+                    if (col >> 1 == r) hv = hcur[r];
+                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)hv, lane);
+                hq = (int)(int16_t)((col & 1) ? (x >> 16) : (x & 0xffffu));
+            }
+            if (end == qlen) {                       // A.4: j == qlen; h1 = H(i, qlen - 1)
                 if (!(gsc > hq)) max_ie = i;
                 gsc = max(gsc, hq);
             }
@@ -315,7 +310,19 @@ __global__ __launch_bounds__(64) void wv_kernel(const KParams kp, const int32_t 
                 const int dz = (di > dj) ? best - m - (di - dj) * kp.e_del : best - m - (dj - di) * kp.e_ins;
                 if (dz > kp.zdrop) break;
             }
-            const int lp1 = (int)wave_max_u32(lp);             // 1 + lastH
+            // 1 + lastH: H(i, end - 1) > 0 gives lastH = end - 1 at once;
+            // only rows whose band end shrinks pay the wave reduction of the last positive column
+            int lp1 = end;
+            if (hq <= 0) {
+                uint32_t lp = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t plo = (hm[r] & 0xffffu) ? (jj[r] & 0xffffu) + 1u : 0u;
+                    const uint32_t phi = (hm[r] >> 16) ? (jj[r] >> 16) + 1u : 0u;
+                    lp = max(lp, max(plo, phi));
+                }
+                lp1 = (int)wave_max_u32(lp);
+            }
             endc = min(lp1 + 2, qlen);
         }
         if (ln == 0) {
