@@ -441,7 +441,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
     const uint32_t ed2 = (uint32_t)kp.e_del * 0x10001u;
     uint32_t ctr[4] = {0, 0, 0, 0};                       // BSW_PC_STATS group-path counters
 #ifdef BSW_PC_STATS
-    uint32_t nrows = 0, nlast = 0;
+    uint32_t nrows = 0, nlast = 0, nue = 0;
 #endif
 
     for (int i = 0;; ++i) {
@@ -529,6 +529,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             }
 #ifdef BSW_PC_STATS
             nrows += 1;
+            nue += (emax == emin);         // every live lane has the same band end
 #endif
             if (alive) {                           // end_{i+1} = min(lastH + 3, ...), DESIGN.md §3
                 const bool need = h1 == 0;         // H(i, end-1) == 0 -> lastH < end - 1
@@ -549,6 +550,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
     {   // per wave: rows (max over lanes), group paths, lastpos scans; lane 0 adds
         const unsigned rows = (unsigned)wave_max((int)nrows);
         const unsigned nl = (unsigned)wave_max((int)nlast);
+        const unsigned nu = (unsigned)wave_max((int)nue);
         unsigned cmax[4];
         for (int k = 0; k < 4; ++k) cmax[k] = (unsigned)wave_max((int)ctr[k]);   // the longest lane
         if ((threadIdx.x & 63) == 0) {
@@ -556,6 +558,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             for (int k = 0; k < 4; ++k) atomicAdd(&g_pc_stats[1 + k], (unsigned long long)cmax[k]);
             atomicAdd(&g_pc_stats[5], (unsigned long long)nl);
             atomicAdd(&g_pc_stats[6], 1ull);
+            atomicAdd(&g_pc_stats[7], (unsigned long long)nu);
         }
     }
 #endif
@@ -570,7 +573,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
 }
 
 #ifdef BSW_PC_STATS
-// [rows, groups entered, fast, masked-R, masked-L, lastpos scans, waves] summed over waves
+// [rows, groups entered, fast, masked-R, masked-L, lastpos scans, waves, uniform-end rows] summed over waves
 extern "C" int bsw_pc_stats(unsigned long long *out, int reset)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pc_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return -5;

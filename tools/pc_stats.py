@@ -21,7 +21,8 @@ eng.get_scores_device(d[0].ptr, d[1].ptr, d[2].ptr, len(pairs), 100, 16)
 L.bsw_pc_stats(st, 1)
 eng.get_scores_device(d[0].ptr, d[1].ptr, d[2].ptr, len(pairs), 100, 16)
 L.bsw_pc_stats(st, 0)
-rows, ent, fast, mr, ml, lp, waves = (int(st[k]) for k in range(7))
+rows, ent, fast, mr, ml, lp, waves, ue = (int(st[k]) for k in range(8))
 print(f"waves {waves} rows {rows} ({rows / waves:.1f}/wave)  groups entered {ent} ({ent / rows:.2f}/row)")
 print(f"FAST {fast / ent:.3f}  masked-R {mr / ent:.3f}  masked-L {ml / ent:.3f}  lastpos rows {lp / rows:.3f}")
+print(f"uniform-end rows {ue / rows:.3f} (every live lane of the wave at the same band end)")
 print(f"kernel_ms {eng.last_stats().kernel_ms:.3f}")
