@@ -399,6 +399,21 @@ def test_pc_kernel_bucket_edges(eng, cell_bits):
     assert eng.last_stats().n_packed > 0
 
 
+@pytest.mark.parametrize("q", [4, 5, 6, 7, 8, 64, 97, 148, 149, 150, 151, 158])
+@pytest.mark.parametrize("w", [3, 100])
+def test_pc_kernel_qlen_tail(eng, q, w):
+    """Waves of one qlen whose rows all end at qlen run the qlen-tail group body (FAST body,
+    key limited to slots <= qlen, h1 from slot qlen): every residue qlen & 3, related reads
+    (the synthetic C2 generator) so the band reaches qlen, a narrow and the C2 band."""
+    cfg = bsw.synth_cfg(qlen=q, tlen=2 * q + 3, h0_lo=0, h0_hi=min(95, 255 - q))
+    pairs, ref, qer = bsw.synth_batch(8192, pair_base=1000 * q + w, cfg=cfg)
+    want, got = pairs.copy(), pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+    eng.get_scores(got, ref, qer, w)
+    _assert_same(want, got, f"qlen tail q={q} w={w}")
+    assert eng.last_stats().n_packed == len(pairs)
+
+
 def test_lane_kernel_random(eng_lane):
     pairs, ref, qer = bswgen.random_pairs(6000, seed=77, qlen=(0, 160), tlen=(0, 330), h0=(0, 95))
     want, got = pairs.copy(), pairs.copy()
