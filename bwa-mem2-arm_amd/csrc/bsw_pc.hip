@@ -51,12 +51,16 @@ struct PcRow {                           // per-row uniform (SGPR) group sets, b
     uint64_t left;                       // groups containing some lane's beg (masked-L)
 };
 
-// groups lo .. lo + n - 1 as a bit set (uniform; bits >= 64 dropped, only bits < QMAX / 4 are read)
+// groups lo .. lo + n - 1 as a bit set (uniform; only bits < QMAX / 4 <= 40 are read).  Callers
+// pass n >= 0 and lo < 40 whenever n > 0 (lo: a live lane's group; the FAST set's lo may pass 63
+// only with n == 0), so a width clamped to 63 and one s_bfm_b64 give every bit that is read --
+// no branches in the row's scalar chain
 __device__ __forceinline__ uint64_t gbits(int lo, int n)
 {
-    if (lo >= 64 || n <= 0) return 0;
-    n = min(n, 64 - lo);
-    return (n >= 64 ? ~0ull : ((1ull << n) - 1)) << lo;
+    uint64_t m;
+    asm("s_bfm_b64 %0, %1, %2" : "=s"(m)
+        : "s"(__builtin_amdgcn_readfirstlane(min(n, 63))), "s"(__builtin_amdgcn_readfirstlane(lo)));
+    return m;
 }
 
 // {v, v} as two int16 halves
@@ -488,7 +492,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             const int flo = __builtin_amdgcn_readfirstlane(max(0, i - wl_min));  // max beg
             const int fhi = __builtin_amdgcn_readfirstlane(emin);                // min end
             const int glo = ulo >> 2;
-            const int gsp = max(min(uhi, QMAX - 1) / 4 - glo, -1);
+            const int gsp = max((min(uhi, QMAX - 1) >> 2) - glo, -1);      // uhi >= 0: a live lane
             // FAST needs 4G > every beg (entering chain valid) -- or one common beg == 4G with
             // nothing computed before it -- and 4G + 4 <= every end
             const int gfa = (ulo == flo && (flo & 3) == 0) ? (flo >> 2) : (flo >> 2) + 1;
