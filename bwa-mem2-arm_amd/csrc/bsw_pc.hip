@@ -519,17 +519,20 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
                 if (!(gsc > h1)) max_ie = i;
                 gsc = max(gsc, h1);
             }
-            if (m <= 0) {
-                alive = false;
-            } else if (m > best) {
-                best = m; best_i = i; best_j = mj;
-                moff = max(moff, abs(mj - i));
-            } else if (kp.zdrop > 0) {
+            // A.4 row end as selects, no branches on the row's path: m <= 0 ends the lane; a new
+            // best moves (best, best_i, best_j, max_off); otherwise z-drop against the old best
+            {
                 const int di = i - best_i, dj = mj - best_j;
                 // |di - dj| and e are small and non-negative: 24-bit multiplies (full rate)
                 const int dz = (di > dj) ? best - m - (int)__umul24((unsigned)(di - dj), (unsigned)kp.e_del)
                                          : best - m - (int)__umul24((unsigned)(dj - di), (unsigned)kp.e_ins);
-                if (dz > kp.zdrop) alive = false;
+                const bool better = m > best;              // best >= h0 >= 0: never with m <= 0
+                const bool zdropped = kp.zdrop > 0 && dz > kp.zdrop;
+                alive = m > 0 && (better || !zdropped);
+                moff = better ? max(moff, abs(mj - i)) : moff;
+                best_i = better ? i : best_i;
+                best_j = better ? mj : best_j;
+                best = better ? m : best;
             }
 #ifdef BSW_PC_STATS
             nrows += 1;
