@@ -504,7 +504,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
         }
         if (act) {
             // h1 = H(i, j-1) entering each group, in the HIGH half (PC_FAST_CHAIN)
-            int h1 = (beg == 0) ? (int)((uint32_t)max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) << 16) : 0;
+            // (a mask, not a select: the compiler turned the select into an exec-masked block)
+            int h1 = (int)((uint32_t)max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) << 16) & -(int)(beg == 0);
             int f = 0;
             uint32_t key = 0;
             const uint32_t endw = pack2(end);
@@ -515,9 +516,10 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             h1 = (int)((uint32_t)h1 >> 16);               // H(i, end-1)
             const uint32_t k32 = max(key & 0xffffu, key >> 16);
             const int m = (int)(k32 >> 8), mj = (int)(k32 & 0xffu);
-            if (end == qlen) {                    // A.4: j == qlen; h1 = H(i, qlen - 1)
-                if (!(gsc > h1)) max_ie = i;
-                gsc = max(gsc, h1);
+            {                                     // A.4: j == qlen; h1 = H(i, qlen - 1)
+                const bool atq = end == qlen;
+                max_ie = (atq && !(gsc > h1)) ? i : max_ie;
+                gsc = atq ? max(gsc, h1) : gsc;
             }
             // A.4 row end as selects, no branches on the row's path: m <= 0 ends the lane; a new
             // best moves (best, best_i, best_j, max_off); otherwise z-drop against the old best
@@ -538,8 +540,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             nrows += 1;
             nue += (emax == emin);         // every live lane has the same band end
 #endif
-            if (alive) {                           // end_{i+1} = min(lastH + 3, ...), DESIGN.md §3
-                const bool need = h1 == 0;         // H(i, end-1) == 0 -> lastH < end - 1
+            {                                      // end_{i+1} = min(lastH + 3, ...), DESIGN.md §3
+                const bool need = alive && h1 == 0;  // H(i, end-1) == 0 -> lastH < end - 1
                 int lp1 = end;
                 if (__ballot(need)) {
 #ifdef BSW_PC_STATS
@@ -547,9 +549,9 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
 #endif
                     const int lp = pc_lastpos<QMAX>(std::make_integer_sequence<int, NG>{}, hh, end, need,
                                                     emax >> 2);
-                    if (need) lp1 = lp;
+                    lp1 = need ? lp : end;
                 }
-                endc = min(lp1 + 2, qlen);
+                endc = alive ? min(lp1 + 2, qlen) : endc;
             }
         }
     }
