@@ -454,31 +454,28 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
         if (__ballot(act) == 0) break;
         // the row's target base and score profile first: their LDS reads then overlap the band
         // bookkeeping below instead of stalling the first group (lgkmcnt wait)
-        uint2 pr = make_uint2(0u, 0u);
-        if (act) {
-            if ((i & 3) == 0) {            // new 4-row block: 4 target bases from LDS
-                if ((i & 63) == 0) {          // chunk boundary: its DMA was issued 64 rows ago
-                    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                const int k = (i >> 2) & 15;
-                // the two dwords by inline asm: the compiler would otherwise put a vmcnt(0) before
-                // every LDS read (it cannot tell this buffer from the one the in-flight LDS-DMA
-                // refill writes) -- this chunk's DMA was waited for at its first row above
-                const uint32_t la = (uint32_t)(uintptr_t)(lptr_t)&s_tgt[wv][(i >> 6) & 1][k][ln];
-                uint2 d;
-                asm volatile("ds_read2st64_b32 %0, %1 offset1:1\n\ts_waitcnt lgkmcnt(0)"
-                             : "=v"(d) : "v"(la) : "memory");
-                tcur = __builtin_amdgcn_alignbyte(d.y, d.x, tsh);
-                if ((i & 63) == 0) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (i > 0) issue_chunk((i >> 6) + 1);   // refill the buffer just drained
-                }
+        // every lane reads (a dead lane's slots are harmless): no exec-masked block on the row's path
+        if ((i & 3) == 0) {                // new 4-row block: 4 target bases from LDS
+            if ((i & 63) == 0) {              // chunk boundary: its DMA was issued 64 rows ago
+                __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
+                __builtin_amdgcn_sched_barrier(0);
             }
-            // per-row score profile of target base t (8 bytes: mat[t][q], q = 0..7)
-            const uint32_t t = (tcur >> (8 * (i & 3))) & 0xffu;
-            pr = s_prof[min(t, 7u)];                     // one ds_read_b64 (codes > 4 score as N)
+            const int k = (i >> 2) & 15;
+            // the two dwords by inline asm: the compiler would otherwise put a vmcnt(0) before
+            // every LDS read (it cannot tell this buffer from the one the in-flight LDS-DMA
+            // refill writes) -- this chunk's DMA was waited for at its first row above
+            const uint32_t la = (uint32_t)(uintptr_t)(lptr_t)&s_tgt[wv][(i >> 6) & 1][k][ln];
+            uint2 d;
+            asm volatile("ds_read2st64_b32 %0, %1 offset1:1\n\ts_waitcnt lgkmcnt(0)"
+                         : "=v"(d) : "v"(la) : "memory");
+            tcur = __builtin_amdgcn_alignbyte(d.y, d.x, tsh);
+            if ((i & 63) == 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (i > 0 && act) issue_chunk((i >> 6) + 1);   // refill the buffer just drained
+            }
         }
+        // per-row score profile of target base t (8 bytes: mat[t][q], q = 0..7)
+        const uint2 pr = s_prof[min((tcur >> (8 * (i & 3))) & 0xffu, 7u)];   // one ds_read_b64 (codes > 4 score as N)
         __builtin_amdgcn_sched_barrier(0);
         const int beg = max(0, i - wl);
         const int end = min(min(endc, i + wl + 1), qlen);
@@ -502,7 +499,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             r.fast = gbits(gfa, gfn);
             r.left = gbits(glo, gln + 1);
         }
-        if (act) {
+        {   // every lane runs the row (dead lanes' registers take garbage); state updates are
+            // gated by act below, so no exec-masked block wraps the row
             // h1 = H(i, j-1) entering each group, in the HIGH half (PC_FAST_CHAIN)
             // (a mask, not a select: the compiler turned the select into an exec-masked block)
             int h1 = (int)((uint32_t)max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) << 16) & -(int)(beg == 0);
@@ -517,7 +515,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             const uint32_t k32 = max(key & 0xffffu, key >> 16);
             const int m = (int)(k32 >> 8), mj = (int)(k32 & 0xffu);
             {                                     // A.4: j == qlen; h1 = H(i, qlen - 1)
-                const bool atq = end == qlen;
+                const bool atq = act && end == qlen;
                 max_ie = (atq && !(gsc > h1)) ? i : max_ie;
                 gsc = atq ? max(gsc, h1) : gsc;
             }
@@ -528,17 +526,17 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
                 // |di - dj| and e are small and non-negative: 24-bit multiplies (full rate)
                 const int dz = (di > dj) ? best - m - (int)__umul24((unsigned)(di - dj), (unsigned)kp.e_del)
                                          : best - m - (int)__umul24((unsigned)(dj - di), (unsigned)kp.e_ins);
-                const bool better = m > best;              // best >= h0 >= 0: never with m <= 0
+                const bool better = act && m > best;       // best >= h0 >= 0: never with m <= 0
                 const bool zdropped = kp.zdrop > 0 && dz > kp.zdrop;
-                alive = m > 0 && (better || !zdropped);
+                alive = act && m > 0 && (better || !zdropped);
                 moff = better ? max(moff, abs(mj - i)) : moff;
                 best_i = better ? i : best_i;
                 best_j = better ? mj : best_j;
                 best = better ? m : best;
             }
 #ifdef BSW_PC_STATS
-            nrows += 1;
-            nue += (emax == emin);         // every live lane has the same band end
+            nrows += act;
+            nue += act && (emax == emin);  // every live lane has the same band end
 #endif
             {                                      // end_{i+1} = min(lastH + 3, ...), DESIGN.md §3
                 const bool need = alive && h1 == 0;  // H(i, end-1) == 0 -> lastH < end - 1
