@@ -509,8 +509,12 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             const uint32_t endw = pack2(end);
             const uint32_t endm1w = pack2(end - 1);                         // end = 0: {-1, -1}
             const uint32_t begm2w = pack2(beg - 2);
+            // wave priority: the row's serial scalar / DPP chain (row end, next row's head) issues
+            // ahead of the partner wave's group VALU; the groups themselves run at the base level
+            __builtin_amdgcn_s_setprio(0);
             pc_row<QMAX>(std::make_integer_sequence<int, (NG + pc_seg_len<QMAX>() - 1) / pc_seg_len<QMAX>()>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
                          oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg, ctr);
+            __builtin_amdgcn_s_setprio(2);
             h1 = (int)((uint32_t)h1 >> 16);               // H(i, end-1)
             const uint32_t k32 = max(key & 0xffffu, key >> 16);
             const int m = (int)(k32 >> 8), mj = (int)(k32 & 0xffu);
