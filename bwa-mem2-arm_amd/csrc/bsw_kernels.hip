@@ -584,8 +584,12 @@ __global__ __launch_bounds__(64, 2) void lane_kernel(const KParams kp, const int
             pr = (t == 0) ? make_uint2(kp.prof[0][0], kp.prof[0][1]) : pr;
             int h1 = (beg == 0) ? max(h0 - (kp.o_del + kp.e_del * (i + 1)), 0) : 0;
             int f = 0, key = -1, lp1 = 0;
+            // wave priority as in pc_kernel: the row's serial scalar chain at 2,
+            // the group sequence at 0
+            __builtin_amdgcn_s_setprio(0);
             lane_row<QMAX, SM, SYM>(std::make_integer_sequence<int, QMAX / 4 + 1>{}, eh, q4, pr,
                                     beg, end, f, h1, key, lp1, r, cx);
+            __builtin_amdgcn_s_setprio(2);
             const int m = key >> 16, mj = key & 0xffff;
             if (end == qlen) {                    // A.4: j == qlen (beg <= end always)
                 if (!(gsc > h1)) max_ie = i;
