@@ -195,6 +195,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
         "5:\n\t"                                                                             \
         "s_bitcmp1_b64 %[men], %[g]\n\t"             /* outside [min beg, max end]: skip */ \
         "s_cbranch_scc0 3b\n\t"                                                              \
+        "s_setprio 2\n\t"                            /* masked bodies: short per-cell chains */\
         PC_CNT(0)                                                                            \
         "v_lshrrev_b32_e32 %[h1], 16, %[h1]\n\t"     /* masked bodies: h1 as a clean int */ \
         PC_SCORES                                                                            \
@@ -207,6 +208,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
                   PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"),                        \
                   KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t", "", "")           \
         "v_lshlrev_b32_e32 %[h1], 16, %[h1]\n\t"                                              \
+        "s_setprio 0\n\t"                                                                    \
         "s_branch 3b\n"                                                                      \
         "4:\n\t"                                                                             \
         PC_CNT(3)                                                                            \
@@ -217,6 +219,7 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
                   KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t",                    \
                   PC_LEFTMASK("a"), PC_LEFTMASK("b"))                                        \
         "v_lshlrev_b32_e32 %[h1], 16, %[h1]\n\t"                                              \
+        "s_setprio 0\n\t"                                                                    \
         "s_branch 3b\n"                                                                      \
         ".subsection 0\n"                                                                    \
         : [ha] "+v"(ha), [hb] "+v"(hb), [ea] "+v"(ea), [eb] "+v"(eb), [f] "+v"(f),           \
