@@ -24,6 +24,7 @@ namespace {
 
 struct ChainParams {
     int32_t o_del, e_del, o_ins, e_ins, a, w;
+    int64_t ref_len, l_pac;
 };
 
 __device__ __forceinline__ int d_cal_max_gap(const ChainParams &p, int qlen)
@@ -73,11 +74,15 @@ __global__ void k_runs(const int32_t *__restrict__ sr, int32_t ns, int32_t n_rea
 }
 
 // per read: regions zeroed, chain order (insertion sort of each chain: score desc, index desc)
+// and each chain's target window (mem_chain2aln's rmax[]: min / max of its seeds' reach, clipped
+// to the reference, the first seed's side of l_pac) at cwin[2 * head]
 __global__ void k_prep(int32_t n_reads, const int32_t *__restrict__ sbeg, const int32_t *__restrict__ send,
-                       const bsw_seed_t *__restrict__ seeds, const int32_t *__restrict__ sc, int32_t a,
-                       int32_t *__restrict__ order, int32_t *__restrict__ chain_of, int32_t *__restrict__ pos,
+                       const bsw_seed_t *__restrict__ seeds, const int32_t *__restrict__ sc,
+                       const int32_t *__restrict__ read_len, const ChainParams p, int32_t *__restrict__ order,
+                       int32_t *__restrict__ chain_of, int64_t *__restrict__ cwin, int32_t *__restrict__ pos,
                        int32_t *__restrict__ nav, bsw_alnreg_t *__restrict__ out, int32_t *__restrict__ ext)
 {
+    const int32_t a = p.a;
     const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_reads) return;
     const int32_t b = sbeg[r], e = send[r];
@@ -91,6 +96,24 @@ __global__ void k_prep(int32_t n_reads, const int32_t *__restrict__ sbeg, const 
         int32_t c1 = c0;
         const int32_t cid = sc[c0];
         while (c1 < e && sc[c1] == cid) ++c1;
+        const int l_query = read_len[r];
+        int64_t lo = p.ref_len, hi = 0, first = -1;
+        for (int32_t i = c0; i < c1; ++i) {
+            const bsw_seed_t t = seeds[i];
+            if (t.len <= 0) continue;
+            if (first < 0) first = t.rbeg;
+            const int qe = t.qbeg + t.len;
+            lo = min(lo, t.rbeg - (int64_t)(t.qbeg + d_cal_max_gap(p, t.qbeg)));
+            hi = max(hi, t.rbeg + t.len + (int64_t)((l_query - qe) + d_cal_max_gap(p, l_query - qe)));
+        }
+        lo = max(lo, (int64_t)0);
+        hi = min(hi, p.ref_len);
+        if (p.l_pac > 0 && lo < p.l_pac && p.l_pac < hi) {
+            if (first < p.l_pac) hi = p.l_pac;
+            else lo = p.l_pac;
+        }
+        cwin[2 * (int64_t)c0] = lo;
+        cwin[2 * (int64_t)c0 + 1] = hi;
         for (int32_t i = c0; i < c1; ++i) {
             chain_of[i] = c0;
             // insert i into order[c0 .. i): (len * a, index) descending
@@ -116,13 +139,14 @@ __global__ __launch_bounds__(64) void k_pick(int32_t n_reads, const int32_t *__r
                                              const int32_t *__restrict__ send, const bsw_seed_t *__restrict__ seeds,
                                              const int64_t *__restrict__ read_off,
                                              const int32_t *__restrict__ read_len, const int32_t *__restrict__ order,
-                                             const int32_t *__restrict__ chain_of, const int32_t *__restrict__ ext,
+                                             const int32_t *__restrict__ chain_of, const int64_t *__restrict__ cwin,
+                                             const int32_t *__restrict__ ext,
                                              const bsw_alnreg_t *__restrict__ out, const int32_t *__restrict__ av,
                                              const int32_t *__restrict__ nav, int32_t *__restrict__ pos,
                                              const ChainParams p, int32_t *__restrict__ cnt,
                                              int32_t *__restrict__ jsi, int32_t *__restrict__ jrun,
                                              int64_t *__restrict__ joff, int32_t *__restrict__ jlen,
-                                             bsw_seed_t *__restrict__ jseed)
+                                             bsw_seed_t *__restrict__ jseed, int64_t *__restrict__ jwin)
 {
     const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     int32_t pick = -1;
@@ -169,6 +193,9 @@ __global__ __launch_bounds__(64) void k_pick(int32_t n_reads, const int32_t *__r
         joff[j] = read_off[r];
         jlen[j] = read_len[r];
         jseed[j] = seeds[pick];
+        const int64_t h = chain_of[pick];
+        jwin[2 * j] = cwin[2 * h];
+        jwin[2 * j + 1] = cwin[2 * h + 1];
     }
 }
 
@@ -195,7 +222,7 @@ float ms_since(std::chrono::steady_clock::time_point t0)
 
 struct Buf {                       // device allocations of one call, freed on every path
     int device;
-    void *p[20] = {};
+    void *p[24] = {};
     int n = 0;
     explicit Buf(int d) : device(d) {}
     template <class T>
@@ -235,11 +262,14 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
     CH_TRY(hipSetDevice(dev));
     bsw_params_t prm;
     ctx_params(ctx, &prm);
-    ChainParams p{prm.o_del, prm.e_del, prm.o_ins, prm.e_ins, prm.mat[0], opt->w};
+    const int64_t ref_len = ctx_refres_len(ctx);
+    if (ref_len < 0) return BSW_E_INVAL;                // no resident reference
+    if (const int rc = ext_opt_check(opt, ref_len)) return rc;
+    ChainParams p{prm.o_del, prm.e_del, prm.o_ins, prm.e_ins, prm.mat[0], opt->w, ref_len, opt->l_pac};
     const auto tp = std::chrono::steady_clock::now();
     Buf B(dev);
     int32_t *sbeg, *send, *order, *chain_of, *pos, *nav, *av, *cnt, *jsi, *jrun, *jlen, *err;
-    int64_t *joff;
+    int64_t *joff, *cwin, *jwin;
     bsw_seed_t *jseed;
     bsw_alnreg_t *jout;
     const size_t nr = (size_t)n_reads;
@@ -248,18 +278,22 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
     CH_TRY(B.get(cnt, 2)); CH_TRY(B.get(err, 1));
     CH_TRY(B.get(jsi, nr)); CH_TRY(B.get(jrun, nr)); CH_TRY(B.get(jlen, nr)); CH_TRY(B.get(joff, nr));
     CH_TRY(B.get(jseed, nr)); CH_TRY(B.get(jout, nr));
+    CH_TRY(B.get(cwin, 2 * (size_t)ns)); CH_TRY(B.get(jwin, 2 * nr));
+    // the pinned word's guard is declared first so it is destroyed last: the stream guard
+    // drains any queued D2H into it before it is freed
+    int32_t *h = nullptr;                               // pinned readback of the round's job count
+    struct HostGuard {
+        int32_t *h;
+        ~HostGuard() { if (h) (void)hipHostFree(h); }
+    } hg{nullptr};
+    CH_TRY(hipHostMalloc((void **)&h, 2 * sizeof(int32_t), 0));
+    hg.h = h;
     hipStream_t st = nullptr;
     CH_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     struct StreamGuard {
         hipStream_t s;
         ~StreamGuard() { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); }
     } sg{st};
-    int32_t *h = nullptr;                               // pinned readback of the round's job count
-    CH_TRY(hipHostMalloc((void **)&h, 2 * sizeof(int32_t), 0));
-    struct HostGuard {
-        int32_t *h;
-        ~HostGuard() { (void)hipHostFree(h); }
-    } hg{h};
     CH_TRY(hipMemsetAsync(sbeg, 0, nr * sizeof(int32_t), st));
     CH_TRY(hipMemsetAsync(send, 0, nr * sizeof(int32_t), st));
     CH_TRY(hipMemsetAsync(err, 0, sizeof(int32_t), st));
@@ -269,8 +303,8 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
     CH_TRY(hipStreamSynchronize(st));
     if (h[0]) return BSW_E_INVAL;                       // unsorted / out-of-range seed_read
     const unsigned gr = (unsigned)((nr + 63) / 64);
-    hipLaunchKernelGGL(k_prep, dim3(gr), dim3(64), 0, st, n_reads, sbeg, send, d_seeds, d_sc, p.a, order, chain_of,
-                       pos, nav, d_out, d_ext);
+    hipLaunchKernelGGL(k_prep, dim3(gr), dim3(64), 0, st, n_reads, sbeg, send, d_seeds, d_sc, d_read_len, p, order,
+                       chain_of, cwin, pos, nav, d_out, d_ext);
     CH_TRY(hipGetLastError());
     CH_TRY(hipStreamSynchronize(st));
     cs->prep_ms = ms_since(tp);
@@ -278,7 +312,8 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
         const auto tc = std::chrono::steady_clock::now();
         CH_TRY(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
         hipLaunchKernelGGL(k_pick, dim3(gr), dim3(64), 0, st, n_reads, sbeg, send, d_seeds, d_read_off, d_read_len,
-                           order, chain_of, d_ext, d_out, av, nav, pos, p, cnt, jsi, jrun, joff, jlen, jseed);
+                           order, chain_of, cwin, d_ext, d_out, av, nav, pos, p, cnt, jsi, jrun, joff, jlen, jseed,
+                           jwin);
         CH_TRY(hipGetLastError());
         CH_TRY(hipMemcpyAsync(h, cnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         CH_TRY(hipStreamSynchronize(st));
@@ -286,7 +321,7 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
         const int32_t nj = h[0];
         if (nj == 0) break;
         const auto te = std::chrono::steady_clock::now();
-        const int rc = bsw_extend_seeds_device(ctx, opt, d_reads, joff, jlen, jseed, nj, jout, nullptr);
+        const int rc = extend_seeds_device_win(ctx, opt, d_reads, joff, jlen, jseed, jwin, nj, jout, nullptr);
         if (rc) return rc;
         cs->ext_ms += ms_since(te);
         bsw_ext_stats_t es{};

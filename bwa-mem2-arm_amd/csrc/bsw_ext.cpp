@@ -44,6 +44,32 @@ int cal_max_gap(const bsw_params_t &p, int a, int w, int qlen)
     return std::min(l, w << 1);
 }
 
+// mem_chain2aln's target window of a chain (include/bsw_ext.h; oracle_chain_window): min / max
+// of the seeds' reach, clipped to [0, ref_len), and with l_pac > 0 the side of the first seed
+// when it crosses the forward-reverse boundary.  seed(i) returns the chain's i-th seed.
+template <class Seed>
+void chain_window(const bsw_params_t &p, int a, const bsw_ext_opt_t &opt, int64_t ref_len, int l_query, int n,
+                  Seed seed, int64_t *rmax0, int64_t *rmax1)
+{
+    int64_t lo = ref_len, hi = 0, first = -1;
+    for (int i = 0; i < n; ++i) {
+        const bsw_seed_t &t = seed(i);
+        if (t.len <= 0) continue;
+        if (first < 0) first = t.rbeg;
+        const int32_t qe = t.qbeg + t.len;
+        lo = std::min<int64_t>(lo, t.rbeg - (t.qbeg + cal_max_gap(p, a, opt.w, t.qbeg)));
+        hi = std::max<int64_t>(hi, t.rbeg + t.len + ((l_query - qe) + cal_max_gap(p, a, opt.w, l_query - qe)));
+    }
+    lo = std::max<int64_t>(lo, 0);
+    hi = std::min<int64_t>(hi, ref_len);
+    if (opt.l_pac > 0 && lo < opt.l_pac && opt.l_pac < hi) {
+        if (first < opt.l_pac) hi = opt.l_pac;
+        else lo = opt.l_pac;
+    }
+    *rmax0 = lo;
+    *rmax1 = hi;
+}
+
 // f(a, b) over [0, n) in pieces on the engine's host pool (bsw_pool.h)
 template <class F>
 void parallel_for(int32_t n, F f)
@@ -112,21 +138,42 @@ extern "C" void bsw_ext_opt_default(bsw_ext_opt_t *opt)
     opt->pen_clip5 = 5;
     opt->pen_clip3 = 5;
     opt->max_band_try = 2;
+    opt->l_pac = 0;
 }
+
+namespace bsw {
+
+int ext_opt_check(const bsw_ext_opt_t *opt, int64_t ref_len)
+{
+    if (opt->w < 0 || opt->max_band_try < 1 || ref_len < 0 || opt->l_pac < 0) return BSW_E_INVAL;
+    if (opt->l_pac > 0 && ref_len != 2 * opt->l_pac) return BSW_E_INVAL;
+    return BSW_OK;
+}
+
+// a seed must lie inside [0, ref_len) and, on a two-strand text, on one strand (upstream's
+// bns_intv2rid drops bridging seeds before chaining)
+bool ext_seed_ok(const bsw_ext_opt_t *opt, const bsw_seed_t &s, int32_t l, int64_t ref_len)
+{
+    if (s.qbeg < 0 || s.qbeg + s.len > l || s.rbeg < 0 || s.rbeg + s.len > ref_len || l > BSW_MAX_LEN) return false;
+    return !(opt->l_pac > 0 && s.rbeg < opt->l_pac && s.rbeg + s.len > opt->l_pac);
+}
+
+}  // namespace bsw
 
 extern "C" int bsw_ext_last_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out)
 {
     return bsw::get_ext_stats(ctx, out);
 }
 
-extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *ref,
-                                int64_t ref_len, const uint8_t *reads, const int64_t *read_off,
-                                const int32_t *read_len, const bsw_seed_t *seeds, int32_t n,
-                                bsw_alnreg_t *out)
+// The extension of n seeds, seed i inside the target window win[2i], win[2i + 1] (a chain's
+// window, mem_chain2aln) or, with win == nullptr, its own one-seed window.
+static int extend_seeds_win(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *ref, int64_t ref_len,
+                            const uint8_t *reads, const int64_t *read_off, const int32_t *read_len,
+                            const bsw_seed_t *seeds, const int64_t *win, int32_t n, bsw_alnreg_t *out)
 {
     if (!ctx || !opt || n < 0 || (n > 0 && (!ref || !reads || !read_off || !read_len || !seeds || !out)))
         return BSW_E_INVAL;
-    if (opt->w < 0 || opt->max_band_try < 1 || ref_len < 0) return BSW_E_INVAL;
+    if (const int rc = bsw::ext_opt_check(opt, ref_len)) return rc;
     // SeqPair idr / idq are int32 offsets into one phase's code buffers: split calls whose
     // buffers could pass 2^31 bytes (window <= read + 2 cal_max_gap <= read + 4w per read)
     {
@@ -139,8 +186,8 @@ extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const 
             bsw_ext_stats_t agg{};
             for (int64_t a0 = 0; a0 < n; a0 += chunk) {
                 const int32_t m = (int32_t)std::min<int64_t>(chunk, n - a0);
-                const int rc = bsw_extend_seeds(ctx, opt, ref, ref_len, reads, read_off + a0,
-                                                read_len + a0, seeds + a0, m, out + a0);
+                const int rc = extend_seeds_win(ctx, opt, ref, ref_len, reads, read_off + a0, read_len + a0,
+                                                seeds + a0, win ? win + 2 * a0 : nullptr, m, out + a0);
                 if (rc) return rc;
                 bsw_ext_stats_t st{};
                 bsw::get_ext_stats(ctx, &st);
@@ -165,14 +212,17 @@ extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const 
         const bsw_seed_t &s = seeds[i];
         if (s.len <= 0) continue;
         const int32_t l = read_len[i];
-        if (s.qbeg < 0 || s.qbeg + s.len > l || s.rbeg < 0 || s.rbeg + s.len > ref_len || l > BSW_MAX_LEN)
+        if (!bsw::ext_seed_ok(opt, s, l, ref_len)) return BSW_E_RANGE;
+        if (win) {
+            rmax0[i] = win[2 * i];
+            rmax1[i] = win[2 * i + 1];
+        } else {
+            chain_window(p, a, *opt, ref_len, l, 1, [&](int) -> const bsw_seed_t & { return s; }, &rmax0[i],
+                         &rmax1[i]);
+        }
+        if (rmax0[i] > s.rbeg || rmax1[i] < s.rbeg + s.len || s.rbeg - rmax0[i] > BSW_MAX_LEN ||
+            rmax1[i] - (s.rbeg + s.len) > BSW_MAX_LEN)
             return BSW_E_RANGE;
-        const int32_t qe = s.qbeg + s.len;
-        const int64_t b = s.rbeg - (s.qbeg + cal_max_gap(p, a, opt->w, s.qbeg));
-        const int64_t e = s.rbeg + s.len + ((l - qe) + cal_max_gap(p, a, opt->w, l - qe));
-        rmax0[i] = std::max<int64_t>(b, 0);
-        rmax1[i] = std::min<int64_t>(e, ref_len);
-        if (s.rbeg - rmax0[i] > BSW_MAX_LEN || rmax1[i] - (s.rbeg + s.len) > BSW_MAX_LEN) return BSW_E_RANGE;
         r.seedlen0 = s.len;
         // no-extension defaults (mem_chain2aln): qbeg == 0 / qe == l_query
         r.score = r.truesc = s.len * a;
@@ -293,6 +343,14 @@ extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const 
     return BSW_OK;
 }
 
+extern "C" int bsw_extend_seeds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *ref,
+                                int64_t ref_len, const uint8_t *reads, const int64_t *read_off,
+                                const int32_t *read_len, const bsw_seed_t *seeds, int32_t n,
+                                bsw_alnreg_t *out)
+{
+    return extend_seeds_win(ctx, opt, ref, ref_len, reads, read_off, read_len, seeds, nullptr, n, out);
+}
+
 // ---------------------------------------------------------------- mem_chain2aln over chains
 // The per-read order of upstream's mem_chain2aln (chains in order, each chain's seeds by score
 // descending; a seed contained "around" an earlier region of the read is skipped unless an
@@ -325,10 +383,10 @@ bool ext_contained(const bsw_params_t &p, int a, const bsw_ext_opt_t &opt, const
     return false;
 }
 
-// extend(nj, job read offsets / lengths / seeds, regions out) runs one round's extensions
+// extend(nj, job read offsets / lengths / seeds / windows, regions out) runs one round's extensions
 template <class Extend>
-int chain_rounds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const int64_t *read_off, const int32_t *read_len,
-                 int32_t n_reads, const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain,
+int chain_rounds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, int64_t ref_len, const int64_t *read_off,
+                 const int32_t *read_len, int32_t n_reads, const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain,
                  int32_t ns, bsw_alnreg_t *out, int32_t *extended, bsw_chain_stats_t *cs, Extend extend)
 {
     bsw_params_t p;
@@ -349,6 +407,7 @@ int chain_rounds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const int64_t *read_o
     // processing order per read: chains in order, each chain's seeds by (score, index) desc;
     // order[] positions of a chain coincide with its seed-index range
     std::vector<int32_t> order((size_t)ns), chain_of((size_t)ns);
+    std::vector<int64_t> cwin(2 * (size_t)ns);          // the chain's target window, per chain head
     parallel_for(nrun, [&](int32_t r0, int32_t r1) {
         for (int32_t r = r0; r < r1; ++r) {
             for (int32_t k = rstart[r]; k < rstart[r + 1]; ++k) { memset(&out[k], 0, sizeof(out[k])); extended[k] = 0; }
@@ -356,6 +415,9 @@ int chain_rounds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const int64_t *read_o
                 int32_t c1 = c0;
                 while (c1 < rstart[r + 1] && seed_chain[c1] == seed_chain[c0]) ++c1;
                 for (int32_t i = c0; i < c1; ++i) { order[i] = i; chain_of[i] = c0; }
+                chain_window(p, a, *opt, ref_len, read_len[seed_read[c0]], c1 - c0,
+                             [&](int i) -> const bsw_seed_t & { return seeds[c0 + i]; }, &cwin[2 * (size_t)c0],
+                             &cwin[2 * (size_t)c0 + 1]);
                 std::sort(order.begin() + c0, order.begin() + c1, [&](int32_t x, int32_t y) {
                     const int64_t kx = (int64_t)seeds[x].len * a, ky = (int64_t)seeds[y].len * a;
                     return kx != ky ? kx > ky : x > y;
@@ -367,7 +429,7 @@ int chain_rounds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const int64_t *read_o
     // per read: next position in order[], regions so far (flat: av[rstart[r] ..], nav[r])
     std::vector<int32_t> pos(rstart.begin(), rstart.end() - 1), av((size_t)ns), nav((size_t)nrun, 0);
     std::vector<int32_t> pick((size_t)nrun), jobs, job_run, jcnt;
-    std::vector<int64_t> joff;
+    std::vector<int64_t> joff, jwin;
     std::vector<int32_t> jlen;
     std::vector<bsw_seed_t> jseed;
     std::vector<bsw_alnreg_t> jout;
@@ -408,15 +470,17 @@ int chain_rounds(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const int64_t *read_o
         cs->check_ms += ms_since(tc);
         if (jobs.empty()) break;
         const int32_t nj = (int32_t)jobs.size();
-        joff.resize(nj); jlen.resize(nj); jseed.resize(nj); jout.resize(nj);
+        joff.resize(nj); jlen.resize(nj); jseed.resize(nj); jout.resize(nj); jwin.resize(2 * (size_t)nj);
         parallel_for(nj, [&](int32_t k0, int32_t k1) {
             for (int32_t k = k0; k < k1; ++k) {
                 const int32_t si = jobs[k], rid = seed_read[si];
                 joff[k] = read_off[rid]; jlen[k] = read_len[rid]; jseed[k] = seeds[si];
+                jwin[2 * k] = cwin[2 * (size_t)chain_of[si]];
+                jwin[2 * k + 1] = cwin[2 * (size_t)chain_of[si] + 1];
             }
         });
         auto te = Clock::now();
-        const int rc = extend(nj, joff.data(), jlen.data(), jseed.data(), jout.data());
+        const int rc = extend(nj, joff.data(), jlen.data(), jseed.data(), jwin.data(), jout.data());
         if (rc) return rc;
         cs->ext_ms += ms_since(te);
         bsw_ext_stats_t es{};
@@ -449,12 +513,13 @@ extern "C" int bsw_chain2aln(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uin
         (n_seeds > 0 && (!ref || !reads || !read_off || !read_len || !seeds || !seed_read || !seed_chain || !out ||
                          !extended)))
         return BSW_E_INVAL;
+    if (const int rc = bsw::ext_opt_check(opt, ref_len)) return rc;
     bsw_chain_stats_t cs{};
-    const int rc = chain_rounds(ctx, opt, read_off, read_len, n_reads, seeds, seed_read, seed_chain, n_seeds, out,
-                                extended, &cs,
+    const int rc = chain_rounds(ctx, opt, ref_len, read_off, read_len, n_reads, seeds, seed_read, seed_chain, n_seeds,
+                                out, extended, &cs,
                                 [&](int32_t nj, const int64_t *jo, const int32_t *jl, const bsw_seed_t *js,
-                                    bsw_alnreg_t *jr) {
-                                    return bsw_extend_seeds(ctx, opt, ref, ref_len, reads, jo, jl, js, nj, jr);
+                                    const int64_t *jw, bsw_alnreg_t *jr) {
+                                    return extend_seeds_win(ctx, opt, ref, ref_len, reads, jo, jl, js, jw, nj, jr);
                                 });
     bsw::set_chain_stats(ctx, cs);
     return rc;

@@ -8,9 +8,9 @@
 // Layout: jobs are SPARSE -- job slot i belongs to read i (an empty SeqPair, len 0, when read i
 // has no extension on that side), so no compaction is needed; the engine's plan / sort puts
 // the empty slots in their own cheap wavefronts.  Code buffers use fixed per-read strides
-// (qstride = max read length, tstride = max read length + 2w + 1 >= any window, since
-// cal_max_gap <= 2w): LEFT writes the reversed query prefix and the reversed window, RIGHT the
-// forward suffix and window.
+// (qstride = the longest seeded read, tstride = the longest target window either side uses,
+// both found by ext_scan): LEFT writes the reversed query prefix and the reversed window, RIGHT
+// the forward suffix and window.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "bsw_ext_k.h"
@@ -27,38 +27,76 @@ __device__ __forceinline__ int cal_max_gap_d(const ExtDevParams &p, int qlen)
     return min(l, p.w << 1);
 }
 
-// Per block (LDS), then one global atomic per block and word into slot blockIdx % 32 (own 64-B
-// line): meta[slot * 16 + k], k = 0 max read length, 1 input error, 2 / 3 LEFT / RIGHT job counts.
-__global__ void ext_scan_kernel(const int32_t *__restrict__ read_len, const bsw_seed_t *__restrict__ seeds,
-                                int32_t n, int64_t ref_len, int32_t *__restrict__ meta)
+// mem_chain2aln's target window of one seed taken as a chain of one (bsw_ext.cpp chain_window)
+__device__ __forceinline__ void seed_window_d(const ExtDevParams &p, const bsw_seed_t &s, int l, int64_t *r0,
+                                              int64_t *r1)
 {
-    __shared__ int s_m[4];
-    if (threadIdx.x < 4) s_m[threadIdx.x] = 0;
+    const int qe = s.qbeg + s.len;
+    int64_t lo = s.rbeg - (s.qbeg + cal_max_gap_d(p, s.qbeg));
+    int64_t hi = s.rbeg + s.len + ((l - qe) + cal_max_gap_d(p, l - qe));
+    lo = lo > 0 ? lo : 0;
+    hi = hi < p.ref_len ? hi : p.ref_len;
+    if (p.l_pac > 0 && lo < p.l_pac && p.l_pac < hi) {
+        if (s.rbeg < p.l_pac) hi = p.l_pac;
+        else lo = p.l_pac;
+    }
+    *r0 = lo;
+    *r1 = hi;
+}
+
+// Per read: validation and the target window (given per job in win, else the seed's own) into
+// wout; per block (LDS), then one global atomic per block and word into slot blockIdx % 32 (own
+// 64-B line): meta[slot * 16 + k], k = 0 max read length, 1 input error, 2 / 3 LEFT / RIGHT job
+// counts, 4 longest target window.  A seeded read is rejected exactly as the host form rejects
+// it (bsw_ext.cpp): seed outside the read / reference or across l_pac, read or either side's
+// window longer than BSW_MAX_LEN, a given window that does not hold the seed.
+__global__ void ext_scan_kernel(const ExtDevParams p, const int32_t *__restrict__ read_len,
+                                const bsw_seed_t *__restrict__ seeds, const int64_t *__restrict__ win, int32_t n,
+                                int64_t *__restrict__ wout, int32_t *__restrict__ meta)
+{
+    __shared__ int s_m[5];
+    if (threadIdx.x < 5) s_m[threadIdx.x] = 0;
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    int l = 0, err = 0, nl = 0, nr = 0;
+    int l = 0, err = 0, nl = 0, nr = 0, tl = 0;
     if (i < n) {
         const bsw_seed_t s = seeds[i];
+        int64_t r0 = 0, r1 = 0;
         if (s.len > 0) {            // only seeded reads are validated and sized (as bsw_extend_seeds)
             l = read_len[i];
             if (l < 0 || l > BSW_MAX_LEN || s.qbeg < 0 || s.qbeg + s.len > l || s.rbeg < 0 ||
-                s.rbeg + s.len > ref_len) {
+                s.rbeg + s.len > p.ref_len || (p.l_pac > 0 && s.rbeg < p.l_pac && s.rbeg + s.len > p.l_pac)) {
                 err = 1;
-                l = 0;
             } else {
-                nl = s.qbeg > 0;
-                nr = s.qbeg + s.len < l;
+                if (win) {
+                    r0 = win[2 * i];
+                    r1 = win[2 * i + 1];
+                } else {
+                    seed_window_d(p, s, l, &r0, &r1);
+                }
+                const int64_t lt = s.rbeg - r0, rt = r1 - (s.rbeg + s.len);
+                if (lt < 0 || rt < 0 || lt > BSW_MAX_LEN || rt > BSW_MAX_LEN) {
+                    err = 1;
+                } else {
+                    nl = s.qbeg > 0;
+                    nr = s.qbeg + s.len < l;
+                    tl = (int)max(nl ? lt : 0, nr ? rt : 0);
+                }
             }
+            if (err) l = 0;
         }
+        wout[2 * i] = r0;
+        wout[2 * i + 1] = r1;
     }
     const int lane = threadIdx.x & 63;
-    const int wl = wave_max(l);
+    const int wl = wave_max(l), wt = wave_max(tl);
     const unsigned long long be = __ballot(err), bl = __ballot(nl), br = __ballot(nr);
     if (lane == 0) {
         atomicMax(&s_m[0], wl);
         if (be) atomicOr(&s_m[1], 1);
         if (bl) atomicAdd(&s_m[2], __popcll(bl));
         if (br) atomicAdd(&s_m[3], __popcll(br));
+        atomicMax(&s_m[4], wt);
     }
     __syncthreads();
     int32_t *slot = meta + (blockIdx.x % kExtMetaSpread) * 16;
@@ -66,14 +104,15 @@ __global__ void ext_scan_kernel(const int32_t *__restrict__ read_len, const bsw_
     if (threadIdx.x == 1 && s_m[1]) atomicOr(&slot[1], 1);
     if (threadIdx.x == 2 && s_m[2]) atomicAdd(&slot[2], s_m[2]);
     if (threadIdx.x == 3 && s_m[3]) atomicAdd(&slot[3], s_m[3]);
+    if (threadIdx.x == 4 && s_m[4]) atomicMax(&slot[4], s_m[4]);
 }
 
 __global__ void ext_left_build_kernel(const ExtDevParams p, const uint8_t *__restrict__ reads,
                                       const int64_t *__restrict__ read_off, const int32_t *__restrict__ read_len,
-                                      const bsw_seed_t *__restrict__ seeds, int32_t n, const uint8_t *__restrict__ ref,
-                                      ExtState *__restrict__ st, SeqPair *__restrict__ pairs,
-                                      uint8_t *__restrict__ qbuf, uint8_t *__restrict__ tbuf,
-                                      bsw_alnreg_t *__restrict__ out)
+                                      const bsw_seed_t *__restrict__ seeds, const int64_t *__restrict__ win,
+                                      int32_t n, const uint8_t *__restrict__ ref, ExtState *__restrict__ st,
+                                      SeqPair *__restrict__ pairs, uint8_t *__restrict__ qbuf,
+                                      uint8_t *__restrict__ tbuf, bsw_alnreg_t *__restrict__ out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -85,11 +124,9 @@ __global__ void ext_left_build_kernel(const ExtDevParams p, const uint8_t *__res
     sp.id = i;
     const bsw_seed_t s = seeds[i];
     if (s.len > 0) {
-        const int l = read_len[i], qe = s.qbeg + s.len;
-        const int64_t b = s.rbeg - (s.qbeg + cal_max_gap_d(p, s.qbeg));
-        const int64_t e = s.rbeg + s.len + ((l - qe) + cal_max_gap_d(p, l - qe));
-        x.rmax0 = b > 0 ? b : 0;
-        x.rmax1 = e < p.ref_len ? e : p.ref_len;
+        const int l = read_len[i];
+        x.rmax0 = win[2 * i];                           // the window ext_scan validated
+        x.rmax1 = win[2 * i + 1];
         r.seedlen0 = s.len;
         r.score = r.truesc = s.len * p.a;               // no-extension defaults (mem_chain2aln)
         r.qb = 0; r.rb = s.rbeg;
@@ -227,24 +264,24 @@ __global__ void ext_interp_kernel(const ExtDevParams p, const int32_t *__restric
 
 static inline dim3 grid_of(int32_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
-hipError_t launch_ext_scan(const int32_t *read_len, const bsw_seed_t *seeds, int32_t n, int64_t ref_len,
-                           int32_t *meta, hipStream_t s)
+hipError_t launch_ext_scan(const ExtDevParams &p, const int32_t *read_len, const bsw_seed_t *seeds, const int64_t *win,
+                           int32_t n, int64_t *wout, int32_t *meta, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(meta, 0, kExtMetaSpread * 16 * sizeof(int32_t), s);
     if (e != hipSuccess || n <= 0) return e;
-    hipLaunchKernelGGL(ext_scan_kernel, grid_of(n), dim3(256), 0, s, read_len, seeds, n, ref_len, meta);
+    hipLaunchKernelGGL(ext_scan_kernel, grid_of(n), dim3(256), 0, s, p, read_len, seeds, win, n, wout, meta);
     return hipGetLastError();
 }
 
 hipError_t launch_ext_build(int left, const ExtDevParams &p, const uint8_t *reads, const int64_t *read_off,
-                            const int32_t *read_len, const bsw_seed_t *seeds, int32_t n, const uint8_t *ref,
-                            ExtState *st, SeqPair *pairs, uint8_t *qbuf, uint8_t *tbuf, bsw_alnreg_t *out,
-                            hipStream_t s)
+                            const int32_t *read_len, const bsw_seed_t *seeds, const int64_t *win, int32_t n,
+                            const uint8_t *ref, ExtState *st, SeqPair *pairs, uint8_t *qbuf, uint8_t *tbuf,
+                            bsw_alnreg_t *out, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
     if (left)
         hipLaunchKernelGGL(ext_left_build_kernel, grid_of(n), dim3(256), 0, s, p, reads, read_off, read_len, seeds,
-                           n, ref, st, pairs, qbuf, tbuf, out);
+                           win, n, ref, st, pairs, qbuf, tbuf, out);
     else
         hipLaunchKernelGGL(ext_right_build_kernel, grid_of(n), dim3(256), 0, s, p, reads, read_off, read_len, seeds,
                            n, ref, st, pairs, qbuf, tbuf);

@@ -212,6 +212,7 @@ struct Slot {
     SeqPair *d_xpairs = nullptr, *d_xsub = nullptr; size_t cap_xpairs = 0, cap_xsub = 0;
     uint8_t *d_xq = nullptr, *d_xt = nullptr; size_t cap_xq = 0, cap_xt = 0;
     ExtState *d_xst = nullptr; size_t cap_xst = 0;
+    int64_t *d_xwin = nullptr; size_t cap_xwin = 0;   // per-read target windows (ext_scan)
     // class launches of one batch fork over side streams (independent pairs; small batches are
     // bound by the longest wave of each class, so classes run side by side instead of in turn)
     static constexpr int kSide = 3;
@@ -276,6 +277,7 @@ struct DeviceCtx {
         if (s->h_gmeta) (void)hipHostFree(s->h_gmeta);
         (void)hipFree(s->d_xpairs); (void)hipFree(s->d_xsub); (void)hipFree(s->d_xq); (void)hipFree(s->d_xt);
         (void)hipFree(s->d_xst);
+        (void)hipFree(s->d_xwin);
         if (s->ev2) (void)hipEventDestroy(s->ev2);
         if (s->ev3) (void)hipEventDestroy(s->ev3);
         if (s->h_meta) (void)hipHostFree(s->h_meta);
@@ -1284,12 +1286,12 @@ static int glob_device(const GlobParams &gp, Slot &s, SeqPair *d_pairs, const ui
 // readback and one retry count per retry round.
 static int ext_side_device(const KParams &kp0, Slot &s, const ExtDevParams &xp, int left, const bsw_ext_opt_t &opt,
                            const uint8_t *d_reads, const int64_t *d_off, const int32_t *d_len,
-                           const bsw_seed_t *d_seeds, int32_t n, const uint8_t *d_ref, bsw_alnreg_t *d_out,
-                           int32_t *d_cnt, hipStream_t st, bsw_ext_stats_t &es)
+                           const bsw_seed_t *d_seeds, const int64_t *d_win, int32_t n, const uint8_t *d_ref,
+                           bsw_alnreg_t *d_out, int32_t *d_cnt, hipStream_t st, bsw_ext_stats_t &es)
 {
     KParams kp = kp0;
     kp.end_bonus = left ? opt.pen_clip5 : opt.pen_clip3;
-    BSW_TRY(launch_ext_build(left, xp, d_reads, d_off, d_len, d_seeds, n, d_ref, s.d_xst, s.d_xpairs, s.d_xq,
+    BSW_TRY(launch_ext_build(left, xp, d_reads, d_off, d_len, d_seeds, d_win, n, d_ref, s.d_xst, s.d_xpairs, s.d_xq,
                              s.d_xt, d_out, st));
     int r = run_device(kp, s, s.d_xpairs, s.d_xt, s.d_xq, n, opt.w, 16, st);
     if (r) return r;
@@ -1457,6 +1459,12 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
 
 void ctx_params(const bsw_ctx_t *ctx, bsw_params_t *out) { *out = ctx->params; }
 int ctx_device(const bsw_ctx_t *ctx) { return ctx->devs[0]->device; }
+int64_t ctx_refres_len(bsw_ctx_t *ctx)
+{
+    bsw::DeviceCtx &dc = *ctx->devs[0];
+    std::shared_lock<std::shared_mutex> g(dc.refmu);
+    return dc.d_refres ? dc.refres_len : -1;
+}
 
 void *pinned_acquire(bsw_ctx_t *ctx, int which, size_t bytes)
 {
@@ -1492,42 +1500,6 @@ int get_chain_stats(bsw_ctx_t *ctx, bsw_chain_stats_t *out)
     if (!ctx || !out) return BSW_E_INVAL;
     std::lock_guard<std::mutex> g(ctx->stats_mu);
     *out = ctx->chain_last;
-    return BSW_OK;
-}
-
-DevJobs::~DevJobs()
-{
-    if (device < 0) return;
-    (void)hipSetDevice(device);
-    (void)hipFree(d_off); (void)hipFree(d_len); (void)hipFree(d_seed); (void)hipFree(d_out);
-}
-
-int ext_device_jobs(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads, DevJobs &dj, int32_t nj,
-                    const int64_t *off, const int32_t *len, const bsw_seed_t *seeds, bsw_alnreg_t *out)
-{
-    if (nj <= 0) return BSW_OK;
-    BSW_TRY(hipSetDevice(ctx->devs[0]->device));
-    if ((size_t)nj > dj.cap) {
-        if (dj.device >= 0) {
-            (void)hipFree(dj.d_off); (void)hipFree(dj.d_len); (void)hipFree(dj.d_seed); (void)hipFree(dj.d_out);
-        }
-        dj.device = ctx->devs[0]->device;
-        dj.d_off = dj.d_len = dj.d_seed = dj.d_out = nullptr;
-        dj.cap = 0;
-        const size_t cap = std::max((size_t)nj, (size_t)4096);
-        BSW_TRY(hipMalloc(&dj.d_off, cap * sizeof(int64_t)));
-        BSW_TRY(hipMalloc(&dj.d_len, cap * sizeof(int32_t)));
-        BSW_TRY(hipMalloc(&dj.d_seed, cap * sizeof(bsw_seed_t)));
-        BSW_TRY(hipMalloc(&dj.d_out, cap * sizeof(bsw_alnreg_t)));
-        dj.cap = cap;
-    }
-    BSW_TRY(hipMemcpy(dj.d_off, off, (size_t)nj * sizeof(int64_t), hipMemcpyHostToDevice));
-    BSW_TRY(hipMemcpy(dj.d_len, len, (size_t)nj * sizeof(int32_t), hipMemcpyHostToDevice));
-    BSW_TRY(hipMemcpy(dj.d_seed, seeds, (size_t)nj * sizeof(bsw_seed_t), hipMemcpyHostToDevice));
-    const int rc = bsw_extend_seeds_device(ctx, opt, d_reads, (const int64_t *)dj.d_off, (const int32_t *)dj.d_len,
-                                           (const bsw_seed_t *)dj.d_seed, nj, (bsw_alnreg_t *)dj.d_out, nullptr);
-    if (rc) return rc;
-    BSW_TRY(hipMemcpy(out, dj.d_out, (size_t)nj * sizeof(bsw_alnreg_t), hipMemcpyDeviceToHost));
     return BSW_OK;
 }
 
@@ -1852,12 +1824,21 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
                             const int64_t *d_read_off, const int32_t *d_read_len, const bsw_seed_t *d_seeds,
                             int32_t n, bsw_alnreg_t *d_out, void *stream)
 {
+    return bsw::extend_seeds_device_win(ctx, opt, d_reads, d_read_off, d_read_len, d_seeds, nullptr, n, d_out, stream);
+}
+
+}  // extern "C"
+
+int bsw::extend_seeds_device_win(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
+                                 const int64_t *d_read_off, const int32_t *d_read_len, const bsw_seed_t *d_seeds,
+                                 const int64_t *d_win, int32_t n, bsw_alnreg_t *d_out, void *stream)
+{
     if (!ctx || !opt || n < 0 || (n > 0 && (!d_reads || !d_read_off || !d_read_len || !d_seeds || !d_out)))
         return BSW_E_INVAL;
-    if (opt->w < 0 || opt->max_band_try < 1) return BSW_E_INVAL;
     bsw::DeviceCtx &dc = *ctx->devs[0];
     std::shared_lock<std::shared_mutex> refg(dc.refmu);   // the resident reference stays put
     if (!dc.d_refres) return BSW_E_INVAL;
+    if (const int rc = bsw::ext_opt_check(opt, dc.refres_len)) return rc;
     if (n == 0) return BSW_OK;
     const auto t0 = std::chrono::steady_clock::now();
     int rc = BSW_OK;
@@ -1869,28 +1850,30 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
         BSW_TRY(hipSetDevice(dc.device));
         hipStream_t st = stream ? (hipStream_t)stream : s.stream;
         const bsw_params_t &p = ctx->params;
-        // scan: max read length, input errors, job counts
-        BSW_TRY(bsw::launch_ext_scan(d_read_len, d_seeds, n, dc.refres_len, s.d_meta, st));
-        static_assert(bsw::kExtMetaSpread * 16 <= bsw::kMetaWords, "ext meta fits d_meta");
-        BSW_TRY(hipMemcpyAsync(s.h_meta, s.d_meta, bsw::kExtMetaSpread * 16 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        BSW_TRY(hipStreamSynchronize(st));
-        int32_t m[4] = {0, 0, 0, 0};
-        for (int sl = 0; sl < bsw::kExtMetaSpread; ++sl) {
-            const int32_t *v = s.h_meta + sl * 16;
-            m[0] = std::max(m[0], v[0]); m[1] |= v[1]; m[2] += v[2]; m[3] += v[3];
-        }
-        if (m[1]) return BSW_E_RANGE;
-        es.n_pairs[0] = m[2];
-        es.n_pairs[2] = m[3];
         bsw::ExtDevParams xp{};
         xp.w = opt->w; xp.pen_clip5 = opt->pen_clip5; xp.pen_clip3 = opt->pen_clip3; xp.a = p.mat[0];
         xp.o_del = p.o_del; xp.e_del = p.e_del; xp.o_ins = p.o_ins; xp.e_ins = p.e_ins;
-        xp.qstride = std::max(m[0], 1);
-        xp.tstride = m[0] + 2 * opt->w + 1;             // cal_max_gap <= 2w
         xp.ref_len = dc.refres_len;
-        if ((int64_t)xp.tstride > BSW_MAX_LEN) return BSW_E_RANGE;
+        xp.l_pac = opt->l_pac;
+        // scan: per-read validation and windows, longest read / window, job counts
+        BSW_TRY(bsw::grow(s.d_xwin, s.cap_xwin, 2 * (size_t)n));
+        BSW_TRY(bsw::launch_ext_scan(xp, d_read_len, d_seeds, d_win, n, s.d_xwin, s.d_meta, st));
+        static_assert(bsw::kExtMetaSpread * 16 <= bsw::kMetaWords, "ext meta fits d_meta");
+        BSW_TRY(hipMemcpyAsync(s.h_meta, s.d_meta, bsw::kExtMetaSpread * 16 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        BSW_TRY(hipStreamSynchronize(st));
+        int32_t m[5] = {0, 0, 0, 0, 0};
+        for (int sl = 0; sl < bsw::kExtMetaSpread; ++sl) {
+            const int32_t *v = s.h_meta + sl * 16;
+            m[0] = std::max(m[0], v[0]); m[1] |= v[1]; m[2] += v[2]; m[3] += v[3]; m[4] = std::max(m[4], v[4]);
+        }
+        if (m[1]) return BSW_E_RANGE;                   // per read, as the host form (bsw_ext.cpp)
+        es.n_pairs[0] = m[2];
+        es.n_pairs[2] = m[3];
+        xp.qstride = std::max(m[0], 1);                 // longest seeded read
+        xp.tstride = std::max(m[4], 1);                 // longest target window (<= BSW_MAX_LEN)
         // SeqPair idr / idq are int32: chunk so i * tstride stays below 2^31
-        const int32_t chunk = (int32_t)std::min<int64_t>(std::min<int64_t>(n, (int64_t)INT32_MAX / xp.tstride - 1),
+        const int32_t chunk = (int32_t)std::min<int64_t>(std::min<int64_t>(n, (int64_t)INT32_MAX /
+                                                                                  std::max(xp.tstride, xp.qstride) - 1),
                                                          bsw::ext_chunk_cap(ctx));
         BSW_TRY(bsw::grow(s.d_xpairs, s.cap_xpairs, (size_t)chunk));
         BSW_TRY(bsw::grow(s.d_xsub, s.cap_xsub, (size_t)chunk));
@@ -1903,7 +1886,8 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
             const int32_t b = std::min(n, a + chunk);
             for (int left = 1; left >= 0; --left) {
                 const int r = bsw::ext_side_device(ctx->kp, s, xp, left, *opt, d_reads, d_read_off + a, d_read_len + a,
-                                                   d_seeds + a, b - a, dc.d_refres, d_out + a, d_cnt, st, es);
+                                                   d_seeds + a, s.d_xwin + 2 * (size_t)a, b - a, dc.d_refres,
+                                                   d_out + a, d_cnt, st, es);
                 if (r) return r;
             }
         }
@@ -1916,6 +1900,8 @@ int bsw_extend_seeds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint
     bsw::set_ext_stats(ctx, es);
     return BSW_OK;
 }
+
+extern "C" {
 
 int bsw_split_by_cells(const SeqPair *pairs, int32_t n, int32_t w, int32_t parts, int32_t *cut)
 {

@@ -12,6 +12,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
               const uint8_t *qer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *st);
 void ctx_params(const bsw_ctx_t *ctx, bsw_params_t *out);
 int ctx_device(const bsw_ctx_t *ctx);          // HIP device of the context's first device slot pool
+int64_t ctx_refres_len(bsw_ctx_t *ctx);        // length of the resident reference (-1: none)
 // Per-context pinned host staging buffer `which` (0, 1) of at least `bytes`: DMA-speed H2D for
 // the extension pipeline's code buffers.  Returns nullptr when another call holds it (the
 // caller then uses pageable memory); release with pinned_release.
@@ -22,16 +23,14 @@ int64_t ext_chunk_cap(const bsw_ctx_t *ctx);   // reads per extension chunk (BSW
 int get_ext_stats(bsw_ctx_t *ctx, bsw_ext_stats_t *out);
 void set_chain_stats(bsw_ctx_t *ctx, const bsw_chain_stats_t &s);
 int get_chain_stats(bsw_ctx_t *ctx, bsw_chain_stats_t *out);
-// Device buffers of one round of bsw_chain2aln_device (job arrays up, regions down).
-struct DevJobs {
-    void *d_off = nullptr, *d_len = nullptr, *d_seed = nullptr, *d_out = nullptr;
-    size_t cap = 0;
-    int device = -1;
-    ~DevJobs();
-};
-// bsw_extend_seeds_device over nj jobs given on the host (reads resident at d_reads)
-int ext_device_jobs(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads, DevJobs &dj, int32_t nj,
-                    const int64_t *off, const int32_t *len, const bsw_seed_t *seeds, bsw_alnreg_t *out);
+// bsw_ext_opt_t / seed checks shared by the host and device extension forms (bsw_ext.cpp)
+int ext_opt_check(const bsw_ext_opt_t *opt, int64_t ref_len);
+bool ext_seed_ok(const bsw_ext_opt_t *opt, const bsw_seed_t &s, int32_t l, int64_t ref_len);
+// bsw_extend_seeds_device with each job's target window given (d_win[2j], d_win[2j + 1]: the
+// chain's window, mem_chain2aln) or computed per seed (d_win == nullptr)
+int extend_seeds_device_win(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads,
+                            const int64_t *d_read_off, const int32_t *d_read_len, const bsw_seed_t *d_seeds,
+                            const int64_t *d_win, int32_t n, bsw_alnreg_t *d_out, void *stream);
 // mem_chain2aln rounds with every per-read decision on the GPU (bsw_chain.hip): inputs and
 // outputs device-resident on the context's first device
 int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t *d_reads, const int64_t *d_read_off,

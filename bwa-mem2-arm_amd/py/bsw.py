@@ -262,7 +262,7 @@ def read_batch(path: str):
 class ExtOpt(ctypes.Structure):
     """Mirror of bsw_ext_opt_t (include/bsw_ext.h)."""
     _fields_ = [("w", ctypes.c_int32), ("pen_clip5", ctypes.c_int32), ("pen_clip3", ctypes.c_int32),
-                ("max_band_try", ctypes.c_int32)]
+                ("max_band_try", ctypes.c_int32), ("l_pac", ctypes.c_int64)]
 
 
 class ExtStats(ctypes.Structure):

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BSW_ABI_VERSION 4
+#define BSW_ABI_VERSION 5
 
 enum {
     BSW_OK = 0,

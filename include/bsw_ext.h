@@ -9,8 +9,11 @@
  * [UPSTREAM-RECALL, SURVEY.md a9]:
  *
  *   seed (qbeg, rbeg, len) of a read of length l_query, seed score sc = len * a
- *   target window rmax = [rbeg - qbeg - gap(qbeg), rbeg + len + (l_query - qe) + gap(l_query - qe))
- *     clipped to the reference, gap(l) = min(max((l*a - o)/e + 1, 1), 2w)   (cal_max_gap)
+ *   target window rmax = [min over the CHAIN's seeds of rbeg - qbeg - gap(qbeg),
+ *                         max over the chain's seeds of rbeg + len + (l_query - qe) + gap(l_query - qe))
+ *     clipped to [0, ref_len), gap(l) = min(max((l*a - o)/e + 1, 1), 2w)   (cal_max_gap); with
+ *     opt->l_pac > 0 a window crossing l_pac keeps the side of the chain's first seed
+ *     (mem_chain2aln's rmax[] computation).  bsw_extend_seeds treats every seed as a chain of one.
  *   LEFT  (qbeg > 0): query = reverse(read[0, qbeg)), target = reverse(ref[rmax0, rbeg)),
  *         h0 = sc, end_bonus = pen_clip5, band w << k for k < max_band_try (retry while the
  *         score changed and max_off >= 3/4 of the band)
@@ -48,6 +51,11 @@ typedef struct bsw_ext_opt_t {
     int32_t w;                       /* band width (bwa -w, default 100)                        */
     int32_t pen_clip5, pen_clip3;    /* clipping penalties (bwa -L, default 5,5)                */
     int32_t max_band_try;            /* band doublings incl. the first try (bwa: 2)             */
+    int64_t l_pac;                   /* > 0: ref is bwa's forward + reverse-complement text of
+                                        2 * l_pac bases (bns->l_pac), and a target window that
+                                        crosses l_pac keeps the strand of the chain's first
+                                        seed (mem_chain2aln); 0 (default): ref is one strand,
+                                        windows are clipped to [0, ref_len) only               */
 } bsw_ext_opt_t;
 
 typedef struct bsw_alnreg_t {        /* the mem_alnreg_t fields the extension determines       */

@@ -33,22 +33,47 @@ static int cal_max_gap(const oracle_params_t *p, int a, int w, int qlen)
     return l < w << 1 ? l : w << 1;
 }
 
-/* one seed's extension (the body of mem_chain2aln's per-seed step) */
+/* mem_chain2aln's target window over seeds[0, n) of one chain (bwa 0.7.x src/bwamem.c, the rmax[]
+ * loop at the top of mem_chain2aln): min / max over the seeds of the per-seed reach, clipped to
+ * [0, ref_len); with l_pac > 0 (ref = forward + reverse-complement text) a window crossing l_pac
+ * keeps the side of the chain's first seed.  Seeds with len <= 0 (no seed) take no part. */
+void oracle_chain_window(const oracle_params_t *p, const bsw_ext_opt_t *opt, int64_t ref_len, int l_query,
+                         const bsw_seed_t *const *seeds, int n, int64_t *rmax0, int64_t *rmax1)
+{
+    const int a = p->mat[0];
+    int64_t lo = ref_len, hi = 0, first = -1;
+    for (int i = 0; i < n; ++i) {
+        const bsw_seed_t *t = seeds[i];
+        if (t->len <= 0) continue;
+        if (first < 0) first = t->rbeg;
+        const int64_t b = t->rbeg - (t->qbeg + cal_max_gap(p, a, opt->w, t->qbeg));
+        const int64_t e = t->rbeg + t->len + ((l_query - t->qbeg - t->len) +
+                                              cal_max_gap(p, a, opt->w, l_query - t->qbeg - t->len));
+        lo = lo < b ? lo : b;
+        hi = hi > e ? hi : e;
+    }
+    lo = lo > 0 ? lo : 0;
+    hi = hi < ref_len ? hi : ref_len;
+    if (opt->l_pac > 0 && lo < opt->l_pac && opt->l_pac < hi) {   /* crossing the forward-reverse boundary */
+        if (first < opt->l_pac) hi = opt->l_pac;
+        else lo = opt->l_pac;
+    }
+    *rmax0 = lo;
+    *rmax1 = hi;
+}
+
+/* one seed's extension inside the window [rmax0, rmax1) (the body of mem_chain2aln's per-seed step) */
 static void oracle_extend_one(const oracle_params_t *p, const bsw_ext_opt_t *opt, const uint8_t *ref,
-                              int64_t ref_len, const uint8_t *query, int l_query, const bsw_seed_t *s,
-                              bsw_alnreg_t *r)
+                              int64_t rmax0, int64_t rmax1, const uint8_t *query, int l_query,
+                              const bsw_seed_t *s, bsw_alnreg_t *r)
 {
     const int a = p->mat[0];
     {
         int qle, tle, gtle, gscore, max_off[2] = {0, 0}, aw[2];
         memset(r, 0, sizeof(*r));
         if (s->len <= 0) return;
-        int64_t rmax0 = s->rbeg - (s->qbeg + cal_max_gap(p, a, opt->w, s->qbeg));
-        int64_t rmax1 = s->rbeg + s->len + ((l_query - s->qbeg - s->len) +
-                                            cal_max_gap(p, a, opt->w, l_query - s->qbeg - s->len));
-        rmax0 = rmax0 > 0 ? rmax0 : 0;
-        rmax1 = rmax1 < ref_len ? rmax1 : ref_len;
         aw[0] = aw[1] = opt->w;
+        r->score = r->truesc = -1;                       /* as upstream: the first try's prev */
         r->seedlen0 = s->len;
         if (s->qbeg) {                                   /* left extension */
             int tmp = (int)(s->rbeg - rmax0);
@@ -105,8 +130,12 @@ void oracle_extend_seeds(const oracle_params_t *p, const bsw_ext_opt_t *opt, con
                          const int32_t *read_len, const bsw_seed_t *seeds, int32_t n,
                          bsw_alnreg_t *out)
 {
-    for (int32_t i = 0; i < n; ++i)
-        oracle_extend_one(p, opt, ref, ref_len, reads + read_off[i], read_len[i], &seeds[i], &out[i]);
+    for (int32_t i = 0; i < n; ++i) {                   /* every seed a chain of one */
+        const bsw_seed_t *s = &seeds[i];
+        int64_t r0 = 0, r1 = 0;
+        oracle_chain_window(p, opt, ref_len, read_len[i], &s, 1, &r0, &r1);
+        oracle_extend_one(p, opt, ref, r0, r1, reads + read_off[i], read_len[i], s, &out[i]);
+    }
 }
 
 /* mem_chain2aln over the chains of every read, literal per-read order (bwa 0.7.x src/bwamem.c,
@@ -116,7 +145,8 @@ void oracle_extend_seeds(const oracle_params_t *p, const bsw_ext_opt_t *opt, con
  * skipped when an earlier region of the READ (any chain) contains it "around" the same
  * diagonal -- unless an extended, at least 95%-as-long seed of its own chain overlaps it on a
  * different diagonal; otherwise it is extended (oracle_extend_one) and its region appended.
- * Seeds are grouped by read (seed_read non-decreasing), chains are runs of equal seed_chain. */
+ * Seeds are grouped by read (seed_read non-decreasing), chains are runs of equal seed_chain; every
+ * seed of a chain extends inside the chain's one target window (oracle_chain_window). */
 static int oracle_contained(const oracle_params_t *p, const bsw_ext_opt_t *opt, const bsw_seed_t *s,
                             int l_query, const bsw_alnreg_t *out, const int32_t *av, int nav)
 {
@@ -159,6 +189,13 @@ void oracle_chain2aln(const oracle_params_t *p, const bsw_ext_opt_t *opt, const 
             int32_t c1 = c0;
             while (c1 < r1 && seed_chain[c1] == seed_chain[c0]) ++c1;
             const int n = c1 - c0;
+            int64_t rmax0 = 0, rmax1 = 0;                   /* the chain's target window */
+            {
+                const bsw_seed_t **cs = (const bsw_seed_t **)malloc(sizeof(*cs) * (size_t)n);
+                for (int i = 0; i < n; ++i) cs[i] = &seeds[c0 + i];
+                oracle_chain_window(p, opt, ref_len, l_query, cs, n, &rmax0, &rmax1);
+                free(cs);
+            }
             /* srt ascending by (score, index); processed from the top down */
             for (int i = 0; i < n; ++i) srt[i] = c0 + i;
             for (int i = 1; i < n; ++i)
@@ -185,7 +222,7 @@ void oracle_chain2aln(const oracle_params_t *p, const bsw_ext_opt_t *opt, const 
                     }
                     if (i == n) continue;                   /* skipped: not extended */
                 }
-                oracle_extend_one(p, opt, ref, ref_len, query, l_query, s, &out[si]);
+                oracle_extend_one(p, opt, ref, rmax0, rmax1, query, l_query, s, &out[si]);
                 extended[si] = 1;
                 av[nav++] = si;
             }

@@ -73,7 +73,7 @@ def test_params_default_and_abi_version():
     assert (p.o_del, p.e_del, p.o_ins, p.e_ins, p.zdrop, p.end_bonus) == (6, 1, 6, 1, 100, 5)
     mat = np.frombuffer(bytes(p.mat), np.int8).reshape(5, 5)
     assert mat[0, 0] == 1 and mat[0, 1] == -4 and mat[4, 4] == -1 and mat[2, 4] == -1
-    assert lib.bsw_abi_version() == 4
+    assert lib.bsw_abi_version() == 5
     ref = bsw.default_params()
     assert bytes(ref.mat) == bytes(p.mat)
 
@@ -127,12 +127,12 @@ def test_ext_header_layouts_compile(tmp_path):
         "_Static_assert(sizeof(bsw_alnreg_t) == 40, \"alnreg\");\n"
         "_Static_assert(offsetof(bsw_alnreg_t, qb) == 16, \"qb\");\n"
         "_Static_assert(offsetof(bsw_alnreg_t, seedlen0) == 36, \"seedlen0\");\n"
-        "_Static_assert(sizeof(bsw_ext_opt_t) == 16, \"opt\");\n")
+        "_Static_assert(sizeof(bsw_ext_opt_t) == 24, \"opt\");\n")
     r = subprocess.run(["gcc", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert bsw.SEED_DTYPE.itemsize == 16 and bsw.ALNREG_DTYPE.itemsize == 40
-    assert ctypes.sizeof(bsw.ExtOpt) == 16
+    assert ctypes.sizeof(bsw.ExtOpt) == 24
 
 
 def _static_cells(q, t, w):

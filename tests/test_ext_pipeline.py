@@ -27,8 +27,28 @@ def _cal_max_gap(p, a, w, qlen):
     return min(max(max(l_del, l_ins), 1), w << 1)
 
 
-def py_extend(p, opt, ref, reads, off, lens, seeds):
-    """Independent transcription of the extension half of mem_chain2aln, one seed per read."""
+def py_chain_window(p, opt, ref_len, l_query, chain):
+    """mem_chain2aln's rmax[] (bwa src/bwamem.c): min / max of the chain's seeds' reach, clipped
+    to the text, and on a two-strand text (opt.l_pac > 0) the first seed's side of l_pac."""
+    a = p.mat[0]
+    lo, hi = ref_len, 0
+    for s in chain:
+        qbeg, rbeg, slen = int(s["qbeg"]), int(s["rbeg"]), int(s["len"])
+        lo = min(lo, rbeg - (qbeg + _cal_max_gap(p, a, opt.w, qbeg)))
+        qe = qbeg + slen
+        hi = max(hi, rbeg + slen + (l_query - qe) + _cal_max_gap(p, a, opt.w, l_query - qe))
+    lo, hi = max(lo, 0), min(hi, ref_len)
+    if opt.l_pac > 0 and lo < opt.l_pac < hi:
+        if int(chain[0]["rbeg"]) < opt.l_pac:
+            hi = opt.l_pac
+        else:
+            lo = opt.l_pac
+    return lo, hi
+
+
+def py_extend(p, opt, ref, reads, off, lens, seeds, windows=None):
+    """Independent transcription of the extension half of mem_chain2aln, one seed per read
+    (windows[i] = the chain's target window; default: the seed's own, a chain of one)."""
     a = p.mat[0]
     mat = list(p.mat)
     out = np.zeros(len(seeds), dtype=bsw.ALNREG_DTYPE)
@@ -37,13 +57,12 @@ def py_extend(p, opt, ref, reads, off, lens, seeds):
             continue
         q = reads[off[i]:off[i] + lens[i]]
         l_query, qbeg, rbeg, slen = int(lens[i]), int(s["qbeg"]), int(s["rbeg"]), int(s["len"])
-        rmax0 = max(rbeg - (qbeg + _cal_max_gap(p, a, opt.w, qbeg)), 0)
+        rmax0, rmax1 = windows[i] if windows is not None else py_chain_window(p, opt, len(ref), l_query, [s])
         qe = qbeg + slen
-        rmax1 = min(rbeg + slen + (l_query - qe) + _cal_max_gap(p, a, opt.w, l_query - qe), len(ref))
         r = out[i]
         aw = [opt.w, opt.w]
         r["seedlen0"] = slen
-        score = 0
+        score = -1                                        # a->score before the first band try
         if qbeg:
             qs = q[:qbeg][::-1]
             rs = ref[rmax0:rbeg][::-1]
@@ -262,4 +281,43 @@ def test_gpu_pipelines_no_fork():
     dev = bsw.extend_seeds_resident(eng, reads, off, lens, seeds, opt)
     _same(want, host, "host-built pipeline, no fork")
     _same(want, dev, "device pipeline, no fork")
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_host_and_device_pipelines_accept_the_same_reads():
+    """Both forms validate per read (the device form used to reject a whole batch when the
+    longest read + 2w + 1 passed BSW_MAX_LEN): a 32,700-base read whose windows fit is accepted
+    by both and equals the oracle; a read whose LEFT window passes BSW_MAX_LEN is rejected by
+    both; a seed across l_pac of a two-strand text is rejected by both."""
+    ref = bsw.synth_reference(200_000, seed=8)
+    ref[ref == 4] = 1
+    L = 32_700
+    reads = np.concatenate([ref[1000:1000 + L], ref[50_000:50_150]]).astype(np.uint8)
+    off = np.array([0, L], np.int64)
+    lens = np.array([L, 150], np.int32)
+    seeds = np.zeros(2, dtype=bsw.SEED_DTYPE)
+    seeds[0]["rbeg"], seeds[0]["qbeg"], seeds[0]["len"] = 1000 + 16_000, 16_000, 40
+    seeds[1]["rbeg"], seeds[1]["qbeg"], seeds[1]["len"] = 50_020, 20, 30
+    opt = bsw.ext_opt()
+    want = oracle.extend_seeds(oracle.make_params(), opt, ref, reads, off, lens, seeds)
+    eng = bsw.Engine()
+    bsw.set_reference(eng, ref)
+    _same(want, bsw.extend_seeds(eng, ref, reads, off, lens, seeds, opt), "host, long read")
+    _same(want, bsw.extend_seeds_resident(eng, reads, off, lens, seeds, opt), "device, long read")
+    bad = seeds.copy()
+    bad[0]["qbeg"], bad[0]["rbeg"], bad[0]["len"] = L - 20, 1000 + L - 20, 20   # LEFT window > BSW_MAX_LEN
+    for f in (lambda: bsw.extend_seeds(eng, ref, reads, off, lens, bad, opt),
+              lambda: bsw.extend_seeds_resident(eng, reads, off, lens, bad, opt)):
+        with pytest.raises(bsw.BswError):
+            f()
+    T = np.concatenate([ref, np.where(ref < 4, 3 - ref, ref)[::-1]]).astype(np.uint8)
+    opt2 = bsw.ext_opt(l_pac=len(ref))
+    cross = seeds[1:].copy()
+    cross[0]["rbeg"], cross[0]["qbeg"], cross[0]["len"] = len(ref) - 10, 20, 30
+    bsw.set_reference(eng, T)
+    for f in (lambda: bsw.extend_seeds(eng, T, reads, off[1:], lens[1:], cross, opt2),
+              lambda: bsw.extend_seeds_resident(eng, reads, off[1:], lens[1:], cross, opt2)):
+        with pytest.raises(bsw.BswError):
+            f()
     eng.close()
