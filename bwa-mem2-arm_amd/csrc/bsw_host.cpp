@@ -90,6 +90,9 @@ __device__ __forceinline__ int wv_class(const KParams &kp, int32_t w, int qlen, 
 {
     if (kp.maxsc != 1 || qlen > kWvQmax || h0 < 0) return -1;
     if ((int64_t)kp.e_ins * qlen >= 2700) return -1;
+    // E and F live in int16 lanes updated by wrapping v_pk_sub_i16 (bsw_wv.hip): keep the gap
+    // steps far from the int16 range
+    if (128 + kp.o_del + 2 * kp.e_del >= 30000 || 128 + kp.o_ins + 2 * kp.e_ins >= 30000) return -1;
     if ((int64_t)h0 + min(qlen, tlen) + (int64_t)kp.e_ins * (qlen + 1) >= 30000) return -1;
     int wl = w;
     const int ni = qlen * kp.maxsc + kp.end_bonus - kp.o_ins;
@@ -251,6 +254,7 @@ static hipError_t grow(T *&p, size_t &cap, size_t need)   // cap counts elements
 
 struct DeviceCtx {
     int device = 0;
+    std::atomic<int> inflight{0};       // host-buffer calls running on this logical device
     std::mutex mu;
     std::vector<std::unique_ptr<Slot>> free_slots;
     uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
@@ -339,6 +343,8 @@ struct bsw_ctx {
     int64_t ext_chunk = 0;              // BSW_OPT_EXT_CHUNK (0: the int32-offset bound)
     int32_t host_chunk = 262144;        // BSW_OPT_HOST_CHUNK: pairs per host-buffer pipeline chunk
     int host_pack = 2;                  // BSW_OPT_HOST_PACK: 2-bit (2) or nibble (4) staging
+    int64_t split_min = 131072;         // BSW_OPT_SPLIT_MIN: smaller calls go whole to one device
+    std::atomic<unsigned> rr{0};        // tie-break rotation of the one-device pick
     ~bsw_ctx()
     {
         for (auto &b : pin)
@@ -1342,23 +1348,32 @@ static bool params_ok(const bsw_params_t *p)
     return true;
 }
 
-int bsw_create(const bsw_params_t *params, int device0, int n_gpus, bsw_ctx_t **out)
+int bsw_create_on(const bsw_params_t *params, const int *devices, int n_devices, bsw_ctx_t **out)
 {
-    if (!params || !out || n_gpus < 1 || device0 < 0 || !params_ok(params)) return BSW_E_INVAL;
+    if (!params || !out || !devices || n_devices < 1 || !params_ok(params)) return BSW_E_INVAL;
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return BSW_E_NODEV;
-    if (device0 + n_gpus > ndev) return BSW_E_NODEV;
+    for (int d = 0; d < n_devices; ++d)
+        if (devices[d] < 0 || devices[d] >= ndev) return BSW_E_NODEV;
     auto *c = new bsw_ctx();
     c->params = *params;
     bsw::make_kparams(*params, c->kp);
-    for (int d = 0; d < n_gpus; ++d) {
+    for (int d = 0; d < n_devices; ++d) {
         auto dc = std::make_unique<bsw::DeviceCtx>();
-        dc->device = device0 + d;
+        dc->device = devices[d];
         c->devs.push_back(std::move(dc));
     }
     *out = c;
     return BSW_OK;
+}
+
+int bsw_create(const bsw_params_t *params, int device0, int n_gpus, bsw_ctx_t **out)
+{
+    if (!params || !out || n_gpus < 1 || device0 < 0 || n_gpus > 4096) return BSW_E_INVAL;
+    std::vector<int> devs((size_t)n_gpus);
+    for (int d = 0; d < n_gpus; ++d) devs[d] = device0 + d;
+    return bsw_create_on(params, devs.data(), n_gpus, out);
 }
 
 void bsw_destroy(bsw_ctx_t *ctx) { delete ctx; }
@@ -1406,6 +1421,32 @@ static std::vector<int32_t> split_by_cells(const SeqPair *pairs, int32_t n, int3
     return cut;
 }
 
+// Multi-device policy (a context over several logical devices): a call of fewer than
+// split_min items runs whole on ONE device -- the one with the fewest host-buffer calls in
+// flight, ties rotating -- so kt_for-sized calls from concurrent workers spread over the
+// devices instead of each paying every device's launch latency for a sliver of work; larger
+// calls split into contiguous ranges, one per device.  Returns the device, or -1: split.
+struct Inflight {
+    DeviceCtx &dc;
+    explicit Inflight(DeviceCtx &d) : dc(d) { dc.inflight.fetch_add(1); }
+    ~Inflight() { dc.inflight.fetch_sub(1); }
+};
+
+static int one_device(bsw_ctx_t *ctx, int64_t n)
+{
+    const int nd = (int)ctx->devs.size();
+    if (nd == 1) return 0;
+    if (n >= ctx->split_min) return -1;
+    const unsigned r = ctx->rr.fetch_add(1);
+    int best = -1, load = INT32_MAX;
+    for (int k = 0; k < nd; ++k) {
+        const int d = (int)((r + (unsigned)k) % (unsigned)nd);
+        const int l = ctx->devs[d]->inflight.load();
+        if (l < load) { load = l; best = d; }
+    }
+    return best;
+}
+
 int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *seqBufRef,
               const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *out)
 {
@@ -1417,7 +1458,8 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
     if (!seqBufRef || !seqBufQer) return BSW_E_INVAL;
     KParams kp = ctx->kp;
     kp.end_bonus = end_bonus;
-    const int nd = (int)ctx->devs.size();
+    const int one = one_device(ctx, n);
+    const int nd = one >= 0 ? 1 : (int)ctx->devs.size();
     // one device: host_shard's parallel pre-pass validates; several: validate the whole batch
     // before any device starts
     if (nd > 1)
@@ -1428,7 +1470,8 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
     std::vector<int> rcs(nd, BSW_OK);
     std::vector<bsw_stats_t> st(nd);
     if (nd == 1) {
-        rcs[0] = host_shard(kp, *ctx->devs[0], pairs, seqBufRef, seqBufQer, n, w, cell_bits, ctx->host_chunk,
+        Inflight g(*ctx->devs[one]);
+        rcs[0] = host_shard(kp, *ctx->devs[one], pairs, seqBufRef, seqBufQer, n, w, cell_bits, ctx->host_chunk,
                             ctx->host_pack == 2, &st[0]);
     } else {
         // contiguous pair ranges of equal estimated work (static band cells)
@@ -1437,6 +1480,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
         for (int d = 0; d < nd; ++d) {
             const int32_t a = cut[d], b = cut[d + 1];
             th.emplace_back([&, d, a, b] {
+                Inflight g(*ctx->devs[d]);
                 rcs[d] = host_shard(kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a, w,
                                     cell_bits, ctx->host_chunk, ctx->host_pack == 2, &st[d]);
             });
@@ -1453,6 +1497,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
         agg.stage_ms = std::max(agg.stage_ms, st[d].stage_ms);
         agg.host_ms = std::max(agg.host_ms, st[d].host_ms);
     }
+    agg.n_devices = nd;
     *out = agg;
     return BSW_OK;
 }
@@ -1627,16 +1672,24 @@ static int mate_host_shard(const MateParams &mp, DeviceCtx &dc, const SeqPair *p
 
 // Run shard(d, a, b) for contiguous job ranges [a, b) on every device of the context (one host
 // thread per device; jobs are independent), first non-zero status wins.
+// Small calls run whole on one device (one_device's policy).
 template <class F>
 static int shard_devices(bsw_ctx_t *ctx, int32_t n, F shard)
 {
+    const int one = one_device(ctx, n);
+    if (one >= 0) {
+        Inflight g(*ctx->devs[one]);
+        return shard(one, 0, n);
+    }
     const int nd = (int)ctx->devs.size();
-    if (nd == 1) return shard(0, 0, n);
     std::vector<int> rcs(nd, BSW_OK);
     std::vector<std::thread> th;
     for (int d = 0; d < nd; ++d) {
         const int32_t a = (int32_t)((int64_t)n * d / nd), b = (int32_t)((int64_t)n * (d + 1) / nd);
-        th.emplace_back([&, d, a, b] { rcs[d] = shard(d, a, b); });
+        th.emplace_back([&, d, a, b] {
+            Inflight g(*ctx->devs[d]);
+            rcs[d] = shard(d, a, b);
+        });
     }
     for (auto &t : th) t.join();
     for (int r : rcs)
@@ -1925,6 +1978,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     case BSW_OPT_HOST_CHUNK: if (value < 1 || value > INT32_MAX) return BSW_E_INVAL; ctx->host_chunk = (int32_t)value; return BSW_OK;
     case BSW_OPT_HOST_PACK: if (value != 2 && value != 4) return BSW_E_INVAL; ctx->host_pack = (int)value; return BSW_OK;
     case BSW_OPT_SMALL_BATCH: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.small_batch = (int32_t)value; return BSW_OK;
+    case BSW_OPT_SPLIT_MIN: if (value < 0) return BSW_E_INVAL; ctx->split_min = value; return BSW_OK;
     case BSW_OPT_TEST_MISROUTE: if (!b01) return BSW_E_INVAL; ctx->kp.misroute = (int8_t)value; return BSW_OK;
     default: return BSW_E_INVAL;
     }

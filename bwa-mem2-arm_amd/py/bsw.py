@@ -26,7 +26,7 @@ OUT_FIELDS = ("score", "tle", "gtle", "qle", "gscore", "max_off")
 assert SEQPAIR_DTYPE.itemsize == 56
 
 # Every symbol include/bsw.h declares (tests check the library exports all of them).
-ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_scores",
+ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_create_on", "bsw_destroy", "bsw_get_scores",
                "bsw_get_scores_device", "bsw_last_stats", "bsw_strerror", "bsw_abi_version",
                "bsw_ext_opt_default", "bsw_extend_seeds", "bsw_ext_last_stats",
                "bswb_write", "bswb_read_header", "bswb_read",
@@ -41,6 +41,7 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_destroy", "bsw_get_score
 # include/bsw.h engine options (bsw_set_option)
 OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK, OPT_LONG, OPT_HOST_PACK = 1, 2, 3, 4, 5, 6, 7, 8
 OPT_SMALL_BATCH = 9
+OPT_SPLIT_MIN = 10
 OPT_TEST_MISROUTE = 100
 
 # include/bsw_ext.h structs
@@ -69,7 +70,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_float), ("n_i16", ctypes.c_int32),
                 ("n_u8", ctypes.c_int32), ("n_wide", ctypes.c_int32),
                 ("n_launches", ctypes.c_int32), ("n_packed", ctypes.c_int32),
-                ("stage_ms", ctypes.c_float), ("host_ms", ctypes.c_float), ("n_wave", ctypes.c_int32)]
+                ("stage_ms", ctypes.c_float), ("host_ms", ctypes.c_float), ("n_wave", ctypes.c_int32),
+                ("n_devices", ctypes.c_int32)]
 
 
 def default_params(a=1, b=4, o_del=6, e_del=1, o_ins=6, e_ins=1, zdrop=100, end_bonus=5,
@@ -103,6 +105,7 @@ def hip_lib():
         P = ctypes.c_void_p
         L.bsw_params_default.argtypes = [P]
         L.bsw_create.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
+        L.bsw_create_on.argtypes = [P, P, ctypes.c_int, ctypes.POINTER(P)]
         L.bsw_destroy.argtypes = [P]
         L.bsw_get_scores.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
         L.bsw_get_scores_device.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32,
@@ -143,7 +146,7 @@ def hip_lib():
                                                   P, P]
         L.bsw_fmi_sa_device.argtypes = [P, P, ctypes.c_int64, P, P]
         L.bsw_fmi_last_kernel_ms.argtypes = [P, P]
-        for f in ("bsw_create", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
+        for f in ("bsw_create", "bsw_create_on", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
                   "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
@@ -168,17 +171,23 @@ def _ptr(a: np.ndarray):
 class Engine:
     """Python mirror of the C++ shim: one engine = one bsw_ctx_t."""
 
-    def __init__(self, params: Params | None = None, device: int = 0, n_gpus: int = 1, **options):
+    def __init__(self, params: Params | None = None, device: int = 0, n_gpus: int = 1,
+                 devices: list[int] | None = None, **options):
+        """devices: explicit logical-device -> HIP-device map (bsw_create_on; repeats allowed,
+        the rehearsal of an n-GPU context on a smaller box); else devices [device, device + n_gpus)."""
         self.params = params if params is not None else default_params()
         self._ctx = ctypes.c_void_p()
-        _check(hip_lib().bsw_create(ctypes.byref(self.params), device, n_gpus,
-                                    ctypes.byref(self._ctx)))
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            _check(hip_lib().bsw_create_on(ctypes.byref(self.params), arr, len(devices), ctypes.byref(self._ctx)))
+        else:
+            _check(hip_lib().bsw_create(ctypes.byref(self.params), device, n_gpus, ctypes.byref(self._ctx)))
         for k, v in options.items():
             self.set_option(k, v)
 
     _OPTS = {"kernel8": OPT_KERNEL8, "fork": OPT_FORK, "sortkey": OPT_SORTKEY, "glob_band": OPT_GLOB_BAND,
              "ext_chunk": OPT_EXT_CHUNK, "host_chunk": OPT_HOST_CHUNK, "long": OPT_LONG, "host_pack": OPT_HOST_PACK,
-             "small_batch": OPT_SMALL_BATCH, "test_misroute": OPT_TEST_MISROUTE}
+             "small_batch": OPT_SMALL_BATCH, "split_min": OPT_SPLIT_MIN, "test_misroute": OPT_TEST_MISROUTE}
 
     def set_option(self, name, value: int):
         """bsw_set_option by name (kernel8, fork, sortkey, glob_band, ext_chunk, host_chunk, test_misroute)

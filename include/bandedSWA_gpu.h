@@ -13,8 +13,12 @@
 // convention is kept: void members, and on any engine error a message on stderr followed
 // by exit(EXIT_FAILURE) (style of docs-archive/ARM-BATCHED-SAM-PLAN.md:93-110).
 // numThreads is accepted for signature compatibility; concurrency comes from the device.
-// Environment: BSW_GPUS = number of GPUs to shard each batch over (default 1),
-//              BSW_DEVICE0 = first HIP device index (default 0).
+// Environment: BSW_GPUS = number of GPUs (default 1), BSW_DEVICE0 = first HIP device index
+//              (default 0): devices [BSW_DEVICE0, BSW_DEVICE0 + BSW_GPUS); or BSW_GPU_MAP =
+//              "d0,d1,..." = the HIP device of each logical device (repeats allowed: the
+//              rehearsal of an n-GPU node on a smaller box).  With several devices a
+//              getScores* call of fewer than 131072 pairs runs whole on the least-busy device
+//              and larger ones are split by band cells (bsw.h, BSW_OPT_SPLIT_MIN).
 #ifndef BANDEDSWA_GPU_H
 #define BANDEDSWA_GPU_H
 
@@ -45,9 +49,19 @@ public:
         p.zdrop = zdrop; p.end_bonus = end_bonus;
         if (mat_) memcpy(p.mat, mat_, 25);
         p.w_match = w_match; p.w_mismatch = w_mismatch; p.w_ambig = -1;
-        const char *g = getenv("BSW_GPUS"), *d0 = getenv("BSW_DEVICE0");
+        const char *g = getenv("BSW_GPUS"), *d0 = getenv("BSW_DEVICE0"), *map = getenv("BSW_GPU_MAP");
         const int ngpu = g ? atoi(g) : 1, dev0 = d0 ? atoi(d0) : 0;
-        check(bsw_create(&p, dev0, ngpu > 0 ? ngpu : 1, &ctx_), "bsw_create");
+        if (map && *map) {
+            int devs[256], nd = 0;
+            for (const char *c = map; *c && nd < 256;) {
+                devs[nd++] = atoi(c);
+                while (*c && *c != ',') ++c;
+                if (*c == ',') ++c;
+            }
+            check(bsw_create_on(&p, devs, nd, &ctx_), "bsw_create_on (BSW_GPU_MAP)");
+        } else {
+            check(bsw_create(&p, dev0, ngpu > 0 ? ngpu : 1, &ctx_), "bsw_create");
+        }
         params_ = p;
         record_ = getenv("BSW_RECORD");   // capture every batch as <prefix>.<n>.bswb (bsw_batch.h)
     }

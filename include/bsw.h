@@ -69,8 +69,15 @@ typedef struct bsw_ctx bsw_ctx_t;
 void bsw_params_default(bsw_params_t *p);
 
 /* Create an engine on HIP devices [device0, device0 + n_gpus).  n_gpus >= 1.
- * Host-buffer calls shard each batch across those devices by contiguous pair range. */
+ * Multi-device policy of host-buffer calls: a call of fewer than BSW_OPT_SPLIT_MIN pairs
+ * (default 131072) runs whole on one device -- the one with the fewest calls in flight, ties
+ * rotating -- so concurrent kt_for-sized calls spread over the devices; larger calls are
+ * split into contiguous pair ranges of equal static band cells, one per device. */
 int  bsw_create(const bsw_params_t *params, int device0, int n_gpus, bsw_ctx_t **out);
+/* The same over an explicit list: logical device k runs on HIP device devices[k].  Entries may
+ * repeat (several logical devices with their own streams and buffers on one GPU): the
+ * rehearsal form of an n-GPU context on a smaller box (ABI version 5). */
+int  bsw_create_on(const bsw_params_t *params, const int *devices, int n_devices, bsw_ctx_t **out);
 void bsw_destroy(bsw_ctx_t *ctx);
 
 /* Blocking host-buffer call (drop-in for getScores16 / getScores8).
@@ -101,6 +108,8 @@ typedef struct bsw_stats_t {
                                    host thread (staging + H2D + kernels + D2H)           */
     int32_t n_wave;             /* of n_i16: pairs run on the wave-per-alignment kernel
                                    (queries past 160 columns; ABI version 4)             */
+    int32_t n_devices;          /* host-buffer calls: logical devices the call ran on
+                                   (1, or all of them when split; ABI version 5)         */
 } bsw_stats_t;
 int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
 
@@ -137,6 +146,9 @@ enum {
                                  lives ~1.2 ms at any batch size, a wave per alignment spreads
                                  the pair over 64 lanes -- kt_for-sized calls are latency-bound.
                                  Outputs are identical either way                              */
+    BSW_OPT_SPLIT_MIN = 10,   /* contexts over several devices: host-buffer calls of fewer pairs
+                                 (mate / global calls: jobs) run whole on one device (default
+                                 131072; 0 = always split)                                    */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };

@@ -26,13 +26,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, q):
+def _worker(rank, world, port, n, q, engine):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
     pairs, ref, qer = bsw.synth_batch(n, pair_base=rank * n)
-    oracle.sse41_get_scores16(oracle.make_params(), pairs, ref, qer, 100, 1)
+    if engine == "hip":            # the product engine (every rank on the box's GPU)
+        e = bsw.Engine()
+        e.get_scores(pairs, ref, qer, 100)
+        e.close()
+    else:                          # CPU container: the SSE4.1 restatement stands in per rank
+        oracle.sse41_get_scores16(oracle.make_params(), pairs, ref, qer, 100, 1)
     out = torch.from_numpy(pairs.view(np.int32).reshape(n, 14).copy())
     gathered = [torch.zeros_like(out) for _ in range(world)]
     dist.all_gather(gathered, out)
@@ -45,12 +50,13 @@ def _worker(rank, world, port, n, q):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_shards_equal_single_process():
+@pytest.mark.parametrize("engine", ["sse41", pytest.param("hip", marks=pytest.mark.gpu)])
+def test_two_rank_shards_equal_single_process(engine):
     n, world = 600, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q, engine)) for r in range(world)]
     for p in procs:
         p.start()
     got, tmax = q.get(timeout=240)

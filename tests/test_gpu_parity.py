@@ -359,6 +359,58 @@ def test_multi_gpu_context_shards(c2_full):
     _assert_same(want[:100_000], got, f"n_gpus={n}")
 
 
+@pytest.mark.parametrize("nlog", [2, 4])
+def test_multi_device_policy_rehearsal(c2_full, nlog):
+    """A context of nlog logical devices on the box's one GPU (bsw_create_on with a repeated
+    device, the rehearsal of an nlog-GPU node): calls below BSW_OPT_SPLIT_MIN run whole on one
+    device (n_devices == 1), larger calls split over all of them, split_min = 0 splits every
+    call; 8 concurrent callers of 1K / 10K pairs; mate-rescue and global calls through the same
+    policy -- all equal the oracle."""
+    pairs, ref, qer, want = c2_full
+    e = bsw.Engine(devices=[0] * nlog)
+    for m, nd in ((1000, 1), (10_000, 1), (200_000, nlog)):
+        got = pairs[:m].copy()
+        e.get_scores(got, ref, qer, 100)
+        _assert_same(want[:m], got, f"{nlog} logical devices, {m} pairs")
+        assert e.last_stats().n_devices == nd
+    e.set_option("split_min", 0)
+    got = pairs[:3000].copy()
+    e.get_scores(got, ref, qer, 100)
+    _assert_same(want[:3000], got, f"{nlog} logical devices, forced split")
+    assert e.last_stats().n_devices == nlog
+    e.set_option("split_min", 131072)
+    errs = []
+
+    def caller(k, m):
+        try:
+            for r in range(4):
+                a = ((k * 4 + r) * m) % (len(pairs) - m)
+                got = pairs[a:a + m].copy()
+                e.get_scores(got, ref, qer, 100, 8 if r & 1 else 16)
+                _assert_same(want[a:a + m], got, f"caller {k} round {r}")
+        except Exception as x:  # noqa: BLE001
+            errs.append(x)
+    for m in (1000, 10_000):
+        th = [threading.Thread(target=caller, args=(k, m)) for k in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    assert not errs, errs[0]
+    mref = bsw.synth_reference(400_000, seed=9)
+    mp, mq = bsw.synth_mates(mref, 3000)
+    mwant = oracle.ksw_align2_batch(mp, mref, mq, bwa_fill_scmat(), nthreads=8)
+    ref_one = bsw.Engine()
+    for w_split in (131072, 0):
+        e.set_option("split_min", w_split)
+        got = bsw.ksw_align2(e, mp, mref, mq)
+        assert np.array_equal(got, bsw.ksw_align2(ref_one, mp, mref, mq))
+        for f in ("score", "te", "qe"):
+            assert np.array_equal(got[f], mwant[f]), f
+    e.close()
+    ref_one.close()
+
+
 @pytest.fixture(scope="module")
 def eng_lane():
     """Engine with the packed-column kernel disabled (BSW_OPT_KERNEL8 = 0): every pair runs on
@@ -496,3 +548,55 @@ def test_options_api(eng):
     assert lib.bsw_set_option(eng._ctx, bsw.OPT_EXT_CHUNK, -1) == -22
     assert lib.bsw_set_option(None, bsw.OPT_FORK, 1) == -22
     assert lib.bsw_set_option(eng._ctx, bsw.OPT_SORTKEY, 1) == 0
+
+
+@pytest.mark.parametrize("gaps", [(100, 16400, 6, 1), (6, 1, 30000, 2700), (16000, 16000, 16000, 16000)])
+def test_extreme_gap_penalties(gaps):
+    """Legal but extreme gap penalties (o + e up to 32767) on the default (small-batch) routing
+    and with every eligible pair forced to the wave kernel: the wave kernel's int16 E/F lanes
+    must not see them (wv_class bound), results equal the oracle."""
+    o_del, e_del, o_ins, e_ins = gaps
+    sc = dict(a=1, b=4, o_del=o_del, e_del=e_del, o_ins=o_ins, e_ins=e_ins, zdrop=100, end_bonus=5)
+    pairs, ref, qer = bswgen.random_pairs(1500, seed=sum(gaps), tlen=(0, 320), qlen=(0, 200))
+    want = pairs.copy()
+    oracle.get_scores(_oparams(sc), want, ref, qer, 100, nthreads=8)
+    for opts in ({}, {"long": 2}):
+        e = bsw.Engine(_gparams(sc), **opts)
+        got = pairs.copy()
+        e.get_scores(got, ref, qer, 100)
+        _assert_same(want, got, f"gaps {gaps} {opts}")
+        assert e.last_stats().n_wave == 0
+        e.close()
+
+
+def test_host_pipeline_2bit_pieces_over_8mb():
+    """One staged chunk spanning ~19 MB of reference and ~11 MB of query bytes, so stage_2bit
+    splits both buffers into several parallel pieces (cuts at multiples of 64 codes, 4 MB
+    apart): N bases sit on both sides of every 64-code boundary (positions 0 and 63 mod 64 of
+    the 64-aligned sequences), so each piece's AVX2/SSE tail and its exception words' offsets
+    (pos0) are exercised.  2-bit staging and nibble staging both equal the oracle."""
+    rng = np.random.default_rng(64)
+    n, TS, QS = 60_000, 320, 192
+    ref = rng.integers(0, 4, n * TS, dtype=np.uint8)
+    qer = np.zeros(n * QS, dtype=np.uint8)
+    pairs = np.zeros(n, dtype=oracle.SEQPAIR_DTYPE)
+    idx = np.arange(n)
+    pairs["idr"], pairs["idq"] = idx * TS, idx * QS
+    pairs["len1"], pairs["len2"], pairs["id"] = 300, 150, idx
+    pairs["h0"] = rng.integers(19, 100, n)
+    q = ref.reshape(n, TS)[:, :150].copy()
+    mut = rng.random(q.shape) < 0.02
+    q[mut] = (q[mut] + rng.integers(1, 4, int(mut.sum()))) % 4
+    qer.reshape(n, QS)[:, :150] = q
+    pos = np.arange(len(ref))
+    ref[(pos % 64 == 0) | (pos % 64 == 63)] = 4
+    qpos = np.arange(len(qer))
+    qer[(qpos % 128 == 0) | (qpos % 128 == 127)] = 4
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    for pack in (2, 4):
+        e = bsw.Engine(host_chunk=1 << 17, host_pack=pack, small_batch=0)
+        got = pairs.copy()
+        e.get_scores(got, ref, qer, 100)
+        _assert_same(want, got, f"pieces > 8 MB, host_pack {pack}")
+        e.close()
