@@ -32,6 +32,7 @@
 #include <thread>
 #include <vector>
 #include "../../include/bsw_fmi.h"
+#include "bsw_fmi_internal.h"
 
 namespace {
 
@@ -439,6 +440,14 @@ struct bsw_fmi {
     void *h_stage = nullptr;                  // host-buffer calls: device copies
     std::mutex mu;                            // one seeding call at a time per index
 };
+
+int bsw::fmi_view(bsw_fmi_t *f, FmiView *out)
+{
+    if (!f) return BSW_E_INVAL;
+    if (f->device < 0) return BSW_E_NODEV;
+    *out = FmiView{f->device, f->d_sa, (int64_t)f->n, (int64_t)f->n / 2, f->stream, &f->mu};
+    return BSW_OK;
+}
 
 namespace {
 

@@ -36,7 +36,7 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_create_on", "bsw_destroy
                "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats",
                "bsw_chain2aln_resident", "bsw_mem_opt_default", "bsw_fmi_build", "bsw_fmi_destroy", "bsw_fmi_get_info", "bsw_fmi_copy_sa",
                "bsw_fmi_copy_bwt", "bsw_mem_collect_intv", "bsw_mem_collect_intv_device", "bsw_fmi_sa_device",
-               "bsw_fmi_last_kernel_ms")
+               "bsw_fmi_last_kernel_ms", "bsw_chain_opt_default", "bsw_mem_chain_device")
 
 # include/bsw.h engine options (bsw_set_option)
 OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK, OPT_LONG, OPT_HOST_PACK = 1, 2, 3, 4, 5, 6, 7, 8
@@ -146,6 +146,10 @@ def hip_lib():
                                                   P, P]
         L.bsw_fmi_sa_device.argtypes = [P, P, ctypes.c_int64, P, P]
         L.bsw_fmi_last_kernel_ms.argtypes = [P, P]
+        L.bsw_chain_opt_default.argtypes = [P]
+        L.bsw_mem_chain_device.argtypes = [P, P, P, ctypes.c_int32, P, ctypes.c_int32, P, P, P, P, ctypes.c_int64,
+                                           P, P]
+        L.bsw_mem_chain_device.restype = ctypes.c_int
         for f in ("bsw_create", "bsw_create_on", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
@@ -717,3 +721,57 @@ class Fmi:
         v = ctypes.c_float()
         _check(hip_lib().bsw_fmi_last_kernel_ms(self._f, ctypes.byref(v)))
         return v.value
+
+    def mem_chain_device(self, d_len: int, n: int, d_mems: int, cap: int, d_cnt: int, d_seeds: int, d_sr: int,
+                         d_sc: int, seed_cap: int, opt: "ChainOpt | None" = None, stream: int = 0):
+        """bsw_mem_chain_device -> (status, seeds needed / written)"""
+        o = opt if opt is not None else chain_opt()
+        ns = ctypes.c_int64(0)
+        rc = hip_lib().bsw_mem_chain_device(self._f, ctypes.byref(o), ctypes.c_void_p(d_len), n,
+                                            ctypes.c_void_p(d_mems), cap, ctypes.c_void_p(d_cnt),
+                                            ctypes.c_void_p(d_seeds or None), ctypes.c_void_p(d_sr or None),
+                                            ctypes.c_void_p(d_sc or None), seed_cap, ctypes.byref(ns),
+                                            ctypes.c_void_p(stream or None))
+        return rc, ns.value
+
+
+class ChainOpt(ctypes.Structure):
+    """Mirror of bsw_chain_opt_t (include/bsw_fmi.h)."""
+    _fields_ = [("max_occ", ctypes.c_int32), ("w", ctypes.c_int32), ("max_chain_gap", ctypes.c_int32),
+                ("min_chain_weight", ctypes.c_int32), ("min_seed_len", ctypes.c_int32),
+                ("max_chain_extend", ctypes.c_int32), ("drop_ratio", ctypes.c_float), ("mask_level", ctypes.c_float)]
+
+
+def chain_opt(**kw) -> ChainOpt:
+    o = ChainOpt()
+    hip_lib().bsw_chain_opt_default(ctypes.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def seed_and_chain(fmi: Fmi, d_reads, read_off, read_len, cap: int = 256, mopt=None, copt=None):
+    """The GPU seeding front end of mem_align1_core over resident reads: bsw_mem_collect_intv_device
+    -> bsw_mem_chain_device.  d_reads: a hiprt.DeviceBuffer of the reads.  Returns host copies
+    (seeds, seed_read, seed_chain) and the device buffers holding them (d_seeds, d_sr, d_sc)."""
+    import hiprt
+    read_off = np.ascontiguousarray(read_off, dtype=np.int64)
+    read_len = np.ascontiguousarray(read_len, dtype=np.int32)
+    n = len(read_len)
+    d_off, d_len = hiprt.DeviceBuffer.from_array(read_off), hiprt.DeviceBuffer.from_array(read_len)
+    d_mems = hiprt.DeviceBuffer(max(1, n * cap) * BWTINTV_DTYPE.itemsize)
+    d_cnt = hiprt.DeviceBuffer(max(1, n) * 4)
+    _check(fmi.collect_intv_device(d_reads.ptr, d_off.ptr, d_len.ptr, n, int(read_len.max(initial=0)), d_mems.ptr, cap,
+                                   d_cnt.ptr, mopt))
+    rc, need = fmi.mem_chain_device(d_len.ptr, n, d_mems.ptr, cap, d_cnt.ptr, 0, 0, 0, 0, copt)
+    if rc not in (0, -34):
+        _check(rc)
+    d_seeds = hiprt.DeviceBuffer(max(1, need) * SEED_DTYPE.itemsize)
+    d_sr, d_sc = hiprt.DeviceBuffer(max(1, need) * 4), hiprt.DeviceBuffer(max(1, need) * 4)
+    rc, got = fmi.mem_chain_device(d_len.ptr, n, d_mems.ptr, cap, d_cnt.ptr, d_seeds.ptr, d_sr.ptr, d_sc.ptr, need, copt)
+    _check(rc)
+    assert got == need
+    seeds = d_seeds.download(np.zeros(need, dtype=SEED_DTYPE)) if need else np.zeros(0, SEED_DTYPE)
+    sr = d_sr.download(np.zeros(need, dtype=np.int32)) if need else np.zeros(0, np.int32)
+    sc = d_sc.download(np.zeros(need, dtype=np.int32)) if need else np.zeros(0, np.int32)
+    return (seeds, sr, sc), (d_seeds, d_sr, d_sc), (d_off, d_len)

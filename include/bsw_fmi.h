@@ -30,6 +30,7 @@
 
 #include <stdint.h>
 #include "bsw.h"
+#include "bsw_ext.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -94,6 +95,49 @@ int  bsw_fmi_sa_device(bsw_fmi_t *fmi, const uint64_t *d_k, int64_t n, int64_t *
 
 /* The last seeding call's SMEM kernel time (HIP events). */
 int  bsw_fmi_last_kernel_ms(const bsw_fmi_t *fmi, float *ms);
+
+/* ---------------------------------------------------------------- seeds -> chains
+ * mem_chain + mem_chain_flt (bwa src/bwamem.c, kept by bwa-mem2's src/bwamem.cpp;
+ * [UPSTREAM-RECALL]: the reference holds no source of them), per read over its
+ * mem_collect_intv intervals, on the GPU (csrc/bsw_memchain.hip):
+ *   for each interval (in info order), step = s > max_occ ? s / max_occ : 1, and for
+ *   k = 0, 1 step, ... while k < s and fewer than max_occ taken: seed = (rbeg = SA[k0 + k],
+ *   qbeg, len = score = qend - qbeg); a seed across the forward / reverse boundary l_pac is
+ *   dropped (bns_intv2rid < 0); otherwise the chain with the largest start <= rbeg (kbtree
+ *   kb_intervalp) absorbs it when test_and_merge says so (contained seed, or same strand and
+ *   |diagonal drift| <= w with gaps < max_chain_gap from the chain's last seed), else it
+ *   starts a new chain.  Chains in start order, then mem_chain_flt: weight = min(query, ref)
+ *   coverage of the chain's seeds; chains below min_chain_weight dropped; sorted by weight
+ *   descending (klib ks_introsort, as upstream -- ties in its order); a chain significantly
+ *   overlapping (>= mask_level of the shorter, shorter < max_chain_gap) a kept heavier one is
+ *   dropped when lighter than drop_ratio of it by >= 2 * min_seed_len, else kept as
+ *   secondary; max_chain_extend bounds the secondaries.
+ * Output = the input bsw_chain2aln_resident takes: seeds grouped by read (seed_read
+ * ascending), each read's chains as runs of seed_chain (0, 1, ... in processing order), each
+ * chain's seeds in chain order.  Duplicate chain starts follow a single-leaf kbtree (a new
+ * chain goes right after the first chain of equal start). */
+typedef struct bsw_chain_opt_t {
+    int32_t max_occ;                 /* bwa -c: occurrences sampled per interval (500)            */
+    int32_t w;                       /* bwa -w: band of test_and_merge (100)                      */
+    int32_t max_chain_gap;           /* 10000                                                     */
+    int32_t min_chain_weight;        /* bwa -W (0)                                                */
+    int32_t min_seed_len;            /* bwa -k (19): mem_chain_flt's "much lighter" margin / 2    */
+    int32_t max_chain_extend;        /* secondaries extended at most (1 << 30)                    */
+    float   drop_ratio;              /* bwa -D (0.5)                                              */
+    float   mask_level;              /* 0.5                                                       */
+} bsw_chain_opt_t;
+
+void bsw_chain_opt_default(bsw_chain_opt_t *opt);
+
+/* Seeds and chains of n_reads reads from their intervals (d_mems[i * cap + t], t < d_n_mems[i],
+ * as bsw_mem_collect_intv_device leaves them) against the index's suffix array, all device
+ * arrays on the index's device.  Writes at most seed_cap seeds (d_seeds, d_seed_read,
+ * d_seed_chain) and their number to *n_seeds; BSW_E_RANGE (with *n_seeds = the number needed)
+ * when seed_cap is too small.  Blocking. */
+int  bsw_mem_chain_device(bsw_fmi_t *fmi, const bsw_chain_opt_t *opt, const int32_t *d_read_len, int32_t n_reads,
+                          const bsw_bwtintv_t *d_mems, int32_t cap, const int32_t *d_n_mems, bsw_seed_t *d_seeds,
+                          int32_t *d_seed_read, int32_t *d_seed_chain, int64_t seed_cap, int64_t *n_seeds,
+                          void *stream);
 
 #ifdef __cplusplus
 }

@@ -298,3 +298,48 @@ class FmiRef:
             lib().oracle_fmi_free(self._buf)
         except Exception:
             pass
+
+
+# ---- seeds -> chains (oracle/chain_ref.c: mem_chain + mem_chain_flt)
+
+class ChainOpt(ctypes.Structure):
+    """bsw_chain_opt_t (include/bsw_fmi.h)"""
+    _fields_ = [("max_occ", ctypes.c_int32), ("w", ctypes.c_int32), ("max_chain_gap", ctypes.c_int32),
+                ("min_chain_weight", ctypes.c_int32), ("min_seed_len", ctypes.c_int32),
+                ("max_chain_extend", ctypes.c_int32), ("drop_ratio", ctypes.c_float), ("mask_level", ctypes.c_float)]
+
+
+def chain_opt(**kw):
+    """bwa mem defaults: -c 500 -w 100, max_chain_gap 10000, -W 0, -k 19, max_chain_extend 1 << 30,
+    -D 0.5, mask_level 0.5"""
+    o = ChainOpt(500, 100, 10000, 0, 19, 1 << 30, 0.5, 0.5)
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def mem_chain(sa, l_pac, read_len, mems, n_mems, opt=None):
+    """oracle_mem_chain over every read: (seeds SEED layout, seed_read, seed_chain) as bsw_fmi.h"""
+    import bsw as _bsw
+    L = lib()
+    P = ctypes.c_void_p
+    L.oracle_mem_chain.restype = ctypes.c_int64
+    L.oracle_mem_chain.argtypes = [P, P, ctypes.c_int64, P, ctypes.c_int32, P, ctypes.c_int32, P, P, P, P,
+                                   ctypes.c_int64]
+    o = opt if opt is not None else chain_opt()
+    sa = np.ascontiguousarray(sa, dtype=np.int64)
+    read_len = np.ascontiguousarray(read_len, dtype=np.int32)
+    mems = np.ascontiguousarray(mems)
+    n_mems = np.ascontiguousarray(n_mems, dtype=np.int32)
+    n, cap = mems.shape
+    cnt = 0
+    for _ in range(2):
+        seeds = np.zeros(max(cnt, 1), dtype=_bsw.SEED_DTYPE)
+        sr = np.zeros(max(cnt, 1), dtype=np.int32)
+        sc = np.zeros(max(cnt, 1), dtype=np.int32)
+        need = L.oracle_mem_chain(ctypes.byref(o), _ptr(sa), l_pac, _ptr(read_len), n, _ptr(mems), cap, _ptr(n_mems),
+                                  _ptr(seeds), _ptr(sr), _ptr(sc), cnt)
+        if need <= cnt:
+            return seeds[:need], sr[:need], sc[:need]
+        cnt = need
+    raise RuntimeError("oracle_mem_chain: seed count changed between passes")
