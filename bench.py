@@ -276,8 +276,10 @@ def main():
     ap.add_argument("--tlen", type=int, default=300, help="target window length (C2: 300)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (drop-in ABI) rates")
-    ap.add_argument("--workload", default="c2", choices=("c2", "c1", "c4", "c4seed", "mate", "global", "smem"),
-                    help="c2 (default): resident SeqPair batch; c1: 10K exact SE reads vs 1 Mb (plumbing); "
+    ap.add_argument("--workload", default="c2", choices=("c2", "c1", "c4mem", "c4", "c4seed", "mate", "global", "smem"),
+                    help="c2 (default): resident SeqPair batch; c1: the reference's own 10K exact SE reads vs "
+                         "its 1 Mb reference through GPU seeding -> chaining -> mem_chain2aln; c4mem: the same "
+                         "front end on --reads PE reads vs a --ref-mb reference; "
                          "c4: paired-end reads with several seeds / chains each through mem_chain2aln "
                          "(bsw_chain2aln_device); c4seed: one seed per read through the extension pipeline; "
                          "mate: resident mate-rescue batch (ksw_align2 jobs, SURVEY.md §8(f) row 2); "
@@ -312,8 +314,9 @@ def main():
     if args.scaling == "strong":
         return main_strong(args, rank, local, world)
     if args.workload == "c1":          # BASELINE configs[0]: 10K exact 150 bp SE reads vs 1 Mb
-        args.reads, args.ref_mb, args.exact = 10_000, 1, True
-        return main_c4(args, rank, local, world)
+        return main_mem(args, rank, local, world, c1=True)
+    if args.workload == "c4mem":
+        return main_mem(args, rank, local, world, c1=False)
     if args.workload == "c4":
         return main_c4pe(args, rank, local, world)
     if args.workload == "c4seed":
@@ -713,6 +716,165 @@ def main_c4pe(args, rank, local, world):
                                              all(np.array_equal(want[f], out[:S][f]) for f in bsw.ALNREG_DTYPE.names)),
         }
     out_j["synth_gen_s"] = round(gen_s, 2)
+    print(json.dumps(out_j), flush=True)
+
+
+def pe_reads(ref, npairs: int, L: int = 150, seed: int = 42, ins=(400, 600), p_sub=0.01, p_n=0.001):
+    """npairs fragments (insert uniform in `ins`) from either strand of ref: read 2k from the
+    fragment's start, read 2k+1 the reverse complement of its end; 1% substitutions, 0.1% N."""
+    rng = np.random.default_rng(seed)
+    ln = rng.integers(ins[0], ins[1] + 1, npairs)
+    st = rng.integers(0, len(ref) - ins[1] - 1, npairs)
+    a = ref[st[:, None] + np.arange(L)[None, :]]
+    b = ref[(st + ln - L)[:, None] + np.arange(L)[None, :]]
+    b = (3 - b[:, ::-1]).astype(np.uint8)
+    flip = rng.random(npairs) < 0.5                     # fragment from the reverse strand
+    a[flip], b[flip] = b[flip].copy(), a[flip].copy()
+    reads = np.stack([a, b], axis=1).reshape(2 * npairs, L)
+    sub = rng.random(reads.shape) < p_sub
+    reads[sub] = ((reads[sub] + rng.integers(1, 4, int(sub.sum()))) % 4).astype(np.uint8)
+    reads[rng.random(reads.shape) < p_n] = 4
+    n = 2 * npairs
+    return np.ascontiguousarray(reads).reshape(-1), np.arange(n, dtype=np.int64) * L, np.full(n, L, np.int32)
+
+
+def main_mem(args, rank, local, world, c1: bool):
+    """The GPU front end of mem_align1_core over resident reads: FM-index SMEM seeding
+    (bsw_mem_collect_intv_device) -> SA lookups + chaining + chain filtering
+    (bsw_mem_chain_device) -> mem_chain2aln with contained-seed skipping
+    (bsw_chain2aln_resident) against the resident two-strand text (l_pac clamp).  c1: BASELINE
+    configs[0] -- the reference's own 10K exact 150 bp SE reads vs its 1 Mb reference
+    (bwa-mem2-arm_amd/py/c1data.py, regenerated bit-exactly); else C4: --reads PE reads vs a
+    --ref-mb random reference.  The index is built on the host before timing (build time
+    reported); a step = the three stages over every read, seeding time included."""
+    import c1data
+    t0 = time.perf_counter()
+    if c1:
+        ref, reads, off, lens, _ = c1data.workload()
+    else:
+        ref = bsw.synth_reference(args.ref_mb * 1_000_000, seed=7)
+        nb = ref > 3                                     # bwa's .pac: N -> a random base
+        ref[nb] = np.random.default_rng(1).integers(0, 4, int(nb.sum()), dtype=np.uint8)
+        reads, off, lens = pe_reads(ref, max(1, args.reads // 2), seed=42 + rank)
+    n = len(lens)
+    gen_s = time.perf_counter() - t0
+    t = time.perf_counter()
+    fmi = bsw.Fmi(ref, device=local)
+    build_s = time.perf_counter() - t
+    T = np.concatenate([ref, (3 - ref[::-1])]).astype(np.uint8)
+    eng = bsw.Engine(device=local)
+    bsw.set_reference(eng, T)
+    opt = bsw.ext_opt(w=args.w, l_pac=len(ref))
+    mopt, copt = bsw.mem_opt(), bsw.chain_opt()
+    cap = 256
+    d_reads = hiprt.DeviceBuffer.from_array(reads)
+    d_off, d_len = hiprt.DeviceBuffer.from_array(off), hiprt.DeviceBuffer.from_array(lens)
+    d_mems = hiprt.DeviceBuffer(n * cap * bsw.BWTINTV_DTYPE.itemsize)
+    d_cnt = hiprt.DeviceBuffer(n * 4)
+    sc_cap = [max(16, 4 * n)]
+    bufs = {}
+
+    def alloc(m):
+        bufs.update(seeds=hiprt.DeviceBuffer(m * bsw.SEED_DTYPE.itemsize), sr=hiprt.DeviceBuffer(m * 4),
+                    sc=hiprt.DeviceBuffer(m * 4), out=hiprt.DeviceBuffer(m * bsw.ALNREG_DTYPE.itemsize),
+                    ext=hiprt.DeviceBuffer(m * 4))
+        sc_cap[0] = m
+    alloc(sc_cap[0])
+
+    def step():
+        ta = time.perf_counter()
+        bsw._check(fmi.collect_intv_device(d_reads.ptr, d_off.ptr, d_len.ptr, n, 150, d_mems.ptr, cap, d_cnt.ptr, mopt))
+        tb = time.perf_counter()
+        rc, ns = fmi.mem_chain_device(d_len.ptr, n, d_mems.ptr, cap, d_cnt.ptr, bufs["seeds"].ptr, bufs["sr"].ptr,
+                                      bufs["sc"].ptr, sc_cap[0], copt)
+        if rc == -34:                                    # more seeds than room: grow, redo (counted)
+            alloc(int(ns * 1.25) + 16)
+            rc, ns = fmi.mem_chain_device(d_len.ptr, n, d_mems.ptr, cap, d_cnt.ptr, bufs["seeds"].ptr,
+                                          bufs["sr"].ptr, bufs["sc"].ptr, sc_cap[0], copt)
+        bsw._check(rc)
+        tc = time.perf_counter()
+        bsw.chain2aln_resident(eng, d_reads.ptr, d_off.ptr, d_len.ptr, n, bufs["seeds"].ptr, bufs["sr"].ptr,
+                               bufs["sc"].ptr, ns, bufs["out"].ptr, bufs["ext"].ptr, opt)
+        td = time.perf_counter()
+        return ns, bsw.chain_last_stats(eng), (tb - ta, tc - tb, td - tc)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    t = time.perf_counter()
+    n_ext, sts, parts = 0, [], []
+    for _ in range(args.steps):
+        ns, st, pt = step()
+        n_ext += sum(st.n_pairs)
+        sts.append(st)
+        parts.append(pt)
+    barrier(world)
+    dt = time.perf_counter() - t
+    dt_max = allreduce_max(dt, world)
+    n_ext_all = allreduce_sum(n_ext, world)
+    if rank != 0:
+        return
+    seeds = bufs["seeds"].download(np.zeros(ns, dtype=bsw.SEED_DTYPE))
+    sr = bufs["sr"].download(np.zeros(ns, dtype=np.int32))
+    sc = bufs["sc"].download(np.zeros(ns, dtype=np.int32))
+    out = bufs["out"].download(np.zeros(ns, dtype=bsw.ALNREG_DTYPE))
+    ext = bufs["ext"].download(np.zeros(ns, dtype=np.int32))
+    st = sts[-1]
+    pm = np.mean(np.array(parts), axis=0) * 1e3
+    reads_s = n * world * args.steps / dt_max / 1e6
+    best = np.zeros(n, np.int32)
+    np.maximum.at(best, sr[ext == 1], out["truesc"][ext == 1])
+    value = reads_s if c1 else n_ext_all / dt_max / 1e6
+    out_j = {
+        "metric": "M reads/sec through GPU seeding + chaining + extension (C1)" if c1 else METRIC,
+        "value": round(value, 3), "unit": "M reads/s" if c1 else UNIT, "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16",
+        "data": ("the reference's own C1 data (benchmark_threading.sh:42-70 generator, regenerated bit-exactly)"
+                 if c1 else "synthetic PE reads (bench.pe_reads) from a bsw_synth.c random reference"),
+        "config": {"workload": ("C1: 10K exact 150 bp SE reads vs the 1 Mb reference" if c1 else
+                                f"C4 front end: {n} PE 150 bp reads/GPU vs a {args.ref_mb} Mb random reference") +
+                               " -- FM-index SMEM seeding -> SA + mem_chain + mem_chain_flt -> mem_chain2aln, all on "
+                               "the GPU, index / reads / two-strand text resident in HBM",
+                   "reads_per_gpu": n, "ref_bases": int(len(ref)), "parallelism": f"shard{world} (independent reads)"},
+        "reads_per_s_M": round(reads_s, 3),
+        "extensions_per_s_M": round(n_ext_all / dt_max / 1e6, 3),
+        "stage_ms": {"smem": round(float(pm[0]), 3), "chain": round(float(pm[1]), 3),
+                     "chain2aln": round(float(pm[2]), 3)},
+        "smem_kernel_ms": round(fmi.last_kernel_ms(), 3),
+        "seeds_per_read": round(ns / n, 3), "chains_per_read": round(float(len(np.unique(sr * 4096 + sc))) / n, 3),
+        "extended_fraction": round(st.n_extended / max(1, ns), 4), "rounds": st.rounds,
+        "extensions_per_step_rank0": list(st.n_pairs),
+        "full_length_fraction": round(float(np.mean(best == 150)), 4) if c1 else None,
+        "index_build_s": round(build_s, 2), "synth_gen_s": round(gen_s, 2),
+    }
+    if world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # CPU baseline leg only (test infrastructure)
+        S = min(n, 20_000)
+        fr = oracle.FmiRef(ref, sa=fmi.sa())             # the product's SA: skips the oracle's sort
+        t = time.perf_counter()
+        mems, cnt = fr.collect_intv(reads[:int(off[S - 1] + lens[S - 1])], off[:S], lens[:S], cap=cap)
+        w_seeds, w_sr, w_sc = oracle.mem_chain(fr.sa(), len(ref), lens[:S], mems, cnt)
+        want, wext = oracle.chain2aln(oracle.make_params(), opt, T, reads, off[:S], lens[:S], w_seeds, w_sr, w_sc)
+        dt_cpu = time.perf_counter() - t
+        k = int(np.searchsorted(sr, S))
+        same = bool(len(w_seeds) == k and np.array_equal(w_sr, sr[:k]) and np.array_equal(w_sc, sc[:k]) and
+                    np.array_equal(wext, ext[:k]) and all(np.array_equal(want[f], out[:k][f])
+                                                          for f in bsw.ALNREG_DTYPE.names))
+        out_j["cpu_baseline"] = {
+            "value": round(S / dt_cpu / 1e6, 5) if c1 else None, "unit": "M reads/s", "cores": 1, "kind": "port",
+            "reads_per_s_M": round(S / dt_cpu / 1e6, 5),
+            "sample": f"first {S} reads; oracle/fmi_ref.c collect_intv + oracle/chain_ref.c mem_chain/mem_chain_flt + "
+                      f"oracle/ext_ref.c chain2aln (scalar ksw_extend2), 1 thread (index built from the product's "
+                      f"suffix array, not timed)",
+            "outputs_identical_to_gpu": same,
+        }
+        if not c1:
+            n_cpu = int(np.sum(wext * ((w_seeds["qbeg"] > 0).astype(int) +
+                                       ((w_seeds["qbeg"] + w_seeds["len"]) < lens[w_sr]).astype(int))))
+            out_j["cpu_baseline"].update(value=round(n_cpu / dt_cpu / 1e6, 5), unit=UNIT)
+    fmi.close()
     print(json.dumps(out_j), flush=True)
 
 

@@ -222,12 +222,14 @@ float ms_since(std::chrono::steady_clock::time_point t0)
 
 struct Buf {                       // device allocations of one call, freed on every path
     int device;
-    void *p[24] = {};
+    static constexpr int kMax = 24;
+    void *p[kMax] = {};
     int n = 0;
     explicit Buf(int d) : device(d) {}
     template <class T>
     hipError_t get(T *&out, size_t count)
     {
+        if (n == kMax) return hipErrorInvalidValue;
         void *q = nullptr;
         const hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
         if (e == hipSuccess) { p[n++] = q; out = (T *)q; }

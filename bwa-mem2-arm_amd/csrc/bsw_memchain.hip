@@ -345,13 +345,15 @@ int hip_rc(hipError_t e) { return e == hipSuccess ? BSW_OK : (e == hipErrorOutOf
     } while (0)
 
 struct DevBufs {                                        // one call's scratch, freed on every path
+    static constexpr int kMax = 16;
     int device;
-    void *p[12] = {};
+    void *p[kMax] = {};
     int n = 0;
     explicit DevBufs(int d) : device(d) {}
     template <class T>
     hipError_t get(T *&out, size_t count)
     {
+        if (n == kMax) return hipErrorInvalidValue;
         void *q = nullptr;
         const hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
         if (e == hipSuccess) { p[n++] = q; out = (T *)q; }
@@ -369,14 +371,13 @@ int run_chain(const bsw::FmiView &f, const COpt &o, const int32_t *d_len, int32_
               int64_t *n_seeds, hipStream_t s)
 {
     DevBufs B(f.device);
-    int64_t *cnt, *off, *kcnt, *koff, *tot;
+    int64_t *cnt, *off, *kcnt, *koff;
     int32_t *n_kept;
     MC_TRY(B.get(cnt, (size_t)n + 1));
     MC_TRY(B.get(off, (size_t)n + 1));
     MC_TRY(B.get(kcnt, (size_t)n + 1));
     MC_TRY(B.get(koff, (size_t)n + 1));
     MC_TRY(B.get(n_kept, (size_t)n));
-    MC_TRY(B.get(tot, 2));
     const dim3 g((unsigned)((n + 63) / 64)), b(64);
     hipLaunchKernelGGL(k_count, g, b, 0, s, o, d_len, n, d_mems, cap, d_nm, cnt);
     MC_TRY(hipGetLastError());

@@ -88,6 +88,39 @@ int oracle_fmi_build(const uint8_t *ref, int64_t len, fmi_ref_t *f)
     return 0;
 }
 
+/* The same index from a caller-supplied suffix array of T$ (n + 1 entries): the bench's CPU
+ * baseline leg uses the product's suffix array to skip the comparison sort on large
+ * references; the tests build with oracle_fmi_build (and compare the two arrays). */
+int oracle_fmi_build_with_sa(const uint8_t *ref, int64_t len, const int64_t *sa, fmi_ref_t *f)
+{
+    memset(f, 0, sizeof(*f));
+    int64_t n = 2 * len;
+    f->n = n;
+    f->t = (uint8_t *)malloc(n > 0 ? n : 1);
+    f->sa = (int64_t *)malloc(sizeof(int64_t) * (n + 1));
+    f->bwt = (uint8_t *)malloc(n + 1);
+    f->occ = (int64_t *)malloc(sizeof(int64_t) * 4 * (n + 2));
+    if (!f->t || !f->sa || !f->bwt || !f->occ) return -1;
+    for (int64_t i = 0; i < len; ++i) {
+        if (ref[i] > 3) return -1;
+        f->t[i] = ref[i];
+        f->t[n - 1 - i] = (uint8_t)(3 - ref[i]);
+    }
+    memcpy(f->sa, sa, sizeof(int64_t) * (n + 1));
+    for (int64_t r = 0; r <= n; ++r) {
+        f->bwt[r] = f->sa[r] == 0 ? 4 : f->t[f->sa[r] - 1];
+        if (f->sa[r] == 0) f->sentinel = r;
+    }
+    for (int c = 0; c < 4; ++c) f->occ[c] = 0;
+    for (int64_t r = 0; r <= n; ++r)
+        for (int c = 0; c < 4; ++c) f->occ[4 * (r + 1) + c] = f->occ[4 * r + c] + (f->bwt[r] == c);
+    int64_t tot[4] = {0, 0, 0, 0};
+    for (int64_t i = 0; i < n; ++i) tot[f->t[i]]++;
+    f->count[0] = 1;
+    for (int c = 0; c < 4; ++c) f->count[c + 1] = f->count[c] + tot[c];
+    return 0;
+}
+
 void oracle_fmi_free(fmi_ref_t *f)
 {
     free(f->t); free(f->sa); free(f->bwt); free(f->occ);

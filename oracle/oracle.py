@@ -239,7 +239,8 @@ class FmiRef:
     """The oracle's FM-index of ref + reverse-complement(ref) (comparison-sorted suffix array,
     prefix-count occurrence table) and its SMEM passes."""
 
-    def __init__(self, ref):
+    def __init__(self, ref, sa=None):
+        """sa: build from this suffix array of T$ instead of sorting (bench CPU leg only)"""
         L = lib()
         P = ctypes.c_void_p
         L.oracle_fmi_sizeof.restype = ctypes.c_size_t
@@ -255,7 +256,14 @@ class FmiRef:
         L.oracle_collect_intv_mt.argtypes = [P, P, P, P, P, ctypes.c_int32, P, ctypes.c_int32, P, ctypes.c_int]
         self._buf = ctypes.create_string_buffer(L.oracle_fmi_sizeof())
         self.ref = np.ascontiguousarray(ref, dtype=np.uint8)
-        if L.oracle_fmi_build(_ptr(self.ref), len(self.ref), self._buf) != 0:
+        if sa is not None:
+            L.oracle_fmi_build_with_sa.argtypes = [P, ctypes.c_int64, P, P]
+            sa = np.ascontiguousarray(sa, dtype=np.int64)
+            assert len(sa) == 2 * len(self.ref) + 1
+            rc = L.oracle_fmi_build_with_sa(_ptr(self.ref), len(self.ref), _ptr(sa), self._buf)
+        else:
+            rc = L.oracle_fmi_build(_ptr(self.ref), len(self.ref), self._buf)
+        if rc != 0:
             raise ValueError("oracle_fmi_build failed (codes must be 0..3)")
         self.n = L.oracle_fmi_n(self._buf)
         self.sentinel = L.oracle_fmi_sentinel(self._buf)
