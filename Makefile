@@ -96,3 +96,39 @@ ab:
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(ABLIB) $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_ab.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_batch.o -lpthread
 
 .PHONY: all product synth oracle clean stats ab
+
+# host sanitizer build: AddressSanitizer + UBSan over the host C / C++ of the
+# product (bsw_pack.cpp, bsw_ext.cpp, bsw_batch.c, bsw_synth.c) and the oracle, driven by
+# tools/asan/asan_driver.cpp with an oracle-backed engine stub (no GPU).  Log: tools/asan/asan.log
+ASAN_DIR   := tools/asan
+ASAN_FLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined -g -O1 -Iinclude
+ASAN_BIN   := $(ASAN_DIR)/asan_driver
+ASAN_C     := $(CSRC)/bsw_batch.c $(CSRC)/bsw_synth.c oracle/ksw_ext_ref.c oracle/ext_ref.c oracle/ksw_align_ref.c oracle/ksw_global_ref.c oracle/fmi_ref.c oracle/chain_ref.c
+ASAN_SSE   := oracle/bsw_sse41.c
+ASAN_CXX   := $(ASAN_DIR)/asan_driver.cpp $(ASAN_DIR)/engine_stub.cpp $(CSRC)/bsw_ext.cpp $(CSRC)/bsw_pack.cpp
+$(ASAN_BIN): $(ASAN_C) $(ASAN_SSE) $(ASAN_CXX) $(CSRC)/bsw_internal.h include/bsw_ext.h include/bsw_fmi.h
+	mkdir -p $(ASAN_DIR)/obj
+	for f in $(ASAN_C); do gcc $(ASAN_FLAGS) -std=gnu11 -c $$f -o $(ASAN_DIR)/obj/$$(basename $$f).o || exit 1; done
+	gcc $(ASAN_FLAGS) -std=gnu11 -msse4.1 -c $(ASAN_SSE) -o $(ASAN_DIR)/obj/bsw_sse41.c.o
+	g++ $(ASAN_FLAGS) -std=c++17 -o $@ $(ASAN_CXX) $(ASAN_DIR)/obj/*.o -lpthread
+asan: $(ASAN_BIN)
+	ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
+	  ./$(ASAN_BIN) > $(ASAN_DIR)/asan.log 2>&1; rc=$$?; cat $(ASAN_DIR)/asan.log; exit $$rc
+# the CPU test suite (-m "not gpu") against sanitized builds of the oracle and the synthetic
+# generator (LD_PRELOAD of the sanitizer runtimes into python; leak checks off: the interpreter
+# keeps its arenas).  Log: tools/asan/asan_suite.log
+ASAN_ORACLE := $(ASAN_DIR)/liboracle_asan.so
+ASAN_SYNTH  := $(ASAN_DIR)/libbsw_synth_asan.so
+$(ASAN_ORACLE): $(ORACLE_SRCS) include/bsw_seqpair.h include/bsw_ext.h include/bsw_fmi.h
+	mkdir -p $(ASAN_DIR)
+	gcc $(ASAN_FLAGS) -fPIC -msse4.1 -shared -o $@ $(ORACLE_SRCS) -lpthread
+$(ASAN_SYNTH): $(CSRC)/bsw_synth.c include/bsw_seqpair.h
+	mkdir -p $(ASAN_DIR)
+	gcc $(ASAN_FLAGS) -fPIC -shared -o $@ $(CSRC)/bsw_synth.c
+asan-suite: $(ASAN_ORACLE) $(ASAN_SYNTH)
+	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so)" \
+	  ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
+	  BSW_ORACLE_LIB=$(ASAN_ORACLE) BSW_SYNTH_LIB=$(ASAN_SYNTH) \
+	  python -m pytest tests -q -m "not gpu" -p no:cacheprovider > $(ASAN_DIR)/asan_suite.log 2>&1; rc=$$?; \
+	  tail -5 $(ASAN_DIR)/asan_suite.log; exit $$rc
+.PHONY: asan asan-suite

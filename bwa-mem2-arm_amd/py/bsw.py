@@ -16,7 +16,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBDIR = os.path.join(PKG, "lib")
 HIP_LIB = os.environ.get("BSW_HIP_LIB") or os.path.join(LIBDIR, "libbsw_hip.so")   # override: experiment builds
-SYNTH_LIB = os.path.join(LIBDIR, "libbsw_synth.so")
+SYNTH_LIB = os.environ.get("BSW_SYNTH_LIB") or os.path.join(LIBDIR, "libbsw_synth.so")   # override: `make asan-suite`
 
 SEQPAIR_DTYPE = np.dtype(
     [(n, "<i4") for n in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid",

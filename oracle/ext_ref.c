@@ -233,3 +233,52 @@ void oracle_chain2aln(const oracle_params_t *p, const bsw_ext_opt_t *opt, const 
     free(av);
     free(srt);
 }
+
+/* oracle_chain2aln over nthreads pthreads, reads split into contiguous runs (reads are
+ * independent; the bench's multi-thread CPU baseline leg). */
+#include <pthread.h>
+typedef struct {
+    const oracle_params_t *p;
+    const bsw_ext_opt_t *opt;
+    const uint8_t *ref, *reads;
+    int64_t ref_len;
+    const int64_t *read_off;
+    const int32_t *read_len;
+    const bsw_seed_t *seeds;
+    const int32_t *seed_read, *seed_chain;
+    int32_t a, b;
+    bsw_alnreg_t *out;
+    int32_t *extended;
+} c2a_job_t;
+
+static void *c2a_worker(void *arg)
+{
+    c2a_job_t *j = (c2a_job_t *)arg;
+    oracle_chain2aln(j->p, j->opt, j->ref, j->ref_len, j->reads, j->read_off, j->read_len, j->seeds + j->a,
+                     j->seed_read + j->a, j->seed_chain + j->a, j->b - j->a, j->out + j->a, j->extended + j->a);
+    return NULL;
+}
+
+void oracle_chain2aln_mt(const oracle_params_t *p, const bsw_ext_opt_t *opt, const uint8_t *ref, int64_t ref_len,
+                         const uint8_t *reads, const int64_t *read_off, const int32_t *read_len,
+                         const bsw_seed_t *seeds, const int32_t *seed_read, const int32_t *seed_chain, int32_t ns,
+                         bsw_alnreg_t *out, int32_t *extended, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    c2a_job_t jobs[256];
+    int32_t a = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        int32_t b = (int32_t)((int64_t)ns * (t + 1) / nthreads);
+        while (b > a && b < ns && seed_read[b] == seed_read[b - 1]) ++b;     /* whole reads per thread */
+        if (b < a) b = a;
+        c2a_job_t j = {p, opt, ref, reads, ref_len, read_off, read_len, seeds, seed_read, seed_chain, a, b, out,
+                       extended};
+        jobs[t] = j;
+        a = b;
+    }
+    jobs[nthreads - 1].b = ns;
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, c2a_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}

@@ -337,7 +337,7 @@ int oracle_collect_intv(const fmi_ref_t *f, const oracle_mem_opt_t *opt, const u
             }
         }
     }
-    qsort(mem.a, (size_t)mem.n, sizeof(ref_intv_t), cmp_intv);
+    if (mem.n) qsort(mem.a, (size_t)mem.n, sizeof(ref_intv_t), cmp_intv);   /* qsort(NULL, 0): UB */
     int n = (int)mem.n;
     for (i = 0; i < n && i < cap; ++i) out[i] = mem.a[i];
     free(mem.a); free(mem1.a); free(t0.a); free(t1.a);

@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATH = os.environ.get("BSW_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")   # override: `make asan-suite`
 
 SEQPAIR_DTYPE = np.dtype(
     [(n, "<i4") for n in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid",
@@ -107,12 +107,14 @@ def sse41_get_scores16(params: OracleParams, pairs: np.ndarray, ref: np.ndarray,
                                     len(pairs), w, nthreads)
 
 
-def chain2aln(params, opt, ref, reads, read_off, read_len, seeds, seed_read, seed_chain):
-    """oracle_chain2aln (oracle/ext_ref.c): literal per-read mem_chain2aln -> (regions, extended)."""
+def chain2aln(params, opt, ref, reads, read_off, read_len, seeds, seed_read, seed_chain, nthreads=1):
+    """oracle_chain2aln (oracle/ext_ref.c): literal per-read mem_chain2aln -> (regions, extended);
+    nthreads > 1 splits the reads over pthreads (oracle_chain2aln_mt)."""
     import bsw  # dtypes of the product binding (ALNREG_DTYPE)
     L = lib()
     P = ctypes.c_void_p
     L.oracle_chain2aln.argtypes = [P, P, P, ctypes.c_int64, P, P, P, P, P, P, ctypes.c_int32, P, P]
+    L.oracle_chain2aln_mt.argtypes = [P, P, P, ctypes.c_int64, P, P, P, P, P, P, ctypes.c_int32, P, P, ctypes.c_int]
     ptr = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
     arrs = [np.ascontiguousarray(x, dtype=d) for x, d in ((ref, np.uint8), (reads, np.uint8), (read_off, np.int64),
                                                            (read_len, np.int32), (seed_read, np.int32),
@@ -120,8 +122,14 @@ def chain2aln(params, opt, ref, reads, read_off, read_len, seeds, seed_read, see
     seeds = np.ascontiguousarray(seeds)
     out = np.zeros(len(seeds), dtype=bsw.ALNREG_DTYPE)
     ext = np.zeros(len(seeds), dtype=np.int32)
-    L.oracle_chain2aln(ctypes.byref(params), ctypes.byref(opt), ptr(arrs[0]), len(arrs[0]), ptr(arrs[1]), ptr(arrs[2]),
-                       ptr(arrs[3]), ptr(seeds), ptr(arrs[4]), ptr(arrs[5]), len(seeds), ptr(out), ptr(ext))
+    if nthreads > 1:
+        L.oracle_chain2aln_mt(ctypes.byref(params), ctypes.byref(opt), ptr(arrs[0]), len(arrs[0]), ptr(arrs[1]),
+                              ptr(arrs[2]), ptr(arrs[3]), ptr(seeds), ptr(arrs[4]), ptr(arrs[5]), len(seeds), ptr(out),
+                              ptr(ext), nthreads)
+    else:
+        L.oracle_chain2aln(ctypes.byref(params), ctypes.byref(opt), ptr(arrs[0]), len(arrs[0]), ptr(arrs[1]),
+                           ptr(arrs[2]), ptr(arrs[3]), ptr(seeds), ptr(arrs[4]), ptr(arrs[5]), len(seeds), ptr(out),
+                           ptr(ext))
     return out, ext
 
 
