@@ -19,7 +19,12 @@ ORACLE   := oracle/liboracle.so
 HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pc.hip $(CSRC)/bsw_wv.hip $(CSRC)/bsw_mate.hip $(CSRC)/bsw_global.hip $(CSRC)/bsw_ext_dev.hip $(CSRC)/bsw_fmi.hip $(CSRC)/bsw_memchain.hip $(CSRC)/bsw_chain.hip $(CSRC)/bsw_host.cpp $(CSRC)/bsw_ext.cpp $(CSRC)/bsw_pack.cpp
 HIP_HDRS := $(CSRC)/bsw_pool.h $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h $(CSRC)/bsw_fmi_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h include/bsw_fmi.h
 
-all: product synth oracle
+all: product synth oracle percall
+
+PERCALL := $(LIBDIR)/percall_bench
+percall: $(PERCALL)
+$(PERCALL): tools/percall_bench.cpp $(PRODUCT) $(SYNTH) include/bsw.h
+	g++ -O2 -std=c++17 -pthread -Iinclude -o $@ $< $(PRODUCT) $(SYNTH) -Wl,-rpath,'$$ORIGIN'
 
 product: $(PRODUCT)
 synth: $(SYNTH)
@@ -95,7 +100,7 @@ ab:
 	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/bsw_pc.hip -o $(LIBDIR)/bsw_pc_ab.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(ABLIB) $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_ab.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_batch.o -lpthread
 
-.PHONY: all product synth oracle clean stats ab
+.PHONY: all product synth oracle percall clean stats ab
 
 # host sanitizer build: AddressSanitizer + UBSan over the host C / C++ of the
 # product (bsw_pack.cpp, bsw_ext.cpp, bsw_batch.c, bsw_synth.c) and the oracle, driven by

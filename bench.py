@@ -251,6 +251,10 @@ def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
     }
 
 
+def coalesce_opt(eng):
+    return getattr(eng, "coalesce_setting", 32768)
+
+
 def host_path_rates(eng, pairs, ref, qer, w, cell_bits, want, curve_sizes=(1_000, 10_000, 100_000)):
     """The drop-in path: bsw_get_scores on HOST buffers (pageable numpy memory, as upstream's
     getScores16 caller hands them over), PCIe both ways included.  Whole batch (median of 3
@@ -306,6 +310,7 @@ def host_path_rates(eng, pairs, ref, qer, w, cell_bits, want, curve_sizes=(1_000
                       "M_pairs_per_s_1_caller": round(m / statistics.median(lat) / 1e6, 3),
                       "M_pairs_per_s_8_callers": round(nthr * per * m / dt8 / 1e6, 3)})
     return {"value": round(n / t_all / 1e6, 3), "ms": round(t_all * 1e3, 3),
+            "coalesce_max_pairs": coalesce_opt(eng),
             "ms_all_calls": [round(x * 1e3, 2) for x in ts],
             "last_call": {"host_ms": round(st.host_ms, 3), "stage_ms": round(st.stage_ms, 3),
                           "dp_kernel_ms": round(st.kernel_ms, 3), "launches": st.n_launches},
@@ -468,6 +473,24 @@ def main():
         out["abi_inclusive"] = dict(hp, unit=UNIT, note="bsw_get_scores on pageable host buffers: staging "
                                     "(2-bit codes, 20-B input records) + H2D + plan/sort/DP + D2H of the outputs, "
                                     "chunked pipeline over three slots")
+        # the same curve from C++ kt_for-style threads through the C ABI (tools/percall_bench.cpp:
+        # no Python between calls), with and without cross-call coalescing
+        import subprocess
+        exe = os.path.join(ROOT, "bwa-mem2-arm_amd", "lib", "percall_bench")
+        if os.path.exists(exe):
+            try:
+                r = subprocess.run([exe, "1000000", "8", "1000", "10000", "100000"], capture_output=True, text=True,
+                                   timeout=120)
+                if r.returncode == 0:
+                    out["abi_inclusive"]["per_call_curve_cpp_callers"] = json.loads(r.stdout.strip().splitlines()[-1])
+            except (subprocess.SubprocessError, ValueError, IndexError):
+                pass
+        eng.set_option("coalesce", 0)                  # per-call curve without cross-call coalescing (A/B)
+        eng.coalesce_setting = 0
+        hp0 = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res)
+        eng.set_option("coalesce", 32768)
+        eng.coalesce_setting = 32768
+        out["abi_inclusive"]["per_call_curve_without_coalescing"] = hp0["per_call_curve"]
         eng.set_option("host_pack", 4)                 # the nibble staging beside it (same box, same batch)
         hp4 = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res, curve_sizes=())
         eng.set_option("host_pack", 2)

@@ -252,9 +252,17 @@ static hipError_t grow(T *&p, size_t &cap, size_t need)   // cap counts elements
     return e;
 }
 
+struct AggReq;
 struct DeviceCtx {
     int device = 0;
     std::atomic<int> inflight{0};       // host-buffer calls running on this logical device
+    // cross-call coalescing (coalesced_call): small host-buffer calls queue here; up to
+    // agg_leaders_max of their threads at a time each run everything queued as ONE batch
+    std::mutex agg_mu;
+    std::condition_variable agg_cv;
+    std::deque<AggReq *> agg_q;
+    int agg_leaders = 0;
+    int agg_leaders_max = 4;            // BSW_OPT_COALESCE_LEADERS
     std::mutex mu;
     std::vector<std::unique_ptr<Slot>> free_slots;
     uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
@@ -344,6 +352,7 @@ struct bsw_ctx {
     int32_t host_chunk = 262144;        // BSW_OPT_HOST_CHUNK: pairs per host-buffer pipeline chunk
     int host_pack = 2;                  // BSW_OPT_HOST_PACK: 2-bit (2) or nibble (4) staging
     int64_t split_min = 131072;         // BSW_OPT_SPLIT_MIN: smaller calls go whole to one device
+    int32_t coalesce = 32768;           // BSW_OPT_COALESCE: calls of <= this many pairs coalesce
     std::atomic<unsigned> rr{0};        // tie-break rotation of the one-device pick
     ~bsw_ctx()
     {
@@ -1119,6 +1128,257 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     return rc;
 }
 
+// ---------------------------------------------------------------- cross-call coalescing
+// Upstream's kt_for workers each hand getScores* a few thousand pairs per call.  Run one by one,
+// every such call pays a plan / sort / DP launch sequence whose lane-per-pair waves live ~1 ms
+// whatever the batch size, and 8 workers' calls contend for the runtime.  Here a small call
+// (<= BSW_OPT_COALESCE pairs) is queued on its device; the first caller that finds fewer than
+// agg_leaders_max batches in flight becomes a leader, takes EVERY queued call of the same
+// (w, cell_bits, end_bonus) -- its own or others' -- and runs them as one device batch: the
+// callers' contiguous byte extents 2-bit-packed side by side in one pinned staging buffer
+// (records rebased), one H2D, one plan / sort / DP, 24 B of outputs per pair back, scattered
+// to each caller's records.  A lone caller leads its own one-call batch at once (no added
+// wait); under load, calls that arrive while a batch is on the GPU form the next one.
+// Outputs are identical to separate calls (pairs are independent).
+struct AggReq {
+    SeqPair *pairs;
+    const uint8_t *ref, *qer;
+    int32_t n, w;
+    int cell_bits;
+    int32_t eb;
+    int rc = BSW_OK;
+    bsw_stats_t st{};
+    bool done = false;
+};
+constexpr int32_t kAggMaxPairs = 262144;        // pairs per coalesced batch
+
+struct AggSeg {                                 // one call inside a coalesced batch
+    AggReq *r;
+    int64_t r_lo, r_hi, q_lo, q_hi;             // the call's byte extents in its own buffers
+    int64_t r_off, q_off;                       // their offsets in the batch's code space
+    int32_t p_off;                              // first record in the batch
+};
+
+static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg> &segs, int32_t N, int64_t r_tot,
+                            int64_t q_tot, int32_t w, int cell_bits, bsw_stats_t &st)
+{
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    Slot &s = *slot;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        const size_t rs = (size_t)(r_tot + 3) / 4, qs = (size_t)(q_tot + 3) / 4;
+        const size_t exc_cap = (size_t)(r_tot + q_tot) / 32 + 1024;
+        const size_t pair_off = 0, ref_off = align256((size_t)N * sizeof(PairIn));
+        const size_t qer_off = align256(ref_off + rs + 4), exc_off = align256(qer_off + qs + 4);
+        const size_t bytes = std::max(exc_off + exc_cap * 4, (size_t)N * 24);
+        if (bytes > s.cap_stage) {
+            const size_t cap = std::max(bytes, s.cap_stage * 3 / 2);
+            if (s.h_stage) (void)hipHostFree(s.h_stage);
+            s.h_stage = nullptr; s.cap_stage = 0;
+            BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));
+            s.cap_stage = cap;
+        }
+        const auto tg0 = std::chrono::steady_clock::now();
+        uint8_t *h = (uint8_t *)s.h_stage;
+        memset(h + ref_off, 0, rs + 4);                 // the padding between calls' extents
+        memset(h + qer_off, 0, qs + 4);
+        // tasks: per call its records, and its ref / qer extents in pieces of <= 1 MB cut at
+        // multiples of 64 codes (every call's extent starts 64-aligned in the code space)
+        struct Task { int seg, kind; int64_t a, b; };
+        std::vector<Task> tasks;
+        constexpr int64_t kPiece = (int64_t)1 << 20;
+        for (int g = 0; g < (int)segs.size(); ++g) {
+            tasks.push_back(Task{g, 0, 0, 0});
+            for (int kind = 1; kind <= 2; ++kind) {
+                const int64_t len = kind == 1 ? segs[g].r_hi - segs[g].r_lo : segs[g].q_hi - segs[g].q_lo;
+                for (int64_t a = 0; a < len; a += kPiece) tasks.push_back(Task{g, kind, a, std::min(len, a + kPiece)});
+            }
+        }
+        std::vector<std::vector<uint32_t>> ex(tasks.size());
+        PairIn *pin = (PairIn *)(h + pair_off);
+        HostPool::get().parallel_for((int)tasks.size(), [&](int t) {
+            const Task &k = tasks[t];
+            const AggSeg &g = segs[k.seg];
+            if (k.kind == 0) {
+                const SeqPair *p = g.r->pairs;
+                for (int32_t i = 0; i < g.r->n; ++i) {
+                    PairIn &o = pin[g.p_off + i];
+                    o.idr = p[i].len1 > 0 ? (int32_t)(p[i].idr - g.r_lo + g.r_off) : 0;
+                    o.idq = p[i].len2 > 0 ? (int32_t)(p[i].idq - g.q_lo + g.q_off) : 0;
+                    o.len1 = p[i].len1; o.len2 = p[i].len2; o.h0 = p[i].h0;
+                }
+            } else if (k.kind == 1) {
+                pack_2bit(h + ref_off + (g.r_off + k.a) / 4, g.r->ref + g.r_lo + k.a, (size_t)(k.b - k.a),
+                          (uint32_t)(g.r_off + k.a), ex[t]);
+            } else {
+                pack_2bit(h + qer_off + (g.q_off + k.a) / 4, g.r->qer + g.q_lo + k.a, (size_t)(k.b - k.a),
+                          (uint32_t)(g.q_off + k.a), ex[t]);
+            }
+        });
+        size_t n_r = 0, n_q = 0;
+        for (size_t t = 0; t < tasks.size(); ++t) (tasks[t].kind == 1 ? n_r : n_q) += ex[t].size();
+        if (n_r + n_q > exc_cap) return 1;              // too many non-ACGT bytes: caller splits
+        uint32_t *exw = (uint32_t *)(h + exc_off);
+        size_t o_r = 0, o_q = n_r;
+        for (size_t t = 0; t < tasks.size(); ++t) {
+            if (ex[t].empty()) continue;
+            size_t &o = tasks[t].kind == 1 ? o_r : o_q;
+            memcpy(exw + o, ex[t].data(), ex[t].size() * 4);
+            o += ex[t].size();
+        }
+        const size_t up = exc_off + (n_r + n_q) * 4;
+        const auto tg1 = std::chrono::steady_clock::now();
+        BSW_TRY(grow(s.d_stage, s.cap_dstage, std::max(up, (size_t)N * 24)));
+        BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, up, hipMemcpyHostToDevice, s.stream));
+        BSW_TRY(grow(s.d_ref, s.cap_ref, (size_t)r_tot + 4));
+        BSW_TRY(grow(s.d_qer, s.cap_qer, (size_t)q_tot + 4));
+        BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)N));
+        BSW_TRY(hipMemsetAsync(s.d_ref + r_tot, 0, 4, s.stream));
+        BSW_TRY(hipMemsetAsync(s.d_qer + q_tot, 0, 4, s.stream));
+        const int64_t tr = (r_tot + 15) / 16, tq = (q_tot + 15) / 16;
+        if (tr > 0)
+            hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, s.stream,
+                               s.d_stage + ref_off, s.d_ref, r_tot);
+        if (tq > 0)
+            hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, s.stream,
+                               s.d_stage + qer_off, s.d_qer, q_tot);
+        const int32_t ne = (int32_t)(n_r + n_q);
+        if (ne > 0)
+            hipLaunchKernelGGL(patch_codes_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s.stream,
+                               (const uint32_t *)(s.d_stage + exc_off), (int32_t)n_r, ne, s.d_ref, s.d_qer);
+        hipLaunchKernelGGL(expand_pairs_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s.stream,
+                           (const PairIn *)(s.d_stage + pair_off), s.d_pairs, N);
+        BSW_TRY(hipGetLastError());
+        PlanCall pc;
+        pc.d_pairs = s.d_pairs; pc.d_ref = s.d_ref; pc.d_qer = s.d_qer;
+        pc.n = N; pc.w = w; pc.cell_bits = cell_bits; pc.stream = s.stream;
+        int r = run_plan(kp, s, pc);
+        const auto tg2 = std::chrono::steady_clock::now();
+        if (!r) r = run_dp(kp, s);
+        const auto tg3 = std::chrono::steady_clock::now();
+        if (r) {
+            (void)hipStreamSynchronize(s.stream);
+            return r;
+        }
+        hipLaunchKernelGGL(gather_outputs_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s.stream,
+                           s.d_pairs, (int32_t *)s.d_stage, N);
+        BSW_TRY(hipGetLastError());
+        BSW_TRY(hipMemcpyAsync(s.h_stage, s.d_stage, (size_t)N * 24, hipMemcpyDeviceToHost, s.stream));
+        if ((r = finish_stats(s))) return r;
+        const auto tg4 = std::chrono::steady_clock::now();
+        if (getenv("BSW_DEBUG_AGG")) {
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            fprintf(stderr, "agg batch %d calls %d pairs: stage %.3f enqueue %.3f plan-wait %.3f dp+d2h %.3f (kernel %.3f)\n",
+                    (int)segs.size(), N, ms(tg0, tg1), ms(tg1, tg2), ms(tg2, tg3), ms(tg3, tg4), s.stats.kernel_ms);
+        }
+        const int32_t *out = (const int32_t *)s.h_stage;
+        HostPool::get().parallel_for((int)segs.size(), [&](int g) {
+            SeqPair *p = segs[g].r->pairs;
+            const int32_t *q = out + 6 * (int64_t)segs[g].p_off;
+            for (int32_t i = 0; i < segs[g].r->n; ++i, q += 6) {
+                p[i].score = q[0]; p[i].tle = q[1]; p[i].gtle = q[2];
+                p[i].qle = q[3]; p[i].gscore = q[4]; p[i].max_off = q[5];
+            }
+        });
+        st = s.stats;
+        st.stage_ms = (float)std::chrono::duration<double, std::milli>(tg1 - tg0).count();
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot));
+    return rc;
+}
+
+// One coalesced batch: calls that fail validation get BSW_E_RANGE; calls whose buffers are not
+// contiguous (scattered idr / idq) and batches with too many non-ACGT bytes run on their own
+// through host_shard.
+static void run_group(const KParams &kp, DeviceCtx &dc, std::vector<AggReq *> &G, int32_t chunk, bool two_bit)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<AggSeg> segs;
+    std::vector<AggReq *> alone;
+    int64_t r_tot = 0, q_tot = 0;
+    int32_t N = 0;
+    for (AggReq *r : G) {
+        std::vector<BlkStat> bs;
+        if (!prepass(r->pairs, r->n, bs)) { r->rc = BSW_E_RANGE; continue; }
+        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
+        for (const auto &b : bs) {
+            r_lo = std::min(r_lo, b.r_lo); r_hi = std::max(r_hi, b.r_hi); r_sum += b.r_sum;
+            q_lo = std::min(q_lo, b.q_lo); q_hi = std::max(q_hi, b.q_hi); q_sum += b.q_sum;
+        }
+        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+        const bool bulk = (r_hi - r_lo) <= r_sum + r_sum / 4 + 4096 && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096;
+        if (!two_bit || !bulk) { alone.push_back(r); continue; }
+        segs.push_back(AggSeg{r, r_lo, r_hi, q_lo, q_hi, r_tot, q_tot, N});
+        r_tot = (r_tot + (r_hi - r_lo) + 63) & ~(int64_t)63;
+        q_tot = (q_tot + (q_hi - q_lo) + 63) & ~(int64_t)63;
+        N += r->n;
+    }
+    if (!segs.empty()) {
+        bsw_stats_t st{};
+        const int rc = (r_tot < ((int64_t)1 << 28) && q_tot < ((int64_t)1 << 28))
+                           ? run_group_staged(kp, dc, segs, N, r_tot, q_tot, segs[0].r->w, segs[0].r->cell_bits, st)
+                           : 1;
+        if (rc == 1) {
+            for (auto &g : segs) alone.push_back(g.r);
+        } else {
+            st.n_devices = 1;
+            st.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            for (auto &g : segs) { g.r->rc = rc; g.r->st = st; }
+        }
+    }
+    for (AggReq *r : alone) {
+        bsw_stats_t st{};
+        r->rc = host_shard(kp, dc, r->pairs, r->ref, r->qer, r->n, r->w, r->cell_bits, chunk, two_bit, &st);
+        st.n_devices = 1;
+        r->st = st;
+    }
+}
+
+static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref, const uint8_t *qer,
+                          int32_t n, int32_t w, int cell_bits, int32_t chunk, bool two_bit, bsw_stats_t *st)
+{
+    AggReq me{pairs, ref, qer, n, w, cell_bits, kp.end_bonus};
+    std::unique_lock<std::mutex> lk(dc.agg_mu);
+    dc.agg_q.push_back(&me);
+    while (!me.done) {
+        if (dc.agg_leaders < dc.agg_leaders_max && !dc.agg_q.empty()) {
+            // lead: every queued call with the front call's (w, cell_bits, end_bonus), FIFO
+            ++dc.agg_leaders;
+            std::vector<AggReq *> G;
+            const AggReq *f = dc.agg_q.front();
+            const int32_t fw = f->w, feb = f->eb;
+            const int fcb = f->cell_bits;
+            int64_t tot = 0;
+            for (auto it = dc.agg_q.begin(); it != dc.agg_q.end();) {
+                AggReq *r = *it;
+                if (r->w == fw && r->cell_bits == fcb && r->eb == feb && (G.empty() || tot + r->n <= kAggMaxPairs)) {
+                    G.push_back(r);
+                    tot += r->n;
+                    it = dc.agg_q.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+            lk.unlock();
+            KParams gk = kp;
+            gk.end_bonus = feb;
+            run_group(gk, dc, G, chunk, two_bit);
+            lk.lock();
+            --dc.agg_leaders;
+            for (AggReq *r : G) r->done = true;
+            dc.agg_cv.notify_all();
+        } else {
+            dc.agg_cv.wait(lk);
+        }
+    }
+    if (st) *st = me.st;
+    return me.rc;
+}
+
 // ---------------------------------------------------------------- mate rescue (bsw_mate.h)
 static void make_mate_params(const bsw_params_t &p, MateParams &mp)
 {
@@ -1471,8 +1731,12 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
     std::vector<bsw_stats_t> st(nd);
     if (nd == 1) {
         Inflight g(*ctx->devs[one]);
-        rcs[0] = host_shard(kp, *ctx->devs[one], pairs, seqBufRef, seqBufQer, n, w, cell_bits, ctx->host_chunk,
-                            ctx->host_pack == 2, &st[0]);
+        if (n <= ctx->coalesce)             // kt_for-sized: coalesce with concurrent callers
+            rcs[0] = coalesced_call(kp, *ctx->devs[one], pairs, seqBufRef, seqBufQer, n, w, cell_bits,
+                                    ctx->host_chunk, ctx->host_pack == 2, &st[0]);
+        else
+            rcs[0] = host_shard(kp, *ctx->devs[one], pairs, seqBufRef, seqBufQer, n, w, cell_bits,
+                                ctx->host_chunk, ctx->host_pack == 2, &st[0]);
     } else {
         // contiguous pair ranges of equal estimated work (static band cells)
         const std::vector<int32_t> cut = split_by_cells(pairs, n, w, nd);
@@ -1979,6 +2243,14 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     case BSW_OPT_HOST_PACK: if (value != 2 && value != 4) return BSW_E_INVAL; ctx->host_pack = (int)value; return BSW_OK;
     case BSW_OPT_SMALL_BATCH: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.small_batch = (int32_t)value; return BSW_OK;
     case BSW_OPT_SPLIT_MIN: if (value < 0) return BSW_E_INVAL; ctx->split_min = value; return BSW_OK;
+    case BSW_OPT_COALESCE: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->coalesce = (int32_t)value; return BSW_OK;
+    case BSW_OPT_COALESCE_LEADERS:
+        if (value < 1 || value > 16) return BSW_E_INVAL;
+        for (auto &d : ctx->devs) {
+            std::lock_guard<std::mutex> g(d->agg_mu);
+            d->agg_leaders_max = (int)value;
+        }
+        return BSW_OK;
     case BSW_OPT_TEST_MISROUTE: if (!b01) return BSW_E_INVAL; ctx->kp.misroute = (int8_t)value; return BSW_OK;
     default: return BSW_E_INVAL;
     }

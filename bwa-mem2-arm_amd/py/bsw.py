@@ -42,6 +42,8 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_create_on", "bsw_destroy
 OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK, OPT_LONG, OPT_HOST_PACK = 1, 2, 3, 4, 5, 6, 7, 8
 OPT_SMALL_BATCH = 9
 OPT_SPLIT_MIN = 10
+OPT_COALESCE = 11
+OPT_COALESCE_LEADERS = 12
 OPT_TEST_MISROUTE = 100
 
 # include/bsw_ext.h structs
@@ -191,7 +193,8 @@ class Engine:
 
     _OPTS = {"kernel8": OPT_KERNEL8, "fork": OPT_FORK, "sortkey": OPT_SORTKEY, "glob_band": OPT_GLOB_BAND,
              "ext_chunk": OPT_EXT_CHUNK, "host_chunk": OPT_HOST_CHUNK, "long": OPT_LONG, "host_pack": OPT_HOST_PACK,
-             "small_batch": OPT_SMALL_BATCH, "split_min": OPT_SPLIT_MIN, "test_misroute": OPT_TEST_MISROUTE}
+             "small_batch": OPT_SMALL_BATCH, "split_min": OPT_SPLIT_MIN, "coalesce": OPT_COALESCE, "coalesce_leaders": OPT_COALESCE_LEADERS,
+             "test_misroute": OPT_TEST_MISROUTE}
 
     def set_option(self, name, value: int):
         """bsw_set_option by name (kernel8, fork, sortkey, glob_band, ext_chunk, host_chunk, test_misroute)

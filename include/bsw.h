@@ -149,6 +149,12 @@ enum {
     BSW_OPT_SPLIT_MIN = 10,   /* contexts over several devices: host-buffer calls of fewer pairs
                                  (mate / global calls: jobs) run whole on one device (default
                                  131072; 0 = always split)                                    */
+    BSW_OPT_COALESCE = 11,    /* host-buffer calls of at most this many pairs (default 32768; 0 =
+                                 off) coalesce with concurrent callers on their device: queued
+                                 calls of equal (w, cell_bits, end_bonus) run as ONE batch (one
+                                 staging buffer, one plan / sort / DP, outputs scattered back);
+                                 a lone caller runs at once.  Outputs are identical either way */
+    BSW_OPT_COALESCE_LEADERS = 12, /* coalesced batches in flight per device (1..16, default 4) */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };

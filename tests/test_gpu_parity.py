@@ -600,3 +600,51 @@ def test_host_pipeline_2bit_pieces_over_8mb():
         e.get_scores(got, ref, qer, 100)
         _assert_same(want, got, f"pieces > 8 MB, host_pack {pack}")
         e.close()
+
+
+def test_coalesced_small_calls(c2_full):
+    """Cross-call coalescing (BSW_OPT_COALESCE): 8 kt_for-style threads issue small calls of
+    varying sizes, w and cell_bits -- some with scattered (non-contiguous) buffers, one with a pair
+    past BSW_MAX_LEN -- concurrently on one context; every call returns its own outputs (== the
+    oracle), the bad call alone gets BSW_E_RANGE, and coalescing off gives the same."""
+    pairs, ref, qer, want = c2_full
+    want200 = None
+    for co in (32768, 0):
+        e = bsw.Engine(coalesce=co)
+        errs, bad_seen = [], []
+        rng = np.random.default_rng(7)
+        plan = [[(int(rng.integers(0, len(pairs) - 60000)), int(rng.choice([1, 57, 1000, 3000, 10000, 20000])),
+                  int(rng.choice([100, 200])), int(rng.choice([16, 8]))) for _ in range(12)] for _ in range(8)]
+
+        def caller(k):
+            try:
+                for j, (a, m, w, cb) in enumerate(plan[k]):
+                    got = pairs[a:a + m].copy()
+                    if k == 3 and j == 5:                       # one bad call among them
+                        got[m // 2]["len1"] = 40000
+                        with pytest.raises(bsw.BswError):
+                            e.get_scores(got, ref, qer, w, cb)
+                        bad_seen.append(1)
+                        continue
+                    if k == 5 and j % 3 == 0:                   # scattered: every 3rd pair of a range
+                        got = pairs[a:a + 3 * m:3].copy()       # (extents 3x the bytes: not bulk)
+                        wv = want[a:a + 3 * m:3]
+                    else:
+                        wv = want[a:a + m]
+                    e.get_scores(got, ref, qer, w, cb)
+                    if w == 100:
+                        _assert_same(wv, got, f"caller {k} call {j}")
+                    else:
+                        ref_out = got.copy()
+                        oracle.get_scores(_oparams(), ref_out, ref, qer, w, nthreads=2)
+                        _assert_same(ref_out, got, f"caller {k} call {j} w {w}")
+            except Exception as x:  # noqa: BLE001
+                errs.append(x)
+        th = [threading.Thread(target=caller, args=(k,)) for k in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs[0]
+        assert bad_seen == [1]
+        e.close()

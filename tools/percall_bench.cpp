@@ -1,0 +1,98 @@
+// percall_bench.cpp -- the drop-in regime measured the way upstream calls it: C++ kt_for-style
+// worker threads issuing getScores16-sized host-buffer calls through the C ABI (bsw_get_scores),
+// no Python in the loop.  C2-shaped pairs from libbsw_synth.so (splitmix64, seed 42).
+//   percall_bench [pairs_total] [threads] [sizes...]
+// For every call size: median single-caller latency (1 thread, 200 calls after warm-up) and the
+// aggregate rate of `threads` concurrent callers (each issuing calls back to back over its own
+// slice of the batch for ~0.5 s), once with cross-call coalescing (default) and once without
+// (BSW_OPT_COALESCE = 0); one JSON line on stdout.  Outputs are checked against a whole-batch
+// call (bit-identical required).
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+#include "../include/bsw.h"
+
+extern "C" {
+typedef struct { uint64_t seed; int32_t tlen, qlen, h0_lo, h0_hi; double p_sub, p_indel, p_unrelated, p_n; } synth_cfg;
+void bsw_synth_default(synth_cfg *c);
+void bsw_synth_batch(const synth_cfg *c, int64_t base, int32_t n, SeqPair *pairs, uint8_t *ref, uint8_t *qer);
+}
+
+using Clock = std::chrono::steady_clock;
+static double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+int main(int argc, char **argv)
+{
+    const int32_t N = argc > 1 ? atoi(argv[1]) : 1000000;
+    const int T = argc > 2 ? atoi(argv[2]) : 8;
+    std::vector<int32_t> sizes;
+    for (int k = 3; k < argc; ++k) sizes.push_back(atoi(argv[k]));
+    if (sizes.empty()) sizes = {1000, 10000, 100000};
+    synth_cfg c;
+    bsw_synth_default(&c);
+    std::vector<SeqPair> pairs(N);
+    std::vector<uint8_t> ref((size_t)N * c.tlen), qer((size_t)N * c.qlen);
+    bsw_synth_batch(&c, 0, N, pairs.data(), ref.data(), qer.data());
+    bsw_params_t p;
+    bsw_params_default(&p);
+    bsw_ctx_t *ctx = nullptr;
+    if (bsw_create(&p, 0, 1, &ctx) != BSW_OK) { fprintf(stderr, "bsw_create failed\n"); return 2; }
+    if (const char *l = getenv("PERCALL_LEADERS")) bsw_set_option(ctx, BSW_OPT_COALESCE_LEADERS, atoi(l));
+    std::vector<SeqPair> want = pairs;
+    if (bsw_get_scores(ctx, want.data(), ref.data(), qer.data(), N, 100, 16) != BSW_OK) return 3;
+    printf("{\"tool\": \"percall_bench\", \"threads\": %d, \"pairs\": %d, \"curve\": [", T, N);
+    bool first = true;
+    std::atomic<long> bad{0};
+    for (int co = 1; co >= 0; --co) {
+        bsw_set_option(ctx, BSW_OPT_COALESCE, co ? 32768 : 0);
+        for (int32_t m : sizes) {
+            if (m > N / T) continue;
+            // one caller: median latency
+            std::vector<SeqPair> buf(pairs.begin(), pairs.begin() + m);
+            std::vector<double> lat;
+            for (int k = 0; k < 203; ++k) {
+                const int32_t a = (int32_t)(((int64_t)k * m) % (N - m + 1));
+                std::copy(pairs.begin() + a, pairs.begin() + a + m, buf.begin());
+                const auto t0 = Clock::now();
+                if (bsw_get_scores(ctx, buf.data(), ref.data(), qer.data(), m, 100, 16) != BSW_OK) return 4;
+                if (k >= 3) lat.push_back(secs(t0, Clock::now()));
+                for (int32_t i = 0; i < m; ++i) bad += memcmp(&buf[i].score, &want[a + i].score, 24) != 0;
+            }
+            std::sort(lat.begin(), lat.end());
+            const double med = lat[lat.size() / 2];
+            // T concurrent callers, each over its own contiguous slice, calls back to back
+            std::atomic<long> done{0};
+            std::atomic<bool> stop{false};
+            std::vector<std::thread> th;
+            const int32_t slice = N / T;
+            const auto t0 = Clock::now();
+            for (int t = 0; t < T; ++t)
+                th.emplace_back([&, t] {
+                    std::vector<SeqPair> b(m);
+                    for (int32_t k = 0; !stop.load(std::memory_order_relaxed); ++k) {
+                        const int32_t a = t * slice + (int32_t)(((int64_t)k * m) % (slice - m + 1));
+                        std::copy(pairs.begin() + a, pairs.begin() + a + m, b.begin());
+                        if (bsw_get_scores(ctx, b.data(), ref.data(), qer.data(), m, 100, 16) != BSW_OK) { bad += 1000000; return; }
+                        for (int32_t i = 0; i < m; ++i) bad += memcmp(&b[i].score, &want[a + i].score, 24) != 0;
+                        done.fetch_add(m);
+                        if (secs(t0, Clock::now()) > 0.5) break;
+                    }
+                });
+            for (auto &x : th) x.join();
+            const double dt = secs(t0, Clock::now());
+            printf("%s{\"pairs_per_call\": %d, \"coalescing\": %s, \"latency_ms_median\": %.3f, "
+                   "\"M_pairs_per_s_1_caller\": %.3f, \"M_pairs_per_s_%d_callers\": %.3f}",
+                   first ? "" : ", ", m, co ? "true" : "false", med * 1e3, m / med / 1e6, T, done.load() / dt / 1e6);
+            first = false;
+            fflush(stdout);
+        }
+    }
+    printf("], \"outputs_identical\": %s}\n", bad.load() == 0 ? "true" : "false");
+    bsw_destroy(ctx);
+    return bad.load() == 0 ? 0 : 5;
+}
