@@ -350,7 +350,8 @@ def main():
     ap.add_argument("--total-pairs", type=int, default=10_000_000, help="strong: pairs in the whole batch")
     ap.add_argument("--rehearse", action="store_true",
                     help="allow more ranks than visible GPUs (ranks share GPUs; rehearsal only)")
-    ap.add_argument("--dump", default="", help="strong: rank 0 writes the gathered outputs here (.npy)")
+    ap.add_argument("--dump", default="", help="strong: rank 0 writes the gathered outputs here (.npy); c4 / "
+                                               "c4mem: every rank writes <dump>.rank<r>.npz")
     args = ap.parse_args()
 
     rank, local, world = dist_init()
@@ -736,6 +737,8 @@ def main_c4pe(args, rank, local, world):
     n_ext_all = allreduce_sum(n_ext, world)
     out = d_out.download(out_buf)
     ext = d_ext.download(ext_buf)
+    if args.dump:                                    # every rank: its shard's regions (tests)
+        np.savez(f"{args.dump}.rank{rank}.npz", out=out, ext=ext)
     # the host-array form (bsw_chain2aln_device: seeds up, regions down inside the call)
     t = time.perf_counter()
     for _ in range(2):
@@ -900,13 +903,15 @@ def main_mem(args, rank, local, world, c1: bool):
     dt = time.perf_counter() - t
     dt_max = allreduce_max(dt, world)
     n_ext_all = allreduce_sum(n_ext, world)
-    if rank != 0:
-        return
     seeds = bufs["seeds"].download(np.zeros(ns, dtype=bsw.SEED_DTYPE))
     sr = bufs["sr"].download(np.zeros(ns, dtype=np.int32))
     sc = bufs["sc"].download(np.zeros(ns, dtype=np.int32))
     out = bufs["out"].download(np.zeros(ns, dtype=bsw.ALNREG_DTYPE))
     ext = bufs["ext"].download(np.zeros(ns, dtype=np.int32))
+    if args.dump:                                    # every rank: its shard's seeds and regions (tests)
+        np.savez(f"{args.dump}.rank{rank}.npz", seeds=seeds, sr=sr, sc=sc, out=out, ext=ext)
+    if rank != 0:
+        return
     st = sts[-1]
     pm = np.mean(np.array(parts), axis=0) * 1e3
     reads_s = n * world * args.steps / dt_max / 1e6

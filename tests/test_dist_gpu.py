@@ -51,3 +51,48 @@ def test_ranks_strong_split_equal_oracle(tmp_path, world):
     oracle.get_scores(oracle.make_params(), want, ref, qer, 100, nthreads=16)
     for f in ("len1", "len2", "h0") + bsw.OUT_FIELDS:
         assert np.array_equal(got[f], want[f]), f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["c4", "c4mem"])
+def test_ranks_c4_pe_workload_equal_oracle(tmp_path, workload):
+    """The C4 / C5 workload (paired-end reads; c4: ground-truth seed chains through
+    mem_chain2aln, c4mem: the whole GPU front end -- SMEM seeding, chaining, mem_chain2aln)
+    under a 2-rank torchrun rehearsal on the box's one GPU: every rank's shard of reads
+    (its own pair_base / read seed) equals the oracle run on that shard."""
+    world, reads = 2, 20_000
+    dump = str(tmp_path / "c4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--workload", workload, "--reads", str(reads),
+           "--ref-mb", "4", "--steps", "1", "--warmup", "1", "--rehearse", "--no-cpu", "--dump", dump]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == world
+    import bench
+    import hiprt  # noqa: F401
+    ref = bsw.synth_reference(4_000_000, seed=7)
+    P = oracle.make_params()
+    for rank in range(world):
+        z = np.load(f"{dump}.rank{rank}.npz")
+        if workload == "c4":
+            npairs = reads // 2
+            rd, off, lens, seeds, sr, sc = bsw.synth_pe_seeds(ref, npairs, pair_base=rank * npairs)
+            want, wext = oracle.chain2aln(P, bsw.ext_opt(), ref, rd, off, lens, seeds, sr, sc, nthreads=8)
+        else:
+            nb = ref > 3
+            ref2 = ref.copy()
+            ref2[nb] = np.random.default_rng(1).integers(0, 4, int(nb.sum()), dtype=np.uint8)
+            rd, off, lens = bench.pe_reads(ref2, reads // 2, seed=42 + rank)
+            f = oracle.FmiRef(ref2)
+            mems, cnt = f.collect_intv(rd, off, lens, cap=256, nthreads=8)
+            seeds, sr, sc = oracle.mem_chain(f.sa(), len(ref2), lens, mems, cnt)
+            assert np.array_equal(z["sr"], sr) and np.array_equal(z["sc"], sc)
+            assert np.array_equal(z["seeds"]["rbeg"], seeds["rbeg"])
+            T = np.concatenate([ref2, 3 - ref2[::-1]]).astype(np.uint8)
+            want, wext = oracle.chain2aln(P, bsw.ext_opt(l_pac=len(ref2)), T, rd, off, lens, seeds, sr, sc, nthreads=8)
+        assert np.array_equal(z["ext"], wext), f"rank {rank}"
+        for fld in bsw.ALNREG_DTYPE.names:
+            assert np.array_equal(z["out"][fld], want[fld]), (rank, fld)
