@@ -36,18 +36,15 @@
 
 namespace {
 
-struct alignas(64) FmiBlock {
-    uint32_t cnt[4];
-    uint32_t pad[4];
-    uint64_t bits[4];
-};
-static_assert(sizeof(FmiBlock) == 64, "one 64-byte block per 64 rows");
+using bsw::FmiBlock;
+using bsw::FmiBlockW;
 
-struct FmiDev {                      // kernel view of the resident index
-    const FmiBlock *blk;
-    uint32_t count[5];
-    uint32_t sentinel;
-    uint32_t n;                      // |T|
+template <class U>
+struct FmiDevT {                     // kernel view of the resident index (U = row / count width)
+    const void *blk;
+    U count[5];
+    U sentinel;
+    U n;                             // |T|
 };
 
 struct MemOpt {
@@ -56,80 +53,104 @@ struct MemOpt {
 
 // ---------------------------------------------------------------- device: index queries
 
-__device__ __forceinline__ void load_block(const FmiBlock *b, uint4 &cnt, ulonglong2 &b01, ulonglong2 &b23)
+template <class U>
+struct Occ4 {                        // one block: the running counts and the four masks
+    U c[4];
+    uint64_t b[4];
+};
+
+__device__ __forceinline__ void load_block(const void *blk, uint32_t bi, Occ4<uint32_t> &o)
 {
-    const uint4 *p = reinterpret_cast<const uint4 *>(b);
-    cnt = p[0];
-    b01 = reinterpret_cast<const ulonglong2 *>(b)[2];
-    b23 = reinterpret_cast<const ulonglong2 *>(b)[3];
+    const FmiBlock *b = (const FmiBlock *)blk + bi;
+    const uint4 cnt = *reinterpret_cast<const uint4 *>(b);
+    const ulonglong2 b01 = reinterpret_cast<const ulonglong2 *>(b)[2];
+    const ulonglong2 b23 = reinterpret_cast<const ulonglong2 *>(b)[3];
+    o.c[0] = cnt.x; o.c[1] = cnt.y; o.c[2] = cnt.z; o.c[3] = cnt.w;
+    o.b[0] = b01.x; o.b[1] = b01.y; o.b[2] = b23.x; o.b[3] = b23.y;
+}
+__device__ __forceinline__ void load_block(const void *blk, uint64_t bi, Occ4<uint64_t> &o)
+{
+    const FmiBlockW *b = (const FmiBlockW *)blk + bi;
+    const ulonglong2 c01 = reinterpret_cast<const ulonglong2 *>(b)[0];
+    const ulonglong2 c23 = reinterpret_cast<const ulonglong2 *>(b)[1];
+    const ulonglong2 b01 = reinterpret_cast<const ulonglong2 *>(b)[2];
+    const ulonglong2 b23 = reinterpret_cast<const ulonglong2 *>(b)[3];
+    o.c[0] = c01.x; o.c[1] = c01.y; o.c[2] = c23.x; o.c[3] = c23.y;
+    o.b[0] = b01.x; o.b[1] = b01.y; o.b[2] = b23.x; o.b[3] = b23.y;
 }
 
-__device__ __forceinline__ uint32_t occ_of(const uint4 &cnt, const ulonglong2 &b01, const ulonglong2 &b23,
-                                           int c, uint64_t mask)
+template <class U>
+__device__ __forceinline__ U occ_of(const Occ4<U> &o, int c, uint64_t mask)
 {
-    const uint32_t cc = c == 0 ? cnt.x : c == 1 ? cnt.y : c == 2 ? cnt.z : cnt.w;
-    const uint64_t bb = c == 0 ? b01.x : c == 1 ? b01.y : c == 2 ? b23.x : b23.y;
-    return cc + (uint32_t)__builtin_popcountll(bb & mask);
+    const U cc = c == 0 ? o.c[0] : c == 1 ? o.c[1] : c == 2 ? o.c[2] : o.c[3];
+    const uint64_t bb = c == 0 ? o.b[0] : c == 1 ? o.b[1] : c == 2 ? o.b[2] : o.b[3];
+    return cc + (U)__builtin_popcountll(bb & mask);
 }
 
-struct Iv {
-    uint32_t k, l, s;
+template <class U>
+struct IvT {
+    U k, l, s;
 };
 
 // FMI_search::backwardExt restricted to the one base the caller keeps
-__device__ __forceinline__ Iv backward_ext(const FmiDev &f, Iv in, int a)
+template <class U>
+__device__ __forceinline__ IvT<U> backward_ext(const FmiDevT<U> &f, IvT<U> in, int a)
 {
-    const uint32_t sp = in.k, ep = in.k + in.s;
-    uint4 c0, c1;
-    ulonglong2 a01, a23, e01, e23;
-    load_block(f.blk + (sp >> 6), c0, a01, a23);
-    if ((ep >> 6) == (sp >> 6)) {
-        c1 = c0; e01 = a01; e23 = a23;
-    } else {
-        load_block(f.blk + (ep >> 6), c1, e01, e23);
-    }
+    const U sp = in.k, ep = in.k + in.s;
+    Occ4<U> o0, o1;
+    load_block(f.blk, sp >> 6, o0);
+    if ((ep >> 6) == (sp >> 6)) o1 = o0;
+    else load_block(f.blk, ep >> 6, o1);
     const uint64_t ms = (sp & 63) ? (~0ull >> (64 - (sp & 63))) : 0ull;
     const uint64_t me = (ep & 63) ? (~0ull >> (64 - (ep & 63))) : 0ull;
-    uint32_t osp[4], oep[4];
+    U osp[4], oep[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-        osp[b] = occ_of(c0, a01, a23, b, ms);
-        oep[b] = occ_of(c1, e01, e23, b, me);
+        osp[b] = occ_of(o0, b, ms);
+        oep[b] = occ_of(o1, b, me);
     }
-    uint32_t l = in.l + ((sp <= f.sentinel && ep > f.sentinel) ? 1u : 0u);
+    U l = in.l + ((sp <= f.sentinel && ep > f.sentinel) ? (U)1 : (U)0);
     // l[3] = l + sent; l[b] = l[b + 1] + s[b + 1]
 #pragma unroll
     for (int b = 3; b > 0; --b)
         if (b > a) l += oep[b] - osp[b];
-    Iv o;
-    const uint32_t ca = a == 0 ? f.count[0] : a == 1 ? f.count[1] : a == 2 ? f.count[2] : f.count[3];
-    const uint32_t oa = a == 0 ? osp[0] : a == 1 ? osp[1] : a == 2 ? osp[2] : osp[3];
-    const uint32_t ea = a == 0 ? oep[0] : a == 1 ? oep[1] : a == 2 ? oep[2] : oep[3];
+    IvT<U> o;
+    const U ca = a == 0 ? f.count[0] : a == 1 ? f.count[1] : a == 2 ? f.count[2] : f.count[3];
+    const U oa = a == 0 ? osp[0] : a == 1 ? osp[1] : a == 2 ? osp[2] : osp[3];
+    const U ea = a == 0 ? oep[0] : a == 1 ? oep[1] : a == 2 ? oep[2] : oep[3];
     o.k = ca + oa;
     o.s = ea - oa;
     o.l = l;
     return o;
 }
 
-__device__ __forceinline__ Iv forward_ext(const FmiDev &f, Iv in, int q)   // q = read base 0..3
+template <class U>
+__device__ __forceinline__ IvT<U> forward_ext(const FmiDevT<U> &f, IvT<U> in, int q)   // q = read base 0..3
 {
-    Iv sw = {in.l, in.k, in.s};
-    Iv o = backward_ext(f, sw, 3 - q);
-    return Iv{o.l, o.k, o.s};
+    IvT<U> sw = {in.l, in.k, in.s};
+    IvT<U> o = backward_ext(f, sw, 3 - q);
+    return IvT<U>{o.l, o.k, o.s};
 }
 
-__device__ __forceinline__ Iv set_intv(const FmiDev &f, int c)
+template <class U>
+__device__ __forceinline__ IvT<U> set_intv(const FmiDevT<U> &f, int c)
 {
-    const uint32_t k = f.count[c], k1 = f.count[c + 1], l = f.count[3 - c];
-    return Iv{k, l, k1 - k};
+    const U k = f.count[c], k1 = f.count[c + 1], l = f.count[3 - c];
+    return IvT<U>{k, l, k1 - k};
 }
 
 // ---------------------------------------------------------------- device: per-read passes
 
+template <class U>
+struct alignas(16) EntT {            // one interval-vector entry: (k, l, s) and the match end
+    U k, l, s, e;
+};
+
+template <class U>
 struct Lane {
     const uint8_t *q;
     int len;
-    uint4 *sa, *sb;          // scratch vectors, element j at [j * stride]
+    EntT<U> *sa, *sb;        // scratch vectors, element j at [j * stride]
     size_t stride;
     int scap;                // scratch entries per vector
     bsw_bwtintv_t *out;      // this read's output slots
@@ -138,7 +159,8 @@ struct Lane {
     int overflow;            // scratch overflow (cannot happen for scap >= len + 1)
 };
 
-__device__ __forceinline__ void push_out(Lane &L, Iv v, uint32_t start, uint32_t end)
+template <class U>
+__device__ __forceinline__ void push_out(Lane<U> &L, IvT<U> v, uint32_t start, uint32_t end)
 {
     if (L.nout < L.cap) {
         bsw_bwtintv_t o;
@@ -151,45 +173,46 @@ __device__ __forceinline__ void push_out(Lane &L, Iv v, uint32_t start, uint32_t
 
 // bwt_smem1a with max_intv = 0 (bwt_smem1): SMEMs overlapping x with occurrence >= min_intv;
 // those of length >= keep_len go to the output.  Returns the next x.
-__device__ int smem1(const FmiDev &f, Lane &L, int x, uint32_t min_intv, int keep_len)
+template <class U>
+__device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int keep_len)
 {
     const uint8_t *q = L.q;
     const int len = L.len;
     const int qx = q[x];
     if (qx > 3) return x + 1;
     if (min_intv < 1) min_intv = 1;
-    uint4 *curr = L.sa, *prev = L.sb;
+    EntT<U> *curr = L.sa, *prev = L.sb;
     const size_t st = L.stride;
-    Iv ik = set_intv(f, qx);
-    uint32_t ikend = (uint32_t)(x + 1);
+    IvT<U> ik = set_intv(f, qx);
+    U ikend = (U)(x + 1);
     int nc = 0, i;
     for (i = x + 1; i < len; ++i) {                      // forward search
         const int qi = q[i];
         if (qi < 4) {
-            const Iv ok = forward_ext(f, ik, qi);
+            const IvT<U> ok = forward_ext(f, ik, qi);
             if (ok.s != ik.s) {
-                if (nc < L.scap) curr[(size_t)nc * st] = make_uint4(ik.k, ik.l, ik.s, ikend);
+                if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
                 else L.overflow = 1;
                 ++nc;
                 if (ok.s < min_intv) break;
             }
-            ik = ok; ikend = (uint32_t)(i + 1);
+            ik = ok; ikend = (U)(i + 1);
         } else {
-            if (nc < L.scap) curr[(size_t)nc * st] = make_uint4(ik.k, ik.l, ik.s, ikend);
+            if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
             else L.overflow = 1;
             ++nc;
             break;
         }
     }
     if (i == len) {
-        if (nc < L.scap) curr[(size_t)nc * st] = make_uint4(ik.k, ik.l, ik.s, ikend);
+        if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
         else L.overflow = 1;
         ++nc;
     }
     nc = min(nc, L.scap);
     // upstream reverses curr (longest matches first); here prev is read back to front once
-    const int ret = (int)curr[(size_t)(nc - 1) * st].w;
-    { uint4 *t = curr; curr = prev; prev = t; }
+    const int ret = (int)curr[(size_t)(nc - 1) * st].e;
+    { EntT<U> *t = curr; curr = prev; prev = t; }
     int np = nc;
     bool rev = true;
     int nmem = 0;
@@ -197,22 +220,22 @@ __device__ int smem1(const FmiDev &f, Lane &L, int x, uint32_t min_intv, int kee
     for (i = x - 1; i >= -1; --i) {                      // backward search
         const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
         nc = 0;
-        uint32_t last_cs = 0;
+        U last_cs = 0;
         for (int j = 0; j < np; ++j) {
-            const uint4 pv = prev[(size_t)(rev ? np - 1 - j : j) * st];
-            const Iv p = {pv.x, pv.y, pv.z};
-            Iv ok = {0, 0, 0};
+            const EntT<U> pv = prev[(size_t)(rev ? np - 1 - j : j) * st];
+            const IvT<U> p = {pv.k, pv.l, pv.s};
+            IvT<U> ok = {0, 0, 0};
             if (c >= 0) ok = backward_ext(f, p, c);
             if (c < 0 || ok.s < min_intv) {
                 if (nc == 0) {
                     if (nmem == 0 || (uint32_t)(i + 1) < last_start) {
                         last_start = (uint32_t)(i + 1);
                         ++nmem;
-                        if ((int)(pv.w - last_start) >= keep_len) push_out(L, p, last_start, pv.w);
+                        if ((int)((uint32_t)pv.e - last_start) >= keep_len) push_out(L, p, last_start, (uint32_t)pv.e);
                     }
                 }
             } else if (nc == 0 || ok.s != last_cs) {
-                if (nc < L.scap) curr[(size_t)nc * st] = make_uint4(ok.k, ok.l, ok.s, pv.w);
+                if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ok.k, ok.l, ok.s, pv.e};
                 else L.overflow = 1;
                 ++nc;
                 last_cs = ok.s;
@@ -221,22 +244,23 @@ __device__ int smem1(const FmiDev &f, Lane &L, int x, uint32_t min_intv, int kee
         if (nc == 0) break;
         np = min(nc, L.scap);
         rev = false;
-        { uint4 *t = curr; curr = prev; prev = t; }
+        { EntT<U> *t = curr; curr = prev; prev = t; }
     }
     return ret;
 }
 
 // bwt_seed_strategy1
-__device__ int seed_strategy1(const FmiDev &f, Lane &L, int x, int min_len, uint32_t max_intv)
+template <class U>
+__device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U> &L, int x, int min_len, U max_intv)
 {
     const uint8_t *q = L.q;
     const int qx = q[x];
     if (qx > 3) return x + 1;
-    Iv ik = set_intv(f, qx);
+    IvT<U> ik = set_intv(f, qx);
     for (int i = x + 1; i < L.len; ++i) {
         const int qi = q[i];
         if (qi < 4) {
-            const Iv ok = forward_ext(f, ik, qi);
+            const IvT<U> ok = forward_ext(f, ik, qi);
             if (ok.s < max_intv && i - x >= min_len) {
                 if (ok.s > 0) push_out(L, ok, (uint32_t)x, (uint32_t)(i + 1));
                 return i + 1;
@@ -262,13 +286,14 @@ __device__ __forceinline__ bool iv_less(const bsw_bwtintv_t &a, const bsw_bwtint
 // writes them: a per-lane state machine doing one extension per iteration (so that a wave's time
 // is its busiest lane's work instead of the sum of per-phase maxima) measured 1.4x SLOWER (31.9
 // vs 22.1 ms on 1M reads x 16 Mb) -- the bookkeeping transitions cost whole iterations.
-__device__ int smem_read(const FmiDev &f, const MemOpt &opt, const uint8_t *__restrict__ reads,
+template <class U>
+__device__ int smem_read(const FmiDevT<U> &f, const MemOpt &opt, const uint8_t *__restrict__ reads,
                          const int64_t *__restrict__ read_off, const int32_t *__restrict__ read_len, int32_t n0,
-                         int32_t n, int t, uint4 *__restrict__ scratch, int32_t scap, bsw_bwtintv_t *__restrict__ mems,
-                         int32_t cap, int32_t *__restrict__ n_mems)
+                         int32_t n, int t, EntT<U> *__restrict__ scratch, int32_t scap,
+                         bsw_bwtintv_t *__restrict__ mems, int32_t cap, int32_t *__restrict__ n_mems)
 {
     const int r = n0 + t;                                    // read index
-    Lane L;
+    Lane<U> L;
     L.q = reads + read_off[r];
     L.len = read_len[r];
     L.stride = (size_t)n;
@@ -286,7 +311,7 @@ __device__ int smem_read(const FmiDev &f, const MemOpt &opt, const uint8_t *__re
     // pass 1: SMEMs
     int x = 0;
     while (x < L.len) {
-        if (L.q[x] < 4) x = smem1(f, L, x, 1, opt.min_seed_len);
+        if (L.q[x] < 4) x = smem1(f, L, x, (U)1, opt.min_seed_len);
         else ++x;
     }
     // pass 2: re-seeding inside long SMEMs of few occurrences
@@ -295,13 +320,13 @@ __device__ int smem_read(const FmiDev &f, const MemOpt &opt, const uint8_t *__re
         const bsw_bwtintv_t p = L.out[k];
         const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
         if (end - start < opt.split_len || p.x[2] > (uint64_t)opt.split_width) continue;
-        smem1(f, L, (start + end) >> 1, (uint32_t)p.x[2] + 1, opt.min_seed_len);
+        smem1(f, L, (start + end) >> 1, (U)(p.x[2] + 1), opt.min_seed_len);
     }
     // pass 3: LAST-like seeds
     if (opt.max_mem_intv > 0) {
         x = 0;
         while (x < L.len) {
-            if (L.q[x] < 4) x = seed_strategy1(f, L, x, opt.min_seed_len, (uint32_t)opt.max_mem_intv);
+            if (L.q[x] < 4) x = seed_strategy1(f, L, x, opt.min_seed_len, (U)opt.max_mem_intv);
             else ++x;
         }
     }
@@ -320,10 +345,12 @@ __device__ int smem_read(const FmiDev &f, const MemOpt &opt, const uint8_t *__re
     return (L.nout > cap ? 1 : 0) | (L.overflow ? 2 : 0);
 }
 
-__global__ __launch_bounds__(64) void smem_kernel(const FmiDev f, const MemOpt opt, const uint8_t *__restrict__ reads,
+template <class U>
+__global__ __launch_bounds__(64) void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
+                                                  const uint8_t *__restrict__ reads,
                                                   const int64_t *__restrict__ read_off,
                                                   const int32_t *__restrict__ read_len, int32_t n0, int32_t n,
-                                                  uint4 *__restrict__ scratch, int32_t scap,
+                                                  EntT<U> *__restrict__ scratch, int32_t scap,
                                                   bsw_bwtintv_t *__restrict__ mems, int32_t cap,
                                                   int32_t *__restrict__ n_mems, int32_t *__restrict__ err)
 {
@@ -333,8 +360,9 @@ __global__ __launch_bounds__(64) void smem_kernel(const FmiDev f, const MemOpt o
     if (e) atomicOr(err, e);
 }
 
-__global__ void sa_kernel(const uint32_t *__restrict__ sa, uint32_t nrows, const uint64_t *__restrict__ k,
-                          int64_t n, int64_t *__restrict__ pos)
+template <class S>
+__global__ void sa_kernel(const S *__restrict__ sa, uint64_t nrows, const uint64_t *__restrict__ k, int64_t n,
+                          int64_t *__restrict__ pos)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -422,19 +450,25 @@ void build_sa(const uint8_t *t, uint32_t n, std::vector<uint32_t> &sa)
 
 struct bsw_fmi {
     int device = 0;
-    uint32_t n = 0;
-    FmiDev dv{};
-    FmiBlock *d_blk = nullptr;
-    uint32_t *d_sa = nullptr;
-    std::vector<uint32_t> sa;                 // host copies (tests, bwt_sa on the host side)
+    int64_t n = 0;                            // |T|
+    bool wide = false;                        // 64-bit rows / counts / suffix array
+    bool gpu_built = false;
+    FmiDevT<uint32_t> dv32{};
+    FmiDevT<uint64_t> dv64{};
+    void *d_blk = nullptr;                    // FmiBlock (narrow) or FmiBlockW (wide)
+    void *d_sa = nullptr;                     // uint32_t (narrow) or uint64_t (wide)
+    uint8_t *d_bwt = nullptr;                 // GPU-built index: BWT codes (copy_bwt)
+    std::vector<uint32_t> sa;                 // host-built index: host copies (tests, bwt_sa)
     std::vector<FmiBlock> h_blk;              // host-only index (device < 0): the occurrence blocks
     std::vector<uint8_t> bwt;
     int64_t count[5] = {0, 0, 0, 0, 0};
+    int64_t sentinel = 0;
     int64_t dev_bytes = 0;
+    int64_t tie_groups = 0;
     float build_s = 0, kernel_ms = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    uint4 *d_scratch = nullptr;
+    void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
     int32_t *d_err = nullptr;
     void *h_stage = nullptr;                  // host-buffer calls: device copies
@@ -445,7 +479,7 @@ int bsw::fmi_view(bsw_fmi_t *f, FmiView *out)
 {
     if (!f) return BSW_E_INVAL;
     if (f->device < 0) return BSW_E_NODEV;
-    *out = FmiView{f->device, f->d_sa, (int64_t)f->n, (int64_t)f->n / 2, f->stream, &f->mu};
+    *out = FmiView{f->device, f->d_sa, f->wide, f->n, f->n / 2, f->stream, &f->mu};
     return BSW_OK;
 }
 
@@ -453,19 +487,15 @@ namespace {
 
 int hip_rc(hipError_t e) { return e == hipSuccess ? BSW_OK : (e == hipErrorOutOfMemory ? BSW_E_NOMEM : BSW_E_HIP); }
 
-int run_collect(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads, const int64_t *d_off,
-                const int32_t *d_len, int32_t n, int32_t max_len, bsw_bwtintv_t *d_mems, int32_t cap,
-                int32_t *d_cnt, hipStream_t s)
+template <class U>
+int launch_collect(bsw_fmi_t *f, const FmiDevT<U> &dv, const MemOpt &mo, const uint8_t *d_reads, const int64_t *d_off,
+                   const int32_t *d_len, int32_t n, int32_t max_len, bsw_bwtintv_t *d_mems, int32_t cap,
+                   int32_t *d_cnt, hipStream_t s)
 {
-    MemOpt mo;
-    mo.min_seed_len = opt->min_seed_len;
-    mo.split_width = opt->split_width;
-    mo.max_mem_intv = opt->max_mem_intv;
-    mo.split_len = (int)(opt->min_seed_len * opt->split_factor + .499);
     const int32_t scap = max_len + 1;
     // chunk so the two scratch vectors stay within 16 GB (of 288 GB: one launch for up to ~3M
-    // 151-bp reads)
-    const size_t per_read = (size_t)2 * scap * sizeof(uint4);
+    // 151-bp reads with 16-byte entries, ~1.5M with the wide index's 32-byte ones)
+    const size_t per_read = (size_t)2 * scap * sizeof(EntT<U>);
     const int32_t chunk = (int32_t)std::max<size_t>(64, std::min<size_t>((size_t)n, ((size_t)16 << 30) / per_read));
     const size_t need = per_read * (size_t)std::min(chunk, n);
     if (need > f->scratch_bytes) {
@@ -479,8 +509,8 @@ int run_collect(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads, 
     (void)hipEventRecord(f->ev0, s);
     for (int32_t n0 = 0; n0 < n; n0 += chunk) {
         const int32_t m = std::min(chunk, n - n0);
-        hipLaunchKernelGGL(smem_kernel, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, f->dv, mo, d_reads, d_off,
-                           d_len, n0, m, f->d_scratch, scap, d_mems, cap, d_cnt, f->d_err);
+        hipLaunchKernelGGL(smem_kernel<U>, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, dv, mo, d_reads, d_off,
+                           d_len, n0, m, (EntT<U> *)f->d_scratch, scap, d_mems, cap, d_cnt, f->d_err);
         if (hipGetLastError() != hipSuccess) return BSW_E_HIP;
     }
     (void)hipEventRecord(f->ev1, s);
@@ -489,6 +519,41 @@ int run_collect(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads, 
     if (hipStreamSynchronize(s) != hipSuccess) return BSW_E_HIP;
     (void)hipEventElapsedTime(&f->kernel_ms, f->ev0, f->ev1);
     return herr ? BSW_E_RANGE : BSW_OK;
+}
+
+int run_collect(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads, const int64_t *d_off,
+                const int32_t *d_len, int32_t n, int32_t max_len, bsw_bwtintv_t *d_mems, int32_t cap,
+                int32_t *d_cnt, hipStream_t s)
+{
+    MemOpt mo;
+    mo.min_seed_len = opt->min_seed_len;
+    mo.split_width = opt->split_width;
+    mo.max_mem_intv = opt->max_mem_intv;
+    mo.split_len = (int)(opt->min_seed_len * opt->split_factor + .499);
+    return f->wide ? launch_collect(f, f->dv64, mo, d_reads, d_off, d_len, n, max_len, d_mems, cap, d_cnt, s)
+                   : launch_collect(f, f->dv32, mo, d_reads, d_off, d_len, n, max_len, d_mems, cap, d_cnt, s);
+}
+
+// the runtime objects every device index needs
+int finish_device_index(bsw_fmi_t *f)
+{
+    int rc = BSW_OK;
+    if ((rc = hip_rc(hipMalloc(&f->d_err, sizeof(int32_t)))) == BSW_OK &&
+        (rc = hip_rc(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking))) == BSW_OK &&
+        (rc = hip_rc(hipEventCreate(&f->ev0))) == BSW_OK && (rc = hip_rc(hipEventCreate(&f->ev1))) == BSW_OK) {
+        if (f->wide) {
+            f->dv64.blk = f->d_blk;
+            for (int c = 0; c < 5; ++c) f->dv64.count[c] = (uint64_t)f->count[c];
+            f->dv64.sentinel = (uint64_t)f->sentinel;
+            f->dv64.n = (uint64_t)f->n;
+        } else {
+            f->dv32.blk = f->d_blk;
+            for (int c = 0; c < 5; ++c) f->dv32.count[c] = (uint32_t)f->count[c];
+            f->dv32.sentinel = (uint32_t)f->sentinel;
+            f->dv32.n = (uint32_t)f->n;
+        }
+    }
+    return rc;
 }
 
 }  // namespace
@@ -503,16 +568,42 @@ void bsw_mem_opt_default(bsw_mem_opt_t *opt)
     opt->split_factor = 1.5f;
 }
 
-int bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **out)
+int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, bsw_fmi_t **out)
 {
-    if (!out || (!ref && ref_len > 0) || ref_len < 0) return BSW_E_INVAL;
+    if (!out || (!ref && ref_len > 0) || ref_len < 0 || (flags & ~3)) return BSW_E_INVAL;
     *out = nullptr;
-    if (2 * ref_len + 2 >= (int64_t)UINT32_MAX) return BSW_E_RANGE;
     for (int64_t i = 0; i < ref_len; ++i)
         if (ref[i] > 3) return BSW_E_INVAL;
+    const bool need_wide = 2 * ref_len + 2 >= (int64_t)UINT32_MAX;
+    const bool wide = need_wide || (flags & BSW_FMI_WIDE);
+    const bool gpu = wide || (flags & BSW_FMI_GPU_BUILD) || ref_len >= ((int64_t)64 << 20);
     int ndev = 0;
     if (device >= 0 && (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev)) return BSW_E_NODEV;
+    if (gpu && device < 0) return need_wide ? BSW_E_RANGE : BSW_E_INVAL;
     const auto t0 = std::chrono::steady_clock::now();
+    if (gpu) {
+        bsw::GpuIndex g;
+        const int rc = bsw::fmi_build_gpu(ref, ref_len, device, wide, &g);
+        if (rc) return rc;
+        bsw_fmi_t *f = new bsw_fmi_t;
+        f->device = device;
+        f->n = g.n;
+        f->wide = wide;
+        f->gpu_built = true;
+        f->d_sa = g.d_sa;
+        f->d_blk = g.d_blk;
+        f->d_bwt = g.d_bwt;
+        f->sentinel = g.sentinel;
+        f->tie_groups = g.tie_groups;
+        for (int c = 0; c < 5; ++c) f->count[c] = g.count[c];
+        const int64_t N = f->n + 1, nb = (N >> 6) + 1;
+        f->dev_bytes = nb * 64 + N * (int64_t)(wide ? sizeof(uint64_t) : sizeof(uint32_t)) + N;
+        f->build_s = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
+        const int r2 = finish_device_index(f);
+        if (r2) { bsw_fmi_destroy(f); return r2; }
+        *out = f;
+        return BSW_OK;
+    }
     const uint32_t n = (uint32_t)(2 * ref_len), N = n + 1;
     std::vector<uint8_t> t(n);
     for (int64_t i = 0; i < ref_len; ++i) {
@@ -547,12 +638,13 @@ int bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **o
     f->count[0] = 1;
     for (int c = 0; c < 4; ++c) f->count[c + 1] = f->count[c] + run[c];
     f->build_s = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
-    f->dv.sentinel = sentinel;
-    f->dv.n = n;
+    f->sentinel = sentinel;
     if (device < 0) {                        // host-only index (tests of the builder): no HBM copy
         f->h_blk.swap(blk);
-        f->dv.blk = f->h_blk.data();
-        for (int c = 0; c < 5; ++c) f->dv.count[c] = (uint32_t)f->count[c];
+        f->dv32.blk = f->h_blk.data();
+        for (int c = 0; c < 5; ++c) f->dv32.count[c] = (uint32_t)f->count[c];
+        f->dv32.sentinel = sentinel;
+        f->dv32.n = n;
         *out = f;
         return BSW_OK;
     }
@@ -560,14 +652,10 @@ int bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **o
     if ((rc = hip_rc(hipSetDevice(device))) == BSW_OK &&
         (rc = hip_rc(hipMalloc(&f->d_blk, nb * sizeof(FmiBlock)))) == BSW_OK &&
         (rc = hip_rc(hipMalloc(&f->d_sa, (size_t)N * sizeof(uint32_t)))) == BSW_OK &&
-        (rc = hip_rc(hipMalloc(&f->d_err, sizeof(int32_t)))) == BSW_OK &&
         (rc = hip_rc(hipMemcpy(f->d_blk, blk.data(), nb * sizeof(FmiBlock), hipMemcpyHostToDevice))) == BSW_OK &&
         (rc = hip_rc(hipMemcpy(f->d_sa, f->sa.data(), (size_t)N * sizeof(uint32_t), hipMemcpyHostToDevice))) == BSW_OK &&
-        (rc = hip_rc(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking))) == BSW_OK &&
-        (rc = hip_rc(hipEventCreate(&f->ev0))) == BSW_OK && (rc = hip_rc(hipEventCreate(&f->ev1))) == BSW_OK) {
+        (rc = finish_device_index(f)) == BSW_OK) {
         f->dev_bytes = (int64_t)(nb * sizeof(FmiBlock) + (size_t)N * sizeof(uint32_t));
-        f->dv.blk = f->d_blk;
-        for (int c = 0; c < 5; ++c) f->dv.count[c] = (uint32_t)f->count[c];
         *out = f;
         return BSW_OK;
     }
@@ -575,12 +663,18 @@ int bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **o
     return rc;
 }
 
+int bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **out)
+{
+    return bsw_fmi_build2(ref, ref_len, device, 0, out);
+}
+
 void bsw_fmi_destroy(bsw_fmi_t *f)
 {
     if (!f) return;
-    (void)hipSetDevice(f->device);
+    if (f->device >= 0) (void)hipSetDevice(f->device);
     if (f->d_blk) (void)hipFree(f->d_blk);
     if (f->d_sa) (void)hipFree(f->d_sa);
+    if (f->d_bwt) (void)hipFree(f->d_bwt);
     if (f->d_err) (void)hipFree(f->d_err);
     if (f->d_scratch) (void)hipFree(f->d_scratch);
     if (f->ev0) (void)hipEventDestroy(f->ev0);
@@ -593,7 +687,7 @@ int bsw_fmi_get_info(const bsw_fmi_t *f, bsw_fmi_info_t *out)
 {
     if (!f || !out) return BSW_E_INVAL;
     out->n = f->n;
-    out->sentinel = f->dv.sentinel;
+    out->sentinel = f->sentinel;
     for (int c = 0; c < 5; ++c) out->count[c] = f->count[c];
     out->device_bytes = f->dev_bytes;
     out->build_s = f->build_s;
@@ -603,15 +697,28 @@ int bsw_fmi_get_info(const bsw_fmi_t *f, bsw_fmi_info_t *out)
 int bsw_fmi_copy_sa(const bsw_fmi_t *f, int64_t *sa)
 {
     if (!f || !sa) return BSW_E_INVAL;
-    for (size_t r = 0; r < f->sa.size(); ++r) sa[r] = f->sa[r];
-    return BSW_OK;
+    if (!f->gpu_built) {
+        for (size_t r = 0; r < f->sa.size(); ++r) sa[r] = f->sa[r];
+        return BSW_OK;
+    }
+    const size_t N = (size_t)f->n + 1;
+    if (hipSetDevice(f->device) != hipSuccess) return BSW_E_HIP;
+    if (f->wide) return hip_rc(hipMemcpy(sa, f->d_sa, N * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> t(N);
+    const int rc = hip_rc(hipMemcpy(t.data(), f->d_sa, N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (size_t r = 0; r < N && !rc; ++r) sa[r] = t[r];
+    return rc;
 }
 
 int bsw_fmi_copy_bwt(const bsw_fmi_t *f, uint8_t *bwt)
 {
     if (!f || !bwt) return BSW_E_INVAL;
-    memcpy(bwt, f->bwt.data(), f->bwt.size());
-    return BSW_OK;
+    if (!f->gpu_built) {
+        memcpy(bwt, f->bwt.data(), f->bwt.size());
+        return BSW_OK;
+    }
+    if (hipSetDevice(f->device) != hipSuccess) return BSW_E_HIP;
+    return hip_rc(hipMemcpy(bwt, f->d_bwt, (size_t)f->n + 1, hipMemcpyDeviceToHost));
 }
 
 int bsw_mem_collect_intv_device(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads,
@@ -687,7 +794,12 @@ int bsw_fmi_sa_device(bsw_fmi_t *f, const uint64_t *d_k, int64_t n, int64_t *d_p
     if (n == 0) return BSW_OK;
     if (hipSetDevice(f->device) != hipSuccess) return BSW_E_HIP;
     hipStream_t s = stream ? (hipStream_t)stream : f->stream;
-    hipLaunchKernelGGL(sa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, f->d_sa, f->n + 1, d_k, n, d_pos);
+    if (f->wide)
+        hipLaunchKernelGGL(sa_kernel<uint64_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           (const uint64_t *)f->d_sa, (uint64_t)f->n + 1, d_k, n, d_pos);
+    else
+        hipLaunchKernelGGL(sa_kernel<uint32_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           (const uint32_t *)f->d_sa, (uint64_t)f->n + 1, d_k, n, d_pos);
     if (hipGetLastError() != hipSuccess) return BSW_E_HIP;
     return hipStreamSynchronize(s) == hipSuccess ? BSW_OK : BSW_E_HIP;
 }

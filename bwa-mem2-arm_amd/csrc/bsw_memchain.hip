@@ -192,7 +192,8 @@ __device__ int chain_weight(const ChainRec &c, const PoolSeed *pool, const int32
 }
 
 // per read: region [off, off + cnt) of pool / next / chains / order / wi / list
-__global__ void k_chain(COpt o, const uint32_t *__restrict__ sa, int64_t l_pac, const int32_t *__restrict__ read_len,
+template <class S>
+__global__ void k_chain(COpt o, const S *__restrict__ sa, int64_t l_pac, const int32_t *__restrict__ read_len,
                         int32_t n_reads, const bsw_bwtintv_t *__restrict__ mems, int32_t cap,
                         const int32_t *__restrict__ n_mems, const int64_t *__restrict__ off,
                         PoolSeed *__restrict__ pool_all, int32_t *__restrict__ next_all,
@@ -402,8 +403,12 @@ int run_chain(const bsw::FmiView &f, const COpt &o, const int32_t *d_len, int32_
     MC_TRY(B.get(ord, R));
     MC_TRY(B.get(wi, R));
     MC_TRY(B.get(list, R));
-    hipLaunchKernelGGL(k_chain, g, b, 0, s, o, f.d_sa, f.l_pac, d_len, n, d_mems, cap, d_nm, off, pool, next, chains,
-                       ord, wi, list, n_kept, kcnt);
+    if (f.sa64)
+        hipLaunchKernelGGL(k_chain<uint64_t>, g, b, 0, s, o, (const uint64_t *)f.d_sa, f.l_pac, d_len, n, d_mems, cap,
+                           d_nm, off, pool, next, chains, ord, wi, list, n_kept, kcnt);
+    else
+        hipLaunchKernelGGL(k_chain<uint32_t>, g, b, 0, s, o, (const uint32_t *)f.d_sa, f.l_pac, d_len, n, d_mems, cap,
+                           d_nm, off, pool, next, chains, ord, wi, list, n_kept, kcnt);
     MC_TRY(hipGetLastError());
     MC_TRY(hipMemsetAsync(kcnt + n, 0, sizeof(int64_t), s));
     MC_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, kcnt, koff, n + 1, s));

@@ -36,7 +36,7 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_create_on", "bsw_destroy
                "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats",
                "bsw_chain2aln_resident", "bsw_mem_opt_default", "bsw_fmi_build", "bsw_fmi_destroy", "bsw_fmi_get_info", "bsw_fmi_copy_sa",
                "bsw_fmi_copy_bwt", "bsw_mem_collect_intv", "bsw_mem_collect_intv_device", "bsw_fmi_sa_device",
-               "bsw_fmi_last_kernel_ms", "bsw_chain_opt_default", "bsw_mem_chain_device")
+               "bsw_fmi_last_kernel_ms", "bsw_chain_opt_default", "bsw_mem_chain_device", "bsw_fmi_build2")
 
 # include/bsw.h engine options (bsw_set_option)
 OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK, OPT_LONG, OPT_HOST_PACK = 1, 2, 3, 4, 5, 6, 7, 8
@@ -139,6 +139,8 @@ def hip_lib():
         L.bsw_chain2aln_resident.restype = ctypes.c_int
         L.bsw_mem_opt_default.argtypes = [P]
         L.bsw_fmi_build.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(P)]
+        L.bsw_fmi_build2.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
+        L.bsw_fmi_build2.restype = ctypes.c_int
         L.bsw_fmi_destroy.argtypes = [P]
         L.bsw_fmi_get_info.argtypes = [P, P]
         L.bsw_fmi_copy_sa.argtypes = [P, P]
@@ -659,13 +661,20 @@ def mem_opt(**kw) -> MemOpt:
     return o
 
 
-class Fmi:
-    """One resident FM-index (bsw_fmi_t) of ref + reverse-complement(ref) on `device`."""
+FMI_GPU_BUILD, FMI_WIDE = 1, 2
 
-    def __init__(self, ref: np.ndarray, device: int = 0):
+
+class Fmi:
+    """One resident FM-index (bsw_fmi_t) of ref + reverse-complement(ref) on `device`;
+    flags: FMI_GPU_BUILD / FMI_WIDE (bsw_fmi_build2), None: the library's choice."""
+
+    def __init__(self, ref: np.ndarray, device: int = 0, flags: int | None = None):
         self.ref = np.ascontiguousarray(ref, dtype=np.uint8)
         self._f = ctypes.c_void_p()
-        _check(hip_lib().bsw_fmi_build(_ptr(self.ref), len(self.ref), device, ctypes.byref(self._f)))
+        if flags is None:
+            _check(hip_lib().bsw_fmi_build(_ptr(self.ref), len(self.ref), device, ctypes.byref(self._f)))
+        else:
+            _check(hip_lib().bsw_fmi_build2(_ptr(self.ref), len(self.ref), device, flags, ctypes.byref(self._f)))
 
     def close(self):
         if self._f:

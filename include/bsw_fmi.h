@@ -16,11 +16,11 @@
  *   then sorted by info (qbeg << 32 | qend); ties (upstream's introsort leaves them unordered)
  *   by k, s, l.
  *
- * Index (built on the host, resident in HBM): T = ref + reverse-complement(ref), the BWT of T$
- * with the sentinel kept, count[c] = 1 + #{bases < c}, occurrence counts in 64-base blocks of
- * 64 bytes (4 x uint32 counts + 4 x uint64 one-hot masks: one block load per Occ query), the
- * full suffix array as uint32 (|T| < 2^32 - 1; 4 B per text position -- a 3 Gb genome's 6 G
- * positions would need the 64-bit form, not built here).  Intervals are bwa-mem2's:
+ * Index (built on the host below 64 Mb, on the GPU above; resident in HBM): T = ref +
+ * reverse-complement(ref), the BWT of T$ with the sentinel kept, count[c] = 1 + #{bases < c},
+ * occurrence counts in 64-base blocks of 64 bytes (4 x uint32 -- or, in the wide layout, 4 x
+ * uint64 -- counts + 4 x uint64 one-hot masks: one block load per Occ query), the full suffix
+ * array as uint32 (|T| + 1 < 2^32) or uint64 (the wide layout a 3 Gb genome's 6 G rows need).  Intervals are bwa-mem2's:
  * [k, k + s) 0-based over the n + 1 rows of T$, l = k of the reverse-complement string.
  * Reference bases must be 0..3 (ambiguous bases replaced beforehand, as bwa's .pac does);
  * read bases 0..4 (4 = N ends every match).
@@ -61,11 +61,20 @@ typedef struct bsw_fmi_info_t {
 
 void bsw_mem_opt_default(bsw_mem_opt_t *opt);
 
-/* Build the FM-index of ref[0, ref_len) on the host (prefix-doubling suffix array over 27-base
- * keys) and keep it resident on HIP device `device` (device < 0: host-only index -- suffix array,
+/* Build the FM-index of ref[0, ref_len) -- below 64 Mb on the host (prefix-doubling suffix array
+ * over 27-base keys), else on the GPU (bsw_fmi_build2) -- and keep it resident on HIP device
+ * `device` (device < 0: host-only index -- suffix array,
  * BWT and counts for inspection; seeding calls on it return BSW_E_NODEV).  Blocking.
- * BSW_E_INVAL for a base > 3, BSW_E_RANGE if 2 * ref_len + 2 >= 2^32. */
+ * BSW_E_INVAL for a base > 3.  (Host-only indexes are narrow: BSW_E_RANGE past 2^32 rows.) */
 int  bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **out);
+/* The same with builder flags: BSW_FMI_GPU_BUILD builds on the GPU (bucketed radix sort of 27-base
+ * keys in HBM, csrc/bsw_fmi_build.hip), BSW_FMI_WIDE keeps 64-bit rows / counts / suffix array.
+ * bsw_fmi_build picks them itself: references of >= 64 Mb build on the GPU, and a two-strand text
+ * of >= 2^32 - 1 rows (a ~2.1 Gb genome or larger, e.g. GRCh38's 3.1 Gb) needs the wide layout:
+ * 8 B of suffix array + 1 B of occurrence blocks + 1 B of BWT codes per text position, ~60 GB of
+ * HBM for 3 Gb (ABI version 5). */
+enum { BSW_FMI_GPU_BUILD = 1, BSW_FMI_WIDE = 2 };
+int  bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, bsw_fmi_t **out);
 void bsw_fmi_destroy(bsw_fmi_t *fmi);
 int  bsw_fmi_get_info(const bsw_fmi_t *fmi, bsw_fmi_info_t *out);
 /* Host copies of the suffix array (n + 1 entries) and the BWT (n + 1 codes, 4 = '$'). */

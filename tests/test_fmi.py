@@ -267,3 +267,83 @@ def test_gpu_device_api_and_sa_lookup():
     sa = o.sa()
     assert np.array_equal(pos[:-2], sa[ks[:-2].astype(np.int64)]) and (pos[-2:] == -1).all()
     f.close()
+
+
+# --------------------------------------------------------------- GPU-built and wide (64-bit) indexes
+
+def _long_runs_ref(n, seed):
+    """repetitive_ref plus a 400-base homopolymer and a 600-base dinucleotide repeat: tie groups of
+    hundreds of suffixes equal on 27 bases (the builder's host-sorted path)"""
+    ref = repetitive_ref(n, seed)
+    ref[n // 3:n // 3 + 400] = 1
+    ref[n // 2:n // 2 + 600] = np.tile(np.array([0, 3], np.uint8), 300)
+    return ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["repetitive", "random", "long_runs"])
+@pytest.mark.parametrize("flags", [bsw.FMI_GPU_BUILD, bsw.FMI_GPU_BUILD | bsw.FMI_WIDE])
+def test_gpu_builder_equals_host_builder(kind, flags):
+    """bsw_fmi_build2 on the GPU (bucketed radix sort of 27-base keys, tie groups by comparison),
+    narrow and wide (64-bit) layouts: suffix array, BWT, sentinel and counts == the host
+    prefix-doubling builder's"""
+    n = 300_000
+    ref = {"repetitive": lambda: repetitive_ref(n, 2), "long_runs": lambda: _long_runs_ref(n, 3),
+           "random": lambda: np.random.default_rng(5).integers(0, 4, n, dtype=np.uint8)}[kind]()
+    h = bsw.Fmi(ref, device=-1)
+    g = bsw.Fmi(ref, flags=flags)
+    hi, gi = h.info(), g.info()
+    assert gi.n == hi.n and gi.sentinel == hi.sentinel and list(gi.count) == list(hi.count)
+    assert np.array_equal(g.sa(), h.sa())
+    assert np.array_equal(g.bwt(), h.bwt())
+    h.close()
+    g.close()
+
+
+@pytest.mark.gpu
+def test_wide_index_seeding_and_chaining_equal_oracle():
+    """the wide layout (64-bit rows, counts and suffix array -- what a 3 Gb two-strand genome
+    needs) runs mem_collect_intv, bwt_sa and mem_chain exactly like the narrow one: == oracle"""
+    import hiprt
+    ref = _long_runs_ref(200_000, 7)
+    reads, off, lens = sample_reads(ref, 3000, 151, 13)
+    o = oracle.FmiRef(ref)
+    f = bsw.Fmi(ref, flags=bsw.FMI_GPU_BUILD | bsw.FMI_WIDE)
+    for opt in (dict(), dict(min_seed_len=15), dict(split_width=50, min_seed_len=11)):
+        o_out, o_cnt = o.collect_intv(reads, off, lens, cap=2048, opt=oracle.mem_opt(**opt), nthreads=8)
+        g_out, g_cnt = f.collect_intv(reads, off, lens, cap=2048, opt=bsw.mem_opt(**opt))
+        _compare(o_out, o_cnt, g_out, g_cnt)
+    o_out, o_cnt = o.collect_intv(reads, off, lens, cap=2048, nthreads=8)
+    ks = np.concatenate([o_out[i, :o_cnt[i]]["k"] for i in range(len(lens))] + [np.array([o.n + 1], np.uint64)])
+    d_k = hiprt.DeviceBuffer.from_array(ks.astype(np.uint64))
+    d_pos = hiprt.DeviceBuffer(len(ks) * 8)
+    f.sa_device(d_k.ptr, len(ks), d_pos.ptr)
+    pos = d_pos.download(np.zeros(len(ks), dtype=np.int64))
+    assert np.array_equal(pos[:-1], o.sa()[ks[:-1].astype(np.int64)]) and pos[-1] == -1
+    seeds, sr, sc = oracle.mem_chain(o.sa(), len(ref), lens, o_out, o_cnt)
+    d_reads = hiprt.DeviceBuffer.from_array(reads)
+    (gs, gsr, gsc), _, _ = bsw.seed_and_chain(f, d_reads, off, lens, cap=2048)
+    assert np.array_equal(gsr, sr) and np.array_equal(gsc, sc) and np.array_equal(gs["rbeg"], seeds["rbeg"])
+    f.close()
+
+
+@pytest.mark.gpu
+def test_gpu_builder_at_64mb():
+    """bsw_fmi_build's own choice at 64 Mb (GPU builder, narrow) == the wide GPU build, and the
+    suffix array is sorted: 20K sampled adjacent rows compared as strings of T$"""
+    ref = bsw.synth_reference(64_000_000, seed=7)
+    ref[ref > 3] = 2
+    a = bsw.Fmi(ref)
+    b = bsw.Fmi(ref, flags=bsw.FMI_GPU_BUILD | bsw.FMI_WIDE)
+    ia, ib = a.info(), b.info()
+    assert ia.n == ib.n == 2 * len(ref) and ia.sentinel == ib.sentinel and list(ia.count) == list(ib.count)
+    sa = a.sa()
+    assert np.array_equal(sa, b.sa())
+    T = np.concatenate([ref, 3 - ref[::-1]]).astype(np.uint8).tobytes()   # '$' = the end: a prefix sorts first
+    rng = np.random.default_rng(1)
+    for r in rng.integers(0, len(sa) - 1, 20_000):
+        x, y = int(sa[r]), int(sa[r + 1])
+        u, v = T[x:x + 64], T[y:y + 64]
+        assert u < v or (u == v and T[x:] < T[y:]), r
+    a.close()
+    b.close()
