@@ -849,15 +849,19 @@ def main_mem(args, rank, local, world, c1: bool):
         reads, off, lens = pe_reads(ref, max(1, args.reads // 2), seed=42 + rank)
     n = len(lens)
     gen_s = time.perf_counter() - t0
+    log = lambda m: print(f"[bench c4mem rank {rank}] {m} ({time.perf_counter() - t0:.1f} s)", file=sys.stderr,  # noqa: E731
+                          flush=True)
+    log(f"generated {n} reads vs {len(ref)} bases")
     t = time.perf_counter()
     fmi = bsw.Fmi(ref, device=local)
     build_s = time.perf_counter() - t
+    log(f"index built in {build_s:.1f} s")
     T = np.concatenate([ref, (3 - ref[::-1])]).astype(np.uint8)
     eng = bsw.Engine(device=local)
     bsw.set_reference(eng, T)
     opt = bsw.ext_opt(w=args.w, l_pac=len(ref))
     mopt, copt = bsw.mem_opt(), bsw.chain_opt()
-    cap = 256
+    cap = 256 if n <= 2_000_000 else 64                  # interval slots per read (HBM: n * cap * 32 B)
     d_reads = hiprt.DeviceBuffer.from_array(reads)
     d_off, d_len = hiprt.DeviceBuffer.from_array(off), hiprt.DeviceBuffer.from_array(lens)
     d_mems = hiprt.DeviceBuffer(n * cap * bsw.BWTINTV_DTYPE.itemsize)
@@ -891,6 +895,7 @@ def main_mem(args, rank, local, world, c1: bool):
 
     for _ in range(args.warmup):
         step()
+        log("warm-up step done")
     barrier(world)
     t = time.perf_counter()
     n_ext, sts, parts = 0, [], []
@@ -940,8 +945,13 @@ def main_mem(args, rank, local, world, c1: bool):
         "extensions_per_step_rank0": list(st.n_pairs),
         "full_length_fraction": round(float(np.mean(best == 150)), 4) if c1 else None,
         "index_build_s": round(build_s, 2), "synth_gen_s": round(gen_s, 2),
+        "index": {"wide_64bit": bool(2 * len(ref) + 2 >= 2**32), "device_bytes": int(fmi.info().device_bytes),
+                  "built_on": "gpu" if len(ref) >= (64 << 20) else "host"},
     }
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and len(ref) > 512_000_000:
+        out_j["cpu_baseline"] = {"value": None, "note": "not run above 512 Mb: the oracle's plain occurrence table "
+                                 "(32 B per text row) would need ~192 GB of host memory at 3 Gb; see the 64 Mb line"}
+    elif world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # CPU baseline leg only (test infrastructure)
         nt = cpu_leg_threads()

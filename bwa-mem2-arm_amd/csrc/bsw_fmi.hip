@@ -97,6 +97,7 @@ template <class U>
 __device__ __forceinline__ IvT<U> backward_ext(const FmiDevT<U> &f, IvT<U> in, int a)
 {
     const U sp = in.k, ep = in.k + in.s;
+    if (ep > f.n + 1 || ep < sp) return IvT<U>{0, 0, 0};   // never for a consistent index (bsw_fmi_check)
     Occ4<U> o0, o1;
     load_block(f.blk, sp >> 6, o0);
     if ((ep >> 6) == (sp >> 6)) o1 = o0;
@@ -707,6 +708,27 @@ int bsw_fmi_copy_sa(const bsw_fmi_t *f, int64_t *sa)
     std::vector<uint32_t> t(N);
     const int rc = hip_rc(hipMemcpy(t.data(), f->d_sa, N * sizeof(uint32_t), hipMemcpyDeviceToHost));
     for (size_t r = 0; r < N && !rc; ++r) sa[r] = t[r];
+    return rc;
+}
+
+int bsw_fmi_check(bsw_fmi_t *f, int64_t *bad)
+{
+    if (!f || !bad) return BSW_E_INVAL;
+    if (f->device < 0) return BSW_E_NODEV;
+    std::lock_guard<std::mutex> lk(f->mu);
+    if (hipSetDevice(f->device) != hipSuccess) return BSW_E_HIP;
+    uint8_t *d_bwt = f->d_bwt;
+    bool own = false;
+    if (!d_bwt) {                                   // host-built: its BWT codes go up for the check
+        if (hipMalloc(&d_bwt, f->bwt.size()) != hipSuccess) return BSW_E_NOMEM;
+        own = true;
+        if (hipMemcpy(d_bwt, f->bwt.data(), f->bwt.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d_bwt);
+            return BSW_E_HIP;
+        }
+    }
+    const int rc = bsw::fmi_check_gpu(f->device, f->wide, f->d_sa, d_bwt, f->d_blk, f->n, f->count, bad);
+    if (own) (void)hipFree(d_bwt);
     return rc;
 }
 

@@ -28,13 +28,18 @@ namespace {
 
 constexpr int kBuckets = 125;                      // 5^3
 
+// A dispatch holds at most 2^32 - 1 work-items (the AQL packet's 32-bit grid size), and a 3 Gb
+// genome has 6 G rows: every kernel over rows / text positions is grid-stride (kStrideGrid
+// blocks of 256).
+constexpr unsigned kStrideGrid = 1u << 20;
+
 __global__ void k_make_text(const uint8_t *__restrict__ ref, int64_t len, uint8_t *__restrict__ T)
 {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= len) return;
-    const uint8_t c = ref[i];
-    T[i] = c;
-    T[2 * len - 1 - i] = (uint8_t)(3 - c);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t c = ref[i];
+        T[i] = c;
+        T[2 * len - 1 - i] = (uint8_t)(3 - c);
+    }
 }
 
 __device__ __forceinline__ uint64_t key27(const uint8_t *__restrict__ T, int64_t n, int64_t p)
@@ -153,11 +158,11 @@ template <class S>
 __global__ void k_bwt(const uint8_t *__restrict__ T, const S *__restrict__ sa, int64_t N, uint8_t *__restrict__ bwt,
                       unsigned long long *__restrict__ sentinel)
 {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N) return;
-    const int64_t p = (int64_t)sa[r];
-    bwt[r] = p == 0 ? 4 : T[p - 1];
-    if (p == 0) *sentinel = (unsigned long long)r;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = (int64_t)sa[r];
+        bwt[r] = p == 0 ? 4 : T[p - 1];
+        if (p == 0) *sentinel = (unsigned long long)r;
+    }
 }
 
 // masks and per-block counts (cnt[c * nb + b]); one thread per block of 64 rows
@@ -192,6 +197,41 @@ __global__ void k_block_counts(int64_t nb, const unsigned long long *__restrict_
     }
 }
 
+// ---- index self-check (bsw_fmi_check): every invariant the seeding walk relies on
+// blocks: cnt[b + 1] = cnt[b] + popcount(bits[b]) per code, the last block's totals = count[]
+template <class B>
+__global__ void k_chk_blocks(const B *__restrict__ blk, int64_t nb, const int64_t *__restrict__ count,
+                             unsigned long long *__restrict__ bad)
+{
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    for (int c = 0; c < 4; ++c) {
+        const uint64_t next = (uint64_t)blk[b].cnt[c] + (uint64_t)__builtin_popcountll(blk[b].bits[c]);
+        const uint64_t want = b + 1 < nb ? (uint64_t)blk[b + 1].cnt[c] : (uint64_t)(count[c + 1] - count[c]);
+        if (next != want) atomicAdd(bad, 1ull);
+    }
+}
+// SA is a permutation of [0, n]; LF(r) = count[c] + Occ(c, r) with c = BWT[r] satisfies
+// SA[LF(r)] = SA[r] - 1 for every row but the sentinel's (c = '$')
+template <class S, class B>
+__global__ void k_chk_lf(const S *__restrict__ sa, const uint8_t *__restrict__ bwt, const B *__restrict__ blk,
+                         int64_t N, const int64_t *__restrict__ count, unsigned int *__restrict__ seen,
+                         unsigned long long *__restrict__ bad)
+{
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = (uint64_t)sa[r];
+        if (p >= (uint64_t)N) { atomicAdd(bad, 1ull); continue; }
+        if (atomicOr(&seen[p >> 5], 1u << (p & 31)) & (1u << (p & 31))) atomicAdd(bad, 1ull);
+        const int c = bwt[r];
+        if (c > 4 || (c == 4) != (p == 0)) { atomicAdd(bad, 1ull); continue; }
+        if (c == 4) continue;
+        const B &k = blk[r >> 6];
+        const uint64_t m = (r & 63) ? (~0ull >> (64 - (r & 63))) : 0ull;
+        const int64_t lf = count[c] + (int64_t)k.cnt[c] + __builtin_popcountll(k.bits[c] & m);
+        if (lf < 0 || lf >= N || (uint64_t)sa[lf] != p - 1) atomicAdd(bad, 1ull);
+    }
+}
+
 int hrc(hipError_t e) { return e == hipSuccess ? BSW_OK : (e == hipErrorOutOfMemory ? BSW_E_NOMEM : BSW_E_HIP); }
 #define FB_TRY(x)                             \
     do {                                      \
@@ -200,6 +240,7 @@ int hrc(hipError_t e) { return e == hipSuccess ? BSW_OK : (e == hipErrorOutOfMem
     } while (0)
 
 inline unsigned grid_of(int64_t n, int bs = 256) { return (unsigned)std::max<int64_t>(1, (n + bs - 1) / bs); }
+inline unsigned stride_grid(int64_t n) { return std::min<unsigned>(grid_of(n), kStrideGrid); }
 
 struct Scratch {                                       // temporaries of one build, freed on every path
     std::vector<void *> p;
@@ -227,7 +268,7 @@ int build(const uint8_t *ref, int64_t len, bsw::GpuIndex *out)
     FB_TRY(X.get(d_ref, (size_t)len));
     FB_TRY(X.get(T, (size_t)n));
     FB_TRY(hipMemcpy(d_ref, ref, (size_t)len, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_make_text, dim3(grid_of(len)), dim3(256), 0, st, d_ref, len, T);
+    hipLaunchKernelGGL(k_make_text, dim3(stride_grid(len)), dim3(256), 0, st, d_ref, len, T);
     FB_TRY(hipGetLastError());
     // 2. buckets
     unsigned long long *d_cnt, *d_cur;
@@ -310,7 +351,7 @@ int build(const uint8_t *ref, int64_t len, bsw::GpuIndex *out)
     out->d_bwt = bwt;
     unsigned long long *d_sent;
     FB_TRY(X.get(d_sent, 1));
-    hipLaunchKernelGGL(k_bwt<S>, dim3(grid_of(N)), dim3(256), 0, st, T, sa, N, bwt, d_sent);
+    hipLaunchKernelGGL(k_bwt<S>, dim3(stride_grid(N)), dim3(256), 0, st, T, sa, N, bwt, d_sent);
     FB_TRY(hipGetLastError());
     const int64_t nb = (N >> 6) + 1;                   // covers row N (= k + s at most)
     B *blk = nullptr;
@@ -347,6 +388,40 @@ int build(const uint8_t *ref, int64_t len, bsw::GpuIndex *out)
 }
 
 }  // namespace
+
+int bsw::fmi_check_gpu(int device, bool wide, const void *d_sa, const uint8_t *d_bwt, const void *d_blk, int64_t n,
+                       const int64_t *count, int64_t *bad)
+{
+    *bad = -1;
+    if (hipSetDevice(device) != hipSuccess) return BSW_E_HIP;
+    const int64_t N = n + 1, nb = (N >> 6) + 1;
+    Scratch X;
+    int64_t *d_count;
+    unsigned int *seen;
+    unsigned long long *d_bad;
+    FB_TRY(X.get(d_count, 5));
+    FB_TRY(X.get(seen, (size_t)(N + 31) / 32));
+    FB_TRY(X.get(d_bad, 1));
+    FB_TRY(hipMemcpy(d_count, count, 5 * sizeof(int64_t), hipMemcpyHostToDevice));
+    FB_TRY(hipMemset(seen, 0, (size_t)(N + 31) / 32 * sizeof(unsigned int)));
+    FB_TRY(hipMemset(d_bad, 0, sizeof(unsigned long long)));
+    if (wide) {
+        hipLaunchKernelGGL(k_chk_blocks<FmiBlockW>, dim3(grid_of(nb)), dim3(256), 0, 0, (const FmiBlockW *)d_blk, nb,
+                           d_count, d_bad);
+        hipLaunchKernelGGL((k_chk_lf<uint64_t, FmiBlockW>), dim3(stride_grid(N)), dim3(256), 0, 0, (const uint64_t *)d_sa,
+                           d_bwt, (const FmiBlockW *)d_blk, N, d_count, seen, d_bad);
+    } else {
+        hipLaunchKernelGGL(k_chk_blocks<FmiBlock>, dim3(grid_of(nb)), dim3(256), 0, 0, (const FmiBlock *)d_blk, nb,
+                           d_count, d_bad);
+        hipLaunchKernelGGL((k_chk_lf<uint32_t, FmiBlock>), dim3(stride_grid(N)), dim3(256), 0, 0, (const uint32_t *)d_sa,
+                           d_bwt, (const FmiBlock *)d_blk, N, d_count, seen, d_bad);
+    }
+    FB_TRY(hipGetLastError());
+    unsigned long long b = 0;
+    FB_TRY(hipMemcpy(&b, d_bad, sizeof(b), hipMemcpyDeviceToHost));
+    *bad = (int64_t)b;
+    return BSW_OK;
+}
 
 int bsw::fmi_build_gpu(const uint8_t *ref, int64_t ref_len, int device, bool wide, GpuIndex *out)
 {

@@ -33,6 +33,10 @@ struct GpuIndex {
 // suffix array by bucketing (first 3 bases) + per-bucket radix sort of 27-base keys + direct
 // comparison of the remaining tie groups, then BWT and occurrence blocks.  Blocking.
 int fmi_build_gpu(const uint8_t *ref, int64_t ref_len, int device, bool wide, GpuIndex *out);
+// Invariants of a resident index: block counts chain, SA a permutation, LF(r) = SA^-1[SA[r] - 1];
+// *bad = number of violations (0: consistent).  d_bwt: the BWT codes on the device.
+int fmi_check_gpu(int device, bool wide, const void *d_sa, const uint8_t *d_bwt, const void *d_blk, int64_t n,
+                  const int64_t *count, int64_t *bad);
 
 struct FmiView {
     int device;

@@ -36,7 +36,7 @@ ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_create_on", "bsw_destroy
                "bsw_split_by_cells", "bsw_chain2aln", "bsw_chain2aln_device", "bsw_chain_last_stats",
                "bsw_chain2aln_resident", "bsw_mem_opt_default", "bsw_fmi_build", "bsw_fmi_destroy", "bsw_fmi_get_info", "bsw_fmi_copy_sa",
                "bsw_fmi_copy_bwt", "bsw_mem_collect_intv", "bsw_mem_collect_intv_device", "bsw_fmi_sa_device",
-               "bsw_fmi_last_kernel_ms", "bsw_chain_opt_default", "bsw_mem_chain_device", "bsw_fmi_build2")
+               "bsw_fmi_last_kernel_ms", "bsw_chain_opt_default", "bsw_mem_chain_device", "bsw_fmi_build2", "bsw_fmi_check")
 
 # include/bsw.h engine options (bsw_set_option)
 OPT_KERNEL8, OPT_FORK, OPT_SORTKEY, OPT_GLOB_BAND, OPT_EXT_CHUNK, OPT_HOST_CHUNK, OPT_LONG, OPT_HOST_PACK = 1, 2, 3, 4, 5, 6, 7, 8
@@ -141,6 +141,8 @@ def hip_lib():
         L.bsw_fmi_build.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(P)]
         L.bsw_fmi_build2.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
         L.bsw_fmi_build2.restype = ctypes.c_int
+        L.bsw_fmi_check.argtypes = [P, P]
+        L.bsw_fmi_check.restype = ctypes.c_int
         L.bsw_fmi_destroy.argtypes = [P]
         L.bsw_fmi_get_info.argtypes = [P, P]
         L.bsw_fmi_copy_sa.argtypes = [P, P]
@@ -686,6 +688,12 @@ class Fmi:
             self.close()
         except Exception:
             pass
+
+    def check(self) -> int:
+        """bsw_fmi_check: number of violated index invariants (0 = consistent)"""
+        bad = ctypes.c_int64(-1)
+        _check(hip_lib().bsw_fmi_check(self._f, ctypes.byref(bad)))
+        return bad.value
 
     def info(self) -> FmiInfo:
         i = FmiInfo()

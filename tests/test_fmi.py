@@ -347,3 +347,13 @@ def test_gpu_builder_at_64mb():
         assert u < v or (u == v and T[x:] < T[y:]), r
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+def test_index_self_check():
+    """bsw_fmi_check: 0 violations on host-built, GPU-built narrow and wide indexes"""
+    ref = _long_runs_ref(120_000, 11)
+    for flags in (None, bsw.FMI_GPU_BUILD, bsw.FMI_GPU_BUILD | bsw.FMI_WIDE):
+        f = bsw.Fmi(ref, flags=flags)
+        assert f.check() == 0, flags
+        f.close()
