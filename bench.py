@@ -940,7 +940,7 @@ def main_mem(args, rank, local, world, c1: bool):
         "stage_ms": {"smem": round(float(pm[0]), 3), "chain": round(float(pm[1]), 3),
                      "chain2aln": round(float(pm[2]), 3)},
         "smem_kernel_ms": round(fmi.last_kernel_ms(), 3),
-        "seeds_per_read": round(ns / n, 3), "chains_per_read": round(float(len(np.unique(sr * 4096 + sc))) / n, 3),
+        "seeds_per_read": round(ns / n, 3), "chains_per_read": round(float(len(np.unique(sr.astype(np.int64) * 65536 + sc))) / n, 3),
         "extended_fraction": round(st.n_extended / max(1, ns), 4), "rounds": st.rounds,
         "extensions_per_step_rank0": list(st.n_pairs),
         "full_length_fraction": round(float(np.mean(best == 150)), 4) if c1 else None,
