@@ -53,7 +53,8 @@ constexpr int kMetaCounts = 16;             // class counters per slot (one 64-B
 constexpr int kMetaSpread = 32;             // slots: block b adds into slot b % 32 (no hot line)
 constexpr int kMetaMaxq = kMetaCounts * kMetaSpread;   // d_meta: counts[32][16], maxq_wide, err
 constexpr int kMetaErr = kMetaMaxq + 1;
-constexpr int kMetaWords = kMetaErr + 1;
+constexpr int kMetaFlag = kMetaErr + 1;     // row-group kernel: a pair outside its contract
+constexpr int kMetaWords = kMetaFlag + 1;
 constexpr int kKeyBits = 32;                // 4 class + 8 qlen + 1 related + 11 tlen + 8 h0 bits
 static_assert(kNumClasses <= kMetaCounts, "class counts");
 
@@ -179,6 +180,12 @@ struct PlanCall {
     int32_t n = 0, w = 0;
     int cell_bits = 16;
     hipStream_t stream = nullptr;
+    // small batches: > 0 = the host checked every pair against the row-group kernel's contract
+    // (value = its columns per lane); 0 = not checked (the kernel flags misfits, run_dp falls
+    // back to the planned path); -1 = some pair does not fit (planned path at once)
+    int gq_cols = 0;
+    int32_t *d_out24 = nullptr;         // row-group kernel, host-checked batch: outputs as 6 x int32
+                                        //   per pair here instead of into d_pairs
 };
 
 struct Slot {
@@ -228,6 +235,8 @@ struct Slot {
     hipStream_t pstream = nullptr;      // high-priority stream of run_plan
     hipEvent_t evh = nullptr;           // inputs ready on the call's stream (pstream waits)
     PlanCall plan;                      // arguments of the last run_plan (run_dp's input)
+    int fast = 0;                       // last run_plan launched the row-group kernel: 2 = host-
+                                        //   checked batch, 1 = kernel-checked (flag read back)
 };
 
 static int hip_rc(hipError_t e)
@@ -398,6 +407,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.fork = 1;
     kp.long_route = 1;
     kp.small_batch = 16384;
+    kp.group_kernel = 1;
 }
 
 // keys / keys2 / vals / order (radix-sort buffers) grow together
@@ -428,8 +438,33 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     s.timed = false;
     s.run_stream = pc.stream;
     s.plan = pc;
+    s.fast = 0;
     if (pc.n == 0) return BSW_OK;
     const int32_t n = pc.n;
+    // small batches (kt_for-sized calls): the row-group kernel (bsw_gq.hip) straight on the
+    // call's stream -- no plan, no sort, no class-count readback
+    if (kp.group_kernel && n <= kp.small_batch && pc.gq_cols >= 0 && kp.long_route == 1 && kp.maxsc == 1 &&
+        !kp.misroute) {
+        const bool checked = pc.gq_cols > 0;
+        int32_t *d_err = s.d_meta + kMetaErr;
+        if (!pc.d_out24)                       // (the staged path's input kernel zeroed them)
+            BSW_TRY(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), pc.stream));
+        BSW_TRY(hipEventRecord(s.ev0, pc.stream));
+        BSW_TRY(launch_gq_kernel(checked ? pc.gq_cols : 10, kp, pc.w, pc.d_pairs, nullptr, n, pc.d_ref, pc.d_qer,
+                                 d_err, checked ? nullptr : s.d_meta + kMetaFlag, checked ? pc.d_out24 : nullptr,
+                                 pc.stream));
+        BSW_TRY(hipEventRecord(s.ev1, pc.stream));
+        BSW_TRY(hipMemcpyAsync(s.h_meta + kMetaErr, d_err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, pc.stream));
+        if (!checked) {
+            if (!s.evm) BSW_TRY(hipEventCreateWithFlags(&s.evm, hipEventDisableTiming));
+            BSW_TRY(hipEventRecord(s.evm, pc.stream));
+        }
+        s.stats.n_launches = 1;
+        s.stats.n_i16 = n;
+        s.stats.n_group = n;
+        s.fast = checked ? 2 : 1;
+        return BSW_OK;
+    }
     // plan + sort run on the slot's high-priority stream (ordered after the call's stream by an
     // event): while other chunks' DP kernels fill the GPU, their few blocks are dispatched
     // first instead of queuing behind thousands of DP workgroups (it delays the next chunk's
@@ -482,6 +517,22 @@ static int run_dp(const KParams &kp, Slot &s)
     SeqPair *d_pairs = pc.d_pairs;
     const uint8_t *d_ref = pc.d_ref, *d_qer = pc.d_qer;
     int32_t *d_err = s.d_meta + kMetaErr;
+    if (s.fast) {
+        if (s.fast == 1) {
+            BSW_TRY(hipEventSynchronize(s.evm));   // the row-group kernel's misfit flag
+            if (s.h_meta[kMetaFlag] != 0) {
+                // some pair is outside the row-group kernel's contract: the whole batch again on
+                // the planned path (identical outputs; rare -- long or int16-unsafe pairs)
+                PlanCall again = pc;
+                again.gq_cols = -1;
+                const int r = run_plan(kp, s, again);
+                if (r) return r;
+                return run_dp(kp, s);
+            }
+        }
+        s.timed = true;                            // ev0 / ev1 bracket the kernel; the guard
+        return BSW_OK;                             //   word is on its way to h_meta[kMetaErr]
+    }
     BSW_TRY(hipEventSynchronize(s.evm));           // the class counts are in h_meta
     BSW_TRY(hipStreamWaitEvent(stream, s.evm, 0)); // order / meta written on the plan stream
     int32_t counts[kNumClasses] = {};
@@ -687,6 +738,68 @@ __global__ void expand_pairs_kernel(const PairIn *__restrict__ in, SeqPair *__re
     memset(&sp, 0, sizeof(sp));
     sp.idr = p.idr; sp.idq = p.idq; sp.len1 = p.len1; sp.len2 = p.len2; sp.h0 = p.h0;
     out[i] = sp;
+}
+
+// The whole staged input of a coalesced batch in one launch (what unpack2 x2 + patch_codes +
+// expand_pairs + two pad memsets did in six): index space = ref 16-code units, qer units, pairs.
+// Exception words (pos << 4 | code) are ascending per buffer, so a unit finds its own by a
+// binary search and patches them after unpacking (no second pass, no race).
+__device__ __forceinline__ void unpack_unit(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int64_t n,
+                                            int64_t t, const uint32_t *__restrict__ exc, int32_t ne)
+{
+    const int64_t o = t * 16;
+    uint32_t v = 0;
+    const int64_t ib = t * 4, nin = (n + 3) / 4;
+    if (ib + 4 <= nin) v = *(const uint32_t *)(in + ib);
+    else
+        for (int k = 0; k < 4 && ib + k < nin; ++k) v |= (uint32_t)in[ib + k] << (8 * k);
+    const uint32_t p0 = v & 0x03030303u, p1 = (v >> 2) & 0x03030303u;
+    const uint32_t p2 = (v >> 4) & 0x03030303u, p3 = (v >> 6) & 0x03030303u;
+    const uint32_t a01 = __builtin_amdgcn_perm(p1, p0, 0x05010400u), b01 = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
+    const uint32_t a23 = __builtin_amdgcn_perm(p3, p2, 0x05010400u), b23 = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
+    uint32_t w[4] = {__builtin_amdgcn_perm(a23, a01, 0x05040100u), __builtin_amdgcn_perm(a23, a01, 0x07060302u),
+                     __builtin_amdgcn_perm(b23, b01, 0x05040100u), __builtin_amdgcn_perm(b23, b01, 0x07060302u)};
+    if (ne > 0) {
+        int32_t lo = 0, hi = ne;                       // first exception at or past o
+        while (lo < hi) {
+            const int32_t mid = (lo + hi) >> 1;
+            if ((int64_t)(exc[mid] >> 4) < o) lo = mid + 1; else hi = mid;
+        }
+        for (; lo < ne && (int64_t)(exc[lo] >> 4) < o + 16; ++lo) {
+            const int k = (int)((exc[lo] >> 4) - o);
+            w[k >> 2] = (w[k >> 2] & ~(0xffu << (8 * (k & 3)))) | ((exc[lo] & 15u) << (8 * (k & 3)));
+        }
+    }
+    if (o + 16 <= n) {
+        *(uint4 *)(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (int k = 0; o + k < n; ++k) out[o + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+}
+
+__global__ void stage_in_kernel(const uint8_t *__restrict__ ref2, int64_t r_tot, const uint8_t *__restrict__ qer2,
+                                int64_t q_tot, const uint32_t *__restrict__ exc, int32_t n_r, int32_t ne,
+                                const PairIn *__restrict__ pin, int32_t n, uint8_t *__restrict__ ref,
+                                uint8_t *__restrict__ qer, SeqPair *__restrict__ pairs, int32_t *__restrict__ zero2)
+{
+    const int64_t tr = (r_tot + 15) / 16, tq = (q_tot + 15) / 16;
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        *(uint32_t *)(ref + r_tot) = 0u;          // 4 zero bytes past each buffer
+        *(uint32_t *)(qer + q_tot) = 0u;
+        if (zero2) { zero2[0] = 0; zero2[1] = 0; }
+    }
+    if (t < tr) { unpack_unit(ref2, ref, r_tot, t, exc, n_r); return; }
+    t -= tr;
+    if (t < tq) { unpack_unit(qer2, qer, q_tot, t, exc + n_r, ne - n_r); return; }
+    t -= tq;
+    if (t < n) {
+        const PairIn p = pin[t];
+        SeqPair sp;
+        memset(&sp, 0, sizeof(sp));
+        sp.idr = p.idr; sp.idq = p.idq; sp.len1 = p.len1; sp.len2 = p.len2; sp.h0 = p.h0;
+        pairs[t] = sp;
+    }
 }
 
 // the six outputs of each pair (SeqPair bytes 32..55) -> 24 B per pair for the D2H
@@ -1017,7 +1130,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         unstage_outputs(s, pairs + pend_at[k], pend_n[k], pend_mode[k]);
         agg.kernel_ms += s.stats.kernel_ms;
         agg.n_i16 += s.stats.n_i16; agg.n_u8 += s.stats.n_u8; agg.n_wide += s.stats.n_wide;
-        agg.n_packed += s.stats.n_packed; agg.n_launches += s.stats.n_launches; agg.n_wave += s.stats.n_wave;
+        agg.n_packed += s.stats.n_packed; agg.n_launches += s.stats.n_launches; agg.n_wave += s.stats.n_wave; agg.n_group += s.stats.n_group;
         pend_n[k] = 0;
         return BSW_OK;
     };
@@ -1197,18 +1310,23 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
             }
         }
         std::vector<std::vector<uint32_t>> ex(tasks.size());
+        // per task: the row-group kernel's contract over its records (max qlen, or -1: a misfit)
+        std::vector<int> gq_maxq(tasks.size(), 0);
         PairIn *pin = (PairIn *)(h + pair_off);
         HostPool::get().parallel_for((int)tasks.size(), [&](int t) {
             const Task &k = tasks[t];
             const AggSeg &g = segs[k.seg];
             if (k.kind == 0) {
                 const SeqPair *p = g.r->pairs;
+                int maxq = 0;
                 for (int32_t i = 0; i < g.r->n; ++i) {
                     PairIn &o = pin[g.p_off + i];
                     o.idr = p[i].len1 > 0 ? (int32_t)(p[i].idr - g.r_lo + g.r_off) : 0;
                     o.idq = p[i].len2 > 0 ? (int32_t)(p[i].idq - g.q_lo + g.q_off) : 0;
                     o.len1 = p[i].len1; o.len2 = p[i].len2; o.h0 = p[i].h0;
+                    if (maxq >= 0) maxq = gq_pair_ok(kp, p[i].len2, p[i].len1, p[i].h0) ? std::max(maxq, p[i].len2) : -1;
                 }
+                gq_maxq[t] = maxq;
             } else if (k.kind == 1) {
                 pack_2bit(h + ref_off + (g.r_off + k.a) / 4, g.r->ref + g.r_lo + k.a, (size_t)(k.b - k.a),
                           (uint32_t)(g.r_off + k.a), ex[t]);
@@ -1235,25 +1353,25 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
         BSW_TRY(grow(s.d_ref, s.cap_ref, (size_t)r_tot + 4));
         BSW_TRY(grow(s.d_qer, s.cap_qer, (size_t)q_tot + 4));
         BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)N));
-        BSW_TRY(hipMemsetAsync(s.d_ref + r_tot, 0, 4, s.stream));
-        BSW_TRY(hipMemsetAsync(s.d_qer + q_tot, 0, 4, s.stream));
         const int64_t tr = (r_tot + 15) / 16, tq = (q_tot + 15) / 16;
-        if (tr > 0)
-            hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, s.stream,
-                               s.d_stage + ref_off, s.d_ref, r_tot);
-        if (tq > 0)
-            hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, s.stream,
-                               s.d_stage + qer_off, s.d_qer, q_tot);
         const int32_t ne = (int32_t)(n_r + n_q);
-        if (ne > 0)
-            hipLaunchKernelGGL(patch_codes_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s.stream,
-                               (const uint32_t *)(s.d_stage + exc_off), (int32_t)n_r, ne, s.d_ref, s.d_qer);
-        hipLaunchKernelGGL(expand_pairs_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s.stream,
-                           (const PairIn *)(s.d_stage + pair_off), s.d_pairs, N);
+        const int64_t nthr = tr + tq + N;
+        hipLaunchKernelGGL(stage_in_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s.stream,
+                           s.d_stage + ref_off, r_tot, s.d_stage + qer_off, q_tot,
+                           (const uint32_t *)(s.d_stage + exc_off), (int32_t)n_r, ne,
+                           (const PairIn *)(s.d_stage + pair_off), N, s.d_ref, s.d_qer, s.d_pairs,
+                           s.d_meta + kMetaErr);
         BSW_TRY(hipGetLastError());
         PlanCall pc;
         pc.d_pairs = s.d_pairs; pc.d_ref = s.d_ref; pc.d_qer = s.d_qer;
         pc.n = N; pc.w = w; pc.cell_bits = cell_bits; pc.stream = s.stream;
+        int gq_max = 0;
+        for (size_t t = 0; t < tasks.size(); ++t)
+            if (tasks[t].kind == 0) gq_max = (gq_max < 0 || gq_maxq[t] < 0) ? -1 : std::max(gq_max, gq_maxq[t]);
+        pc.gq_cols = gq_max < 0 ? -1 : gq_cols_for(gq_max);
+        // host-checked row-group batch: the kernel writes the 24 output bytes per pair straight
+        // into the staging buffer (its inputs were expanded out of it above)
+        if (pc.gq_cols > 0) pc.d_out24 = (int32_t *)s.d_stage;
         int r = run_plan(kp, s, pc);
         const auto tg2 = std::chrono::steady_clock::now();
         if (!r) r = run_dp(kp, s);
@@ -1262,9 +1380,11 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
             (void)hipStreamSynchronize(s.stream);
             return r;
         }
-        hipLaunchKernelGGL(gather_outputs_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s.stream,
-                           s.d_pairs, (int32_t *)s.d_stage, N);
-        BSW_TRY(hipGetLastError());
+        if (!(s.fast == 2 && s.plan.d_out24)) {
+            hipLaunchKernelGGL(gather_outputs_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s.stream,
+                               s.d_pairs, (int32_t *)s.d_stage, N);
+            BSW_TRY(hipGetLastError());
+        }
         BSW_TRY(hipMemcpyAsync(s.h_stage, s.d_stage, (size_t)N * 24, hipMemcpyDeviceToHost, s.stream));
         if ((r = finish_stats(s))) return r;
         const auto tg4 = std::chrono::steady_clock::now();
@@ -1757,7 +1877,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
         agg.kernel_ms = std::max(agg.kernel_ms, st[d].kernel_ms);
         agg.n_i16 += st[d].n_i16; agg.n_u8 += st[d].n_u8; agg.n_wide += st[d].n_wide; agg.n_packed += st[d].n_packed;
         agg.n_launches += st[d].n_launches;
-        agg.n_wave += st[d].n_wave;
+        agg.n_wave += st[d].n_wave; agg.n_group += st[d].n_group;
         agg.stage_ms = std::max(agg.stage_ms, st[d].stage_ms);
         agg.host_ms = std::max(agg.host_ms, st[d].host_ms);
     }
@@ -2242,6 +2362,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     case BSW_OPT_HOST_CHUNK: if (value < 1 || value > INT32_MAX) return BSW_E_INVAL; ctx->host_chunk = (int32_t)value; return BSW_OK;
     case BSW_OPT_HOST_PACK: if (value != 2 && value != 4) return BSW_E_INVAL; ctx->host_pack = (int)value; return BSW_OK;
     case BSW_OPT_SMALL_BATCH: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.small_batch = (int32_t)value; return BSW_OK;
+    case BSW_OPT_GROUP_KERNEL: if (!b01) return BSW_E_INVAL; ctx->kp.group_kernel = (int8_t)value; return BSW_OK;
     case BSW_OPT_SPLIT_MIN: if (value < 0) return BSW_E_INVAL; ctx->split_min = value; return BSW_OK;
     case BSW_OPT_COALESCE: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->coalesce = (int32_t)value; return BSW_OK;
     case BSW_OPT_COALESCE_LEADERS:

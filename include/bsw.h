@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BSW_ABI_VERSION 5
+#define BSW_ABI_VERSION 6
 
 enum {
     BSW_OK = 0,
@@ -110,6 +110,8 @@ typedef struct bsw_stats_t {
                                    (queries past 160 columns; ABI version 4)             */
     int32_t n_devices;          /* host-buffer calls: logical devices the call ran on
                                    (1, or all of them when split; ABI version 5)         */
+    int32_t n_group;            /* of n_i16: pairs run on the small-batch row-group kernel
+                                   (16 lanes per pair; ABI version 6)                    */
 } bsw_stats_t;
 int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
 
@@ -155,6 +157,10 @@ enum {
                                  staging buffer, one plan / sort / DP, outputs scattered back);
                                  a lone caller runs at once.  Outputs are identical either way */
     BSW_OPT_COALESCE_LEADERS = 12, /* coalesced batches in flight per device (1..16, default 4) */
+    BSW_OPT_GROUP_KERNEL = 13, /* small batches (BSW_OPT_SMALL_BATCH): 1 = the row-group kernel
+                                 (16 lanes per pair, queries <= 160, no plan / sort; default),
+                                 0 = the planned path with the wave-per-alignment kernel.
+                                 Outputs are identical either way                              */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };

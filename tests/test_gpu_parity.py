@@ -313,24 +313,90 @@ def test_host_pipeline_packing(pack, p_n):
     e.close()
 
 
+@pytest.mark.parametrize("group", [1, 0])
 @pytest.mark.parametrize("n", [1, 63, 1000, 16384, 16385])
-def test_small_batch_route(n, c2_full):
-    """Default routing (BSW_OPT_SMALL_BATCH = 16384): calls of at most 16384 pairs run every
-    int16-safe pair on the wave-per-alignment kernel (latency-bound regime), larger ones on the
-    lane / packed-column classes; both entry points (host buffers, resident) and both cell widths
-    give the oracle's outputs."""
+def test_small_batch_route(n, group, c2_full):
+    """Default routing (BSW_OPT_SMALL_BATCH = 16384): calls of at most 16384 pairs run on the
+    row-group kernel (16 lanes per pair, no plan / sort; BSW_OPT_GROUP_KERNEL 1) or, with it off,
+    every int16-safe pair on the wave-per-alignment kernel; larger calls on the lane /
+    packed-column classes.  Both entry points (host buffers, resident) and both cell widths give
+    the oracle's outputs."""
     pairs, ref, qer, want = c2_full
-    e = bsw.Engine()
+    e = bsw.Engine(group_kernel=group)
+    small = n <= 16384
     for cell_bits in (16, 8):
         got = pairs[:n].copy()
         e.get_scores(got, ref, qer, 100, cell_bits)
         _assert_same(want[:n], got, f"n {n} cell_bits {cell_bits}")
         st = e.last_stats()
-        assert st.n_wave == (n if n <= 16384 else 0)
+        assert st.n_group == (n if small and group else 0)
+        assert st.n_wave == (n if small and not group else 0)
         assert st.n_i16 + st.n_u8 + st.n_wide == n
     dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (pairs[:n].copy(), ref, qer))
     e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, n, 100, 16)
     _assert_same(want[:n], dp.download(np.empty_like(pairs[:n])), f"device n {n}")
+    assert e.last_stats().n_group == (n if small and group else 0)
+    e.close()
+
+
+@pytest.mark.parametrize("w", [0, 1, 7, 100, 200])
+def test_group_kernel_random(w):
+    """The row-group kernel over random shapes (queries 0..160, targets 0..400, h0 0..200),
+    both entry points: host buffers (host-checked contract) and device buffers (kernel-checked,
+    flag read back)."""
+    e = bsw.Engine()
+    pairs, ref, qer = bswgen.random_pairs(3000, seed=900 + w, tlen=(0, 400), qlen=(0, 160), h0=(0, 200))
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+    got = pairs.copy()
+    e.get_scores(got, ref, qer, w)
+    _assert_same(want, got, f"group kernel host w={w}")
+    assert e.last_stats().n_group == len(pairs)
+    dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (pairs.copy(), ref, qer))
+    e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, len(pairs), w, 16)
+    _assert_same(want, dp.download(np.empty_like(pairs)), f"group kernel device w={w}")
+    assert e.last_stats().n_group == len(pairs)
+    e.close()
+
+
+def test_group_kernel_golden(golden):
+    """Every golden batch on the default engine (small batches: the row-group kernel where the
+    scoring qualifies, the planned path otherwise) and on the device entry point."""
+    engines, ran = {}, 0
+    for name, pairs, ref, qer, w, sc in golden:
+        key = tuple(sorted(sc.items()))
+        if key not in engines:
+            engines[key] = bsw.Engine(_gparams(sc))
+        got = pairs.copy()
+        for f in bsw.OUT_FIELDS:
+            got[f] = -9
+        engines[key].get_scores(got, ref, qer, w)
+        _assert_same(pairs, got, f"golden {name} default route")
+        ran += engines[key].last_stats().n_group
+        dev = pairs.copy()
+        for f in bsw.OUT_FIELDS:
+            dev[f] = -9
+        dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (dev, ref, qer))
+        engines[key].get_scores_device(dp.ptr, dr.ptr, dq.ptr, len(pairs), w, 16)
+        _assert_same(pairs, dp.download(np.empty_like(pairs)), f"golden {name} device route")
+    assert ran > 0
+    for e in engines.values():
+        e.close()
+
+
+def test_group_kernel_fallback_device():
+    """Device entry point, small batch with a few pairs outside the row-group contract (query past
+    160, int16-unsafe h0): the kernel flags them and the whole batch reruns on the planned path."""
+    pairs, ref, qer = bswgen.random_pairs(2000, seed=4242, tlen=(0, 400), qlen=(0, 160), h0=(0, 200))
+    pairs["h0"][7] = 32000
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    e = bsw.Engine()
+    dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (pairs.copy(), ref, qer))
+    e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, len(pairs), 100, 16)
+    _assert_same(want, dp.download(np.empty_like(pairs)), "group kernel fallback")
+    st = e.last_stats()
+    assert st.n_group == 0 and st.n_i16 + st.n_u8 + st.n_wide == len(pairs)
     e.close()
 
 

@@ -43,6 +43,8 @@ int main(int argc, char **argv)
     bsw_ctx_t *ctx = nullptr;
     if (bsw_create(&p, 0, 1, &ctx) != BSW_OK) { fprintf(stderr, "bsw_create failed\n"); return 2; }
     if (const char *l = getenv("PERCALL_LEADERS")) bsw_set_option(ctx, BSW_OPT_COALESCE_LEADERS, atoi(l));
+    if (const char *g = getenv("PERCALL_GROUP")) bsw_set_option(ctx, BSW_OPT_GROUP_KERNEL, atoi(g));
+    if (const char *b = getenv("PERCALL_SMALL")) bsw_set_option(ctx, BSW_OPT_SMALL_BATCH, atoi(b));
     std::vector<SeqPair> want = pairs;
     if (bsw_get_scores(ctx, want.data(), ref.data(), qer.data(), N, 100, 16) != BSW_OK) return 3;
     printf("{\"tool\": \"percall_bench\", \"threads\": %d, \"pairs\": %d, \"curve\": [", T, N);
