@@ -424,8 +424,10 @@ def main():
     # kernel; BSW_PK=1 selects the two-pairs-per-lane kernel for those pairs instead
     packed = 2 * st.n_packed > args.pairs
     wave = 2 * st.n_wave > args.pairs
-    kname = "pc_kernel<160>" if packed else (f"wv_kernel<{wave_cols(cfg.qlen, args.w)}>" if wave
-                                             else "lane_kernel<160>")
+    group = 2 * st.n_group > args.pairs              # small batches: the row-group kernel (device
+    kname = ("gq_kernel<10>" if group else           #   calls run its 10-column form)
+             "pc_kernel<160>" if packed else (f"wv_kernel<{wave_cols(cfg.qlen, args.w)}>" if wave
+                                              else "lane_kernel<160>"))
     roof = {
         "bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
         "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
@@ -448,7 +450,7 @@ def main():
                    "pairs_per_gpu": args.pairs, "parallelism": f"shard{world} (independent pairs)",
                    "distinct_gpus": args.distinct_gpus,
                    "routing": {"n_packed": st.n_packed, "n_i16": st.n_i16, "n_u8": st.n_u8, "n_wide": st.n_wide,
-                               "n_wave": st.n_wave,
+                               "n_wave": st.n_wave, "n_group": st.n_group,
                                "int16_fallback_fraction": (round(st.n_i16 / max(1, st.n_i16 + st.n_u8), 4)
                                                            if args.cell_bits == 8 else None)}},
         "roofline": roof,

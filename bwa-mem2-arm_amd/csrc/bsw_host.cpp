@@ -1141,12 +1141,19 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         int32_t seq = 0;
         const int32_t nblk = (int32_t)bs.size();
         const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
-        // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
-        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
-        for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 2)) {
-            // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
+        // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot).
+        // Larger calls: a one-block head chunk (4K pairs: staged and on the row-group kernel in
+        // ~0.3 ms, so the GPU starts early), then 4, 16 blocks, then `chunk`; the last block is
+        // its own chunk, so the call's tail after the final staging is one short row-group
+        // launch instead of a lane-kernel wave's ~1.2 ms lifetime
+        const bool ramp = nblk > 32;
+        int32_t cur = ramp ? 1 : std::min(cap_blk, nblk);
+        for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 4)) {
+            int32_t want = cur;
+            if (ramp && nblk - b > 1 && nblk - b <= want + 1) want = nblk - b - 1;
+            // `want` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
             int64_t bytes = 0;
-            for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
+            for (nb = 0; nb < want && b + nb < nblk; ++nb) {
                 const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
                 if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
                 bytes += x;

@@ -31,10 +31,10 @@ def rows(pattern):
 def short(name):
     if 'smem_kernel' in name:
         return 'smem_kernel'
-    for kern in ('glob_lane_kernel', 'glob_band_kernel', 'glob_wide_kernel', 'wv_kernel', 'pc_kernel',
+    for kern in ('glob_lane_kernel', 'glob_band_kernel', 'glob_wide_kernel', 'wv_kernel', 'gq_kernel', 'pc_kernel',
                  'pk_kernel', 'lane_kernel', 'mate_kernel'):
         if kern in name:
-            for q in ('160', '128', '96', '80', '64', '48', '32', '16', '8', '4'):
+            for q in ('160', '128', '96', '80', '64', '48', '32', '16', '10', '8', '6', '4'):
                 if f'ILi{q}E' in name or f'<{q},' in name or f'<{q}>' in name:
                     return f'{kern}<{q}>'
             return kern
