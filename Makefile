@@ -16,8 +16,8 @@ SYNTH    := $(LIBDIR)/libbsw_synth.so
 SHIMTEST := $(LIBDIR)/bsw_shim_example
 ORACLE   := oracle/liboracle.so
 
-HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pc.hip $(CSRC)/bsw_wv.hip $(CSRC)/bsw_gq.hip $(CSRC)/bsw_mate.hip $(CSRC)/bsw_global.hip $(CSRC)/bsw_ext_dev.hip $(CSRC)/bsw_fmi.hip $(CSRC)/bsw_fmi_build.hip $(CSRC)/bsw_memchain.hip $(CSRC)/bsw_chain.hip $(CSRC)/bsw_host.cpp $(CSRC)/bsw_ext.cpp $(CSRC)/bsw_pack.cpp
-HIP_HDRS := $(CSRC)/bsw_pool.h $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h $(CSRC)/bsw_fmi_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h include/bsw_fmi.h
+HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pc.hip $(CSRC)/bsw_wv.hip $(CSRC)/bsw_gq.hip $(CSRC)/bsw_mate.hip $(CSRC)/bsw_global.hip $(CSRC)/bsw_ext_dev.hip $(CSRC)/bsw_fmi.hip $(CSRC)/bsw_fmi_build.hip $(CSRC)/bsw_memchain.hip $(CSRC)/bsw_chain.hip $(CSRC)/bsw_host.cpp $(CSRC)/bsw_ext.cpp $(CSRC)/bsw_pack.cpp $(CSRC)/bsw_devcache.cpp
+HIP_HDRS := $(CSRC)/bsw_devcache.h $(CSRC)/bsw_pool.h $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h $(CSRC)/bsw_fmi_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h include/bsw_fmi.h
 
 all: product synth oracle percall
 
@@ -75,10 +75,13 @@ $(LIBDIR)/bsw_ext.o: $(CSRC)/bsw_ext.cpp $(HIP_HDRS) | $(LIBDIR)
 $(LIBDIR)/bsw_pack.o: $(CSRC)/bsw_pack.cpp $(CSRC)/bsw_internal.h | $(LIBDIR)
 	g++ -O3 -std=c++17 -fPIC -Wall -Iinclude -c $< -o $@
 
+$(LIBDIR)/bsw_devcache.o: $(CSRC)/bsw_devcache.cpp $(CSRC)/bsw_devcache.h | $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/bsw_batch.o: $(CSRC)/bsw_batch.c include/bsw_batch.h include/bsw.h | $(LIBDIR)
 	gcc $(CFLAGS) -std=c11 -c $< -o $@
 
-$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_batch.o
+$(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_devcache.o $(LIBDIR)/bsw_batch.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 $(SYNTH): $(CSRC)/bsw_synth.c include/bsw_seqpair.h | $(LIBDIR)
@@ -96,7 +99,7 @@ STATSLIB := $(LIBDIR)/libbsw_hip_stats.so
 stats: $(STATSLIB)
 $(LIBDIR)/bsw_pc_stats.o: $(CSRC)/bsw_pc.hip $(HIP_HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DBSW_PC_STATS -c $< -o $@
-$(STATSLIB): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_stats.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_batch.o
+$(STATSLIB): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_stats.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_devcache.o $(LIBDIR)/bsw_batch.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 # experiment build: the product with bsw_pc.hip compiled under AB_FLAGS (tools/gpu_ab.sh A/B runs)
@@ -104,7 +107,7 @@ ABLIB := $(LIBDIR)/libbsw_hip_ab.so
 AB_FLAGS ?=
 ab:
 	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/bsw_pc.hip -o $(LIBDIR)/bsw_pc_ab.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(ABLIB) $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_ab.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_batch.o -lpthread
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(ABLIB) $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_ab.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_devcache.o $(LIBDIR)/bsw_batch.o -lpthread
 
 .PHONY: all product synth oracle percall clean stats ab
 

@@ -19,6 +19,7 @@
 #include <chrono>
 #include "../../include/bsw_ext.h"
 #include "bsw_internal.h"
+#include "bsw_devcache.h"
 
 namespace {
 
@@ -220,28 +221,6 @@ float ms_since(std::chrono::steady_clock::time_point t0)
     return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-struct Buf {                       // device allocations of one call, freed on every path
-    int device;
-    static constexpr int kMax = 24;
-    void *p[kMax] = {};
-    int n = 0;
-    explicit Buf(int d) : device(d) {}
-    template <class T>
-    hipError_t get(T *&out, size_t count)
-    {
-        if (n == kMax) return hipErrorInvalidValue;
-        void *q = nullptr;
-        const hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
-        if (e == hipSuccess) { p[n++] = q; out = (T *)q; }
-        return e;
-    }
-    ~Buf()
-    {
-        (void)hipSetDevice(device);
-        for (int k = 0; k < n; ++k) (void)hipFree(p[k]);
-    }
-};
-
 #define CH_TRY(x)                                                                            \
     do {                                                                                     \
         const hipError_t e_ = (x);                                                           \
@@ -269,7 +248,19 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
     if (const int rc = ext_opt_check(opt, ref_len)) return rc;
     ChainParams p{prm.o_del, prm.e_del, prm.o_ins, prm.e_ins, prm.mat[0], opt->w, ref_len, opt->l_pac};
     const auto tp = std::chrono::steady_clock::now();
-    Buf B(dev);
+    // a cached stream + pinned readback words and cached scratch (bsw_devcache.h): no driver
+    // allocations per call.  B is destroyed first: it synchronises the stream, then returns its
+    // blocks; the lease goes back last
+    StreamLease L;
+    CH_TRY(stream_lease(dev, L));
+    struct LeaseGuard {
+        StreamLease &l;
+        ~LeaseGuard() { (void)hipStreamSynchronize(l.s); stream_return(l); }
+    } lg{L};
+    hipStream_t st = L.s;
+    int32_t *h = L.h;                                   // pinned readback of the round's job count
+    CachedBufs B(dev);
+    B.stream = st;
     int32_t *sbeg, *send, *order, *chain_of, *pos, *nav, *av, *cnt, *jsi, *jrun, *jlen, *err;
     int64_t *joff, *cwin, *jwin;
     bsw_seed_t *jseed;
@@ -281,21 +272,6 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
     CH_TRY(B.get(jsi, nr)); CH_TRY(B.get(jrun, nr)); CH_TRY(B.get(jlen, nr)); CH_TRY(B.get(joff, nr));
     CH_TRY(B.get(jseed, nr)); CH_TRY(B.get(jout, nr));
     CH_TRY(B.get(cwin, 2 * (size_t)ns)); CH_TRY(B.get(jwin, 2 * nr));
-    // the pinned word's guard is declared first so it is destroyed last: the stream guard
-    // drains any queued D2H into it before it is freed
-    int32_t *h = nullptr;                               // pinned readback of the round's job count
-    struct HostGuard {
-        int32_t *h;
-        ~HostGuard() { if (h) (void)hipHostFree(h); }
-    } hg{nullptr};
-    CH_TRY(hipHostMalloc((void **)&h, 2 * sizeof(int32_t), 0));
-    hg.h = h;
-    hipStream_t st = nullptr;
-    CH_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    struct StreamGuard {
-        hipStream_t s;
-        ~StreamGuard() { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); }
-    } sg{st};
     CH_TRY(hipMemsetAsync(sbeg, 0, nr * sizeof(int32_t), st));
     CH_TRY(hipMemsetAsync(send, 0, nr * sizeof(int32_t), st));
     CH_TRY(hipMemsetAsync(err, 0, sizeof(int32_t), st));
@@ -364,8 +340,9 @@ extern "C" int bsw_chain2aln_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, co
                           sizeof(int32_t) * (size_t)n_seeds, sizeof(bsw_alnreg_t) * (size_t)n_seeds,
                           sizeof(int32_t) * (size_t)n_seeds};
     int rc = BSW_OK;
+    const int dev = bsw::ctx_device(ctx);
     for (int k = 0; k < 7 && rc == BSW_OK; ++k)
-        if (hipMalloc(&d[k], std::max<size_t>(sz[k], 1)) != hipSuccess) rc = BSW_E_NOMEM;
+        if (bsw::devcache_get(dev, std::max<size_t>(sz[k], 1), &d[k]) != hipSuccess) rc = BSW_E_NOMEM;
     const void *src[5] = {read_off, read_len, seeds, seed_read, seed_chain};
     for (int k = 0; k < 5 && rc == BSW_OK; ++k)
         if (hipMemcpy(d[k], src[k], sz[k], hipMemcpyHostToDevice) != hipSuccess) rc = BSW_E_HIP;
@@ -377,8 +354,9 @@ extern "C" int bsw_chain2aln_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, co
     if (rc == BSW_OK && (hipMemcpy(out, d[5], sz[5], hipMemcpyDeviceToHost) != hipSuccess ||
                          hipMemcpy(extended, d[6], sz[6], hipMemcpyDeviceToHost) != hipSuccess))
         rc = BSW_E_HIP;
-    for (int k = 0; k < 7; ++k)
-        if (d[k]) (void)hipFree(d[k]);
+    (void)hipDeviceSynchronize();                      // (blocking copies above; an error path
+    for (int k = 0; k < 7; ++k)                         //  may have left work queued)
+        bsw::devcache_put(dev, d[k], std::max<size_t>(sz[k], 1));
     bsw::set_chain_stats(ctx, cs);
     return rc;
 }

@@ -54,7 +54,8 @@ constexpr int kMetaSpread = 32;             // slots: block b adds into slot b %
 constexpr int kMetaMaxq = kMetaCounts * kMetaSpread;   // d_meta: counts[32][16], maxq_wide, err
 constexpr int kMetaErr = kMetaMaxq + 1;
 constexpr int kMetaFlag = kMetaErr + 1;     // row-group kernel: a pair outside its contract
-constexpr int kMetaWords = kMetaFlag + 1;
+constexpr int kMetaCnt = kMetaFlag + 1;     // extension pipeline: band-retry count readback
+constexpr int kMetaWords = kMetaCnt + 1;
 constexpr int kKeyBits = 32;                // 4 class + 8 qlen + 1 related + 11 tlen + 8 h0 bits
 static_assert(kNumClasses <= kMetaCounts, "class counts");
 
@@ -1141,19 +1142,12 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         int32_t seq = 0;
         const int32_t nblk = (int32_t)bs.size();
         const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
-        // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot).
-        // Larger calls: a one-block head chunk (4K pairs: staged and on the row-group kernel in
-        // ~0.3 ms, so the GPU starts early), then 4, 16 blocks, then `chunk`; the last block is
-        // its own chunk, so the call's tail after the final staging is one short row-group
-        // launch instead of a lane-kernel wave's ~1.2 ms lifetime
-        const bool ramp = nblk > 32;
-        int32_t cur = ramp ? 1 : std::min(cap_blk, nblk);
-        for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 4)) {
-            int32_t want = cur;
-            if (ramp && nblk - b > 1 && nblk - b <= want + 1) want = nblk - b - 1;
-            // `want` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
+        // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
+        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
+        for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 2)) {
+            // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
             int64_t bytes = 0;
-            for (nb = 0; nb < want && b + nb < nblk; ++nb) {
+            for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
                 const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
                 if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
                 bytes += x;
@@ -1688,19 +1682,23 @@ static int ext_side_device(const KParams &kp0, Slot &s, const ExtDevParams &xp, 
                              s.d_xt, d_out, st));
     int r = run_device(kp, s, s.d_xpairs, s.d_xt, s.d_xq, n, opt.w, 16, st);
     if (r) return r;
-    if ((r = finish_stats(s))) return r;
-    es.kernel_ms += s.stats.kernel_ms;
-    for (int t = 1; t < opt.max_band_try; ++t) {
+    // each DP batch, the next band-retry mark and its count readback are queued before one wait
+    // (finish_stats), so a retry level costs one host round trip, not two
+    for (int t = 1;; ++t) {
+        const bool retry = t < opt.max_band_try;
         const int32_t wt = opt.w << (t - 1), wn = opt.w << t;
-        BSW_TRY(launch_ext_retry_mark(t == 1 ? s.d_xpairs : s.d_xsub, s.d_xsub, s.d_xst, n, wt, d_cnt, st));
-        int32_t cnt = 0;
-        BSW_TRY(hipMemcpyAsync(&cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
-        BSW_TRY(hipStreamSynchronize(st));
+        if (retry) {
+            BSW_TRY(launch_ext_retry_mark(t == 1 ? s.d_xpairs : s.d_xsub, s.d_xsub, s.d_xst, n, wt, d_cnt, st));
+            BSW_TRY(hipMemcpyAsync(s.h_meta + kMetaCnt, d_cnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        }
+        if ((r = finish_stats(s))) return r;
+        es.kernel_ms += s.stats.kernel_ms;
+        if (!retry) break;
+        BSW_TRY(hipStreamSynchronize(st));          // (idle already unless the batch was empty)
+        const int32_t cnt = s.h_meta[kMetaCnt];
         if (cnt == 0) break;
         es.n_pairs[(left ? 0 : 2) + 1] += cnt;
         if ((r = run_device(kp, s, s.d_xsub, s.d_xt, s.d_xq, n, wn, 16, st))) return r;
-        if ((r = finish_stats(s))) return r;
-        es.kernel_ms += s.stats.kernel_ms;
         BSW_TRY(launch_ext_retry_merge(s.d_xpairs, s.d_xsub, s.d_xst, n, wn, left, st));
     }
     BSW_TRY(launch_ext_interp(left, xp, d_len, d_seeds, n, s.d_xpairs, s.d_xst, d_out, st));

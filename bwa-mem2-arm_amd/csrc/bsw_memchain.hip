@@ -20,6 +20,7 @@
 #include <algorithm>
 #include "../../include/bsw_fmi.h"
 #include "bsw_fmi_internal.h"
+#include "bsw_devcache.h"
 
 namespace {
 
@@ -345,33 +346,14 @@ int hip_rc(hipError_t e) { return e == hipSuccess ? BSW_OK : (e == hipErrorOutOf
         if (rc_) return rc_;                               \
     } while (0)
 
-struct DevBufs {                                        // one call's scratch, freed on every path
-    static constexpr int kMax = 16;
-    int device;
-    void *p[kMax] = {};
-    int n = 0;
-    explicit DevBufs(int d) : device(d) {}
-    template <class T>
-    hipError_t get(T *&out, size_t count)
-    {
-        if (n == kMax) return hipErrorInvalidValue;
-        void *q = nullptr;
-        const hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
-        if (e == hipSuccess) { p[n++] = q; out = (T *)q; }
-        return e;
-    }
-    ~DevBufs()
-    {
-        (void)hipSetDevice(device);
-        for (int k = 0; k < n; ++k) (void)hipFree(p[k]);
-    }
-};
+using bsw::CachedBufs;
 
 int run_chain(const bsw::FmiView &f, const COpt &o, const int32_t *d_len, int32_t n, const bsw_bwtintv_t *d_mems,
               int32_t cap, const int32_t *d_nm, bsw_seed_t *d_seeds, int32_t *d_sr, int32_t *d_sc, int64_t seed_cap,
               int64_t *n_seeds, hipStream_t s)
 {
-    DevBufs B(f.device);
+    CachedBufs B(f.device);
+    B.stream = s;
     int64_t *cnt, *off, *kcnt, *koff;
     int32_t *n_kept;
     MC_TRY(B.get(cnt, (size_t)n + 1));
