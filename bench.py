@@ -342,6 +342,8 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000, help="c4: reads per GPU per step")
     ap.add_argument("--ref-mb", type=int, default=64, help="c4: random reference size (Mb)")
     ap.add_argument("--smem-ref-mb", type=int, default=16, help="smem: reference size (Mb) of the FM-index")
+    ap.add_argument("--fmi-blocks-only", action="store_true",
+                    help="smem / c1 / c4mem: index without the text-mode data (BSW_FMI_NO_TEXT; A/B)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="weak (default): every rank scores its own resident 1M-pair shard; strong: one "
@@ -855,7 +857,7 @@ def main_mem(args, rank, local, world, c1: bool):
                           flush=True)
     log(f"generated {n} reads vs {len(ref)} bases")
     t = time.perf_counter()
-    fmi = bsw.Fmi(ref, device=local)
+    fmi = bsw.Fmi(ref, device=local, flags=(bsw.FMI_NO_TEXT if args.fmi_blocks_only else None))
     build_s = time.perf_counter() - t
     log(f"index built in {build_s:.1f} s")
     T = np.concatenate([ref, (3 - ref[::-1])]).astype(np.uint8)
@@ -947,7 +949,8 @@ def main_mem(args, rank, local, world, c1: bool):
         "extensions_per_step_rank0": list(st.n_pairs),
         "full_length_fraction": round(float(np.mean(best == 150)), 4) if c1 else None,
         "index_build_s": round(build_s, 2), "synth_gen_s": round(gen_s, 2),
-        "index": {"wide_64bit": bool(2 * len(ref) + 2 >= 2**32), "device_bytes": int(fmi.info().device_bytes),
+        "index": {"wide_64bit": bool(2 * len(ref) + 2 >= 2**32), "text_mode": not args.fmi_blocks_only,
+                  "device_bytes": int(fmi.info().device_bytes),
                   "built_on": "gpu" if len(ref) >= (64 << 20) else "host"},
     }
     if world == 1 and not args.no_cpu and len(ref) > 512_000_000:
@@ -1214,7 +1217,7 @@ def main_smem(args, rank, local, world):
     reads, off, lens = seeding_reads(ref, args.reads, L, seed=11 + rank)
     gen_s = time.perf_counter() - t0
     t0 = time.perf_counter()
-    fmi = bsw.Fmi(ref, device=local)
+    fmi = bsw.Fmi(ref, device=local, flags=(bsw.FMI_NO_TEXT if args.fmi_blocks_only else None))
     build_s = time.perf_counter() - t0
     d_reads, d_off, d_len = (hiprt.DeviceBuffer.from_array(a) for a in (reads, off, lens))
     d_mems = hiprt.DeviceBuffer(args.reads * cap * 32)

@@ -45,7 +45,15 @@ struct FmiDevT {                     // kernel view of the resident index (U = r
     U count[5];
     U sentinel;
     U n;                             // |T|
+    // text mode (null when built with BSW_FMI_NO_TEXT): T with 0xFF padding past n, SA, SA^-1
+    const uint8_t *text;
+    const U *sa;
+    const U *isa;
 };
+
+// text-mode interval entries keep the occurrence's text position in k; their end carries this
+// flag (k, l are resolved through SA^-1 only when the interval is output)
+constexpr uint32_t kTextFlag = 0x80000000u;
 
 struct MemOpt {
     int32_t min_seed_len, split_width, max_mem_intv, split_len;
@@ -140,6 +148,37 @@ __device__ __forceinline__ IvT<U> set_intv(const FmiDevT<U> &f, int c)
     return IvT<U>{k, l, k1 - k};
 }
 
+// 4 bytes at p (any alignment) from aligned dword loads; p .. p + 7 must be readable
+__device__ __forceinline__ uint32_t load4u(const uint8_t *p)
+{
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
+}
+
+// the number of leading j < lim with q[j] == T[tp + j]: the text's 0xFF padding ends a run at
+// the text end and a read N (4) never equals a text base
+__device__ __forceinline__ int match_run(const uint8_t *__restrict__ T, uint64_t tp, const uint8_t *__restrict__ q,
+                                         int lim)
+{
+    int j = 0;
+    while (lim - j >= 8) {
+        const uint32_t x = load4u(T + tp + j) ^ load4u(q + j);
+        if (x) return j + (__builtin_ctz(x) >> 3);
+        j += 4;
+    }
+    while (j < lim && q[j] == T[tp + j]) ++j;
+    return j;
+}
+
+// the (k, l) of q[b, e) occurring (once) at text position p: rows of that suffix and of the
+// reverse complement's occurrence at n - p - (e - b) (T = ref + revcomp(ref))
+template <class U>
+__device__ __forceinline__ IvT<U> text_intv(const FmiDevT<U> &f, U p, int len)
+{
+    return IvT<U>{f.isa[p], f.isa[f.n - p - (U)len], (U)1};
+}
+
 // ---------------------------------------------------------------- device: per-read passes
 
 template <class U>
@@ -187,7 +226,25 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
     IvT<U> ik = set_intv(f, qx);
     U ikend = (U)(x + 1);
     int nc = 0, i;
+    const bool text = f.text && min_intv <= 1;
     for (i = x + 1; i < len; ++i) {                      // forward search
+        if (text && ik.s == 1) {
+            // one occurrence left: every further step keeps s = 1 while the read matches the
+            // text after it, and the first step that does not (mismatch, read N, text end) pushes
+            // ik and stops -- so compare read and text directly, then push ik as a text-mode
+            // entry (its k, l are only needed if it is output)
+            const U p = f.sa[ik.k];
+            const int e = i + match_run(f.text, (uint64_t)p + (uint64_t)(i - x), q + i, len - i);
+            ik.k = p;
+            ikend = (U)((uint32_t)e | kTextFlag);
+            if (e < len) {
+                if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
+                else L.overflow = 1;
+                ++nc;
+            }
+            i = e;
+            break;
+        }
         const int qi = q[i];
         if (qi < 4) {
             const IvT<U> ok = forward_ext(f, ik, qi);
@@ -212,7 +269,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
     }
     nc = min(nc, L.scap);
     // upstream reverses curr (longest matches first); here prev is read back to front once
-    const int ret = (int)curr[(size_t)(nc - 1) * st].e;
+    const int ret = (int)((uint32_t)curr[(size_t)(nc - 1) * st].e & ~kTextFlag);
     { EntT<U> *t = curr; curr = prev; prev = t; }
     int np = nc;
     bool rev = true;
@@ -224,19 +281,33 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
         U last_cs = 0;
         for (int j = 0; j < np; ++j) {
             const EntT<U> pv = prev[(size_t)(rev ? np - 1 - j : j) * st];
-            const IvT<U> p = {pv.k, pv.l, pv.s};
+            const bool tm = ((uint32_t)pv.e & kTextFlag) != 0;   // text mode: pv.k = text position
+            const uint32_t pe = (uint32_t)pv.e & ~kTextFlag;
             IvT<U> ok = {0, 0, 0};
-            if (c >= 0) ok = backward_ext(f, p, c);
+            if (c >= 0) {
+                if (tm) {                                   // one occurrence: the base before it
+                    if (pv.k > 0 && f.text[pv.k - 1] == (uint8_t)c) ok = IvT<U>{pv.k - 1, 0, 1};
+                } else {
+                    ok = backward_ext(f, IvT<U>{pv.k, pv.l, pv.s}, c);
+                }
+            }
             if (c < 0 || ok.s < min_intv) {
                 if (nc == 0) {
                     if (nmem == 0 || (uint32_t)(i + 1) < last_start) {
                         last_start = (uint32_t)(i + 1);
                         ++nmem;
-                        if ((int)((uint32_t)pv.e - last_start) >= keep_len) push_out(L, p, last_start, (uint32_t)pv.e);
+                        if ((int)(pe - last_start) >= keep_len)
+                            push_out(L, tm ? text_intv(f, pv.k, (int)(pe - last_start)) : IvT<U>{pv.k, pv.l, pv.s},
+                                     last_start, pe);
                     }
                 }
             } else if (nc == 0 || ok.s != last_cs) {
-                if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ok.k, ok.l, ok.s, pv.e};
+                // an interval down to one occurrence continues in text mode (one SA load now,
+                // then cached text reads instead of occurrence blocks)
+                const bool to_text = f.text && ok.s == 1;
+                const U k2 = tm ? ok.k : (to_text ? f.sa[ok.k] : ok.k);
+                if (nc < L.scap)
+                    curr[(size_t)nc * st] = EntT<U>{k2, ok.l, ok.s, (U)(pe | ((tm || to_text) ? kTextFlag : 0u))};
                 else L.overflow = 1;
                 ++nc;
                 last_cs = ok.s;
@@ -259,6 +330,21 @@ __device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U> &L, int x, int min_le
     if (qx > 3) return x + 1;
     IvT<U> ik = set_intv(f, qx);
     for (int i = x + 1; i < L.len; ++i) {
+        if (f.text && ik.s == 1 && max_intv > 1) {
+            // one occurrence: the walk returns at i* = max(i, x + min_len) (every s is 0 or 1 <
+            // max_intv) unless a read N comes first; it pushes the interval if the read still
+            // matches the text through i*
+            const int is = max(i, x + min_len);
+            int t = i;
+            const int lim = min(is + 1, L.len);
+            while (t < lim && q[t] < 4) ++t;                 // first N in [i, is]
+            if (t < lim) return t + 1;
+            if (is >= L.len) return L.len;
+            const U p = f.sa[ik.k];
+            if (match_run(f.text, (uint64_t)p + (uint64_t)(i - x), q + i, is + 1 - i) == is + 1 - i)
+                push_out(L, text_intv(f, p, is + 1 - x), (uint32_t)x, (uint32_t)(is + 1));
+            return is + 1;
+        }
         const int qi = q[i];
         if (qi < 4) {
             const IvT<U> ok = forward_ext(f, ik, qi);
@@ -459,6 +545,8 @@ struct bsw_fmi {
     void *d_blk = nullptr;                    // FmiBlock (narrow) or FmiBlockW (wide)
     void *d_sa = nullptr;                     // uint32_t (narrow) or uint64_t (wide)
     uint8_t *d_bwt = nullptr;                 // GPU-built index: BWT codes (copy_bwt)
+    uint8_t *d_text = nullptr;                // text mode: T + 64 bytes of 0xFF padding
+    void *d_isa = nullptr;                    // text mode: SA^-1 (uint32_t or uint64_t)
     std::vector<uint32_t> sa;                 // host-built index: host copies (tests, bwt_sa)
     std::vector<FmiBlock> h_blk;              // host-only index (device < 0): the occurrence blocks
     std::vector<uint8_t> bwt;
@@ -536,6 +624,66 @@ int run_collect(bsw_fmi_t *f, const bsw_mem_opt_t *opt, const uint8_t *d_reads, 
 }
 
 // the runtime objects every device index needs
+// text mode (BSW_FMI_NO_TEXT off): T = ref + revcomp(ref) with 0xFF padding, and SA^-1
+__global__ void k_text_pad(const uint8_t *__restrict__ ref, int64_t len, uint8_t *__restrict__ T)
+{
+    const int64_t n = 2 * len;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len + 64;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < len) {
+            const uint8_t c = ref[i];
+            T[i] = c;
+            T[n - 1 - i] = (uint8_t)(3 - c);
+        } else {
+            T[n + (i - len)] = 0xFF;
+        }
+    }
+}
+template <class S>
+__global__ void k_isa(const S *__restrict__ sa, int64_t N, S *__restrict__ isa)
+{
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x)
+        isa[sa[r]] = (S)r;
+}
+
+int attach_text(bsw_fmi_t *f, const uint8_t *ref, int64_t len)
+{
+    const int64_t n = f->n, N = n + 1;
+    const size_t es = f->wide ? sizeof(uint64_t) : sizeof(uint32_t);
+    int rc = BSW_OK;
+    uint8_t *d_ref = nullptr;
+    if ((rc = hip_rc(hipSetDevice(f->device))) != BSW_OK) return rc;
+    if ((rc = hip_rc(hipMalloc(&f->d_text, (size_t)n + 64))) != BSW_OK) return rc;
+    if ((rc = hip_rc(hipMalloc(&f->d_isa, (size_t)N * es))) != BSW_OK) return rc;
+    if ((rc = hip_rc(hipMalloc(&d_ref, (size_t)std::max<int64_t>(len, 1)))) != BSW_OK) return rc;
+    rc = hip_rc(hipMemcpy(d_ref, ref, (size_t)len, hipMemcpyHostToDevice));
+    const unsigned grid = 1u << 16;                      // grid-stride (an AQL grid is 32-bit)
+    if (rc == BSW_OK) {
+        hipLaunchKernelGGL(k_text_pad, dim3(grid), dim3(256), 0, 0, d_ref, len, f->d_text);
+        if (f->wide)
+            hipLaunchKernelGGL(k_isa<uint64_t>, dim3(grid), dim3(256), 0, 0, (const uint64_t *)f->d_sa, N,
+                               (uint64_t *)f->d_isa);
+        else
+            hipLaunchKernelGGL(k_isa<uint32_t>, dim3(grid), dim3(256), 0, 0, (const uint32_t *)f->d_sa, N,
+                               (uint32_t *)f->d_isa);
+        rc = hip_rc(hipGetLastError());
+    }
+    if (rc == BSW_OK) rc = hip_rc(hipDeviceSynchronize());
+    (void)hipFree(d_ref);
+    if (rc) return rc;
+    f->dev_bytes += (int64_t)n + 64 + N * (int64_t)es;
+    if (f->wide) {
+        f->dv64.text = f->d_text;
+        f->dv64.sa = (const uint64_t *)f->d_sa;
+        f->dv64.isa = (const uint64_t *)f->d_isa;
+    } else {
+        f->dv32.text = f->d_text;
+        f->dv32.sa = (const uint32_t *)f->d_sa;
+        f->dv32.isa = (const uint32_t *)f->d_isa;
+    }
+    return BSW_OK;
+}
+
 int finish_device_index(bsw_fmi_t *f)
 {
     int rc = BSW_OK;
@@ -571,7 +719,8 @@ void bsw_mem_opt_default(bsw_mem_opt_t *opt)
 
 int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, bsw_fmi_t **out)
 {
-    if (!out || (!ref && ref_len > 0) || ref_len < 0 || (flags & ~3)) return BSW_E_INVAL;
+    if (!out || (!ref && ref_len > 0) || ref_len < 0 || (flags & ~7)) return BSW_E_INVAL;
+    const bool text = !(flags & BSW_FMI_NO_TEXT);
     *out = nullptr;
     for (int64_t i = 0; i < ref_len; ++i)
         if (ref[i] > 3) return BSW_E_INVAL;
@@ -600,8 +749,10 @@ int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, b
         const int64_t N = f->n + 1, nb = (N >> 6) + 1;
         f->dev_bytes = nb * 64 + N * (int64_t)(wide ? sizeof(uint64_t) : sizeof(uint32_t)) + N;
         f->build_s = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
-        const int r2 = finish_device_index(f);
+        int r2 = finish_device_index(f);
+        if (!r2 && text) r2 = attach_text(f, ref, ref_len);
         if (r2) { bsw_fmi_destroy(f); return r2; }
+        f->build_s = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
         *out = f;
         return BSW_OK;
     }
@@ -657,8 +808,10 @@ int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, b
         (rc = hip_rc(hipMemcpy(f->d_sa, f->sa.data(), (size_t)N * sizeof(uint32_t), hipMemcpyHostToDevice))) == BSW_OK &&
         (rc = finish_device_index(f)) == BSW_OK) {
         f->dev_bytes = (int64_t)(nb * sizeof(FmiBlock) + (size_t)N * sizeof(uint32_t));
-        *out = f;
-        return BSW_OK;
+        if (!text || (rc = attach_text(f, ref, ref_len)) == BSW_OK) {
+            *out = f;
+            return BSW_OK;
+        }
     }
     bsw_fmi_destroy(f);
     return rc;
@@ -676,6 +829,8 @@ void bsw_fmi_destroy(bsw_fmi_t *f)
     if (f->d_blk) (void)hipFree(f->d_blk);
     if (f->d_sa) (void)hipFree(f->d_sa);
     if (f->d_bwt) (void)hipFree(f->d_bwt);
+    if (f->d_text) (void)hipFree(f->d_text);
+    if (f->d_isa) (void)hipFree(f->d_isa);
     if (f->d_err) (void)hipFree(f->d_err);
     if (f->d_scratch) (void)hipFree(f->d_scratch);
     if (f->ev0) (void)hipEventDestroy(f->ev0);

@@ -664,12 +664,12 @@ def mem_opt(**kw) -> MemOpt:
     return o
 
 
-FMI_GPU_BUILD, FMI_WIDE = 1, 2
+FMI_GPU_BUILD, FMI_WIDE, FMI_NO_TEXT = 1, 2, 4
 
 
 class Fmi:
     """One resident FM-index (bsw_fmi_t) of ref + reverse-complement(ref) on `device`;
-    flags: FMI_GPU_BUILD / FMI_WIDE (bsw_fmi_build2), None: the library's choice."""
+    flags: FMI_GPU_BUILD / FMI_WIDE / FMI_NO_TEXT (bsw_fmi_build2), None: the library's choice."""
 
     def __init__(self, ref: np.ndarray, device: int = 0, flags: int | None = None):
         self.ref = np.ascontiguousarray(ref, dtype=np.uint8)

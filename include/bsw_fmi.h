@@ -73,7 +73,11 @@ int  bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **
  * of >= 2^32 - 1 rows (a ~2.1 Gb genome or larger, e.g. GRCh38's 3.1 Gb) needs the wide layout:
  * 8 B of suffix array + 1 B of occurrence blocks + 1 B of BWT codes per text position, ~60 GB of
  * HBM for 3 Gb (ABI version 5). */
-enum { BSW_FMI_GPU_BUILD = 1, BSW_FMI_WIDE = 2 };
+/* Unless BSW_FMI_NO_TEXT is given the index also keeps the two-strand text (1 B per position) and
+ * the inverse suffix array (4 / 8 B per row) in HBM: once an interval is down to one occurrence
+ * the SMEM walk extends it by comparing read and text directly instead of one dependent
+ * occurrence-block load per base (outputs identical). */
+enum { BSW_FMI_GPU_BUILD = 1, BSW_FMI_WIDE = 2, BSW_FMI_NO_TEXT = 4 };
 int  bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, bsw_fmi_t **out);
 void bsw_fmi_destroy(bsw_fmi_t *fmi);
 int  bsw_fmi_get_info(const bsw_fmi_t *fmi, bsw_fmi_info_t *out);

@@ -199,13 +199,16 @@ def _compare(o_out, o_cnt, g_out, g_cnt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("flags", [None, bsw.FMI_NO_TEXT], ids=["text_mode", "blocks_only"])
 @pytest.mark.parametrize("kind,n_ref,n_reads,L", [("random", 200_000, 4000, 151), ("repetitive", 100_000, 3000, 151),
                                                   ("repetitive", 50_000, 500, 250)])
-def test_gpu_collect_intv_equals_oracle(kind, n_ref, n_reads, L):
+def test_gpu_collect_intv_equals_oracle(kind, n_ref, n_reads, L, flags):
+    """GPU mem_collect_intv == the oracle, with the text-mode walk (single-occurrence intervals
+    extended by comparing read and text, BSW_FMI_NO_TEXT off) and with occurrence blocks only."""
     ref = repetitive_ref(n_ref, 9) if kind == "repetitive" else np.random.default_rng(9).integers(0, 4, n_ref, dtype=np.uint8)
     reads, off, lens = sample_reads(ref, n_reads, L, 21)
     o = oracle.FmiRef(ref)
-    f = bsw.Fmi(ref)
+    f = bsw.Fmi(ref, flags=flags)
     for opt in (dict(), dict(min_seed_len=15), dict(max_mem_intv=0), dict(split_width=50, min_seed_len=11)):
         o_out, o_cnt = o.collect_intv(reads, off, lens, cap=320, opt=oracle.mem_opt(**opt), nthreads=8)
         g_out, g_cnt = f.collect_intv(reads, off, lens, cap=320, opt=bsw.mem_opt(**opt))
@@ -214,10 +217,11 @@ def test_gpu_collect_intv_equals_oracle(kind, n_ref, n_reads, L):
 
 
 @pytest.mark.gpu
-def test_gpu_collect_intv_edges():
+@pytest.mark.parametrize("flags", [None, bsw.FMI_NO_TEXT], ids=["text_mode", "blocks_only"])
+def test_gpu_collect_intv_edges(flags):
     ref = repetitive_ref(20_000, 4)
     o = oracle.FmiRef(ref)
-    f = bsw.Fmi(ref)
+    f = bsw.Fmi(ref, flags=flags)
     seg = len(ref) // 10
     rd = [np.zeros(0, np.uint8), np.array([2], np.uint8), np.full(30, 4, np.uint8),
           np.concatenate([[4], ref[100:160], [4]]).astype(np.uint8), ref[7 * seg - 10:7 * seg + 90].copy(),
