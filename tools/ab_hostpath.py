@@ -7,8 +7,10 @@ sys.path.insert(0, os.path.join(ROOT, "bwa-mem2-arm_amd", "py"))
 import numpy as np
 import bsw
 
-libs = [ctypes.CDLL(p) for p in sys.argv[1:3]]
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 15
+# optional per-library host pool sizes (BSW_HOST_THREADS, read when a library's pool starts)
+threads = sys.argv[4:6] if len(sys.argv) > 5 else None
+libs = [ctypes.CDLL(p) for p in sys.argv[1:3]]
 pairs, ref, qer = bsw.synth_batch(1_000_000)
 params = bsw.default_params()
 ctxs = []
@@ -18,6 +20,11 @@ for L in libs:
     ctxs.append(c)
 P = lambda a: ctypes.c_void_p(a.ctypes.data)
 outs = [pairs.copy(), pairs.copy()]
+if threads:
+    for k in (0, 1):                     # first call of each library starts its pool
+        os.environ["BSW_HOST_THREADS"] = threads[k]
+        assert libs[k].bsw_get_scores(ctxs[k], P(outs[k]), P(ref), P(qer), len(pairs), 100, 16) == 0
+    print("host threads:", threads)
 ts = [[], []]
 for r in range(reps + 1):
     for k in (0, 1) if r % 2 == 0 else (1, 0):
