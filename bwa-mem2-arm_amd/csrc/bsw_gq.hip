@@ -23,6 +23,7 @@
 // path); with flag == nullptr they raise the range guard *err instead.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "bsw_kernels.h"
 
 namespace bsw {
@@ -192,11 +193,23 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
     // row i's profile, read from LDS one row ahead
     uint2 pr = s_prof[alive && tlen > 0 ? min((int)tb8[0], 7) : 0];
 
+    // static per lane: columns inside the query, and where column qlen - 1 lives (the row end
+    // of every row whose band reaches qlen)
+    uint32_t colm[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) colm[r] = plt(jj[r], pk2(qlen));             // j < qlen
+    const int qc = qlen - 1;
+    const int qr = (qc >= 0 && qc / C == gl) ? (qc % C) >> 1 : -1;          // register holding it
+    const int qsh = (qc & 1) * 16;
+
     int best = h0, best_i = -1, best_j = -1, max_ie = -1, gsc = -1, moff = 0, endc = qlen;
-    for (int i = 0;; ++i) {
-        const bool live = alive && i < tlen;
-        if (!__builtin_amdgcn_ballot_w64(live)) break;
-        if (!live) continue;
+    int i = 0;
+    // One row.  LM: some live pair has beg > 0 (columns left of beg are masked out of the F chain
+    // and the key).  RM: some live pair's band ends before qlen, so writes stop at slot end and E(end)
+    // = 0 (A.7 stale columns); without it every pair's end is qlen and slots past qlen are never
+    // read, so the row writes unmasked and finds H(i, qlen - 1) at a fixed place.
+    auto row = [&](auto LMc, auto RMc) {
+        constexpr bool LM = decltype(LMc)::value, RM = decltype(RMc)::value;
         const uint2 prn = s_prof[min((int)tb8[min(i + 1, tlen - 1)], 7)];
         const int beg = max(0, i - wl);
         const int end = min(min(endc, i + wl + 1), qlen);
@@ -216,13 +229,18 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
             for (int h = 0; h < 2; ++h) {
                 const int r = 2 * g + h;
                 if (r >= R) break;
-                const uint32_t s = h ? sb : sa;
-                const uint32_t m = padd(pmin(s, hh[r]), hh[r]);       // M = hold + min(S, hold)
+                const uint32_t sc = h ? sb : sa;
+                const uint32_t m = padd(pmin(sc, hh[r]), hh[r]);      // M = hold + min(S, hold)
                 me[r] = pmax(m, ee[r]);
                 enew[r] = pmax(psub(ee[r], ed2), psub(m, oed2));      // E' (unclamped)
                 const uint32_t uk = padd(psub(m, oei2), kem[r]);      // U(k) = M(k) - oe + k e
-                lm[r] = plt(jj[r], begw);                             // k < beg
-                u[r] = bsel(lm[r], pk2(kGqNeg), uk);
+                if constexpr (LM) {
+                    lm[r] = plt(jj[r], begw);                         // k < beg
+                    u[r] = bsel(lm[r], pk2(kGqNeg), uk);
+                } else {
+                    lm[r] = 0;
+                    u[r] = uk;
+                }
             }
         }
         pr = prn;
@@ -246,25 +264,33 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
             hcur[r] = pmax(me[r], f);                                 // H(i, j)
         }
         // hold(j) <- H(i, j - 1): one column right (group lane 0 gets the boundary h1b)
-        const uint32_t sh = (uint32_t)GQ_SHR0((int)hcur[R - 1], 1);
-        const uint32_t lastprev = gl == 0 ? pk2(h1b) : sh;
+        const uint32_t shf = (uint32_t)GQ_SHR0((int)hcur[R - 1], 1);
+        const uint32_t lastprev = gl == 0 ? pk2(h1b) : shf;
         // writes: slots <= end (H), slots < end (E), E(end) = 0; slots > end stale.  Row max
         // key (last column on ties) over [beg, end); H(i, end - 1) for gscore / lastH
-        uint32_t key = 0, hq_c = 0, lt[R];
+        uint32_t key = 0, hq_c = 0, hsel = 0, lt[R];
         const int rel = end - 1 - j0;                                 // column end-1 in this lane?
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t hn = __builtin_amdgcn_alignbyte(hcur[r], r == 0 ? lastprev : hcur[r - 1], 2);
-            const uint32_t le = plt(jj[r], endp1w);                  // j <= end
-            lt[r] = plt(jj[r], endw);                                // j < end
-            hh[r] = bsel(le, hn, hh[r]);
-            ee[r] = bsel(le, enew[r] & lt[r], ee[r]);
-            const uint32_t hm = hcur[r] & lt[r] & ~lm[r];
+            if constexpr (RM) {
+                const uint32_t le = plt(jj[r], endp1w);              // j <= end
+                lt[r] = plt(jj[r], endw);                            // j < end
+                hh[r] = bsel(le, hn, hh[r]);
+                ee[r] = bsel(le, enew[r] & lt[r], ee[r]);
+                hq_c = rel == 2 * r ? (hcur[r] & 0xffffu) : hq_c;
+                hq_c = rel == 2 * r + 1 ? (hcur[r] >> 16) : hq_c;
+            } else {
+                lt[r] = colm[r];                                     // end == qlen
+                hh[r] = hn;
+                ee[r] = enew[r];
+                hsel = qr == r ? hcur[r] : hsel;
+            }
+            const uint32_t hm = LM ? (hcur[r] & lt[r] & ~lm[r]) : (hcur[r] & lt[r]);
             key = max(key, max(__builtin_amdgcn_perm(hm, jj[r], 0x05040100u),     // H.lo << 16 | j
                                __builtin_amdgcn_perm(hm, jj[r], 0x07060302u)));   // H.hi << 16 | j+1
-            hq_c = rel == 2 * r ? (hcur[r] & 0xffffu) : hq_c;
-            hq_c = rel == 2 * r + 1 ? (hcur[r] >> 16) : hq_c;
         }
+        if constexpr (!RM) hq_c = qr >= 0 ? (hsel >> qsh) & 0xffffu : 0u;
         const uint32_t kmax = grp_max_u32(key);
         const int m = (int)(kmax >> 16), mj = (int)(kmax & 0xffffu);
         int hq = (int)grp_max_u32(hq_c);                              // H >= 0 in [beg, end)
@@ -289,7 +315,7 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
             uint32_t lp = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const uint32_t hm = hcur[r] & lt[r] & ~lm[r];
+                const uint32_t hm = LM ? (hcur[r] & lt[r] & ~lm[r]) : (hcur[r] & lt[r]);
                 const uint32_t plo = (hm & 0xffffu) ? (jj[r] & 0xffffu) + 1u : 0u;
                 const uint32_t phi = (hm >> 16) ? (jj[r] >> 16) + 1u : 0u;
                 lp = max(lp, max(plo, phi));
@@ -299,6 +325,17 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
         }
         endc = min(lp1 + 2, qlen);
         alive = alive && !stop;
+    };
+    for (;; ++i) {
+        const bool live = alive && i < tlen;
+        if (!__builtin_amdgcn_ballot_w64(live)) break;
+        // wave-uniform row forms (the masks only where some live pair needs them)
+        const bool need_lm = __builtin_amdgcn_ballot_w64(live && i - wl > 0) != 0;
+        const bool need_rm = __builtin_amdgcn_ballot_w64(live && min(min(endc, i + wl + 1), qlen) != qlen) != 0;
+        if (!live) continue;
+        if (need_rm) row(std::true_type{}, std::true_type{});
+        else if (need_lm) row(std::true_type{}, std::false_type{});
+        else row(std::false_type{}, std::false_type{});
     }
     if (idx >= 0 && gl == 0) {
         if (out24) {

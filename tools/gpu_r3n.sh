@@ -1,0 +1,11 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out/r3n
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_ext_pipeline.py tests/test_chain.py -m gpu > gpurun_out/r3n/tests.log 2>&1 || { tail -30 gpurun_out/r3n/tests.log; exit 1; }
+tail -1 gpurun_out/r3n/tests.log
+timeout -k 10 150 ./bwa-mem2-arm_amd/lib/percall_bench 1000000 8 1000 4000 10000 16000 > gpurun_out/r3n/percall.json 2>&1 || { cat gpurun_out/r3n/percall.json; exit 1; }
+python3 -c "
+import json; d=json.load(open('gpurun_out/r3n/percall.json'))
+print(' '.join('%d%s:%.3fms/%.1f/%.1f' % (c['pairs_per_call'], 'c' if c['coalescing'] else 'n', c['latency_ms_median'], c['M_pairs_per_s_1_caller'], c['M_pairs_per_s_8_callers']) for c in d['curve']), d['outputs_identical'])"
+timeout -k 10 100 python bench.py --pairs 16000 --steps 20 --warmup 2 --no-cpu --no-host-path > gpurun_out/r3n/b16k.log 2>&1 || { tail -3 gpurun_out/r3n/b16k.log; exit 1; }
+python3 -c "import json;d=json.loads(open('gpurun_out/r3n/b16k.log').read().strip().splitlines()[-1]);print('16K device', d['value'], d['roofline']['kernel'], d['roofline']['launch_ms'])"
