@@ -55,6 +55,11 @@ struct FmiDevT {                     // kernel view of the resident index (U = r
 // flag (k, l are resolved through SA^-1 only when the interval is output)
 constexpr uint32_t kTextFlag = 0x80000000u;
 
+#ifndef BSW_SMEM_BACK_UNROLL
+#define BSW_SMEM_BACK_UNROLL 2
+#endif
+constexpr int kBackUnroll = BSW_SMEM_BACK_UNROLL;   // backward sweep: entries extended together
+
 struct MemOpt {
     int32_t min_seed_len, split_width, max_mem_intv, split_len;
 };
@@ -279,18 +284,37 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
         const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
         nc = 0;
         U last_cs = 0;
-        for (int j = 0; j < np; ++j) {
-            const EntT<U> pv = prev[(size_t)(rev ? np - 1 - j : j) * st];
-            const bool tm = ((uint32_t)pv.e & kTextFlag) != 0;   // text mode: pv.k = text position
-            const uint32_t pe = (uint32_t)pv.e & ~kTextFlag;
+        // the entries' extensions are independent loads: compute kBackUnroll of them before
+        // their (sequential, order-dependent) bookkeeping, so a lane has that many block loads in
+        // flight instead of one
+        auto ext_of = [&](const EntT<U> &pv) -> IvT<U> {
             IvT<U> ok = {0, 0, 0};
             if (c >= 0) {
-                if (tm) {                                   // one occurrence: the base before it
+                if ((uint32_t)pv.e & kTextFlag) {           // one occurrence: the base before it
                     if (pv.k > 0 && f.text[pv.k - 1] == (uint8_t)c) ok = IvT<U>{pv.k - 1, 0, 1};
                 } else {
                     ok = backward_ext(f, IvT<U>{pv.k, pv.l, pv.s}, c);
                 }
             }
+            return ok;
+        };
+        for (int j0 = 0; j0 < np; j0 += kBackUnroll) {
+          EntT<U> pvs[kBackUnroll];
+          IvT<U> oks[kBackUnroll];
+#pragma unroll
+          for (int u = 0; u < kBackUnroll; ++u) {
+              const int j = min(j0 + u, np - 1);
+              pvs[u] = prev[(size_t)(rev ? np - 1 - j : j) * st];
+          }
+#pragma unroll
+          for (int u = 0; u < kBackUnroll; ++u) oks[u] = ext_of(pvs[u]);
+#pragma unroll
+          for (int u = 0; u < kBackUnroll; ++u) {
+            if (j0 + u >= np) break;
+            const EntT<U> pv = pvs[u];
+            const IvT<U> ok = oks[u];
+            const bool tm = ((uint32_t)pv.e & kTextFlag) != 0;   // text mode: pv.k = text position
+            const uint32_t pe = (uint32_t)pv.e & ~kTextFlag;
             if (c < 0 || ok.s < min_intv) {
                 if (nc == 0) {
                     if (nmem == 0 || (uint32_t)(i + 1) < last_start) {
@@ -312,6 +336,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
                 ++nc;
                 last_cs = ok.s;
             }
+          }
         }
         if (nc == 0) break;
         np = min(nc, L.scap);
