@@ -457,8 +457,13 @@ __device__ int smem_read(const FmiDevT<U> &f, const MemOpt &opt, const uint8_t *
     return (L.nout > cap ? 1 : 0) | (L.overflow ? 2 : 0);
 }
 
+#ifndef BSW_SMEM_BLOCK
+#define BSW_SMEM_BLOCK 64
+#endif
+constexpr int kSmemBlock = BSW_SMEM_BLOCK;          // threads per workgroup of the SMEM kernel
+
 template <class U>
-__global__ __launch_bounds__(64) void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
+__global__ __launch_bounds__(kSmemBlock) void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
                                                   const uint8_t *__restrict__ reads,
                                                   const int64_t *__restrict__ read_off,
                                                   const int32_t *__restrict__ read_len, int32_t n0, int32_t n,
@@ -623,7 +628,8 @@ int launch_collect(bsw_fmi_t *f, const FmiDevT<U> &dv, const MemOpt &mo, const u
     (void)hipEventRecord(f->ev0, s);
     for (int32_t n0 = 0; n0 < n; n0 += chunk) {
         const int32_t m = std::min(chunk, n - n0);
-        hipLaunchKernelGGL(smem_kernel<U>, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, dv, mo, d_reads, d_off,
+        hipLaunchKernelGGL(smem_kernel<U>, dim3((unsigned)((m + kSmemBlock - 1) / kSmemBlock)), dim3(kSmemBlock), 0, s,
+                           dv, mo, d_reads, d_off,
                            d_len, n0, m, (EntT<U> *)f->d_scratch, scap, d_mems, cap, d_cnt, f->d_err);
         if (hipGetLastError() != hipSuccess) return BSW_E_HIP;
     }
