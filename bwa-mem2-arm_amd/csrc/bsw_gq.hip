@@ -71,28 +71,56 @@ __device__ __forceinline__ uint32_t plt(uint32_t a, uint32_t b)
 // (m & a) | (~m & b)
 __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
 
-// DPP inside each 16-lane row (the group).  Values are kept non-negative where a scan needs
-// an identity, so out-of-row sources read as 0 (bound_ctrl) and every step folds into one
-// v_max_*_dpp instead of a mov + max pair.
+// DPP inside each group.  GS = 16: the group is one DPP row (row_shr / row_ror); values are kept
+// non-negative where a scan needs an identity, so out-of-row sources read as 0 (bound_ctrl) and
+// every step folds into one v_max_*_dpp.  GS = 4: the group is a quad (quad_perm; a max scan may
+// let lane 0 read itself, max being idempotent).
 #define GQ_SHR0(x, n) __builtin_amdgcn_update_dpp(0, (x), 0x110 + (n), 0xf, 0xf, true)
 #define GQ_ROR(x, n) __builtin_amdgcn_update_dpp(0, (x), 0x120 + (n), 0xf, 0xf, false)
+#define GQ_QP(x, ctl) __builtin_amdgcn_update_dpp(0, (x), (ctl), 0xf, 0xf, false)
+constexpr int kQpShr1 = 0x90;                      // quad_perm [0, 0, 1, 2]
+constexpr int kQpShr2 = 0x40;                      // quad_perm [0, 0, 0, 1]
+constexpr int kQpXor1 = 0xB1;                      // quad_perm [1, 0, 3, 2]
+constexpr int kQpXor2 = 0x4E;                      // quad_perm [2, 3, 0, 1]
 
-// inclusive max scan over the group's 16 lanes of non-negative x
+// inclusive max scan over the group's lanes of non-negative x
+template <int GS>
 __device__ __forceinline__ int grp_scan_max0(int x)
 {
-    x = max(x, GQ_SHR0(x, 1));
-    x = max(x, GQ_SHR0(x, 2));
-    x = max(x, GQ_SHR0(x, 4));
-    x = max(x, GQ_SHR0(x, 8));
+    if constexpr (GS == 16) {
+        x = max(x, GQ_SHR0(x, 1));
+        x = max(x, GQ_SHR0(x, 2));
+        x = max(x, GQ_SHR0(x, 4));
+        x = max(x, GQ_SHR0(x, 8));
+    } else {
+        x = max(x, GQ_QP(x, kQpShr1));
+        x = max(x, GQ_QP(x, kQpShr2));
+    }
     return x;
 }
-// unsigned max over the group's 16 lanes, result in every lane of the group
+// lane l gets lane l - 1's x inside the group; lane 0 gets 0
+template <int GS>
+__device__ __forceinline__ int grp_shr1_0(int x, int gl)
+{
+    if constexpr (GS == 16) return GQ_SHR0(x, 1);
+    else {
+        const int y = GQ_QP(x, kQpShr1);
+        return gl == 0 ? 0 : y;
+    }
+}
+// unsigned max over the group's lanes, result in every lane of the group
+template <int GS>
 __device__ __forceinline__ uint32_t grp_max_u32(uint32_t x)
 {
-    x = max(x, (uint32_t)GQ_ROR((int)x, 8));
-    x = max(x, (uint32_t)GQ_ROR((int)x, 4));
-    x = max(x, (uint32_t)GQ_ROR((int)x, 2));
-    x = max(x, (uint32_t)GQ_ROR((int)x, 1));
+    if constexpr (GS == 16) {
+        x = max(x, (uint32_t)GQ_ROR((int)x, 8));
+        x = max(x, (uint32_t)GQ_ROR((int)x, 4));
+        x = max(x, (uint32_t)GQ_ROR((int)x, 2));
+        x = max(x, (uint32_t)GQ_ROR((int)x, 1));
+    } else {
+        x = max(x, (uint32_t)GQ_QP((int)x, kQpXor1));
+        x = max(x, (uint32_t)GQ_QP((int)x, kQpXor2));
+    }
     return x;
 }
 
@@ -104,38 +132,42 @@ __device__ __forceinline__ int gq_init_h(int j, int h0, int qlen, int oe_ins, in
 }  // namespace
 
 // Targets are staged in LDS (a global-load prefetch would be waited for at the loop's register
-// copy in the same row), so a target longer than kGqTmax takes the planned path.
-constexpr int kGqTmax = 1024;
+// copy in the same row), so a target longer than gq_tmax(GS) takes the planned path: 1 KB per
+// pair for 16-lane groups (4 per wave), 512 B for quads (16 per wave: 8 KB of LDS per wave).
+__host__ __device__ constexpr int gq_tmax(int gs) { return gs == 16 ? 1024 : 512; }
 
 // Same int16 bounds as the wave kernel (bsw_host.cpp wv_class); the whole query is resident,
 // so the band cap only limits [beg, end).
-__host__ __device__ __forceinline__ bool gq_eligible(const KParams &kp, int qlen, int tlen, int h0, int qmax)
+__host__ __device__ __forceinline__ bool gq_eligible(const KParams &kp, int qlen, int tlen, int h0, int qmax,
+                                                     int tmax)
 {
-    if (kp.maxsc != 1 || qlen < 0 || tlen < 0 || h0 < 0 || qlen > qmax || tlen > kGqTmax) return false;
+    if (kp.maxsc != 1 || qlen < 0 || tlen < 0 || h0 < 0 || qlen > qmax || tlen > tmax) return false;
     if ((int64_t)kp.e_ins * qlen >= 2700) return false;
     if (128 + kp.o_del + 2 * kp.e_del >= 30000 || 128 + kp.o_ins + 2 * kp.e_ins >= 30000) return false;
     if ((int64_t)h0 + (qlen < tlen ? qlen : tlen) + (int64_t)kp.e_ins * (qlen + 1) >= 30000) return false;
     return true;
 }
 
-template <int C>
+template <int C, int GS>
 __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t w, SeqPair *__restrict__ pairs,
                                                 const int32_t *__restrict__ order, const int32_t n,
                                                 const uint8_t *__restrict__ ref, const uint8_t *__restrict__ qer,
                                                 int32_t *__restrict__ err, int32_t *__restrict__ flag,
                                                 int32_t *__restrict__ out24)
 {
-    static_assert(C == 4 || C == 6 || C == 8 || C == 10, "columns per lane");
+    static_assert((GS == 16 && (C == 4 || C == 6 || C == 8 || C == 10)) ||
+                  (GS == 4 && (C == 16 || C == 24 || C == 32 || C == 40)), "group size / columns per lane");
     constexpr int R = C / 2;                       // packed registers per plane
     constexpr int G = (C + 3) / 4;                 // query words per lane (4 codes each)
-    constexpr int QMAX = 16 * C;
-    constexpr int TW = kGqTmax / 4 + 2;            // target words per group (+ alignment slack)
+    constexpr int QMAX = GS * C;
+    constexpr int NG = 64 / GS;                    // pairs per wave
+    constexpr int TW = gq_tmax(GS) / 4 + 2;        // target words per group (+ alignment slack)
     __shared__ uint2 s_prof[8];
-    __shared__ uint32_t s_t[4][TW];                // the four pairs' targets (aligned words)
+    __shared__ uint32_t s_t[NG][TW];               // the wave's pairs' targets (aligned words)
     if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
-    const int gl = threadIdx.x & 15;               // lane in the group
-    const int grp = threadIdx.x >> 4;
-    const int k = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4);   // pair slot
+    const int gl = threadIdx.x & (GS - 1);         // lane in the group
+    const int grp = threadIdx.x / GS;
+    const int k = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GS);   // pair slot
     const int oe_del = kp.o_del + kp.e_del, oe_ins = kp.o_ins + kp.e_ins;
     const uint32_t oed2 = pk2(oe_del), oei2 = pk2(oe_ins - kp.e_ins), ed2 = pk2(kp.e_del);
 
@@ -145,17 +177,17 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
         idx = order ? order[k] : k;
         const SeqPair &sp = pairs[idx];
         idr = sp.idr; idq = sp.idq; tlen = sp.len1; qlen = sp.len2; h0 = sp.h0;
-        alive = gq_eligible(kp, qlen, tlen, h0, QMAX);
+        alive = gq_eligible(kp, qlen, tlen, h0, QMAX, gq_tmax(GS));
         if (!alive && gl == 0) atomicOr(flag ? flag : err, 1);
         if (!alive) idx = -1;
     }
-    // the target's aligned words -> LDS (16 lanes per pair); byte tsh + i is row i's base
+    // the target's aligned words -> LDS (the group's lanes); byte tsh + i is row i's base
     const uint8_t *tp = ref + (alive ? idr : 0);
     const int tsh = (int)((uintptr_t)tp & 3);
     if (alive) {
         const uint32_t *twp = (const uint32_t *)(tp - tsh);
         const int nw = (tsh + tlen + 3) >> 2;
-        for (int b = gl; b < nw; b += 16) s_t[grp][b] = twp[b];
+        for (int b = gl; b < nw; b += GS) s_t[grp][b] = twp[b];
     }
     __syncthreads();
     const uint8_t *tb8 = (const uint8_t *)s_t[grp] + tsh;
@@ -251,8 +283,8 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
 #pragma unroll
         for (int r = 1; r < R; ++r) v[r] = pmax_bhi(ppre(u[r]), v[r - 1]);
         const int tot = ((int)v[R - 1] >> 16) - kGqNeg;               // lane max of U, offset
-        const int inc = grp_scan_max0(tot);
-        const int pin = GQ_SHR0(inc, 1) + kGqNeg;                     // exclusive (lane 0: NEG)
+        const int inc = grp_scan_max0<GS>(tot);
+        const int pin = grp_shr1_0<GS>(inc, gl) + kGqNeg;             // exclusive (lane 0: NEG)
         const uint32_t pw = pk2(pin);
         uint32_t hcur[R];
 #pragma unroll
@@ -264,7 +296,7 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
             hcur[r] = pmax(me[r], f);                                 // H(i, j)
         }
         // hold(j) <- H(i, j - 1): one column right (group lane 0 gets the boundary h1b)
-        const uint32_t shf = (uint32_t)GQ_SHR0((int)hcur[R - 1], 1);
+        const uint32_t shf = (uint32_t)grp_shr1_0<GS>((int)hcur[R - 1], gl);
         const uint32_t lastprev = gl == 0 ? pk2(h1b) : shf;
         // writes: slots <= end (H), slots < end (E), E(end) = 0; slots > end stale.  Row max
         // key (last column on ties) over [beg, end); H(i, end - 1) for gscore / lastH
@@ -291,9 +323,9 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
                                __builtin_amdgcn_perm(hm, jj[r], 0x07060302u)));   // H.hi << 16 | j+1
         }
         if constexpr (!RM) hq_c = qr >= 0 ? (hsel >> qsh) & 0xffffu : 0u;
-        const uint32_t kmax = grp_max_u32(key);
+        const uint32_t kmax = grp_max_u32<GS>(key);
         const int m = (int)(kmax >> 16), mj = (int)(kmax & 0xffffu);
-        int hq = (int)grp_max_u32(hq_c);                              // H >= 0 in [beg, end)
+        int hq = (int)grp_max_u32<GS>(hq_c);                              // H >= 0 in [beg, end)
         hq = end - 1 < beg ? h1b : hq;                                // empty row: h1 = h1b
         // A.4: j == qlen (gscore, max_ie) -- selects, no exec-masked blocks
         const bool atq = end == qlen;
@@ -320,7 +352,7 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
                 const uint32_t phi = (hm >> 16) ? (jj[r] >> 16) + 1u : 0u;
                 lp = max(lp, max(plo, phi));
             }
-            lp = grp_max_u32(lp);
+            lp = grp_max_u32<GS>(lp);
             lp1 = shrink ? (int)lp : lp1;
         }
         endc = min(lp1 + 2, qlen);
@@ -353,31 +385,49 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
     }
 }
 
-int gq_cols_for(int max_qlen)
+int gq_cols_for(int max_qlen, int gs)
 {
-    if (max_qlen <= 64) return 4;
-    if (max_qlen <= 96) return 6;
-    if (max_qlen <= 128) return 8;
-    if (max_qlen <= 160) return 10;
+    if (gs == 16) {
+        if (max_qlen <= 64) return 4;
+        if (max_qlen <= 96) return 6;
+        if (max_qlen <= 128) return 8;
+        if (max_qlen <= 160) return 10;
+    } else {
+        if (max_qlen <= 64) return 16;
+        if (max_qlen <= 96) return 24;
+        if (max_qlen <= 128) return 32;
+        if (max_qlen <= 160) return 40;
+    }
     return -1;
 }
 
-bool gq_pair_ok(const KParams &kp, int qlen, int tlen, int h0) { return gq_eligible(kp, qlen, tlen, h0, 160); }
+bool gq_pair_ok(const KParams &kp, int qlen, int tlen, int h0, int gs)
+{
+    return gq_eligible(kp, qlen, tlen, h0, 160, gq_tmax(gs));
+}
 
-hipError_t launch_gq_kernel(int cols, const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order, int32_t n,
-                            const uint8_t *ref, const uint8_t *qer, int32_t *err, int32_t *flag, int32_t *out24,
-                            hipStream_t s)
+hipError_t launch_gq_kernel(int gs, int cols, const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order,
+                            int32_t n, const uint8_t *ref, const uint8_t *qer, int32_t *err, int32_t *flag,
+                            int32_t *out24, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
-    // one wave (four row groups = four pairs) per workgroup: a small batch spreads over every CU
-    const unsigned grid = (unsigned)((n + 3) / 4);
-    switch (cols) {
-    case 4: hipLaunchKernelGGL(gq_kernel<4>, dim3(grid), dim3(64), 0, s, kp, w, pairs, order, n, ref, qer, err, flag, out24); break;
-    case 6: hipLaunchKernelGGL(gq_kernel<6>, dim3(grid), dim3(64), 0, s, kp, w, pairs, order, n, ref, qer, err, flag, out24); break;
-    case 8: hipLaunchKernelGGL(gq_kernel<8>, dim3(grid), dim3(64), 0, s, kp, w, pairs, order, n, ref, qer, err, flag, out24); break;
-    case 10: hipLaunchKernelGGL(gq_kernel<10>, dim3(grid), dim3(64), 0, s, kp, w, pairs, order, n, ref, qer, err, flag, out24); break;
+    // one wave per workgroup: 64 / gs pairs (a small batch spreads over every CU)
+    const int per = 64 / gs;
+    const unsigned grid = (unsigned)((n + per - 1) / per);
+#define GQ_L(C, GS) hipLaunchKernelGGL((gq_kernel<C, GS>), dim3(grid), dim3(64), 0, s, kp, w, pairs, order, n, ref, qer, \
+                                       err, flag, out24)
+    switch (gs * 100 + cols) {
+    case 1604: GQ_L(4, 16); break;
+    case 1606: GQ_L(6, 16); break;
+    case 1608: GQ_L(8, 16); break;
+    case 1610: GQ_L(10, 16); break;
+    case 416: GQ_L(16, 4); break;
+    case 424: GQ_L(24, 4); break;
+    case 432: GQ_L(32, 4); break;
+    case 440: GQ_L(40, 4); break;
     default: return hipErrorInvalidValue;
     }
+#undef GQ_L
     return hipGetLastError();
 }
 

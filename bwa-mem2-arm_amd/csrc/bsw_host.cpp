@@ -181,10 +181,10 @@ struct PlanCall {
     int32_t n = 0, w = 0;
     int cell_bits = 16;
     hipStream_t stream = nullptr;
-    // small batches: > 0 = the host checked every pair against the row-group kernel's contract
-    // (value = its columns per lane); 0 = not checked (the kernel flags misfits, run_dp falls
-    // back to the planned path); -1 = some pair does not fit (planned path at once)
-    int gq_cols = 0;
+    // row-group kernel contract as the host checked it: gq_maxq >= 0 = every pair fits (longest
+    // query gq_maxq, longest target gq_maxt); -2 = not checked (the kernel flags misfits, run_dp
+    // falls back to the planned path); -1 = some pair does not fit (planned path at once)
+    int gq_maxq = -2, gq_maxt = 0;
     int32_t *d_out24 = nullptr;         // row-group kernel, host-checked batch: outputs as 6 x int32
                                         //   per pair here instead of into d_pairs
 };
@@ -408,6 +408,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.fork = 1;
     kp.long_route = 1;
     kp.small_batch = 16384;
+    kp.mid_batch = 32768;
     kp.group_kernel = 1;
 }
 
@@ -444,14 +445,18 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     const int32_t n = pc.n;
     // small batches (kt_for-sized calls): the row-group kernel (bsw_gq.hip) straight on the
     // call's stream -- no plan, no sort, no class-count readback
-    if (kp.group_kernel && n <= kp.small_batch && pc.gq_cols >= 0 && kp.long_route == 1 && kp.maxsc == 1 &&
-        !kp.misroute) {
-        const bool checked = pc.gq_cols > 0;
+    // medium batches: the quad form (4 lanes per pair, targets <= 512 bytes)
+    const int gs = n <= kp.small_batch ? 16 : 4;
+    const bool gq_size = n <= kp.small_batch || n <= kp.mid_batch;
+    const bool gq_fit = pc.gq_maxq == -2 || (pc.gq_maxq >= 0 && (gs == 16 || pc.gq_maxt <= 512));
+    if (kp.group_kernel && gq_size && gq_fit && kp.long_route == 1 && kp.maxsc == 1 && !kp.misroute) {
+        const bool checked = pc.gq_maxq >= 0;
+        const int cols = checked ? gq_cols_for(pc.gq_maxq, gs) : (gs == 16 ? 10 : 40);
         int32_t *d_err = s.d_meta + kMetaErr;
         if (!pc.d_out24)                       // (the staged path's input kernel zeroed them)
             BSW_TRY(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), pc.stream));
         BSW_TRY(hipEventRecord(s.ev0, pc.stream));
-        BSW_TRY(launch_gq_kernel(checked ? pc.gq_cols : 10, kp, pc.w, pc.d_pairs, nullptr, n, pc.d_ref, pc.d_qer,
+        BSW_TRY(launch_gq_kernel(gs, cols, kp, pc.w, pc.d_pairs, nullptr, n, pc.d_ref, pc.d_qer,
                                  d_err, checked ? nullptr : s.d_meta + kMetaFlag, checked ? pc.d_out24 : nullptr,
                                  pc.stream));
         BSW_TRY(hipEventRecord(s.ev1, pc.stream));
@@ -525,7 +530,7 @@ static int run_dp(const KParams &kp, Slot &s)
                 // some pair is outside the row-group kernel's contract: the whole batch again on
                 // the planned path (identical outputs; rare -- long or int16-unsafe pairs)
                 PlanCall again = pc;
-                again.gq_cols = -1;
+                again.gq_maxq = -1;
                 const int r = run_plan(kp, s, again);
                 if (r) return r;
                 return run_dp(kp, s);
@@ -1312,22 +1317,24 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
         }
         std::vector<std::vector<uint32_t>> ex(tasks.size());
         // per task: the row-group kernel's contract over its records (max qlen, or -1: a misfit)
-        std::vector<int> gq_maxq(tasks.size(), 0);
+        std::vector<int> gq_maxq(tasks.size(), 0), gq_maxt(tasks.size(), 0);
         PairIn *pin = (PairIn *)(h + pair_off);
         HostPool::get().parallel_for((int)tasks.size(), [&](int t) {
             const Task &k = tasks[t];
             const AggSeg &g = segs[k.seg];
             if (k.kind == 0) {
                 const SeqPair *p = g.r->pairs;
-                int maxq = 0;
+                int maxq = 0, maxt = 0;
                 for (int32_t i = 0; i < g.r->n; ++i) {
                     PairIn &o = pin[g.p_off + i];
                     o.idr = p[i].len1 > 0 ? (int32_t)(p[i].idr - g.r_lo + g.r_off) : 0;
                     o.idq = p[i].len2 > 0 ? (int32_t)(p[i].idq - g.q_lo + g.q_off) : 0;
                     o.len1 = p[i].len1; o.len2 = p[i].len2; o.h0 = p[i].h0;
-                    if (maxq >= 0) maxq = gq_pair_ok(kp, p[i].len2, p[i].len1, p[i].h0) ? std::max(maxq, p[i].len2) : -1;
+                    if (maxq >= 0) maxq = gq_pair_ok(kp, p[i].len2, p[i].len1, p[i].h0, 16) ? std::max(maxq, p[i].len2) : -1;
+                    maxt = std::max(maxt, p[i].len1);
                 }
                 gq_maxq[t] = maxq;
+                gq_maxt[t] = maxt;
             } else if (k.kind == 1) {
                 pack_2bit(h + ref_off + (g.r_off + k.a) / 4, g.r->ref + g.r_lo + k.a, (size_t)(k.b - k.a),
                           (uint32_t)(g.r_off + k.a), ex[t]);
@@ -1366,13 +1373,17 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
         PlanCall pc;
         pc.d_pairs = s.d_pairs; pc.d_ref = s.d_ref; pc.d_qer = s.d_qer;
         pc.n = N; pc.w = w; pc.cell_bits = cell_bits; pc.stream = s.stream;
-        int gq_max = 0;
+        int gq_max = 0, gq_mt = 0;
         for (size_t t = 0; t < tasks.size(); ++t)
-            if (tasks[t].kind == 0) gq_max = (gq_max < 0 || gq_maxq[t] < 0) ? -1 : std::max(gq_max, gq_maxq[t]);
-        pc.gq_cols = gq_max < 0 ? -1 : gq_cols_for(gq_max);
+            if (tasks[t].kind == 0) {
+                gq_max = (gq_max < 0 || gq_maxq[t] < 0) ? -1 : std::max(gq_max, gq_maxq[t]);
+                gq_mt = std::max(gq_mt, gq_maxt[t]);
+            }
+        pc.gq_maxq = gq_max;
+        pc.gq_maxt = gq_mt;
         // host-checked row-group batch: the kernel writes the 24 output bytes per pair straight
         // into the staging buffer (its inputs were expanded out of it above)
-        if (pc.gq_cols > 0) pc.d_out24 = (int32_t *)s.d_stage;
+        if (pc.gq_maxq >= 0) pc.d_out24 = (int32_t *)s.d_stage;
         int r = run_plan(kp, s, pc);
         const auto tg2 = std::chrono::steady_clock::now();
         if (!r) r = run_dp(kp, s);
@@ -2367,6 +2378,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     case BSW_OPT_HOST_CHUNK: if (value < 1 || value > INT32_MAX) return BSW_E_INVAL; ctx->host_chunk = (int32_t)value; return BSW_OK;
     case BSW_OPT_HOST_PACK: if (value != 2 && value != 4) return BSW_E_INVAL; ctx->host_pack = (int)value; return BSW_OK;
     case BSW_OPT_SMALL_BATCH: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.small_batch = (int32_t)value; return BSW_OK;
+    case BSW_OPT_MID_BATCH: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.mid_batch = (int32_t)value; return BSW_OK;
     case BSW_OPT_GROUP_KERNEL: if (!b01) return BSW_E_INVAL; ctx->kp.group_kernel = (int8_t)value; return BSW_OK;
     case BSW_OPT_SPLIT_MIN: if (value < 0) return BSW_E_INVAL; ctx->split_min = value; return BSW_OK;
     case BSW_OPT_COALESCE: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->coalesce = (int32_t)value; return BSW_OK;

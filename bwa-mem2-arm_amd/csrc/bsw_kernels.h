@@ -36,6 +36,8 @@ struct KParams {
                                 //   (BSW_OPT_LONG)
     int8_t group_kernel;        // host: small batches on the row-group kernel (bsw_gq.hip,
                                 //   BSW_OPT_GROUP_KERNEL)
+    int32_t mid_batch;          // host: calls / chunks of (small_batch, mid_batch] pairs run on
+                                //   the quad row-group kernel (BSW_OPT_MID_BATCH, 0 = off)
     int32_t small_batch;        // host: calls / chunks of at most this many pairs run every
                                 //   qualifying pair on the wave kernel (latency, not
                                 //   throughput, bounds them; BSW_OPT_SMALL_BATCH, 0 = off)
@@ -65,15 +67,16 @@ constexpr int kWvQmax = 4096;
 hipError_t launch_wv_kernel(int cols, const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order,
                             int32_t n, const uint8_t *ref, const uint8_t *qer, int32_t *err, hipStream_t s);
 
-// Small-batch row-group kernel (bsw_gq.hip): one 16-lane DPP row per SeqPair, cols columns per
-// lane (4, 6, 8 or 10: queries up to 16 * cols), four pairs per wave, no plan or sort needed.
+// Small-batch row-group kernel (bsw_gq.hip): one group of gs lanes per SeqPair -- gs = 16 (one
+// DPP row; cols 4, 6, 8 or 10 per lane) for small batches, gs = 4 (a quad; cols 16, 24, 32 or 40)
+// for medium ones -- queries up to gs * cols, 64 / gs pairs per wave, no plan or sort needed.
 // Pairs outside its contract (gq_pair_ok) are skipped and set *flag (or *err when flag is
 // null).  order may be null (pair k = slot k).
-hipError_t launch_gq_kernel(int cols, const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order, int32_t n,
-                            const uint8_t *ref, const uint8_t *qer, int32_t *err, int32_t *flag, int32_t *out24,
-                            hipStream_t s);
-int gq_cols_for(int max_qlen);                          // -1 past 160 columns
-bool gq_pair_ok(const KParams &kp, int qlen, int tlen, int h0);   // host-side contract check
+hipError_t launch_gq_kernel(int gs, int cols, const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order,
+                            int32_t n, const uint8_t *ref, const uint8_t *qer, int32_t *err, int32_t *flag,
+                            int32_t *out24, hipStream_t s);
+int gq_cols_for(int max_qlen, int gs);                 // -1 past 160 columns
+bool gq_pair_ok(const KParams &kp, int qlen, int tlen, int h0, int gs);   // host-side contract check
 
 // Wide kernel: any qlen/tlen, int32 cells, eh scratch of n * (max_qlen + 2) int2 in HBM.
 hipError_t launch_wide_kernel(const KParams &kp, int32_t w, SeqPair *pairs,

@@ -161,6 +161,10 @@ enum {
                                  (16 lanes per pair, queries <= 160, no plan / sort; default),
                                  0 = the planned path with the wave-per-alignment kernel.
                                  Outputs are identical either way                              */
+    BSW_OPT_MID_BATCH = 14,   /* calls / chunks of more than BSW_OPT_SMALL_BATCH and at most this many
+                                 pairs (default 32768; 0 = off) run on the row-group kernel's quad
+                                 form (4 lanes per pair, targets <= 512 bytes) when
+                                 BSW_OPT_GROUP_KERNEL is on.  Outputs are identical either way  */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };

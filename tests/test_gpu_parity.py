@@ -52,7 +52,7 @@ def _assert_same(want, got, tag=""):
 
 @pytest.fixture(scope="module")
 def eng():
-    e = bsw.Engine(small_batch=0)   # kernel-class tests: small batches stay on their classes
+    e = bsw.Engine(small_batch=0, mid_batch=0)   # kernel-class tests: small batches stay on their classes
     yield e
     e.close()
 
@@ -63,7 +63,7 @@ def test_golden_fixtures(golden, cell_bits):
     for name, pairs, ref, qer, w, sc in golden:
         key = tuple(sorted(sc.items()))
         if key not in engines:
-            engines[key] = bsw.Engine(_gparams(sc), small_batch=0)
+            engines[key] = bsw.Engine(_gparams(sc), small_batch=0, mid_batch=0)
         got = pairs.copy()
         for f in bsw.OUT_FIELDS:
             got[f] = -9
@@ -182,7 +182,7 @@ def test_partial_batches(eng, m):
 
 def test_nondefault_scoring_generic_kernel():
     sc = dict(o_del=5, e_del=2, o_ins=7, e_ins=1, zdrop=50, end_bonus=3, a=2, b=3)
-    e = bsw.Engine(_gparams(sc), small_batch=0)
+    e = bsw.Engine(_gparams(sc), small_batch=0, mid_batch=0)
     pairs, ref, qer = bswgen.random_pairs(2000, seed=31, tlen=(0, 300), qlen=(0, 160))
     want, got = pairs.copy(), pairs.copy()
     oracle.get_scores(_oparams(sc), want, ref, qer, 60, nthreads=8)
@@ -281,7 +281,7 @@ def test_host_pipeline_chunks(chunk):
     permuted ones are gathered pair by pair with rewritten offsets.  Chunks are whole 4096-pair
     blocks: chunk 1 and 8192 give 3 and 3 chunks, 1 << 20 one.  Outputs equal the oracle and
     only the six output fields of the caller's records change."""
-    e = bsw.Engine(host_chunk=chunk, small_batch=0)
+    e = bsw.Engine(host_chunk=chunk, small_batch=0, mid_batch=0)
     pairs, ref, qer = bswgen.random_pairs(20000 if chunk > 1 else 9000, seed=chunk % 1000, qlen=(0, 190), tlen=(0, 330))
     want = pairs.copy()
     oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
@@ -301,7 +301,7 @@ def test_host_pipeline_packing(pack, p_n):
     p_n = 0.1 puts more than 1/32 of the bytes outside 0..3, so those chunks fall back to nibbles.
     Odd extents (lengths 0..331) exercise the unpack tails; outputs equal the oracle either way and
     the caller's input fields are untouched."""
-    e = bsw.Engine(host_chunk=8192, host_pack=pack, small_batch=0)
+    e = bsw.Engine(host_chunk=8192, host_pack=pack, small_batch=0, mid_batch=0)
     pairs, ref, qer = bswgen.random_pairs(20000, seed=int(p_n * 1000) + pack, qlen=(0, 190), tlen=(0, 331), p_n=p_n)
     want = pairs.copy()
     oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
@@ -323,19 +323,49 @@ def test_small_batch_route(n, group, c2_full):
     the oracle's outputs."""
     pairs, ref, qer, want = c2_full
     e = bsw.Engine(group_kernel=group)
-    small = n <= 16384
+    small = n <= 16384                  # 16-lane groups; up to BSW_OPT_MID_BATCH (32768): quads
+    rg = group and n <= 32768
     for cell_bits in (16, 8):
         got = pairs[:n].copy()
         e.get_scores(got, ref, qer, 100, cell_bits)
         _assert_same(want[:n], got, f"n {n} cell_bits {cell_bits}")
         st = e.last_stats()
-        assert st.n_group == (n if small and group else 0)
+        assert st.n_group == (n if rg else 0)
         assert st.n_wave == (n if small and not group else 0)
         assert st.n_i16 + st.n_u8 + st.n_wide == n
     dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (pairs[:n].copy(), ref, qer))
     e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, n, 100, 16)
     _assert_same(want[:n], dp.download(np.empty_like(pairs[:n])), f"device n {n}")
-    assert e.last_stats().n_group == (n if small and group else 0)
+    assert e.last_stats().n_group == (n if rg else 0)
+    e.close()
+
+
+@pytest.mark.parametrize("w", [0, 7, 100, 200])
+def test_group_kernel_quad_random(w):
+    """The quad form of the row-group kernel (4 lanes per pair; BSW_OPT_SMALL_BATCH 0 sends every
+    batch of up to BSW_OPT_MID_BATCH pairs there): random shapes with targets up to its 512 bytes
+    and a few past them (the batch then takes the planned path), both entry points."""
+    e = bsw.Engine(small_batch=0)
+    pairs, ref, qer = bswgen.random_pairs(6000, seed=1900 + w, tlen=(0, 512), qlen=(0, 160), h0=(0, 200))
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+    got = pairs.copy()
+    e.get_scores(got, ref, qer, w)
+    _assert_same(want, got, f"quad host w={w}")
+    assert e.last_stats().n_group == len(pairs)
+    dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (pairs.copy(), ref, qer))
+    e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, len(pairs), w, 16)
+    _assert_same(want, dp.download(np.empty_like(pairs)), f"quad device w={w}")
+    assert e.last_stats().n_group == len(pairs)
+    long_t, r2, q2 = bswgen.random_pairs(3000, seed=2900 + w, tlen=(400, 700), qlen=(0, 160), h0=(0, 200))
+    want2 = long_t.copy()
+    oracle.get_scores(_oparams(), want2, r2, q2, w, nthreads=8)
+    got2 = long_t.copy()
+    e.get_scores(got2, r2, q2, w)
+    _assert_same(want2, got2, f"quad fallback host w={w}")
+    dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (long_t.copy(), r2, q2))
+    e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, len(long_t), w, 16)
+    _assert_same(want2, dp.download(np.empty_like(long_t)), f"quad fallback device w={w}")
     e.close()
 
 
@@ -359,14 +389,16 @@ def test_group_kernel_random(w):
     e.close()
 
 
-def test_group_kernel_golden(golden):
+@pytest.mark.parametrize("quad", [False, True])
+def test_group_kernel_golden(golden, quad):
     """Every golden batch on the default engine (small batches: the row-group kernel where the
-    scoring qualifies, the planned path otherwise) and on the device entry point."""
+    scoring qualifies, the planned path otherwise) and on the device entry point; quad: every
+    batch on the 4-lanes-per-pair form (BSW_OPT_SMALL_BATCH 0)."""
     engines, ran = {}, 0
     for name, pairs, ref, qer, w, sc in golden:
         key = tuple(sorted(sc.items()))
         if key not in engines:
-            engines[key] = bsw.Engine(_gparams(sc))
+            engines[key] = bsw.Engine(_gparams(sc), **({"small_batch": 0} if quad else {}))
         got = pairs.copy()
         for f in bsw.OUT_FIELDS:
             got[f] = -9
@@ -419,7 +451,7 @@ def test_small_batch_mixed():
 def test_multi_gpu_context_shards(c2_full):
     pairs, ref, qer, want = c2_full
     n = hiprt.device_count()
-    e = bsw.Engine(n_gpus=n, small_batch=0)
+    e = bsw.Engine(n_gpus=n, small_batch=0, mid_batch=0)
     got = pairs[:100_000].copy()
     e.get_scores(got, ref, qer, 100)
     _assert_same(want[:100_000], got, f"n_gpus={n}")
@@ -481,7 +513,7 @@ def test_multi_device_policy_rehearsal(c2_full, nlog):
 def eng_lane():
     """Engine with the packed-column kernel disabled (BSW_OPT_KERNEL8 = 0): every pair runs on
     the int16 lane kernel (bsw_kernels.hip) or the wide kernel."""
-    e = bsw.Engine(kernel8=0, small_batch=0)
+    e = bsw.Engine(kernel8=0, small_batch=0, mid_batch=0)
     yield e
     e.close()
 
@@ -573,7 +605,7 @@ def test_kernel_range_guard_reports_error():
     queries trip the kernel's range guard, and both call forms must return BSW_E_RANGE (the
     guard word is read back after the DP launches) instead of BSW_OK with unwritten outputs."""
     pairs, ref, qer = bswgen.c2_like(500, seed=41)
-    e = bsw.Engine(test_misroute=1, small_batch=0)
+    e = bsw.Engine(test_misroute=1, small_batch=0, mid_batch=0)
     got = pairs.copy()
     with pytest.raises(bsw.BswError, match="-34"):
         e.get_scores(got, ref, qer, 100)
@@ -661,7 +693,7 @@ def test_host_pipeline_2bit_pieces_over_8mb():
     want = pairs.copy()
     oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
     for pack in (2, 4):
-        e = bsw.Engine(host_chunk=1 << 17, host_pack=pack, small_batch=0)
+        e = bsw.Engine(host_chunk=1 << 17, host_pack=pack, small_batch=0, mid_batch=0)
         got = pairs.copy()
         e.get_scores(got, ref, qer, 100)
         _assert_same(want, got, f"pieces > 8 MB, host_pack {pack}")
