@@ -326,6 +326,9 @@ def main():
     ap.add_argument("--w", type=int, default=100)
     ap.add_argument("--cell-bits", type=int, default=16, choices=(8, 16))
     ap.add_argument("--h0-hi", type=int, default=100, help="h0 upper bound (C3 uses 105)")
+    ap.add_argument("--kernel8", type=int, default=1, choices=(0, 1, 2),
+                    help="BSW_OPT_KERNEL8 for the 8-bit-regime pairs: 1 packed-column kernel (default), 2 the same "
+                         "with byte-wide H/E planes (8-bit cells, 3 waves/SIMD at QMAX 160), 0 int16 lane kernel")
     ap.add_argument("--qlen", type=int, default=150, help="query length (C2: 150; long reads: 250 / 500 / 1000)")
     ap.add_argument("--tlen", type=int, default=300, help="target window length (C2: 300)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -393,6 +396,8 @@ def main():
     d_ref = hiprt.DeviceBuffer.from_array(ref)
     d_qer = hiprt.DeviceBuffer.from_array(qer)
     eng = bsw.Engine(device=local)
+    if args.kernel8 != 1:
+        eng.set_option("kernel8", args.kernel8)
 
     def step():
         eng.get_scores_device(d_pairs.ptr, d_ref.ptr, d_qer.ptr, args.pairs, args.w, args.cell_bits)
@@ -428,7 +433,7 @@ def main():
     wave = 2 * st.n_wave > args.pairs
     group = 2 * st.n_group > args.pairs              # small batches: the row-group kernel (device
     kname = ("gq_kernel<10>" if group else           #   calls run its 10-column form)
-             "pc_kernel<160>" if packed else (f"wv_kernel<{wave_cols(cfg.qlen, args.w)}>" if wave
+             ("pc_kernel<160,bytes>" if args.kernel8 == 2 else "pc_kernel<160>") if packed else (f"wv_kernel<{wave_cols(cfg.qlen, args.w)}>" if wave
                                               else "lane_kernel<160>"))
     roof = {
         "bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
@@ -444,10 +449,12 @@ def main():
         "metric": METRIC, "value": round(value, 3), "unit": UNIT, "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int16" if args.cell_bits == 16 else "u8+int16",
+        "scaling": "weak", "vs_baseline": None, "dtype": ("u8 cells (byte H/E planes, int16 arithmetic)" if args.kernel8 == 2 and packed else
+                                                   "int16" if args.cell_bits == 16 else "u8+int16"),
         "data": "synthetic (bsw_synth.c, seed 42)",
         "config": {"workload": f"{'C3' if args.cell_bits == 8 else 'C2' if cfg.qlen <= 160 else 'long reads'}: {args.pairs} SeqPairs/GPU resident in HBM, {cfg.qlen} bp query / "
                                f"{cfg.tlen} bp ref, band w={args.w}, cell_bits={args.cell_bits}, "
+                               f"{'byte-plane kernel8=2, ' if args.kernel8 == 2 else ''}"
                                f"h0 U[{cfg.h0_lo},{cfg.h0_hi}]",
                    "pairs_per_gpu": args.pairs, "parallelism": f"shard{world} (independent pairs)",
                    "distinct_gpus": args.distinct_gpus,

@@ -187,6 +187,8 @@ struct PlanCall {
     int gq_maxq = -2, gq_maxt = 0;
     int32_t *d_out24 = nullptr;         // row-group kernel, host-checked batch: outputs as 6 x int32
                                         //   per pair here instead of into d_pairs
+    bool tput = false;                  // throughput routing: no latency kernels (row-group, small-
+                                        //   batch wave routing) -- a coalesced batch on a busy device
 };
 
 struct Slot {
@@ -410,6 +412,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.small_batch = 16384;
     kp.mid_batch = 32768;
     kp.group_kernel = 1;
+    kp.busy_min = 8192;
 }
 
 // keys / keys2 / vals / order (radix-sort buffers) grow together
@@ -447,7 +450,7 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     // call's stream -- no plan, no sort, no class-count readback
     // medium batches: the quad form (4 lanes per pair, targets <= 512 bytes)
     const int gs = n <= kp.small_batch ? 16 : 4;
-    const bool gq_size = n <= kp.small_batch || n <= kp.mid_batch;
+    const bool gq_size = !pc.tput && (n <= kp.small_batch || n <= kp.mid_batch);
     const bool gq_fit = pc.gq_maxq == -2 || (pc.gq_maxq >= 0 && (gs == 16 || pc.gq_maxt <= 512));
     if (kp.group_kernel && gq_size && gq_fit && kp.long_route == 1 && kp.maxsc == 1 && !kp.misroute) {
         const bool checked = pc.gq_maxq >= 0;
@@ -496,7 +499,7 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     // lane-per-pair wave lives ~1.2 ms whatever the batch size, so they are latency-bound; the
     // wave-per-alignment kernel spreads each pair over 64 lanes -- 0.35 vs 1.39 ms per call at
     // 1K C2 pairs, 1.05 vs 1.58 at 10K, slower past ~20K
-    const int32_t long_route = (kp.long_route == 1 && n <= kp.small_batch) ? 2 : kp.long_route;
+    const int32_t long_route = (kp.long_route == 1 && n <= kp.small_batch && !pc.tput) ? 2 : kp.long_route;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                        pc.d_pairs, n, kp, pc.w, pc_route, long_route, pc.d_ref, pc.d_qer, s.d_keys,
                        s.d_vals, d_counts, d_maxq, (int)kp.keymode, (int)kp.misroute);
@@ -1279,7 +1282,7 @@ struct AggSeg {                                 // one call inside a coalesced b
 };
 
 static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg> &segs, int32_t N, int64_t r_tot,
-                            int64_t q_tot, int32_t w, int cell_bits, bsw_stats_t &st)
+                            int64_t q_tot, int32_t w, int cell_bits, bool busy, bsw_stats_t &st)
 {
     int rc = BSW_OK;
     auto slot = dc.acquire(rc);
@@ -1381,6 +1384,13 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
             }
         pc.gq_maxq = gq_max;
         pc.gq_maxt = gq_mt;
+        // another batch is already on this device (concurrent kt_for callers): the GPU is shared,
+        // so a batch of busy_min pairs or more goes to the packed-column lane kernels (~5x the
+        // row-group kernel's work per cell's instructions) instead of the latency kernels
+        if (busy && kp.busy_min > 0 && N >= kp.busy_min) {
+            pc.tput = true;
+            pc.gq_maxq = -1;
+        }
         // host-checked row-group batch: the kernel writes the 24 output bytes per pair straight
         // into the staging buffer (its inputs were expanded out of it above)
         if (pc.gq_maxq >= 0) pc.d_out24 = (int32_t *)s.d_stage;
@@ -1425,7 +1435,8 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
 // One coalesced batch: calls that fail validation get BSW_E_RANGE; calls whose buffers are not
 // contiguous (scattered idr / idq) and batches with too many non-ACGT bytes run on their own
 // through host_shard.
-static void run_group(const KParams &kp, DeviceCtx &dc, std::vector<AggReq *> &G, int32_t chunk, bool two_bit)
+static void run_group(const KParams &kp, DeviceCtx &dc, std::vector<AggReq *> &G, int32_t chunk, bool two_bit,
+                      bool busy)
 {
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<AggSeg> segs;
@@ -1452,7 +1463,8 @@ static void run_group(const KParams &kp, DeviceCtx &dc, std::vector<AggReq *> &G
     if (!segs.empty()) {
         bsw_stats_t st{};
         const int rc = (r_tot < ((int64_t)1 << 28) && q_tot < ((int64_t)1 << 28))
-                           ? run_group_staged(kp, dc, segs, N, r_tot, q_tot, segs[0].r->w, segs[0].r->cell_bits, st)
+                           ? run_group_staged(kp, dc, segs, N, r_tot, q_tot, segs[0].r->w, segs[0].r->cell_bits, busy,
+                                              st)
                            : 1;
         if (rc == 1) {
             for (auto &g : segs) alone.push_back(g.r);
@@ -1479,6 +1491,7 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
     while (!me.done) {
         if (dc.agg_leaders < dc.agg_leaders_max && !dc.agg_q.empty()) {
             // lead: every queued call with the front call's (w, cell_bits, end_bonus), FIFO
+            const bool busy = dc.agg_leaders > 0;     // another batch in flight on this device
             ++dc.agg_leaders;
             std::vector<AggReq *> G;
             const AggReq *f = dc.agg_q.front();
@@ -1498,7 +1511,7 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
             lk.unlock();
             KParams gk = kp;
             gk.end_bonus = feb;
-            run_group(gk, dc, G, chunk, two_bit);
+            run_group(gk, dc, G, chunk, two_bit, busy);
             lk.lock();
             --dc.agg_leaders;
             for (AggReq *r : G) r->done = true;
@@ -2369,7 +2382,8 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     if (!ctx) return BSW_E_INVAL;
     const bool b01 = value == 0 || value == 1;
     switch (option) {
-    case BSW_OPT_KERNEL8: if (!b01) return BSW_E_INVAL; ctx->kp.kern8 = (int8_t)value; return BSW_OK;
+    case BSW_OPT_BUSY_MIN: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.busy_min = (int32_t)value; return BSW_OK;
+    case BSW_OPT_KERNEL8: if (value < 0 || value > 2) return BSW_E_INVAL; ctx->kp.kern8 = (int8_t)value; return BSW_OK;
     case BSW_OPT_FORK: if (!b01) return BSW_E_INVAL; ctx->kp.fork = (int8_t)value; return BSW_OK;
     case BSW_OPT_SORTKEY: if (!b01) return BSW_E_INVAL; ctx->kp.keymode = value ? 2 : 0; return BSW_OK;
     case BSW_OPT_GLOB_BAND: if (!b01) return BSW_E_INVAL; ctx->glob_band = (int)value; return BSW_OK;

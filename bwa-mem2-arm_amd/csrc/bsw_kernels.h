@@ -38,6 +38,8 @@ struct KParams {
                                 //   BSW_OPT_GROUP_KERNEL)
     int32_t mid_batch;          // host: calls / chunks of (small_batch, mid_batch] pairs run on
                                 //   the quad row-group kernel (BSW_OPT_MID_BATCH, 0 = off)
+    int32_t busy_min;           // host: coalesced batches of at least this many pairs run on the
+                                //   lane kernels when another batch is in flight (BSW_OPT_BUSY_MIN)
     int32_t small_batch;        // host: calls / chunks of at most this many pairs run every
                                 //   qualifying pair on the wave kernel (latency, not
                                 //   throughput, bounds them; BSW_OPT_SMALL_BATCH, 0 = off)

@@ -77,13 +77,17 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
 // max(E~ - e, T~, 0) (as -e < 0).  The F chain clamps instead (f - e saturates at 0, so
 // F >= 0 always) and H = max(ME, F) = max(M, E~, F) equals max(M, E, F) because F >= 0.
 // Bounds: M >= -127, oe < 4096 (pk_ok), so T~, E~ stay far inside int16.
-#define PC_PH1(X, EOUT)                                                                 \
+#define PC_PH1_(X, EOUT, ESUB)                                                          \
     "v_pk_min_i16 %[s" X "], %[s" X "], %[h" X "]\n\t"                                      \
     "v_pk_add_u16 %[s" X "], %[s" X "], %[h" X "]\n\t"                                      \
     "v_pk_sub_i16 %[t" X "], %[s" X "], %[oe2]\n\t"                                         \
     "v_pk_max_i16 %[s" X "], %[s" X "], %[e" X "]\n\t"                                      \
-    "v_pk_sub_i16 " EOUT ", %[e" X "], %[ed2]\n\t"                                          \
+    ESUB                                                                                     \
     "v_pk_max_i16 " EOUT ", " EOUT ", %[t" X "]\n\t"
+#define PC_PH1(X, EOUT) PC_PH1_(X, EOUT, "v_pk_sub_i16 " EOUT ", %[e" X "], %[ed2]\n\t")
+// byte planes (BY kernels): E enters >= 0 (a stored byte), so E - e saturating at 0 makes E'
+// = max(sat(E - e), T~) = max(E - e, T, 0) clamped for free -- a byte again
+#define PC_PH1B(X, EOUT) PC_PH1_(X, EOUT, "v_pk_sub_u16 " EOUT ", %[e" X "], %[ed2] clamp\n\t")
 
 #define PC_SCORES                                                                        \
     "v_perm_b32 %[y], %[phi], %[plo], %[q]\n\t"                                              \
@@ -130,8 +134,9 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
     "v_and_b32_e32 %[p" X "], %[p" X "], %[y]\n\t"
 
 // masked body (chain variant CH), shared by the L (left-reset) and R forms
-#define PC_MASKED(CH0, CH1, CH2, CH3, KA, KB, LA, LB)                                    \
-    PC_PH1("a", "%[xa]") PC_PH1("b", "%[xb]")                                                \
+#define PC_MASKED(CH0, CH1, CH2, CH3, KA, KB, LA, LB) PC_MASKED_(PC_PH1, CH0, CH1, CH2, CH3, KA, KB, LA, LB)
+#define PC_MASKED_(PH, CH0, CH1, CH2, CH3, KA, KB, LA, LB)                               \
+    PH("a", "%[xa]") PH("b", "%[xb]")                                                        \
     CH0 CH1                                                                                  \
     "v_lshl_or_b32 %[pa], %[c0], 16, %[h1]\n\t"                                              \
     CH2 CH3                                                                                  \
@@ -161,17 +166,22 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
 // registers are two byte-aligns, HH[2G] = {H(4G-1), H(4G)}, HH[2G+1] = {H(4G+1), H(4G+2)}.
 // 10 VALU per 4 cells for the chain (12 before) and 2 for the packing.
 #define PC_FAST_CHAIN                                                                    \
+    PC_FAST_CHAIN_("v_alignbyte_b32 %[ha], %[pa], %[h1], 2\n\t", "v_alignbyte_b32 %[hb], %[h1], %[pa], 2\n\t")
+// A1 reads the entering h1 (H(4G-1) in its high half) and pa = {H(4G), H(4G+1)}; A2 the leaving
+// h1 = {H(4G+2), H(4G+3)}: the int16 form builds HH[2G], HH[2G+1]; the byte form (BY) builds
+// HB[G] = bytes {H(4G-1), H(4G), H(4G+1), H(4G+2)} by two v_perm (the same instruction count)
+#define PC_FAST_CHAIN_(A1, A2)                                                           \
     "v_pk_sub_u16 %[fp], %[f], %[e0e] op_sel_hi:[0,1] clamp\n\t"                            \
     "v_pk_max_i16 %[fp], %[fp], %[ta] op_sel_hi:[1,0]\n\t"                                  \
     "v_pk_max_i16 %[pa], %[fp], %[sa]\n\t"                                                  \
     "v_pk_sub_u16 %[fp], %[fp], %[ee2] op_sel:[1,0] clamp\n\t"                              \
     "v_pk_sub_i16 %[y], %[ta], %[e0e] op_sel:[1,0]\n\t"                                     \
     "v_pk_max_i16 %[fp], %[fp], %[y]\n\t"                                                   \
-    "v_alignbyte_b32 %[ha], %[pa], %[h1], 2\n\t"                                            \
+    A1                                                                                       \
     "v_pk_max_i16 %[fp], %[fp], %[tb] op_sel_hi:[1,0]\n\t"                                  \
     "v_pk_max_i16 %[h1], %[fp], %[sb]\n\t"                                                  \
     "v_sub_u32_sdwa %[f], %[fp], %[ed] clamp dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t" \
-    "v_alignbyte_b32 %[hb], %[h1], %[pa], 2\n\t"                                            \
+    A2                                                                                       \
     PC_SDWA("v_max_i32", "%[f]", "%[f]", "sext(%[tb])", "WORD_1")
 
 // Layout: the FAST body is the fall-through path (one bit test, a not-taken branch, no taken
@@ -262,16 +272,143 @@ __device__ __forceinline__ void pc_group(uint32_t &ha, uint32_t &hb, uint32_t &e
     }
 }
 
-template <int QMAX, int G>
-__device__ __forceinline__ void pc_group_if(uint32_t (&hh)[QMAX / 2], uint32_t (&ee)[QMAX / 2],
+// ---- byte planes (BY kernels, BSW_OPT_KERNEL8 = 2): the 8-bit regime's cells stored as bytes
+//   HB[G] = bytes {H(i-1, 4G-1), H(i-1, 4G), H(i-1, 4G+1), H(i-1, 4G+2)}   (slots 4G .. 4G+3)
+//   EB[G] = bytes {E(i, 4G), .., E(i, 4G+3)}
+// half the plane registers of the int16 form.  A group unpacks its two bytes words into the
+// int16 pairs the shared arithmetic runs on (4 v_perm, after the skip test: skipped groups pay
+// nothing), and packs back: H by the two v_perm that replace the FAST chain's byte-aligns, E by
+// one v_perm; the row-max key is built from HB by one v_perm per pair of slots (as v_lshl_or
+// before).  Every stored H, E is in [0, 255] (H <= h0 + min(qlen, tlen) <= 255, the planner's
+// contract; E <= H and E' clamped at 0 by PC_PH1B).
+constexpr uint32_t kSelLo = 0x0C010C00u;       // {b0, b1} of a bytes word -> two int16 halves
+constexpr uint32_t kSelHi = 0x0C030C02u;       // {b2, b3}
+constexpr uint32_t kSelPk = 0x06040200u;       // v_perm(hi, lo): {lo.w0, lo.w1, hi.w0, hi.w1} -> bytes
+constexpr uint32_t kSelA1 = 0x0C060402u;       // v_perm(pa, h1 in): {h1.b2, pa.b0, pa.b2, 0}
+constexpr uint32_t kSelA2 = 0x04020100u;       // v_perm(h1 out, t): {t.b0, t.b1, t.b2, h1.b0}
+constexpr uint32_t kSelKa = 0x05020400u;       // v_perm(HB, jj): {jj.b0, HB.b0, jj.b2, HB.b1} = H << 8 | j
+constexpr uint32_t kSelKb = 0x07020600u;       // {jj.b0, HB.b2, jj.b2, HB.b3}
+constexpr uint32_t kSelK0 = 0x050C0C0Cu;       // group 0: {0, 0, 0, HB.b1} (slot 0 is no cell)
+
+#define PCB_UNPACK                                                                       \
+    "v_perm_b32 %[ha], %[hw], %[hw], %[slo]\n\t"                                             \
+    "v_perm_b32 %[hb], %[hw], %[hw], %[shi]\n\t"                                             \
+    "v_perm_b32 %[ea], %[ew], %[ew], %[slo]\n\t"                                             \
+    "v_perm_b32 %[eb], %[ew], %[ew], %[shi]\n\t"
+#define PCB_PACK                                                                         \
+    "v_perm_b32 %[hw], %[hb], %[ha], %[spk]\n\t"                                             \
+    "v_perm_b32 %[ew], %[eb], %[ea], %[spk]\n\t"
+
+#define PCB_GROUP_ASM(KEYA_FAST, KEYA_MASK)                                               \
+    asm volatile(                                                                            \
+        "s_bitcmp1_b64 %[mfa], %[g]\n\t"             /* every live lane in band: FAST */    \
+        "s_cbranch_scc0 5f\n\t"                                                              \
+        PC_CNT(0) PC_CNT(1)                                                                  \
+        PCB_UNPACK                                                                           \
+        PC_SCORES                                                                            \
+        PC_PH1B("a", "%[ea]") PC_PH1B("b", "%[eb]")                                          \
+        PC_FAST_CHAIN_("v_perm_b32 %[hw], %[pa], %[h1], %[sa1]\n\t",                         \
+                       "v_perm_b32 %[hw], %[h1], %[hw], %[sa2]\n\t")                         \
+        "v_perm_b32 %[ew], %[eb], %[ea], %[spk]\n\t"                                         \
+        KEYA_FAST                                                                            \
+        "v_pk_max_u16 %[key], %[key], %[pa]\n\t"                                             \
+        "v_perm_b32 %[pb], %[hw], %[jjb], %[vkb]\n\t"                                        \
+        "v_pk_max_u16 %[key], %[key], %[pb]\n"                                               \
+        "3:\n"                                                                               \
+        ".subsection 1\n"                                                                    \
+        "5:\n\t"                                                                             \
+        "s_bitcmp1_b64 %[men], %[g]\n\t"             /* outside [min beg, max end]: skip */ \
+        "s_cbranch_scc0 3b\n\t"                                                              \
+        "s_setprio 2\n\t"                                                                    \
+        PC_CNT(0)                                                                            \
+        PCB_UNPACK                                                                           \
+        "v_lshrrev_b32_e32 %[h1], 16, %[h1]\n\t"                                             \
+        PC_SCORES                                                                            \
+        "s_bitcmp1_b64 %[mle], %[g]\n\t"             /* some lane's beg in this group: L */ \
+        "s_cbranch_scc1 4f\n\t"                                                              \
+        PC_CNT(2)                                                                            \
+        PC_MASKED_(PC_PH1B,                                                                  \
+                  PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"),                        \
+                  PC_MCELL("%[c1]", "%[c0]", "a", "WORD_1", "%[j1]"),                        \
+                  PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"),                        \
+                  PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"),                        \
+                  KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t", "", "")           \
+        PCB_PACK                                                                             \
+        "v_lshlrev_b32_e32 %[h1], 16, %[h1]\n\t"                                             \
+        "s_setprio 0\n\t"                                                                    \
+        "s_branch 3b\n"                                                                      \
+        "4:\n\t"                                                                             \
+        PC_CNT(3)                                                                            \
+        PC_MASKED_(PC_PH1B,                                                                  \
+                  PC_RESET("%[h1]", "%[r0]") PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"), \
+                  PC_RESET("%[c0]", "%[j1]") PC_MCELL("%[c1]", "%[c0]", "a", "WORD_1", "%[j1]"), \
+                  PC_RESET("%[c1]", "%[j2]") PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"), \
+                  PC_RESET("%[c2]", "%[j3]") PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"), \
+                  KEYA_MASK, "v_lshl_or_b32 %[pb], %[pb], 8, %[jjb]\n\t",                    \
+                  PC_LEFTMASK("a"), PC_LEFTMASK("b"))                                        \
+        PCB_PACK                                                                             \
+        "v_lshlrev_b32_e32 %[h1], 16, %[h1]\n\t"                                             \
+        "s_setprio 0\n\t"                                                                    \
+        "s_branch 3b\n"                                                                      \
+        ".subsection 0\n"                                                                    \
+        : [hw] "+v"(hw), [ew] "+v"(ew), [ha] "=&v"(ha), [hb] "=&v"(hb), [ea] "=&v"(ea),      \
+          [eb] "=&v"(eb), [f] "+v"(f),                                                       \
+          [h1] "+v"(h1), [key] "+v"(key), [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb),     \
+          [ta] "=&v"(ta), [tb] "=&v"(tb), [xa] "=&v"(xa), [xb] "=&v"(xb), [c0] "=&v"(c0),    \
+          [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb), [fp] "=&v"(fp)    \
+          PC_CNT_OPS                                                                         \
+        : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe2] "s"(oe2), [ed2] "s"(ed2),        \
+          [ed] "s"(ed), [e0e] "s"(e0e), [ee2] "s"(ee2), [men] "s"(r.enter), [mfa] "s"(r.fast), [mle] "s"(r.left),           \
+          [endw] "v"(endw), [endm1w] "v"(endm1w),                                            \
+          [begm2w] "v"(begm2w), [endv] "v"(endv), [begv] "v"(begv), [g] "i"(G),             \
+          [jja] "s"(JJA), [jjb] "s"(JJB), [j0] "i"(4 * G), [j1] "i"(4 * G + 1),              \
+          [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [r0] "i"(R0),                            \
+          [slo] "s"(kSelLo), [shi] "s"(kSelHi), [spk] "s"(kSelPk), [sa1] "s"(kSelA1),         \
+          [sa2] "s"(kSelA2), [sk0] "s"(kSelK0), [vka] "v"(bs.ka), [vkb] "v"(bs.kb)            \
+        : "vcc", "scc")
+
+struct PcbSel { uint32_t ka, kb; };            // the key selectors (VGPRs: v_perm takes one SGPR)
+
+template <int G>
+__device__ __forceinline__ void pcb_group(uint32_t &hw, uint32_t &ew, uint32_t q, uint32_t plo, uint32_t phi,
+                                          int &f, int &h1, uint32_t &key, uint32_t oe2, uint32_t ed2, int ed,
+                                          const PcRow &r, uint32_t endw, uint32_t endm1w, uint32_t begm2w,
+                                          int endv, int begv, const PcbSel &bs, uint32_t (&ctr)[4])
+{
+    (void)ctr;
+    constexpr uint32_t JJA = ((uint32_t)(4 * G - 1) & 0xffffu) | ((uint32_t)(4 * G) << 16);
+    constexpr uint32_t JJB = (uint32_t)(4 * G + 1) | ((uint32_t)(4 * G + 2) << 16);
+    constexpr int R0 = (G == 0) ? -1 : 4 * G;
+    uint32_t ha, hb, ea, eb, y, sa, sb, ta, tb, xa, xb, c0, c1, c2, pa, pb, fp;
+    const uint32_t e0e = (uint32_t)ed << 16;
+    const uint32_t ee2 = (uint32_t)ed | ((uint32_t)(2 * ed) << 16);
+    if constexpr (G == 0) {
+        PCB_GROUP_ASM("v_perm_b32 %[pa], %[hw], %[hw], %[sk0]\n\t",
+                      "v_lshl_or_b32 %[pa], %[c0], 24, 0\n\t");
+    } else {
+        PCB_GROUP_ASM("v_perm_b32 %[pa], %[hw], %[jja], %[vka]\n\t",
+                      "v_lshl_or_b32 %[pa], %[pa], 8, %[jja]\n\t");
+    }
+}
+
+// plane registers per pair: two columns per VGPR (int16), four (bytes)
+template <int QMAX, bool BY> struct PcNp { static constexpr int v = BY ? QMAX / 4 : QMAX / 2; };
+
+template <int QMAX, bool BY, int G>
+__device__ __forceinline__ void pc_group_if(uint32_t (&hh)[(BY ? QMAX / 4 : QMAX / 2)], uint32_t (&ee)[(BY ? QMAX / 4 : QMAX / 2)],
                                             const uint32_t (&qs)[QMAX / 4], uint32_t plo, uint32_t phi, int &f,
                                             int &h1, uint32_t &key, uint32_t oe2, uint32_t ed2, int ed,
                                             const PcRow &r, uint32_t endw, uint32_t endm1w, uint32_t begm2w, int endv,
-                                            int begv, uint32_t (&ctr)[4])
+                                            int begv, const PcbSel &bs, uint32_t (&ctr)[4])
 {
-    if constexpr (G < QMAX / 4)
-        pc_group<G>(hh[2 * G], hh[2 * G + 1], ee[2 * G], ee[2 * G + 1], qs[G], plo, phi, f, h1, key, oe2, ed2, ed,
-                    r, endw, endm1w, begm2w, endv, begv, ctr);
+    if constexpr (G < QMAX / 4) {
+        if constexpr (BY)
+            pcb_group<G>(hh[G], ee[G], qs[G], plo, phi, f, h1, key, oe2, ed2, ed, r, endw, endm1w, begm2w, endv,
+                         begv, bs, ctr);
+        else
+            pc_group<G>(hh[2 * G], hh[2 * G + 1], ee[2 * G], ee[2 * G + 1], qs[G], plo, phi, f, h1, key, oe2, ed2,
+                        ed, r, endw, endm1w, begm2w, endv, begv, ctr);
+    }
 }
 
 // Segments of 8 groups behind one uniform test of the row's entered set: a segment no lane's
@@ -283,30 +420,30 @@ __device__ __forceinline__ void pc_group_if(uint32_t (&hh)[QMAX / 2], uint32_t (
 #endif
 constexpr int kPcSeg = BSW_PC_SEG;
 template <int QMAX> constexpr int pc_seg_len() { return QMAX <= 64 ? QMAX / 4 : kPcSeg; }
-template <int QMAX, int S, int... K>
-__device__ __forceinline__ void pc_seg(std::integer_sequence<int, K...>, uint32_t (&hh)[QMAX / 2],
-                                       uint32_t (&ee)[QMAX / 2], const uint32_t (&qs)[QMAX / 4], uint32_t plo,
+template <int QMAX, bool BY, int S, int... K>
+__device__ __forceinline__ void pc_seg(std::integer_sequence<int, K...>, uint32_t (&hh)[(BY ? QMAX / 4 : QMAX / 2)],
+                                       uint32_t (&ee)[(BY ? QMAX / 4 : QMAX / 2)], const uint32_t (&qs)[QMAX / 4], uint32_t plo,
                                        uint32_t phi, int &f, int &h1, uint32_t &key, uint32_t oe2, uint32_t ed2,
                                        int ed, const PcRow &r, uint32_t endw, uint32_t endm1w, uint32_t begm2w,
-                                       int endv, int begv, uint32_t (&ctr)[4])
+                                       int endv, int begv, const PcbSel &bs, uint32_t (&ctr)[4])
 {
     constexpr int kSeg = sizeof...(K);
     constexpr uint64_t kSegMask = ((1ull << kSeg) - 1) << (kSeg * S);
     if (kSeg == QMAX / 4 || (r.enter & kSegMask))
-        (pc_group_if<QMAX, kSeg * S + K>(hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r, endw, endm1w, begm2w,
-                                           endv, begv, ctr), ...);
+        (pc_group_if<QMAX, BY, kSeg * S + K>(hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r, endw, endm1w,
+                                               begm2w, endv, begv, bs, ctr), ...);
 }
 
-template <int QMAX, int... S>
-__device__ __forceinline__ void pc_row(std::integer_sequence<int, S...>, uint32_t (&hh)[QMAX / 2],
-                                       uint32_t (&ee)[QMAX / 2], const uint32_t (&qs)[QMAX / 4],
+template <int QMAX, bool BY, int... S>
+__device__ __forceinline__ void pc_row(std::integer_sequence<int, S...>, uint32_t (&hh)[(BY ? QMAX / 4 : QMAX / 2)],
+                                       uint32_t (&ee)[(BY ? QMAX / 4 : QMAX / 2)], const uint32_t (&qs)[QMAX / 4],
                                        uint32_t plo, uint32_t phi, int &f, int &h1, uint32_t &key,
                                        uint32_t oe2, uint32_t ed2, int ed, const PcRow &r,
                                        uint32_t endw, uint32_t endm1w, uint32_t begm2w, int endv,
-                                       int begv, uint32_t (&ctr)[4])
+                                       int begv, const PcbSel &bs, uint32_t (&ctr)[4])
 {
-    (pc_seg<QMAX, S>(std::make_integer_sequence<int, pc_seg_len<QMAX>()>{}, hh, ee, qs, plo, phi, f, h1, key, oe2, ed2, ed, r,
-                     endw, endm1w, begm2w, endv, begv, ctr), ...);
+    (pc_seg<QMAX, BY, S>(std::make_integer_sequence<int, pc_seg_len<QMAX>()>{}, hh, ee, qs, plo, phi, f, h1, key, oe2,
+                         ed2, ed, r, endw, endm1w, begm2w, endv, begv, bs, ctr), ...);
 }
 
 // Lazy last positive column: when H(i, end-1) == 0 the lanes that need it
@@ -331,32 +468,37 @@ __device__ __forceinline__ void pc_lastpos_reg(uint32_t hv, uint32_t endp1w, uin
         : [h] "v"(hv), [sc] "s"(SC), [e1] "v"(endp1w));
 }
 
-template <int QMAX, int GG>
-__device__ __forceinline__ bool pc_lastpos_group(const uint32_t (&hh)[QMAX / 2], uint32_t endp1w, bool pending,
-                                                 uint32_t &lp, int gstart)
+template <int QMAX, bool BY, int GG>
+__device__ __forceinline__ bool pc_lastpos_group(const uint32_t (&hh)[(BY ? QMAX / 4 : QMAX / 2)], uint32_t endp1w,
+                                                 bool pending, uint32_t &lp, int gstart)
 {
     if (GG > gstart) return pending;                      // uniform: above every lane's end
     if (__ballot(pending) == 0) return false;             // uniform: all found
-    if constexpr (2 * GG + 1 < QMAX / 2) pc_lastpos_reg<2 * GG + 1>(hh[2 * GG + 1], endp1w, lp);
-    pc_lastpos_reg<2 * GG>(hh[2 * GG], endp1w, lp);
+    if constexpr (BY) {                                   // slots {4GG+2, 4GG+3}, {4GG, 4GG+1}
+        pc_lastpos_reg<2 * GG + 1>(__builtin_amdgcn_perm(hh[GG], hh[GG], kSelHi), endp1w, lp);
+        pc_lastpos_reg<2 * GG>(__builtin_amdgcn_perm(hh[GG], hh[GG], kSelLo), endp1w, lp);
+    } else {
+        if constexpr (2 * GG + 1 < QMAX / 2) pc_lastpos_reg<2 * GG + 1>(hh[2 * GG + 1], endp1w, lp);
+        pc_lastpos_reg<2 * GG>(hh[2 * GG], endp1w, lp);
+    }
     return pending & (lp == 0u);
 }
 
-template <int QMAX, int... G>
-__device__ __forceinline__ int pc_lastpos(std::integer_sequence<int, G...>, const uint32_t (&hh)[QMAX / 2],
+template <int QMAX, bool BY, int... G>
+__device__ __forceinline__ int pc_lastpos(std::integer_sequence<int, G...>, const uint32_t (&hh)[(BY ? QMAX / 4 : QMAX / 2)],
                                           int end, bool need, int gstart)
 {
     bool pending = need;
     uint32_t lp = 0;
     const uint32_t endp1w = pack2(end + 1);
-    ((pending = pc_lastpos_group<QMAX, QMAX / 4 - 1 - G>(hh, endp1w, pending, lp, gstart)), ...);
+    ((pending = pc_lastpos_group<QMAX, BY, QMAX / 4 - 1 - G>(hh, endp1w, pending, lp, gstart)), ...);
     return (int)max(lp & 0xffffu, lp >> 16);
 }
 
 // WPB waves per workgroup: with 1, a wave's slot (and its LDS) is reused as soon as that wave
 // ends, instead of when the slowest of its block's waves ends.
-template <int QMAX, int WPB>
-__global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const int32_t w,
+template <int QMAX, int WPB, bool BY>
+__global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams kp, const int32_t w,
                                                     SeqPair *__restrict__ pairs,
                                                     const int32_t *__restrict__ order,
                                                     const int32_t n,
@@ -404,17 +546,35 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
         }
     }
     // A.1 first row: slot 0 = h0, slot j = max(h0 - oe_ins - (j-1) e_ins, 0) for 1 <= j <= qlen
-    uint32_t hh[QMAX / 2], ee[QMAX / 2];
+    constexpr int NP = (BY ? QMAX / 4 : QMAX / 2);
+    uint32_t hh[NP], ee[NP];
     {
         const int oe_ins = kp.o_ins + kp.e_ins;
+        if constexpr (BY) {
+            __builtin_amdgcn_sched_barrier(0);     // after the query words: their loads' registers
+                                                   // are dead before the planes are built
 #pragma unroll
-        for (int k = 0; k < QMAX / 2; ++k) {
-            const int j0 = 2 * k, j1 = 2 * k + 1;
-            const uint32_t a = (j0 == 0) ? (uint32_t)h0
-                             : (j0 <= qlen) ? (uint32_t)max(h0 - oe_ins - (j0 - 1) * kp.e_ins, 0) : 0u;
-            const uint32_t b = (j1 <= qlen) ? (uint32_t)max(h0 - oe_ins - (j1 - 1) * kp.e_ins, 0) : 0u;
-            hh[k] = a | (b << 16);
-            ee[k] = 0u;
+            for (int k = 0; k < NP; ++k) {         // h0 <= 255 (the 8-bit regime): bytes
+                uint32_t v[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int j = 4 * k + t;
+                    v[t] = (j == 0) ? (uint32_t)h0 : (j <= qlen) ? (uint32_t)max(h0 - oe_ins - (j - 1) * kp.e_ins, 0) : 0u;
+                }
+                hh[k] = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+                asm volatile("" : "+v"(hh[k]));   // built here, not sunk to the loop (the
+                ee[k] = 0u;                        // bytes of every word live at once: +40 VGPRs)
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const int j0 = 2 * k, j1 = 2 * k + 1;
+                const uint32_t a = (j0 == 0) ? (uint32_t)h0
+                                 : (j0 <= qlen) ? (uint32_t)max(h0 - oe_ins - (j0 - 1) * kp.e_ins, 0) : 0u;
+                const uint32_t b = (j1 <= qlen) ? (uint32_t)max(h0 - oe_ins - (j1 - 1) * kp.e_ins, 0) : 0u;
+                hh[k] = a | (b << 16);
+                ee[k] = 0u;
+            }
         }
     }
     // A.2 per-lane band cap, integer form of (int)((double)N / e + 1.)
@@ -447,6 +607,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
     const uint32_t oe2 = (uint32_t)(kp.o_del + kp.e_del) * 0x10001u;
     const uint32_t ed2 = (uint32_t)kp.e_del * 0x10001u;
     uint32_t ctr[4] = {0, 0, 0, 0};                       // BSW_PC_STATS group-path counters
+    const PcbSel bs{kSelKa, kSelKb};
 #ifdef BSW_PC_STATS
     uint32_t nrows = 0, nlast = 0, nue = 0;
 #endif
@@ -515,8 +676,9 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
             // wave priority: the row's serial scalar / DPP chain (row end, next row's head) issues
             // ahead of the partner wave's group VALU; the groups themselves run at the base level
             __builtin_amdgcn_s_setprio(0);
-            pc_row<QMAX>(std::make_integer_sequence<int, (NG + pc_seg_len<QMAX>() - 1) / pc_seg_len<QMAX>()>{}, hh, ee, qs, pr.x, pr.y, f, h1, key,
-                         oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg, ctr);
+            pc_row<QMAX, BY>(std::make_integer_sequence<int, (NG + pc_seg_len<QMAX>() - 1) / pc_seg_len<QMAX>()>{}, hh, ee,
+                             qs, pr.x, pr.y, f, h1, key, oe2, ed2, kp.e_del, r, endw, endm1w, begm2w, end, beg, bs,
+                             ctr);
             __builtin_amdgcn_s_setprio(2);
             h1 = (int)((uint32_t)h1 >> 16);               // H(i, end-1)
             const uint32_t k32 = max(key & 0xffffu, key >> 16);
@@ -552,8 +714,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void pc_kernel(const KParams kp, const
 #ifdef BSW_PC_STATS
                     nlast += 1;
 #endif
-                    const int lp = pc_lastpos<QMAX>(std::make_integer_sequence<int, NG>{}, hh, end, need,
-                                                    emax >> 2);
+                    const int lp = pc_lastpos<QMAX, BY>(std::make_integer_sequence<int, NG>{}, hh, end, need,
+                                                        emax >> 2);
                     lp1 = need ? lp : end;
                 }
                 endc = alive ? min(lp1 + 2, qlen) : endc;
@@ -603,12 +765,17 @@ template <int QMAX>
 static void launch_pc_q(const KParams &kp, int32_t w, SeqPair *pairs, const int32_t *order, int32_t n,
                         const uint8_t *ref, const uint8_t *qer, int32_t *err, hipStream_t s)
 {
+    const unsigned grid = (unsigned)((n + 63) / 64);
     // one wave per workgroup: a finished wave's slot and LDS are reused at once
 #ifndef BSW_PC_LDS_PAD          // experiment builds only: dynamic LDS per workgroup caps waves per CU
 #define BSW_PC_LDS_PAD 0
 #endif
-    hipLaunchKernelGGL((pc_kernel<QMAX, 1>), dim3((unsigned)((n + 63) / 64)), dim3(64), BSW_PC_LDS_PAD, s, kp, w, pairs,
-                       order, n, ref, qer, err);
+    if (kp.kern8 == 2)                 // byte planes (BSW_OPT_KERNEL8 = 2)
+        hipLaunchKernelGGL((pc_kernel<QMAX, 1, true>), dim3(grid), dim3(64), BSW_PC_LDS_PAD, s, kp, w, pairs, order, n,
+                           ref, qer, err);
+    else
+        hipLaunchKernelGGL((pc_kernel<QMAX, 1, false>), dim3(grid), dim3(64), BSW_PC_LDS_PAD, s, kp, w, pairs, order,
+                           n, ref, qer, err);
 }
 
 hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,

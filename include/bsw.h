@@ -121,7 +121,10 @@ int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
  * an out-of-range value. */
 enum {
     BSW_OPT_KERNEL8 = 1,      /* 8-bit-regime pairs (h0 + min(len1,len2) <= 255, bwa scoring):
-                                 1 = packed-column kernel (default), 0 = int16 lane kernel  */
+                                 1 = packed-column kernel (default), 0 = int16 lane kernel,
+                                 2 = packed-column kernel with byte-wide H/E planes (8-bit
+                                 cells, fewer registers, more waves per SIMD; outputs are
+                                 identical either way)                                         */
     BSW_OPT_FORK = 2,         /* a batch's class launches: 1 = fork over side streams
                                  (default), 0 = serial on the call's stream                   */
     BSW_OPT_SORTKEY = 3,      /* plan sort key: 1 = seed identities before h0 (default),
@@ -165,6 +168,12 @@ enum {
                                  pairs (default 32768; 0 = off) run on the row-group kernel's quad
                                  form (4 lanes per pair, targets <= 512 bytes) when
                                  BSW_OPT_GROUP_KERNEL is on.  Outputs are identical either way  */
+    BSW_OPT_BUSY_MIN = 15,    /* coalesced batches (BSW_OPT_COALESCE) of at least this many pairs
+                                 that start while another batch is in flight on their device run
+                                 on the planned packed-column lane kernels instead of the row-
+                                 group kernel (default 8192; 0 = never): under concurrent callers
+                                 throughput, not one call's latency, bounds the device.  Outputs
+                                 are identical either way                                       */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };
