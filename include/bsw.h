@@ -171,8 +171,8 @@ enum {
     BSW_OPT_BUSY_MIN = 15,    /* coalesced batches (BSW_OPT_COALESCE) of at least this many pairs
                                  that start while another batch is in flight on their device run
                                  on the planned packed-column lane kernels instead of the row-
-                                 group kernel (default 8192; 0 = never): under concurrent callers
-                                 throughput, not one call's latency, bounds the device.  Outputs
+                                 group kernel (default 0 = never: measured slower at 10K-pair
+                                 calls x 8 callers; an experiment knob).  Outputs
                                  are identical either way                                       */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
