@@ -463,7 +463,15 @@ __device__ int smem_read(const FmiDevT<U> &f, const MemOpt &opt, const uint8_t *
 constexpr int kSmemBlock = BSW_SMEM_BLOCK;          // threads per workgroup of the SMEM kernel
 
 template <class U>
-__global__ __launch_bounds__(kSmemBlock) void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
+#ifndef BSW_SMEM_WAVES           // experiment builds: a minimum of waves per SIMD for the walk
+#define BSW_SMEM_WAVES 0         // (0 = the compiler's choice: 4 wide / 6 narrow)
+#endif
+#if BSW_SMEM_WAVES > 0
+#define BSW_SMEM_LB __launch_bounds__(kSmemBlock, BSW_SMEM_WAVES)
+#else
+#define BSW_SMEM_LB __launch_bounds__(kSmemBlock)
+#endif
+__global__ BSW_SMEM_LB void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
                                                   const uint8_t *__restrict__ reads,
                                                   const int64_t *__restrict__ read_off,
                                                   const int32_t *__restrict__ read_len, int32_t n0, int32_t n,

@@ -294,6 +294,28 @@ def test_host_pipeline_chunks(chunk):
     e.close()
 
 
+@pytest.mark.parametrize("bad_at", [10, 150_000, 199_999])
+def test_host_pipeline_invalid_pair_writes_nothing(bad_at):
+    """The pipeline validates the first chunk's blocks, starts it, and validates the rest before
+    any chunk's outputs are written back: an invalid pair anywhere (first chunk, middle, last
+    pair) returns BSW_E_RANGE with every caller record unchanged.  Then the same engine scores the
+    repaired batch (remainder chunk merged into the last one) equal to the oracle."""
+    e = bsw.Engine(host_chunk=65536, small_batch=0, mid_batch=0)
+    pairs, ref, qer = bsw.synth_batch(200_000, pair_base=77)
+    bad = pairs.copy()
+    bad[bad_at]["len1"] = -1
+    before = bad.copy()
+    with pytest.raises(bsw.BswError, match="-34"):
+        e.get_scores(bad, ref, qer, 100)
+    assert np.array_equal(bad, before)
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=16)
+    got = pairs.copy()
+    e.get_scores(got, ref, qer, 100)
+    _assert_same(want, got, f"after the rejected call (bad_at={bad_at})")
+    e.close()
+
+
 @pytest.mark.parametrize("pack,p_n", [(2, 0.0), (2, 0.02), (2, 0.1), (4, 0.02)])
 def test_host_pipeline_packing(pack, p_n):
     """Staging of contiguous sequence buffers (BSW_OPT_HOST_PACK): 2-bit codes + exception words

@@ -52,7 +52,7 @@ int main(int argc, char **argv)
     bool first = true;
     std::atomic<long> bad{0};
     for (int co = 1; co >= 0; --co) {
-        bsw_set_option(ctx, BSW_OPT_COALESCE, co ? 32768 : 0);
+        bsw_set_option(ctx, BSW_OPT_COALESCE, co ? (getenv("PERCALL_COALESCE") ? atoi(getenv("PERCALL_COALESCE")) : 32768) : 0);
         for (int32_t m : sizes) {
             if (m > N / T) continue;
             // one caller: median latency
