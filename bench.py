@@ -320,8 +320,10 @@ def host_path_rates(eng, pairs, ref, qer, w, cell_bits, want, curve_sizes=(1_000
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # default C2 run: 100 x ~7 ms, a timed region of ~0.7 s (long enough for an outside
+    # utilisation sampler); the other workloads: 10 steps, 2 warm-up
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--pairs", type=int, default=1_000_000, help="pairs per GPU")
     ap.add_argument("--w", type=int, default=100)
     ap.add_argument("--cell-bits", type=int, default=16, choices=(8, 16))
@@ -353,11 +355,21 @@ def main():
                          "fixed batch of --total-pairs split over the ranks by band cells, host buffers "
                          "in, PCIe both ways inside the timed region (C5)")
     ap.add_argument("--total-pairs", type=int, default=10_000_000, help="strong: pairs in the whole batch")
+    ap.add_argument("--transport", default="host", choices=("host", "rccl"),
+                    help="strong: host (default) -- every rank holds its range in host memory and the call "
+                         "stages it over its own PCIe link; rccl -- the whole batch resident on GPU 0, scattered "
+                         "to the ranks' GPUs and the outputs gathered back with RCCL over xGMI "
+                         "(torch.distributed backend nccl), BASELINE configs[4]'s batch scatter")
     ap.add_argument("--rehearse", action="store_true",
                     help="allow more ranks than visible GPUs (ranks share GPUs; rehearsal only)")
     ap.add_argument("--dump", default="", help="strong: rank 0 writes the gathered outputs here (.npy); c4 / "
                                                "c4mem: every rank writes <dump>.rank<r>.npz")
     args = ap.parse_args()
+    c2_default = args.workload == "c2" and args.scaling == "weak"
+    if args.steps is None:
+        args.steps = 100 if c2_default else 10
+    if args.warmup is None:
+        args.warmup = 5 if c2_default else 2
 
     rank, local, world = dist_init()
     if world != args.gpus:
@@ -372,6 +384,8 @@ def main():
     local = local % ndev              # --rehearse: more ranks than GPUs share them
     hiprt.set_device(local)
     if args.scaling == "strong":
+        if args.transport == "rccl":
+            return main_strong_rccl(args, rank, local, world)
         return main_strong(args, rank, local, world)
     if args.workload == "c1":          # BASELINE configs[0]: 10K exact 150 bp SE reads vs 1 Mb
         return main_mem(args, rank, local, world, c1=True)
@@ -521,6 +535,95 @@ def main():
         roof["actual_cells_per_s"] = round(args.pairs * acp / (kms_mean * 1e-3) / 1e12, 4)
     out["synth_gen_s"] = round(gen_s, 2)
     print(json.dumps(out), flush=True)
+
+
+def main_strong_rccl(args, rank, local, world):
+    """C5 as BASELINE configs[4] words it: ONE batch of --total-pairs C2 pairs resident on GPU 0,
+    packed per rank (bwa-mem2-arm_amd/py/shards.py: contiguous ranges of equal static band cells,
+    records rebased to their own windows, one padded byte buffer per rank), SCATTERED to the ranks'
+    GPUs with RCCL over xGMI (torch.distributed backend "nccl"), scored in place on each GPU
+    (bsw_get_scores_device on pointers into the received buffer), and the 24 output bytes per pair
+    GATHERED back to GPU 0.  Scatter, compute and gather are inside the timed region; value = total
+    pairs / max-over-ranks step time.  With one rank a device-to-device copy stands in for the
+    scatter (nothing to send)."""
+    import torch
+    import torch.distributed as dist
+    import shards
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    g = dist.new_group(backend="nccl") if world > 1 else None
+    cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
+    N = args.total_pairs
+    t0 = time.perf_counter()
+    meta_t = torch.zeros((world, 3), dtype=torch.int64)
+    src = None
+    if rank == 0:
+        pairs, ref, qer = bsw.synth_batch(N, cfg=cfg)
+        cut = bsw.split_by_cells(pairs, args.w, world)
+        bufs, meta = shards.pack_shards(pairs, ref, qer, cut)
+        del ref, qer
+        meta_t.copy_(torch.from_numpy(meta))
+        src = [torch.from_numpy(bufs[k]).to(dev) for k in range(world)]     # the batch, resident on GPU 0
+        del bufs
+    if world > 1:
+        dist.broadcast(meta_t, src=0)                                      # (gloo, before timing)
+    meta = meta_t.numpy()
+    gen_s = time.perf_counter() - t0
+    S = shards.buffer_bytes(meta)
+    n_me = int(meta[rank, 0])
+    po, ro, qo = shards.offsets(meta[rank])
+    nmax = int(meta[:, 0].max())
+    recv = torch.zeros(S, dtype=torch.uint8, device=dev)
+    out_me = torch.zeros((nmax, 6), dtype=torch.int32, device=dev)
+    gathered = [torch.zeros((nmax, 6), dtype=torch.int32, device=dev) for _ in range(world)] if rank == 0 else None
+    eng = bsw.Engine(device=local)
+    base = recv.data_ptr()
+
+    def step():
+        if world > 1:
+            dist.scatter(recv, src if rank == 0 else None, src=0, group=g)
+        else:
+            recv.copy_(src[0])
+        torch.cuda.current_stream().synchronize()
+        if n_me > 0:
+            eng.get_scores_device(base + po, base + ro, base + qo, n_me, args.w, args.cell_bits)
+            out_me[:n_me] = recv[po:po + 56 * n_me].view(torch.int32).view(n_me, 14)[:, shards.OUT_COLS]
+        if world > 1:
+            dist.gather(out_me, gathered, dst=0, group=g)
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier(world)
+    dt = time.perf_counter() - t
+    dt_max = allreduce_max(dt, world)
+    if rank != 0:
+        return
+    if args.dump:
+        outs = [x.cpu().numpy() for x in gathered] if world > 1 else [out_me.cpu().numpy()]
+        res = pairs.copy()
+        shards.merge_outputs(res, outs, cut)
+        np.save(args.dump, res)
+    value = N * args.steps / dt_max / 1e6
+    out_j = {
+        "metric": METRIC, "value": round(value, 3), "unit": UNIT, "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int16", "data": "synthetic (bsw_synth.c, seed 42)",
+        "config": {"workload": f"C5 strong scaling, RCCL batch scatter: one batch of {N} C2 pairs ({cfg.qlen} bp "
+                               f"query / {cfg.tlen} bp ref, w={args.w}) resident on GPU 0, split over {world} "
+                               f"rank(s) by static band cells, scattered / gathered with RCCL over xGMI inside "
+                               f"the timed region",
+                   "total_pairs": N, "pairs_rank0": n_me, "shard_buffer_bytes": S,
+                   "parallelism": f"split{world} (bsw_split_by_cells; RCCL scatter + gather)",
+                   "distinct_gpus": args.distinct_gpus},
+        "synth_gen_s": round(gen_s, 2),
+    }
+    print(json.dumps(out_j), flush=True)
 
 
 def main_strong(args, rank, local, world):

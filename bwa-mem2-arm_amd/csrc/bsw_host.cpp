@@ -254,7 +254,9 @@ template <class T>
 static hipError_t grow(T *&p, size_t &cap, size_t need)   // cap counts elements (bytes for void)
 {
     if (need <= cap) return hipSuccess;
-    const size_t n = std::max(need, cap * 3 / 2);
+    // 25% headroom: the pipeline's chunks vary (ramp, a merged remainder up to 1.25x) and slots
+    // rotate between them, so exact-fit growth reallocated on many calls (hipFree syncs the device)
+    const size_t n = std::max(need + need / 4, cap * 3 / 2);
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
@@ -901,7 +903,7 @@ static int stage_2bit(Slot &s, const SeqPair *pairs, const uint8_t *ref, const u
     c.exc_off = align256(c.qer_off + qs + 4);
     c.bytes = std::max(c.exc_off + exc_cap * 4, (size_t)n * 24);
     if (c.bytes > s.cap_stage) {
-        const size_t cap = std::max(c.bytes, s.cap_stage * 3 / 2);
+        const size_t cap = std::max(c.bytes + c.bytes / 4, s.cap_stage * 3 / 2);
         if (s.h_stage) (void)hipHostFree(s.h_stage);
         s.h_stage = nullptr; s.cap_stage = 0;
         BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));
@@ -977,7 +979,7 @@ static int stage_chunk(Slot &s, const SeqPair *pairs, const uint8_t *ref, const 
     c.qer_off = (c.ref_off + rs + 4 + 255) & ~(size_t)255;     // +4: kernels' aligned dword loads
     c.bytes = c.qer_off + qs + 4;
     if (c.bytes > s.cap_stage) {
-        const size_t cap = std::max(c.bytes, s.cap_stage * 3 / 2);
+        const size_t cap = std::max(c.bytes + c.bytes / 4, s.cap_stage * 3 / 2);
         if (s.h_stage) (void)hipHostFree(s.h_stage);
         s.h_stage = nullptr; s.cap_stage = 0;
         BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));
@@ -1331,7 +1333,7 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
         const size_t qer_off = align256(ref_off + rs + 4), exc_off = align256(qer_off + qs + 4);
         const size_t bytes = std::max(exc_off + exc_cap * 4, (size_t)N * 24);
         if (bytes > s.cap_stage) {
-            const size_t cap = std::max(bytes, s.cap_stage * 3 / 2);
+            const size_t cap = std::max(bytes + bytes / 4, s.cap_stage * 3 / 2);
             if (s.h_stage) (void)hipHostFree(s.h_stage);
             s.h_stage = nullptr; s.cap_stage = 0;
             BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));

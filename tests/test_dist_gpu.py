@@ -96,3 +96,26 @@ def test_ranks_c4_pe_workload_equal_oracle(tmp_path, workload):
         assert np.array_equal(z["ext"], wext), f"rank {rank}"
         for fld in bsw.ALNREG_DTYPE.names:
             assert np.array_equal(z["out"][fld], want[fld]), (rank, fld)
+
+
+@pytest.mark.gpu
+def test_rccl_transport_one_rank_equal_oracle(tmp_path):
+    """bench.py --scaling strong --transport rccl with one rank: the batch packed into its shard
+    buffer (shards.py), resident on GPU 0 as a torch tensor, scored in place through
+    bsw_get_scores_device on pointers into that tensor, the outputs read back through the same
+    torch views the RCCL gather moves.  (RCCL itself needs one GPU per rank: the N > 1 scatter /
+    gather logic is covered over gloo by tests/test_dist.py; the 8-GPU run is the driver's.)"""
+    n = 150_000
+    dump = str(tmp_path / "rccl.npy")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--scaling", "strong", "--transport", "rccl",
+           "--total-pairs", str(n), "--steps", "2", "--warmup", "1", "--dump", dump]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["scaling"] == "strong" and line["n_gpus"] == 1 and "RCCL" in line["config"]["workload"]
+    got = np.load(dump)
+    full, ref, qer = bsw.synth_batch(n)
+    want = full.copy()
+    oracle.get_scores(oracle.make_params(), want, ref, qer, 100, nthreads=16)
+    for f in ("idr", "idq", "len1", "len2", "h0") + bsw.OUT_FIELDS:
+        assert np.array_equal(got[f], want[f]), f

@@ -12,7 +12,7 @@ chunk = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
 pairs, ref, qer = bsw.synth_batch(1_000_000)
 e = bsw.Engine(host_chunk=chunk)
 buf = pairs.copy()
-for _ in range(3):
+for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 3):
     t = time.perf_counter()
     e.get_scores(buf, ref, qer, 100)
     st = e.last_stats()
