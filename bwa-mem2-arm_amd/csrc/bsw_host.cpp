@@ -1069,16 +1069,11 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     if (n == 0) return BSW_OK;
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto t_start = now();
+    // the whole prepass (validation + per-block byte extents) before chunk 0: validating only chunk
+    // 0's blocks first and the rest after it started measured no faster
+    std::vector<BlkStat> bs;
+    if (!prepass(pairs, n, bs)) return BSW_E_RANGE;
     if (chunk <= 0) chunk = n;
-    // the prepass (validation + per-block byte extents) of the first chunk's blocks only; the
-    // rest runs after chunk 0 is on its way, so the GPU starts ~0.6 ms earlier on a 1M call.
-    // No output is written before the whole prepass passed (outputs land in finish())
-    std::vector<BlkStat> bs((size_t)((n + kStageBlk - 1) / kStageBlk), BlkStat{});
-    const int32_t nblk0 = (int32_t)bs.size();
-    const int32_t cap_blk0 = std::max<int32_t>(1, chunk / kStageBlk);
-    const int32_t first_blk = std::min(cap_blk0, nblk0 <= 32 ? nblk0 : std::max<int32_t>(16, nblk0 / 32));
-    const bool early = getenv("BSW_HP_NO_EARLY") == nullptr && first_blk < nblk0;
-    if (!prepass_range(pairs, n, bs, 0, early ? first_blk : nblk0)) return BSW_E_RANGE;
     constexpr int nslots = 3;  // slots are taken as chunks start (a one-chunk call takes one)
     int rc = BSW_OK;
     std::unique_ptr<Slot> slots[nslots];
@@ -1169,10 +1164,10 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         BSW_TRY(hipSetDevice(dc.device));
         int k = 0;
         int32_t seq = 0;
-        const int32_t nblk = nblk0;
-        const int32_t cap_blk = cap_blk0;
+        const int32_t nblk = (int32_t)bs.size();
+        const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
         // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
-        int32_t cur = first_blk;
+        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
         for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 2)) {
             // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
             int64_t bytes = 0;
@@ -1181,16 +1176,10 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
                 if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
                 bytes += x;
             }
-            if (early && seq == 0) nb = std::min(nb, first_blk);   // only these blocks are known yet
-            else if (b + nb < nblk && (nblk - b - nb) * 4 <= nb && !getenv("BSW_HP_NO_MERGE")) {
-                // a remainder under a quarter of this chunk rides along: as its own chunk it ran
-                // as a small tail launch after the rest (rocprofv3 timeline: a 17K-pair last
-                // chunk of a 1M call ended 0.3 ms after the last full chunk) and waited ~1 ms for
-                // its slot
-                int64_t extra = 0;
-                for (int32_t j = b + nb; j < nblk; ++j) extra += bs[j].r_sum + bs[j].q_sum;
-                if (bytes + extra <= ((int64_t)1 << 29)) nb = nblk - b;
-            }
+            // (a small remainder stays its own chunk: folded into the last full chunk it added a
+            // third, nearly empty generation of waves to that launch -- 262144 pairs are exactly
+            // two generations at two waves per SIMD -- and the call got ~1 ms slower; as its own
+            // launch it runs beside the last chunk on another queue.  Measured)
             const int32_t a = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a;
             const auto tw = now();
             int r = finish(k);                          // slot k's last chunk
@@ -1263,7 +1252,6 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
                 L.q.push_back(Launcher::Job{k, seq, c.mode});
             }
             L.cv.notify_all();
-            if (early && seq == 0 && !prepass_range(pairs, n, bs, first_blk, nblk)) return BSW_E_RANGE;
         }
         for (int j = 0; j < nslots; ++j) {
             const int r = finish(j);
