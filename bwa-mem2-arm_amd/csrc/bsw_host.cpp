@@ -411,7 +411,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.misroute = 0;
     kp.fork = 1;
     kp.long_route = 1;
-    kp.small_batch = 16384;
+    kp.small_batch = 32768;          // 16-lane row-group form up to 32K pairs
     kp.mid_batch = 32768;
     kp.group_kernel = 1;
     kp.busy_min = 0;                 // measured slower at every setting: off

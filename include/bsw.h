@@ -147,7 +147,7 @@ enum {
                                  non-ACGT bytes); outputs are identical                      */
     BSW_OPT_SMALL_BATCH = 9,  /* calls (device calls, or host-buffer pipeline chunks) of at most
                                  this many pairs run every pair the wave-per-alignment kernel
-                                 can take there (default 16384; 0 = off): a lane-per-pair wave
+                                 can take there (default 32768; 0 = off): a lane-per-pair wave
                                  lives ~1.2 ms at any batch size, a wave per alignment spreads
                                  the pair over 64 lanes -- kt_for-sized calls are latency-bound.
                                  Outputs are identical either way                              */
@@ -167,7 +167,9 @@ enum {
     BSW_OPT_MID_BATCH = 14,   /* calls / chunks of more than BSW_OPT_SMALL_BATCH and at most this many
                                  pairs (default 32768; 0 = off) run on the row-group kernel's quad
                                  form (4 lanes per pair, targets <= 512 bytes) when
-                                 BSW_OPT_GROUP_KERNEL is on.  Outputs are identical either way  */
+                                 BSW_OPT_GROUP_KERNEL is on -- an empty range at the defaults (the
+                                 16-lane form measured faster up to 32K pairs; lower
+                                 BSW_OPT_SMALL_BATCH to use it).  Outputs are identical either way */
     BSW_OPT_BUSY_MIN = 15,    /* coalesced batches (BSW_OPT_COALESCE) of at least this many pairs
                                  that start while another batch is in flight on their device run
                                  on the planned packed-column lane kernels instead of the row-

@@ -336,16 +336,16 @@ def test_host_pipeline_packing(pack, p_n):
 
 
 @pytest.mark.parametrize("group", [1, 0])
-@pytest.mark.parametrize("n", [1, 63, 1000, 16384, 16385])
+@pytest.mark.parametrize("n", [1, 63, 1000, 16384, 16385, 32768, 32769])
 def test_small_batch_route(n, group, c2_full):
-    """Default routing (BSW_OPT_SMALL_BATCH = 16384): calls of at most 16384 pairs run on the
-    row-group kernel (16 lanes per pair, no plan / sort; BSW_OPT_GROUP_KERNEL 1) or, with it off,
-    every int16-safe pair on the wave-per-alignment kernel; larger calls on the lane /
+    """Default routing (BSW_OPT_SMALL_BATCH = BSW_OPT_MID_BATCH = 32768): calls of at most 32768
+    pairs run on the row-group kernel (16 lanes per pair, no plan / sort; BSW_OPT_GROUP_KERNEL 1) or,
+    with it off, every int16-safe pair on the wave-per-alignment kernel; larger calls on the lane /
     packed-column classes.  Both entry points (host buffers, resident) and both cell widths give
     the oracle's outputs."""
     pairs, ref, qer, want = c2_full
     e = bsw.Engine(group_kernel=group)
-    small = n <= 16384                  # 16-lane groups; up to BSW_OPT_MID_BATCH (32768): quads
+    small = n <= 32768
     rg = group and n <= 32768
     for cell_bits in (16, 8):
         got = pairs[:n].copy()

@@ -1,4 +1,5 @@
 #!/bin/bash
+# NOTE: the BSW_HP_NO_EARLY / BSW_HP_NO_MERGE switches were removed with the variants after this A/B.
 # Host-buffer pipeline A/B (1M C2 pairs, pageable buffers): early start (first chunk's prepass only,
 # the rest after chunk 0 is enqueued) and the remainder chunk merged, against each switched off
 # (BSW_HP_NO_EARLY / BSW_HP_NO_MERGE, experiment switches); interleaved x3, 3 calls each (the
