@@ -170,6 +170,11 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
     const int k = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GS);   // pair slot
     const int oe_del = kp.o_del + kp.e_del, oe_ins = kp.o_ins + kp.e_ins;
     const uint32_t oed2 = pk2(oe_del), oei2 = pk2(oe_ins - kp.e_ins), ed2 = pk2(kp.e_del);
+    // the z-drop's gap extensions as values pinned in registers: with the plain `c ? x * kp.e_del :
+    // y * kp.e_ins` the compiler selected between the two fields' ADDRESSES and issued a vector load
+    // from the kernarg segment every row, waited for at once (vmcnt(0): an L2 round trip per row)
+    int zd_del = kp.e_del, zd_ins = kp.e_ins;
+    asm volatile("" : "+s"(zd_del), "+s"(zd_ins));
 
     int idx = -1, idr = 0, idq = 0, tlen = 0, qlen = 0, h0 = 0;
     bool alive = false;
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
         gsc = atq ? max(gsc, hq) : gsc;
         const bool better = m > best;                                 // implies m > 0 (best >= 0)
         const int di = i - best_i, dj = mj - best_j;
-        const int dz = (di > dj) ? best - m - (di - dj) * kp.e_del : best - m - (dj - di) * kp.e_ins;
+        const int dz = best - m - ((di > dj) ? (di - dj) * zd_del : (dj - di) * zd_ins);
         const bool stop = m <= 0 || (!better && kp.zdrop > 0 && dz > kp.zdrop);
         moff = better ? max(moff, abs(mj - i)) : moff;
         best_i = better ? i : best_i;
