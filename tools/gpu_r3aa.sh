@@ -3,7 +3,7 @@
 # 262144 (default) / 524288), 10 calls per process, median of the last 7, x2.
 set -o pipefail
 O=gpurun_out/r3aa; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -k "busy_device" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -k "busy_device or host_pipeline" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for rep in 1 2; do
   line="rep $rep"
