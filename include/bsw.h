@@ -176,6 +176,12 @@ enum {
                                  group kernel (default 0 = never: measured slower at 10K-pair
                                  calls x 8 callers; an experiment knob).  Outputs
                                  are identical either way                                       */
+    BSW_OPT_COALESCE_LINGER = 16, /* microseconds (0..100000, default 0) a coalescing leader that
+                                 starts while another batch is in flight on its device waits for
+                                 more queued calls before taking the queue: concurrent callers'
+                                 next calls then ride in the same batch.  A lone caller never
+                                 waits.  An experiment knob: no gain measured.
+                                 Outputs are identical either way                                */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };

@@ -701,6 +701,11 @@ def test_options_api(eng):
     assert lib.bsw_set_option(eng._ctx, bsw.OPT_EXT_CHUNK, -1) == -22
     assert lib.bsw_set_option(None, bsw.OPT_FORK, 1) == -22
     assert lib.bsw_set_option(eng._ctx, bsw.OPT_SORTKEY, 1) == 0
+    assert lib.bsw_set_option(eng._ctx, bsw.OPT_KERNEL8, 3) == -22          # 0, 1, 2 only
+    assert lib.bsw_set_option(eng._ctx, 15, -1) == -22                      # BSW_OPT_BUSY_MIN
+    assert lib.bsw_set_option(eng._ctx, 16, 100001) == -22                  # BSW_OPT_COALESCE_LINGER
+    assert lib.bsw_set_option(eng._ctx, 16, 30) == 0
+    assert lib.bsw_set_option(eng._ctx, 15, 0) == 0
 
 
 @pytest.mark.parametrize("gaps", [(100, 16400, 6, 1), (6, 1, 30000, 2700), (16000, 16000, 16000, 16000)])
@@ -759,11 +764,13 @@ def test_coalesced_small_calls(c2_full):
     """Cross-call coalescing (BSW_OPT_COALESCE): 8 kt_for-style threads issue small calls of
     varying sizes, w and cell_bits -- some with scattered (non-contiguous) buffers, one with a pair
     past BSW_MAX_LEN -- concurrently on one context; every call returns its own outputs (== the
-    oracle), the bad call alone gets BSW_E_RANGE, and coalescing off gives the same."""
+    oracle), the bad call alone gets BSW_E_RANGE, and coalescing off gives the same; a long leader
+    linger (BSW_OPT_COALESCE_LINGER 3000 us: other leaders take the lingering caller's request
+    meanwhile) and none give the same too."""
     pairs, ref, qer, want = c2_full
     want200 = None
-    for co in (32768, 0):
-        e = bsw.Engine(coalesce=co)
+    for co, linger in ((32768, 30), (32768, 3000), (32768, 0), (0, 30)):
+        e = bsw.Engine(coalesce=co, coalesce_linger=linger)
         errs, bad_seen = [], []
         rng = np.random.default_rng(7)
         plan = [[(int(rng.integers(0, len(pairs) - 60000)), int(rng.choice([1, 57, 1000, 3000, 10000, 20000])),

@@ -46,6 +46,7 @@ int main(int argc, char **argv)
     if (const char *g = getenv("PERCALL_GROUP")) bsw_set_option(ctx, BSW_OPT_GROUP_KERNEL, atoi(g));
     if (const char *b = getenv("PERCALL_SMALL")) bsw_set_option(ctx, BSW_OPT_SMALL_BATCH, atoi(b));
     if (const char *b = getenv("PERCALL_BUSY_MIN")) bsw_set_option(ctx, BSW_OPT_BUSY_MIN, atoi(b));
+    if (const char *b = getenv("PERCALL_LINGER")) bsw_set_option(ctx, BSW_OPT_COALESCE_LINGER, atoi(b));
     std::vector<SeqPair> want = pairs;
     if (bsw_get_scores(ctx, want.data(), ref.data(), qer.data(), N, 100, 16) != BSW_OK) return 3;
     printf("{\"tool\": \"percall_bench\", \"threads\": %d, \"pairs\": %d, \"curve\": [", T, N);
