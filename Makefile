@@ -102,7 +102,7 @@ $(LIBDIR)/bsw_pc_stats.o: $(CSRC)/bsw_pc.hip $(HIP_HDRS) | $(LIBDIR)
 $(STATSLIB): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_stats.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_devcache.o $(LIBDIR)/bsw_batch.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
-# experiment build: the product with bsw_pc.hip compiled under AB_FLAGS (tools/gpu_ab.sh A/B runs)
+# experiment build: the product with bsw_pc.hip compiled under AB_FLAGS (same-box A/B runs: tools/ab_lib.sh)
 ABLIB := $(LIBDIR)/libbsw_hip_ab.so
 AB_FLAGS ?=
 ab:

@@ -355,6 +355,9 @@ def main():
                          "fixed batch of --total-pairs split over the ranks by band cells, host buffers "
                          "in, PCIe both ways inside the timed region (C5)")
     ap.add_argument("--total-pairs", type=int, default=10_000_000, help="strong: pairs in the whole batch")
+    ap.add_argument("--rccl-pairs", type=int, default=4_000_000,
+                    help="default C2 line at N > 1: pairs of the strong-scaling RCCL leg reported beside the weak "
+                         "value (one batch on GPU 0, RCCL scatter -> score -> RCCL gather); 0 = off")
     ap.add_argument("--transport", default="host", choices=("host", "rccl"),
                     help="strong: host (default) -- every rank holds its range in host memory and the call "
                          "stages it over its own PCIe link; rccl -- the whole batch resident on GPU 0, scattered "
@@ -385,6 +388,8 @@ def main():
     hiprt.set_device(local)
     if args.scaling == "strong":
         if args.transport == "rccl":
+            if args.workload == "c4mem":
+                return main_mem_strong_rccl(args, rank, local, world)
             return main_strong_rccl(args, rank, local, world)
         return main_strong(args, rank, local, world)
     if args.workload == "c1":          # BASELINE configs[0]: 10K exact 150 bp SE reads vs 1 Mb
@@ -431,6 +436,16 @@ def main():
 
     res = np.empty_like(pairs)
     d_pairs.download(res)
+    # N > 1: the strong-scaling RCCL leg beside the weak value (every rank takes part)
+    rccl = None
+    if world > 1 and args.rccl_pairs > 0:
+        if args.distinct_gpus < world:
+            rccl = {"skipped": f"{world} ranks share {args.distinct_gpus} GPU(s) (--rehearse): RCCL needs one GPU per rank"}
+        else:
+            try:
+                rccl = rccl_c2_leg(args, rank, local, world, args.rccl_pairs, steps=10, warmup=2, eng=eng)
+            except Exception as e:  # noqa: BLE001  (the weak line still prints)
+                rccl = {"error": repr(e)[:400]}
     if rank != 0:
         return
     total_pairs = args.pairs * world * args.steps
@@ -493,6 +508,8 @@ def main():
         e0.close()
     if args.distinct_gpus < world:
         out["rehearsal"] = f"{world} ranks on {args.distinct_gpus} GPU(s): not a scaling measurement"
+    if rccl is not None:
+        out["rccl_strong"] = rccl
     if world == 1 and not args.no_host_path:
         hp = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res)
         out["abi_inclusive_value"] = hp.pop("value")
@@ -537,91 +554,306 @@ def main():
     print(json.dumps(out), flush=True)
 
 
-def main_strong_rccl(args, rank, local, world):
-    """C5 as BASELINE configs[4] words it: ONE batch of --total-pairs C2 pairs resident on GPU 0,
-    packed per rank (bwa-mem2-arm_amd/py/shards.py: contiguous ranges of equal static band cells,
-    records rebased to their own windows, one padded byte buffer per rank), SCATTERED to the ranks'
-    GPUs with RCCL over xGMI (torch.distributed backend "nccl"), scored in place on each GPU
-    (bsw_get_scores_device on pointers into the received buffer), and the 24 output bytes per pair
-    GATHERED back to GPU 0.  Scatter, compute and gather are inside the timed region; value = total
-    pairs / max-over-ranks step time.  With one rank a device-to-device copy stands in for the
-    scatter (nothing to send)."""
+def rccl_group(world):
+    """The data-path process group over RCCL (torch.distributed backend "nccl" on ROCm).  World > 1:
+    a new nccl group beside the gloo control-plane group dist_init made.  World 1: a one-rank nccl
+    group of its own (RCCL still runs the scatter / gather: a one-rank communicator), so the RCCL
+    path is exercised on a one-GPU box too."""
+    import datetime
+    import torch.distributed as dist
+    to = datetime.timedelta(seconds=300)
+    if world > 1:
+        return dist.new_group(backend="nccl", timeout=to)
+    if not dist.is_initialized():
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, timeout=to)
+    return dist.group.WORLD
+
+
+def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump=""):
+    """Strong scaling over RCCL (BASELINE configs[4]'s batch scatter): ONE batch of
+    `total` C2 pairs generated on rank 0 and resident on GPU 0 as one packed shard buffer per rank
+    (shards.BatchScatter: contiguous ranges of equal static band cells, records rebased to their
+    own windows), SCATTERED to the ranks' GPUs by RCCL, scored in place on every GPU
+    (bsw_get_scores_device on pointers into the received buffer), the 24 output bytes per pair
+    GATHERED back to GPU 0 by RCCL -- all three inside the timed region (barrier + device sync on
+    both sides, max over ranks).  Rank 0 then runs the whole batch alone on GPU 0 (the one-GPU
+    time of the same job, and the check that the gathered outputs are identical to it).
+    Returns the leg's dict on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
     import shards
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    g = dist.new_group(backend="nccl") if world > 1 else None
+    g = rccl_group(world)
     cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
-    N = args.total_pairs
     t0 = time.perf_counter()
-    meta_t = torch.zeros((world, 3), dtype=torch.int64)
-    src = None
+    pairs = ref = qer = None
     if rank == 0:
-        pairs, ref, qer = bsw.synth_batch(N, cfg=cfg)
-        cut = bsw.split_by_cells(pairs, args.w, world)
-        bufs, meta = shards.pack_shards(pairs, ref, qer, cut)
-        del ref, qer
-        meta_t.copy_(torch.from_numpy(meta))
-        src = [torch.from_numpy(bufs[k]).to(dev) for k in range(world)]     # the batch, resident on GPU 0
-        del bufs
-    if world > 1:
-        dist.broadcast(meta_t, src=0)                                      # (gloo, before timing)
-    meta = meta_t.numpy()
-    gen_s = time.perf_counter() - t0
-    S = shards.buffer_bytes(meta)
-    n_me = int(meta[rank, 0])
-    po, ro, qo = shards.offsets(meta[rank])
-    nmax = int(meta[:, 0].max())
-    recv = torch.zeros(S, dtype=torch.uint8, device=dev)
-    out_me = torch.zeros((nmax, 6), dtype=torch.int32, device=dev)
-    gathered = [torch.zeros((nmax, 6), dtype=torch.int32, device=dev) for _ in range(world)] if rank == 0 else None
-    eng = bsw.Engine(device=local)
-    base = recv.data_ptr()
+        pairs, ref, qer = bsw.synth_batch(total, cfg=cfg)
+    bs = shards.BatchScatter(rank, world, g, dev, pairs, ref, qer, w=args.w)
+    setup_s = time.perf_counter() - t0
+    own = eng is None
+    if own:
+        eng = bsw.Engine(device=local)
 
-    def step():
-        if world > 1:
-            dist.scatter(recv, src if rank == 0 else None, src=0, group=g)
-        else:
-            recv.copy_(src[0])
-        torch.cuda.current_stream().synchronize()
-        if n_me > 0:
-            eng.get_scores_device(base + po, base + ro, base + qo, n_me, args.w, args.cell_bits)
-            out_me[:n_me] = recv[po:po + 56 * n_me].view(torch.int32).view(n_me, 14)[:, shards.OUT_COLS]
-        if world > 1:
-            dist.gather(out_me, gathered, dst=0, group=g)
-        torch.cuda.synchronize()
+    def score(recv, row):
+        po, ro, qo = shards.offsets(row)
+        base = recv.data_ptr()
+        eng.get_scores_device(base + po, base + ro, base + qo, int(row[0]), args.w, args.cell_bits)
 
-    for _ in range(args.warmup):
-        step()
+    for _ in range(warmup):
+        bs.step(score)
+    for k in bs.ms:
+        bs.ms[k].clear()
     barrier(world)
     t = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for _ in range(steps):
+        bs.step(score)
     barrier(world)
     dt = time.perf_counter() - t
     dt_max = allreduce_max(dt, world)
+    phase = {k: allreduce_max(float(np.mean(v)), world) for k, v in bs.ms.items()}
+    rws = dist.get_world_size(g)
+    if rank != 0:
+        if own:
+            eng.close()
+        return None
+    res = bs.merged()
+    if dump:
+        np.save(dump, res)
+    # the same batch on GPU 0 alone: the one-GPU time of this job and the identity check
+    d_p, d_r, d_q = (hiprt.DeviceBuffer.from_array(a) for a in (pairs, ref, qer))
+    one = []
+    for _ in range(3):
+        d_p.upload(pairs)
+        t = time.perf_counter()
+        eng.get_scores_device(d_p.ptr, d_r.ptr, d_q.ptr, total, args.w, args.cell_bits)
+        one.append(time.perf_counter() - t)
+    single = d_p.download(np.empty_like(pairs))
+    for b in (d_p, d_r, d_q):
+        b.free()
+    same = all(np.array_equal(res[f], single[f]) for f in bsw.OUT_FIELDS)
+    if own:
+        eng.close()
+    ms = dt_max / steps * 1e3
+    one_ms = statistics.median(one) * 1e3
+    return {
+        "value": round(total * steps / dt_max / 1e6, 3), "unit": UNIT, "scaling": "strong",
+        "ms_per_step": round(ms, 3), "steps": steps, "warmup": warmup,
+        "total_pairs": total, "pairs_rank0": bs.n_me, "shard_buffer_bytes": bs.S,
+        "rccl_world_size": rws, "backend": dist.get_backend(g),
+        "phase_ms_max_over_ranks": {k: round(v, 3) for k, v in phase.items()},
+        "single_gpu_ms": round(one_ms, 3), "single_gpu_value": round(total / (one_ms * 1e-3) / 1e6, 3),
+        "strong_speedup_vs_single_gpu": round(one_ms / ms, 3),
+        "outputs_identical_to_single_gpu": bool(same),
+        "setup_s": round(setup_s, 2),
+        "step": "RCCL scatter of the packed shard buffers from GPU 0 -> bsw_get_scores_device in place on "
+                "every GPU -> RCCL gather of 24 output bytes per pair to GPU 0 (all timed)",
+    }
+
+
+def main_strong_rccl(args, rank, local, world):
+    """C5 as BASELINE configs[4] words it, as its own line: rccl_c2_leg over --total-pairs pairs,
+    value = total pairs / max-over-ranks step time (scaling "strong")."""
+    leg = rccl_c2_leg(args, rank, local, world, args.total_pairs, args.steps, args.warmup, dump=args.dump)
     if rank != 0:
         return
-    if args.dump:
-        outs = [x.cpu().numpy() for x in gathered] if world > 1 else [out_me.cpu().numpy()]
-        res = pairs.copy()
-        shards.merge_outputs(res, outs, cut)
-        np.save(args.dump, res)
-    value = N * args.steps / dt_max / 1e6
+    cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
+    N = args.total_pairs
     out_j = {
-        "metric": METRIC, "value": round(value, 3), "unit": UNIT, "n_gpus": world,
+        "metric": METRIC, "value": leg.pop("value"), "unit": UNIT, "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+        "ms_per_step": leg.pop("ms_per_step"), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int16", "data": "synthetic (bsw_synth.c, seed 42)",
         "config": {"workload": f"C5 strong scaling, RCCL batch scatter: one batch of {N} C2 pairs ({cfg.qlen} bp "
                                f"query / {cfg.tlen} bp ref, w={args.w}) resident on GPU 0, split over {world} "
                                f"rank(s) by static band cells, scattered / gathered with RCCL over xGMI inside "
                                f"the timed region",
-                   "total_pairs": N, "pairs_rank0": n_me, "shard_buffer_bytes": S,
+                   "total_pairs": N, "pairs_rank0": leg["pairs_rank0"], "shard_buffer_bytes": leg["shard_buffer_bytes"],
                    "parallelism": f"split{world} (bsw_split_by_cells; RCCL scatter + gather)",
                    "distinct_gpus": args.distinct_gpus},
-        "synth_gen_s": round(gen_s, 2),
+        "rccl": leg,
+    }
+    print(json.dumps(out_j), flush=True)
+
+
+def mem_reference(ref_mb: int) -> np.ndarray:
+    """main_mem's C4 reference: bsw_synth.c random bases, N -> a random base (bwa's .pac)"""
+    ref = bsw.synth_reference(ref_mb * 1_000_000, seed=7)
+    nb = ref > 3
+    ref[nb] = np.random.default_rng(1).integers(0, 4, int(nb.sum()), dtype=np.uint8)
+    return ref
+
+
+class MemFrontEnd:
+    """One rank's GPU front end over reads already in HBM: bsw_mem_collect_intv_device (SMEM
+    seeding) -> bsw_mem_chain_device (SA lookups, mem_chain, mem_chain_flt) ->
+    bsw_chain2aln_resident (mem_chain2aln against the resident two-strand text).  Device
+    buffers are torch tensors; run() returns (seeds, extensions) and leaves the results in
+    self.o[...] (seeds / sr / sc / out / ext, the first `seeds` entries valid)."""
+
+    def __init__(self, fmi, eng, opt, n, cap, dev, seeds_cap):
+        import torch
+        self.torch, self.fmi, self.eng, self.opt, self.n, self.cap, self.dev = torch, fmi, eng, opt, n, cap, dev
+        self.mopt, self.copt = bsw.mem_opt(), bsw.chain_opt()
+        self.mems = torch.empty(max(1, n * cap * bsw.BWTINTV_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        self.cnt = torch.empty(max(1, n * 4), dtype=torch.uint8, device=dev)
+        self.alloc(seeds_cap)
+
+    def alloc(self, m):
+        t = self.torch
+        self.m = m
+        self.o = {k: t.empty(max(1, m * sz), dtype=t.uint8, device=self.dev)
+                  for k, sz in (("seeds", bsw.SEED_DTYPE.itemsize), ("sr", 4), ("sc", 4),
+                                ("out", bsw.ALNREG_DTYPE.itemsize), ("ext", 4))}
+
+    def run(self, p_reads, p_off, p_len, grow=True):
+        P = {k: v.data_ptr() for k, v in self.o.items()}
+        bsw._check(self.fmi.collect_intv_device(p_reads, p_off, p_len, self.n, 150, self.mems.data_ptr(), self.cap,
+                                                self.cnt.data_ptr(), self.mopt))
+        rc, ns = self.fmi.mem_chain_device(p_len, self.n, self.mems.data_ptr(), self.cap, self.cnt.data_ptr(),
+                                           P["seeds"], P["sr"], P["sc"], self.m, self.copt)
+        if rc == -34:                                    # more seeds than room (sizing passes only)
+            if not grow:
+                raise RuntimeError(f"{ns} seeds past the capacity {self.m} inside the timed region")
+            self.alloc(int(ns * 1.25) + 16)
+            return self.run(p_reads, p_off, p_len, grow=False)
+        bsw._check(rc)
+        bsw.chain2aln_resident(self.eng, p_reads, p_off, p_len, self.n, P["seeds"], P["sr"], P["sc"], ns,
+                               P["out"], P["ext"], self.opt)
+        hiprt.synchronize()
+        return ns, sum(bsw.chain_last_stats(self.eng).n_pairs)
+
+    def pack(self, ns, rec):
+        """rec[:ns] = shards.REC_DTYPE rows (17 int32 per seed), on the device"""
+        t = self.torch
+        i32 = lambda k, w: self.o[k][:ns * 4 * w].view(t.int32).view(ns, w)   # noqa: E731
+        rec[:ns, 0:4] = i32("seeds", 4)
+        rec[:ns, 4:5] = i32("sr", 1)
+        rec[:ns, 5:6] = i32("sc", 1)
+        rec[:ns, 6:16] = i32("out", 10)
+        rec[:ns, 16:17] = i32("ext", 1)
+
+    def records(self, ns) -> np.ndarray:
+        import shards
+        rec = self.torch.zeros((max(1, ns), shards.REC_WORDS), dtype=self.torch.int32, device=self.dev)
+        self.pack(ns, rec)
+        return np.ascontiguousarray(rec[:ns].cpu().numpy()).view(shards.REC_DTYPE).reshape(-1)
+
+
+def main_mem_strong_rccl(args, rank, local, world):
+    """C5 as BASELINE configs[4] words it, on the full front end: ONE set of --reads PE reads
+    generated on rank 0 and resident on GPU 0, cut into contiguous read ranges and SCATTERED to the
+    ranks' GPUs by RCCL (shards.ReadScatter); every rank runs SMEM seeding -> chaining ->
+    mem_chain2aln on its shard against its own index of the --ref-mb reference (built on its GPU
+    before timing); every seed's record (seed, read, chain, region, extended flag: 68 B) is
+    GATHERED back to GPU 0 by RCCL.  Scatter, front end and gather are timed (barrier + sync on
+    both sides, max over ranks).  Rank 0 then runs the whole read set alone on GPU 0: the one-GPU
+    time of the same job and the check that the gathered records are identical to it."""
+    import torch
+    import shards
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    g = rccl_group(world)
+    t0 = time.perf_counter()
+    log = lambda m: print(f"[bench c4mem-rccl rank {rank}] {m} ({time.perf_counter() - t0:.1f} s)",  # noqa: E731
+                          file=sys.stderr, flush=True)
+    ref = mem_reference(args.ref_mb)
+    reads = off = lens = None
+    if rank == 0:
+        reads, off, lens = pe_reads(ref, max(1, args.reads // 2), seed=42)
+    rs = shards.ReadScatter(rank, world, g, dev, reads, off, lens)
+    N = int(rs.meta[:, 0].sum())
+    gen_s = time.perf_counter() - t0
+    log(f"{N} reads, {rs.n_me} on this rank")
+    t = time.perf_counter()
+    fmi = bsw.Fmi(ref, device=local, flags=(bsw.FMI_NO_TEXT if args.fmi_blocks_only else None))
+    build_s = time.perf_counter() - t
+    T = np.concatenate([ref, (3 - ref[::-1])]).astype(np.uint8)
+    eng = bsw.Engine(device=local)
+    bsw.set_reference(eng, T)
+    opt = bsw.ext_opt(w=args.w, l_pac=len(ref))
+    cap = 256 if N <= 2_000_000 else 64                  # as one GPU would run the whole set (main_mem)
+    fe = MemFrontEnd(fmi, eng, opt, rs.n_me, cap, dev, max(16, 4 * rs.n_me))
+    o_reads, o_off, o_len = rs.layout()
+
+    def score(recv, row, rec):
+        base = recv.data_ptr()
+        ns, ne = fe.run(base + o_reads, base + o_off, base + o_len, grow=rec is None)
+        score.n_ext += ne
+        if rec is not None:
+            fe.pack(ns, rec)
+        return ns
+    score.n_ext = 0
+    # sizing pass (untimed): the seed count fixes the gathered record capacity
+    rs.scatter()
+    ns0 = score(rs.recv, rs.meta[rank], None) if rs.n_me > 0 else 0
+    rs.size(ns0 + 16)
+    log(f"index built in {build_s:.1f} s; {ns0} seeds on this rank")
+    for _ in range(args.warmup):
+        rs.step(score)
+    for k in rs.ms:
+        rs.ms[k].clear()
+    score.n_ext = 0
+    barrier(world)
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        rs.step(score)
+    barrier(world)
+    dt = time.perf_counter() - t
+    dt_max = allreduce_max(dt, world)
+    n_ext_all = allreduce_sum(score.n_ext, world)
+    phase = {k: allreduce_max(float(np.mean(v)), world) for k, v in rs.ms.items()}
+    import torch.distributed as dist
+    rws = dist.get_world_size(g)
+    if rank != 0:
+        fmi.close()
+        return
+    got = rs.merged()
+    if args.dump:
+        np.save(args.dump, got)
+    # the whole read set on GPU 0 alone (its own buffers; same index and engine)
+    d_r = torch.from_numpy(reads).to(dev)
+    d_o = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_l = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    del fe
+    one_fe = MemFrontEnd(fmi, eng, opt, N, cap, dev, max(16, 4 * N))
+    one = []
+    for k in range(3):
+        t = time.perf_counter()
+        ns1, _ = one_fe.run(d_r.data_ptr(), d_o.data_ptr(), d_l.data_ptr(), grow=(k == 0))
+        one.append(time.perf_counter() - t)
+    want = one_fe.records(ns1)
+    same = bool(len(want) == len(got) and np.array_equal(want.view(np.uint8), got.view(np.uint8)))
+    fmi.close()
+    ms = dt_max / args.steps * 1e3
+    one_ms = statistics.median(one[1:]) * 1e3
+    out_j = {
+        "metric": METRIC, "value": round(n_ext_all / dt_max / 1e6, 3), "unit": UNIT, "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int16",
+        "data": "synthetic PE reads (bench.pe_reads) from a bsw_synth.c random reference",
+        "config": {"workload": f"C5 strong scaling, RCCL read scatter: one set of {N} PE 150 bp reads resident on "
+                               f"GPU 0 vs a {args.ref_mb} Mb random reference, split over {world} rank(s), "
+                               f"scattered with RCCL over xGMI; every rank: FM-index SMEM seeding -> SA + mem_chain "
+                               f"+ mem_chain_flt -> mem_chain2aln on its own GPU-resident index; per-seed records "
+                               f"gathered to GPU 0 with RCCL, inside the timed region",
+                   "total_reads": N, "reads_rank0": rs.n_me, "ref_bases": int(len(ref)),
+                   "parallelism": f"split{world} (contiguous read ranges; RCCL scatter + gather)",
+                   "distinct_gpus": args.distinct_gpus},
+        "reads_per_s_M": round(N * args.steps / dt_max / 1e6, 3),
+        "rccl": {"rccl_world_size": rws, "backend": dist.get_backend(g), "shard_buffer_bytes": rs.S,
+                 "record_bytes_per_seed": shards.REC_DTYPE.itemsize, "record_capacity": rs.cap,
+                 "phase_ms_max_over_ranks": {k: round(v, 3) for k, v in phase.items()}},
+        "seeds": int(len(got)),
+        "single_gpu_ms": round(one_ms, 3), "strong_speedup_vs_single_gpu": round(one_ms / ms, 3),
+        "outputs_identical_to_single_gpu": same,
+        "index_build_s": round(build_s, 2), "synth_gen_s": round(gen_s, 2),
     }
     print(json.dumps(out_j), flush=True)
 

@@ -82,43 +82,37 @@ def test_synth_shards_tile_global_batch():
 
 
 def _scatter_worker(rank, world, port, n, q):
-    """bench.py --scaling strong --transport rccl, on CPU tensors over gloo: rank 0 packs the
-    whole batch (shards.py), scatters one padded buffer per rank, every rank scores its shard in
-    place (the SSE4.1 restatement stands in for the GPU here), the 6 outputs per pair are
-    gathered back to rank 0."""
+    """bench.py's strong-scaling RCCL leg (rccl_c2_leg / --transport rccl) on CPU tensors over
+    gloo, through the same orchestration code (shards.BatchScatter): rank 0 packs the whole
+    batch, scatters one padded buffer per rank, every rank scores its shard in place (the SSE4.1
+    restatement stands in for the GPU here), the 6 outputs per pair are gathered back to rank 0
+    and merged; two steps, so the buffers are reused as in the timed loop."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
     import shards
-    meta_t = torch.zeros((world, 3), dtype=torch.int64)
-    src = None
+    pairs = ref = qer = None
     if rank == 0:
         pairs, ref, qer = bsw.synth_batch(n)
         pairs["len2"][::97] = 0                       # empty queries / targets inside a shard
         pairs["len1"][5::89] = 0
-        cut = bsw.split_by_cells(pairs, 100, world)
-        bufs, meta = shards.pack_shards(pairs, ref, qer, cut)
-        meta_t.copy_(torch.from_numpy(meta))
-        src = [torch.from_numpy(bufs[k].copy()) for k in range(world)]
-    dist.broadcast(meta_t, src=0)
-    meta = meta_t.numpy()
-    recv = torch.zeros(shards.buffer_bytes(meta), dtype=torch.uint8)
-    dist.scatter(recv, src, src=0)
-    p, r, qq = shards.unpack_shard(recv.numpy(), meta[rank])
-    oracle.sse41_get_scores16(oracle.make_params(), p, r, qq, 100, 1)
-    nmax = int(meta[:, 0].max())
-    out = torch.zeros((nmax, 6), dtype=torch.int32)
-    out[:len(p)] = torch.from_numpy(shards.outputs(p))
-    gathered = [torch.zeros_like(out) for _ in range(world)] if rank == 0 else None
-    dist.gather(out, gathered, dst=0)
+    bs = shards.BatchScatter(rank, world, dist.group.WORLD, torch.device("cpu"), pairs, ref, qer, w=100)
+
+    def score(recv, row):
+        p, r, qq = shards.unpack_shard(recv.numpy(), row)
+        oracle.sse41_get_scores16(oracle.make_params(), p, r, qq, 100, 1)
+
+    for _ in range(2):
+        bs.step(score)
     if rank == 0:
-        res = pairs.copy()
-        shards.merge_outputs(res, [x.numpy() for x in gathered], cut)
+        res = bs.merged()
         want = pairs.copy()
         oracle.get_scores(oracle.make_params(), want, ref, qer, 100)
         q.put(all(np.array_equal(res[f], want[f]) for f in bsw.OUT_FIELDS) and
-              all(np.array_equal(res[f], pairs[f]) for f in ("idr", "idq", "len1", "len2", "h0")))
+              all(np.array_equal(res[f], pairs[f]) for f in ("idr", "idq", "len1", "len2", "h0")) and
+              all(len(v) == 2 for v in bs.ms.values()) and
+              int(bs.meta[:, 0].sum()) == n)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -138,3 +132,92 @@ def test_scatter_gather_shards_equal_single_process(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert ok
+
+
+def _read_scatter_worker(rank, world, port, nreads, q):
+    """bench.py --workload c4mem --scaling strong --transport rccl on CPU tensors over gloo,
+    through the same orchestration (shards.ReadScatter): rank 0 holds every PE read, the read
+    shards are scattered, every rank runs the front end on its shard against its own index (the
+    oracle pipeline -- FmiRef.collect_intv -> mem_chain -> chain2aln -- stands in for the GPU),
+    the per-seed records are gathered and merged on rank 0."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    import bench
+    import shards
+    ref = bsw.synth_reference(300_000, seed=7)
+    ref[ref > 3] = 0
+    reads = off = lens = None
+    if rank == 0:
+        reads, off, lens = bench.pe_reads(ref, nreads // 2, seed=42)
+        lens = lens.copy()
+        lens[3] = 0                                   # an empty read inside a shard
+    rs = shards.ReadScatter(rank, world, dist.group.WORLD, torch.device("cpu"), reads, off, lens)
+    P = oracle.make_params()
+    f = oracle.FmiRef(ref)                            # every rank its own index
+    T = np.concatenate([ref, 3 - ref[::-1]]).astype(np.uint8)
+    opt = bsw.ext_opt(l_pac=len(ref))
+
+    def front_end(rd, of, ln):
+        mems, cnt = f.collect_intv(rd, of, ln, cap=256, nthreads=1)
+        seeds, sr, sc = oracle.mem_chain(f.sa(), len(ref), ln, mems, cnt)
+        out, ext = oracle.chain2aln(P, opt, T, rd, of, ln, seeds, sr, sc, nthreads=1)
+        return seeds, sr, sc, out, ext
+
+    def score(recv, row, rec):
+        seeds, sr, sc, out, ext = front_end(*shards.unpack_reads(recv.numpy(), row))
+        ns = len(seeds)
+        if rec is not None:
+            r = rec.numpy()[:ns].view(shards.REC_DTYPE).reshape(-1)
+            r["seed"], r["sr"], r["sc"], r["out"], r["ext"] = seeds, sr, sc, out, ext
+        return ns
+
+    rs.scatter()
+    rs.size(score(rs.recv, rs.meta[rank], None) + 16)
+    for _ in range(2):
+        rs.step(score)
+    if rank == 0:
+        got = rs.merged()
+        seeds, sr, sc, out, ext = front_end(reads, off, lens)
+        q.put(bool(len(got) == len(seeds) and np.array_equal(got["seed"], seeds) and np.array_equal(got["sr"], sr)
+                   and np.array_equal(got["sc"], sc) and np.array_equal(got["out"], out)
+                   and np.array_equal(got["ext"], ext) and len(got) > nreads // 2
+                   and int(rs.meta[:, 0].sum()) == nreads))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_read_scatter_gather_equal_single_process(world):
+    nreads = 600
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_read_scatter_worker, args=(r, world, port, nreads, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert ok
+
+
+def test_read_shard_pack_roundtrip():
+    import shards
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 160, 101).astype(np.int32)
+    off = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64) + 7
+    reads = rng.integers(0, 5, int(off[-1] + lens[-1]) + 11).astype(np.uint8)
+    for world in (1, 2, 3, 7):
+        cut = shards.read_cut(len(lens), world)
+        bufs, meta = shards.pack_reads(reads, off, lens, cut)
+        assert int(meta[:, 0].sum()) == len(lens)
+        for k in range(world):
+            rd, of, ln = shards.unpack_reads(bufs[k], meta[k])
+            lo, hi = int(cut[k]), int(cut[k + 1])
+            assert np.array_equal(ln, lens[lo:hi])
+            for i in range(hi - lo):
+                assert np.array_equal(rd[of[i]:of[i] + ln[i]], reads[off[lo + i]:off[lo + i] + lens[lo + i]])

@@ -113,9 +113,49 @@ def test_rccl_transport_one_rank_equal_oracle(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["scaling"] == "strong" and line["n_gpus"] == 1 and "RCCL" in line["config"]["workload"]
+    # a one-rank RCCL communicator carried the scatter / gather (backend nccl = RCCL on ROCm)
+    assert line["rccl"]["rccl_world_size"] == 1 and line["rccl"]["backend"] == "nccl"
+    assert line["rccl"]["outputs_identical_to_single_gpu"] is True
     got = np.load(dump)
     full, ref, qer = bsw.synth_batch(n)
     want = full.copy()
     oracle.get_scores(oracle.make_params(), want, ref, qer, 100, nthreads=16)
     for f in ("idr", "idq", "len1", "len2", "h0") + bsw.OUT_FIELDS:
         assert np.array_equal(got[f], want[f]), f
+
+
+@pytest.mark.gpu
+def test_rccl_read_scatter_c4mem_one_rank_equal_oracle(tmp_path):
+    """bench.py --workload c4mem --scaling strong --transport rccl with one rank (BASELINE
+    configs[4] on the whole front end): the PE reads packed into their read-shard buffer on GPU 0,
+    scattered by a one-rank RCCL communicator, SMEM seeding -> chaining -> mem_chain2aln on the
+    received buffer in place, the per-seed records gathered by RCCL -- equal to the oracle pipeline
+    on the same reads at 4 Mb, and to the same job run directly on GPU 0."""
+    reads = 20_000
+    dump = str(tmp_path / "c5.npy")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c4mem", "--scaling", "strong",
+           "--transport", "rccl", "--reads", str(reads), "--ref-mb", "4", "--steps", "2", "--warmup", "1",
+           "--dump", dump]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["scaling"] == "strong" and line["rccl"]["rccl_world_size"] == 1
+    assert line["rccl"]["backend"] == "nccl" and line["outputs_identical_to_single_gpu"] is True
+    import bench
+    import shards
+    got = np.load(dump)
+    assert got.dtype == shards.REC_DTYPE
+    ref = bench.mem_reference(4)
+    rd, off, lens = bench.pe_reads(ref, reads // 2, seed=42)
+    f = oracle.FmiRef(ref)
+    mems, cnt = f.collect_intv(rd, off, lens, cap=256, nthreads=8)
+    seeds, sr, sc = oracle.mem_chain(f.sa(), len(ref), lens, mems, cnt)
+    T = np.concatenate([ref, 3 - ref[::-1]]).astype(np.uint8)
+    want, wext = oracle.chain2aln(oracle.make_params(), bsw.ext_opt(l_pac=len(ref)), T, rd, off, lens, seeds, sr, sc,
+                                  nthreads=8)
+    assert len(got) == len(seeds) and line["seeds"] == len(seeds)
+    assert np.array_equal(got["sr"], sr) and np.array_equal(got["sc"], sc)
+    assert np.array_equal(got["seed"], seeds)
+    assert np.array_equal(got["ext"], wext)
+    for fld in bsw.ALNREG_DTYPE.names:
+        assert np.array_equal(got["out"][fld], want[fld]), fld

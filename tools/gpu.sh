@@ -1,0 +1,70 @@
+#!/bin/bash
+# GPU-box recipe runner (gpurun): one script with named steps instead of one-off files.
+#   bash tools/gpu.sh <out-dir-name> <step> [<step> ...]
+# Every step runs under its own timeout and writes its log under gpurun_out/<out-dir-name>/;
+# the first failing step ends the script (nothing more touches the GPU after a failure).
+# Steps:
+#   tests           the whole -m gpu suite, one process, per-test timeout
+#   tests:<expr>    the -m gpu tests matching -k <expr>
+#   smoke           __graft_entry__.smoke()
+#   bench           the default bench line (driver form: python bench.py)
+#   bench:<args>    bench.py with extra arguments (commas for spaces: bench:--workload,c1)
+#   prof            rocprofv3 kernel trace + PMC passes of a short C2 bench (tools/profile.sh)
+#   prof:<args>     the same over bench.py <args> (commas for spaces)
+#   segv            the round-3 traced 8-caller percall_bench (kernel + memory-copy trace) with the
+#                   fault handler armed (PERCALL_SEGV_LOG): one run, diagnostics kept if it faults
+#   percall:<args>  percall_bench <args> (commas for spaces), untraced
+#   py:<file>       python -u <file> (a probe script under tools/)
+# (rounds 1-3 kept one file per gpurun call, tools/gpu_*.sh; they are in git history, baea391)
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+name=${1:?out dir name}; shift
+O=gpurun_out/$name
+mkdir -p "$O"
+export TMPDIR=/tmp
+fail() { echo "step $1 FAILED (rc $2); log tail:"; tail -30 "$3"; exit 1; }
+sp() { echo "${1//,/ }"; }
+for step in "$@"; do
+    kind=${step%%:*}; arg=""; [[ "$step" == *:* ]] && arg=${step#*:}
+    t0=$(date +%s)
+    case "$kind" in
+    tests)
+        log=$O/gpu_tests${arg:+_$arg}.log
+        k=(); [ -n "$arg" ] && k=(-k "$arg")
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${k[@]}" \
+            > "$log" 2>&1 || fail "$step" $? "$log"
+        tail -1 "$log" ;;
+    smoke)
+        log=$O/smoke.log
+        timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 || fail "$step" $? "$log"
+        tail -3 "$log" ;;
+    bench)
+        log=$O/bench${arg:+_$(echo "$arg" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-60)}.log
+        timeout -k 10 600 python bench.py $(sp "$arg") > "$log" 2>&1 || fail "$step" $? "$log"
+        tail -1 "$log" | cut -c1-1500 ;;
+    prof)
+        OUT=$O/prof${arg:+_$(echo "$arg" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-40)} \
+            ARGS="${arg:+$(sp "$arg") }--steps 5 --warmup 1 --no-cpu --no-host-path" \
+            timeout -k 10 1100 bash tools/profile.sh > "$O/prof.log" 2>&1 || fail "$step" $? "$O/prof.log"
+        tail -1 "$O/prof.log" ;;
+    segv)
+        log=$O/segv_trace.log
+        rm -rf "$O/segv_trace"
+        PERCALL_SEGV_LOG=$O/segv_diag.txt timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace \
+            --output-format csv -d "$O/segv_trace" -- bwa-mem2-arm_amd/lib/percall_bench 200000 8 1000 \
+            > "$log" 2>&1; rc=$?
+        [ -f "$O/segv_diag.txt" ] && { echo "FAULT diagnostics:"; head -40 "$O/segv_diag.txt"; }
+        [ $rc -eq 0 ] || fail "$step" $rc "$log"
+        grep '^{' "$log" | cut -c1-600 ;;
+    percall)
+        log=$O/percall.log
+        timeout -k 10 300 bwa-mem2-arm_amd/lib/percall_bench $(sp "$arg") > "$log" 2>&1 || fail "$step" $? "$log"
+        tail -1 "$log" | cut -c1-1500 ;;
+    py)
+        log=$O/$(basename "$arg" .py).log
+        timeout -k 10 600 python -u "$arg" > "$log" 2>&1 || fail "$step" $? "$log"
+        tail -5 "$log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+    echo "== $step done in $(( $(date +%s) - t0 )) s"
+done

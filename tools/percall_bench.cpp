@@ -13,9 +13,57 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <thread>
+#include <ucontext.h>
+#include <unistd.h>
 #include <vector>
 #include "../include/bsw.h"
+
+// Fault diagnostics (PERCALL_SEGV_LOG=<file>): on SIGSEGV / SIGBUS write the faulting address,
+// the faulting PC, every backtrace frame with the object that holds it (dladdr: file, load base,
+// offset, nearest symbol) and the whole /proc/self/maps to <file>, then die with the signal.
+// Replaces whatever handler a profiler installed before main (rocprofv3's glog handler prints
+// bare addresses); not async-signal-safe, which does not matter on the way down.
+static const char *g_segv_log = nullptr;
+static void put_addr(FILE *f, const char *what, void *a)
+{
+    Dl_info di{};
+    if (a && dladdr(a, &di) && di.dli_fname)
+        fprintf(f, "%s %p  %s + 0x%lx  (%s + 0x%lx)\n", what, a, di.dli_fname,
+                (unsigned long)((char *)a - (char *)di.dli_fbase), di.dli_sname ? di.dli_sname : "?",
+                di.dli_saddr ? (unsigned long)((char *)a - (char *)di.dli_saddr) : 0ul);
+    else
+        fprintf(f, "%s %p  (no object: not inside any loaded image)\n", what, a);
+}
+static void on_fault(int sig, siginfo_t *si, void *uc_)
+{
+    FILE *f = fopen(g_segv_log, "w");
+    if (!f) f = stderr;
+    const ucontext_t *uc = (const ucontext_t *)uc_;
+    fprintf(f, "signal %d code %d tid %ld\n", sig, si->si_code, (long)gettid());
+    put_addr(f, "fault address", si->si_addr);
+    put_addr(f, "faulting pc  ", (void *)uc->uc_mcontext.gregs[REG_RIP]);
+    void *fr[64];
+    const int n = backtrace(fr, 64);
+    for (int k = 0; k < n; ++k) {
+        char w[32];
+        snprintf(w, sizeof w, "frame %2d     ", k);
+        put_addr(f, w, fr[k]);
+    }
+    fprintf(f, "---- /proc/self/maps\n");
+    if (FILE *m = fopen("/proc/self/maps", "r")) {
+        char line[512];
+        while (fgets(line, sizeof line, m)) fputs(line, f);
+        fclose(m);
+    }
+    if (f != stderr) fclose(f);
+    fprintf(stderr, "percall_bench: signal %d at %p, diagnostics in %s\n", sig, si->si_addr, g_segv_log);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
 
 extern "C" {
 typedef struct { uint64_t seed; int32_t tlen, qlen, h0_lo, h0_hi; double p_sub, p_indel, p_unrelated, p_n; } synth_cfg;
@@ -28,6 +76,13 @@ static double secs(Clock::time_point a, Clock::time_point b) { return std::chron
 
 int main(int argc, char **argv)
 {
+    if ((g_segv_log = getenv("PERCALL_SEGV_LOG"))) {
+        struct sigaction sa{};
+        sa.sa_sigaction = on_fault;
+        sa.sa_flags = SA_SIGINFO;
+        sigaction(SIGSEGV, &sa, nullptr);
+        sigaction(SIGBUS, &sa, nullptr);
+    }
     const int32_t N = argc > 1 ? atoi(argv[1]) : 1000000;
     const int T = argc > 2 ? atoi(argv[2]) : 8;
     std::vector<int32_t> sizes;
