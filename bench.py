@@ -275,40 +275,48 @@ def host_path_rates(eng, pairs, ref, qer, w, cell_bits, want, curve_sizes=(1_000
     same = all(np.array_equal(buf[f], want[f]) for f in bsw.OUT_FIELDS)
     curve = []
     for m in curve_sizes:
-        if m > n:
+        if m > n // 8:
             continue
-        calls = max(4, min(n // m, int(2e6 // m)))
+        calls = max(20, min(200, int(2e6 // m)))
         lat = []
-        for c in range(calls):
+        for c in range(calls + 3):
             a = (c * m) % (n - m + 1)
             v = buf[a:a + m]
             t = time.perf_counter()
             eng.get_scores(v, ref, qer, w, cell_bits)
             lat.append(time.perf_counter() - t)
-        lat = lat[1:]
-        nthr = 8
-        per = max(2, calls // nthr)
+        lat = lat[3:]
+        # 8 concurrent callers (ctypes releases the GIL), each over its own slice, calls back to
+        # back for 0.5 s after every caller's untimed warm-up calls
+        nthr, run_s = 8, 0.5
+        slice_ = n // nthr
         go = threading.Barrier(nthr + 1)
+        done = [0] * nthr
 
         def worker(k):
-            eng.get_scores(buf[:m], ref, qer, w, cell_bits)      # warm: this caller's slots
-            go.wait()
-            go.wait()
-            for c in range(per):
-                a = ((k * per + c) * m) % (n - m + 1)
+            for c in range(2):
+                a = k * slice_ + (c * m) % (slice_ - m + 1)
                 eng.get_scores(buf[a:a + m], ref, qer, w, cell_bits)
+            go.wait()
+            t0 = time.perf_counter()
+            c = 0
+            while time.perf_counter() - t0 < run_s:
+                a = k * slice_ + ((c + 2) * m) % (slice_ - m + 1)
+                eng.get_scores(buf[a:a + m], ref, qer, w, cell_bits)
+                done[k] += m
+                c += 1
         th = [threading.Thread(target=worker, args=(k,)) for k in range(nthr)]
         for x in th:
             x.start()
         go.wait()
         t = time.perf_counter()
-        go.wait()
         for x in th:
             x.join()
         dt8 = time.perf_counter() - t
         curve.append({"pairs_per_call": m, "latency_ms_median": round(statistics.median(lat) * 1e3, 3),
                       "M_pairs_per_s_1_caller": round(m / statistics.median(lat) / 1e6, 3),
-                      "M_pairs_per_s_8_callers": round(nthr * per * m / dt8 / 1e6, 3)})
+                      "M_pairs_per_s_8_callers": round(sum(done) / dt8 / 1e6, 3),
+                      "seconds_8_callers": round(dt8, 3)})
     return {"value": round(n / t_all / 1e6, 3), "ms": round(t_all * 1e3, 3),
             "coalesce_max_pairs": coalesce_opt(eng),
             "ms_all_calls": [round(x * 1e3, 2) for x in ts],
@@ -528,12 +536,6 @@ def main():
                     out["abi_inclusive"]["per_call_curve_cpp_callers"] = json.loads(r.stdout.strip().splitlines()[-1])
             except (subprocess.SubprocessError, ValueError, IndexError):
                 pass
-        eng.set_option("coalesce", 0)                  # per-call curve without cross-call coalescing (A/B)
-        eng.coalesce_setting = 0
-        hp0 = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res)
-        eng.set_option("coalesce", 32768)
-        eng.coalesce_setting = 32768
-        out["abi_inclusive"]["per_call_curve_without_coalescing"] = hp0["per_call_curve"]
         eng.set_option("host_pack", 4)                 # the nibble staging beside it (same box, same batch)
         hp4 = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res, curve_sizes=())
         eng.set_option("host_pack", 2)
@@ -1295,16 +1297,21 @@ def main_mem(args, rank, local, world, c1: bool):
                   "device_bytes": int(fmi.info().device_bytes),
                   "built_on": "gpu" if len(ref) >= (64 << 20) else "host"},
     }
-    if world == 1 and not args.no_cpu and len(ref) > 512_000_000:
-        out_j["cpu_baseline"] = {"value": None, "note": "not run above 512 Mb: the oracle's plain occurrence table "
-                                 "(32 B per text row) would need ~192 GB of host memory at 3 Gb; see the 64 Mb line"}
-    elif world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # CPU baseline leg only (test infrastructure)
         nt = cpu_leg_threads()
-        S = min(n, 10_000 * nt)
-        fr = oracle.FmiRef(ref, sa=fmi.sa())             # the product's SA: skips the oracle's sort
-        fsa = fr.sa()
+        # the product's SA skips the oracle's comparison sort; past 512 Mb the oracle's LEAN form
+        # (occurrence checkpoints every 64 rows + an SA sampled every 32 rows resolved by LF walks,
+        # ~1.8 B per row) replaces its plain 42-B-per-row tables (~250 GB at 3 Gb)
+        lean = len(ref) > 512_000_000
+        S = min(n, (2_000 if lean else 10_000) * nt)
+        t = time.perf_counter()
+        sa_full = fmi.sa()
+        fr = oracle.FmiRef(ref, sa=sa_full, lean=lean, nthreads=nt)
+        del sa_full
+        fsa = fr if lean else fr.sa()
+        log(f"CPU leg: oracle index ({'lean' if lean else 'full'}) in {time.perf_counter() - t:.1f} s")
 
         def cpu_front(m, threads):
             mm, cn = fr.collect_intv(reads[:int(off[m - 1] + lens[m - 1])], off[:m], lens[:m], cap=cap,
@@ -1312,7 +1319,7 @@ def main_mem(args, rank, local, world, c1: bool):
             a, b, c = oracle.mem_chain(fsa, len(ref), lens[:m], mm, cn)
             return (a, b, c) + oracle.chain2aln(oracle.make_params(), opt, T, reads, off[:m], lens[:m], a, b, c,
                                                 nthreads=threads)
-        S1 = min(n, 10_000)
+        S1 = min(n, 2_000 if lean else 10_000)
         t = time.perf_counter()
         cpu_front(S1, 1)
         dt_1 = time.perf_counter() - t
@@ -1329,7 +1336,9 @@ def main_mem(args, rank, local, world, c1: bool):
             "reads_per_s_M": round(rps, 5), "reads_per_s_M_1thread": round(S1 / dt_1 / 1e6, 5),
             "sample": f"first {S} reads; oracle/fmi_ref.c collect_intv + oracle/chain_ref.c mem_chain/mem_chain_flt + "
                       f"oracle/ext_ref.c chain2aln (scalar ksw_extend2) on {nt} threads (collect and chain2aln "
-                      f"split by read; chaining 1 thread), index built from the product's suffix array, not timed",
+                      f"split by read; chaining 1 thread), index built from the product's suffix array, not timed"
+                      + (" (lean oracle index: 64-row occurrence checkpoints, SA sampled every 32 rows + LF walks)"
+                         if lean else ""),
             "host": host_cpu_info(),
             "outputs_identical_to_gpu": same,
         }

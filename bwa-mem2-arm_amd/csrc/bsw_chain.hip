@@ -354,8 +354,11 @@ extern "C" int bsw_chain2aln_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, co
     if (rc == BSW_OK && (hipMemcpy(out, d[5], sz[5], hipMemcpyDeviceToHost) != hipSuccess ||
                          hipMemcpy(extended, d[6], sz[6], hipMemcpyDeviceToHost) != hipSuccess))
         rc = BSW_E_HIP;
-    (void)hipDeviceSynchronize();                      // (blocking copies above; an error path
-    for (int k = 0; k < 7; ++k)                         //  may have left work queued)
+    // nothing is queued on these blocks here: the copies are blocking, chain_rounds_device drains
+    // its lease stream on every path (LeaseGuard) and the extension calls it makes drain their
+    // slots' streams, failed or not (DeviceCtx::give_back) -- so no device-wide synchronise, which
+    // would stall every other caller's work on the GPU
+    for (int k = 0; k < 7; ++k)
         bsw::devcache_put(dev, d[k], std::max<size_t>(sz[k], 1));
     bsw::set_chain_stats(ctx, cs);
     return rc;

@@ -342,8 +342,16 @@ struct DeviceCtx {
         if ((rc = hip_rc(hipHostMalloc((void **)&s->h_meta, kMetaWords * sizeof(int32_t), 0)))) return nullptr;
         return s;
     }
-    void give_back(std::unique_ptr<Slot> s)
+    // rc != 0: the call failed part-way and may have left work queued on the slot's streams
+    // (or the caller's stream it ran on) that still reads or writes the slot's buffers -- drain
+    // it before another call can take the slot
+    void give_back(std::unique_ptr<Slot> s, int rc = 0)
     {
+        if (rc) {
+            (void)hipSetDevice(s->device);
+            for (hipStream_t st : {s->stream, s->pstream, s->run_stream, s->side[0], s->side[1], s->side[2]})
+                if (st) (void)hipStreamSynchronize(st);
+        }
         std::lock_guard<std::mutex> g(mu);
         free_slots.push_back(std::move(s));
     }
@@ -1454,7 +1462,7 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
         st.stage_ms = (float)std::chrono::duration<double, std::milli>(tg1 - tg0).count();
         return BSW_OK;
     }();
-    dc.give_back(std::move(slot));
+    dc.give_back(std::move(slot), rc);
     return rc;
 }
 
@@ -2051,7 +2059,7 @@ int bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref
         ctx->last = slot->stats;
         return BSW_OK;
     }();
-    dc.give_back(std::move(slot));
+    dc.give_back(std::move(slot), rc);
     return rc;
 }
 
@@ -2077,7 +2085,7 @@ int bsw_ksw_align2_device(bsw_ctx_t *ctx, const SeqPair *d_pairs, const uint8_t 
         ctx->mate_last = ms;
         return BSW_OK;
     }();
-    dc.give_back(std::move(slot));
+    dc.give_back(std::move(slot), rc);
     return rc;
 }
 
@@ -2117,7 +2125,7 @@ static int mate_host_shard(const MateParams &mp, DeviceCtx &dc, const SeqPair *p
         BSW_TRY(hipStreamSynchronize(s.stream));
         return BSW_OK;
     }();
-    dc.give_back(std::move(slot));
+    dc.give_back(std::move(slot), rc);
     return rc;
 }
 
@@ -2211,7 +2219,7 @@ int bsw_ksw_global2_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_re
         ctx->glob_last = gs;
         return BSW_OK;
     }();
-    dc.give_back(std::move(slot));
+    dc.give_back(std::move(slot), rc);
     return rc;
 }
 
@@ -2261,7 +2269,7 @@ static int glob_host_shard(const GlobParams &gp, DeviceCtx &dc, SeqPair *pairs, 
         BSW_TRY(hipStreamSynchronize(s.stream));
         return BSW_OK;
     }();
-    dc.give_back(std::move(slot));
+    dc.give_back(std::move(slot), rc);
     return rc;
 }
 }  // namespace bsw
@@ -2398,7 +2406,7 @@ int bsw::extend_seeds_device_win(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const
         BSW_TRY(hipStreamSynchronize(st));
         return BSW_OK;
     }();
-    dc.give_back(std::move(slot));
+    dc.give_back(std::move(slot), rc);
     if (rc) return rc;
     es.engine_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     bsw::set_ext_stats(ctx, es);

@@ -14,6 +14,9 @@
  *     clipped to [0, ref_len), gap(l) = min(max((l*a - o)/e + 1, 1), 2w)   (cal_max_gap); with
  *     opt->l_pac > 0 a window crossing l_pac keeps the side of the chain's first seed
  *     (mem_chain2aln's rmax[] computation).  bsw_extend_seeds treats every seed as a chain of one.
+ *     Windows are clipped only at the strand boundary: the reference is ONE sequence (upstream
+ *     also clips to the seed's contig, bns_fetch_seq; a multi-contig genome passed concatenated
+ *     is extended across its contig joins -- see include/bsw_fmi.h "Scope").
  *   LEFT  (qbeg > 0): query = reverse(read[0, qbeg)), target = reverse(ref[rmax0, rbeg)),
  *         h0 = sc, end_bonus = pen_clip5, band w << k for k < max_band_try (retry while the
  *         score changed and max_off >= 3/4 of the band)

@@ -14,7 +14,21 @@
  *   pass 3  (max_mem_intv > 0) LAST-like seeds: from x, the shortest forward match of length
  *           >= min_seed_len + 1 with fewer than max_mem_intv occurrences
  *   then sorted by info (qbeg << 32 | qend); ties (upstream's introsort leaves them unordered)
- *   by k, s, l.
+ *   by k, s, l.  No parity gap: equal info is the same read substring, whose SA interval and
+ *   reverse-complement row are unique, so tied records are identical and every order of them
+ *   is the same sequence (tests/test_fmi.py::test_tied_intervals_are_identical).
+ *
+ * Scope of the seeding -> chaining front end (bsw_mem_chain_device, bsw_chain2aln_resident):
+ *   - ONE reference sequence (a bntseq with a single contig).  Upstream also drops seeds that
+ *     span two contigs (bns_intv2rid < 0), refuses chain merges across contigs (seed rid !=
+ *     chain rid) and clips extension windows to the contig (bns_fetch_seq); here the only
+ *     boundary is the forward / reverse strand one (l_pac).  A multi-sequence genome (GRCh38)
+ *     must be given as one concatenated sequence, and seeds / chains / windows that cross its
+ *     contig joins are NOT filtered as upstream filters them.
+ *   - reads shorter than ~720 bp.  Upstream's mem_align1_core runs mem_flt_chained_seeds
+ *     between chaining and extension; it returns at once while MEM_MINSC_COEF * ln(l) >
+ *     MEM_SEEDSW_COEF * l (5.5 ln l > 0.05 l: l <= 720 with min_chain_weight 0) and is not
+ *     restated here, so longer reads' seeds (hence regions) may differ from upstream.
  *
  * Index (built on the host below 64 Mb, on the GPU above; resident in HBM): T = ref +
  * reverse-complement(ref), the BWT of T$ with the sentinel kept, count[c] = 1 + #{bases < c},

@@ -228,7 +228,12 @@ static int chain_flt(const bsw_chain_opt_t *opt, int n_chn, ochain_t *a)
 }
 
 /* mem_chain for one read: chains in start order (the kbtree traversal) */
-static int read_chains(const bsw_chain_opt_t *opt, const int64_t *sa, int64_t l_pac, int len,
+/* SA lookups: a plain array, or an FM-index's bwt_sa (oracle_fmi_sa_at: the lean index's LF walks) */
+typedef struct { const int64_t *sa; const void *fmi; } sa_src_t;
+int64_t oracle_fmi_sa_at(const void *f, int64_t r);
+static int64_t sa_get(const sa_src_t *s, int64_t r) { return s->fmi ? oracle_fmi_sa_at(s->fmi, r) : s->sa[r]; }
+
+static int read_chains(const bsw_chain_opt_t *opt, const sa_src_t *sa, int64_t l_pac, int len,
                        const bsw_bwtintv_t *mem, int n_mem, ochain_t **out)
 {
     int n = 0, m = 16;
@@ -243,7 +248,7 @@ static int read_chains(const bsw_chain_opt_t *opt, const int64_t *sa, int64_t l_
         int count;
         for (k = count = 0; k < (int64_t)p->x[2] && count < opt->max_occ; k += step, ++count) {
             oseed_t s;
-            s.rbeg = sa[p->x[0] + k];
+            s.rbeg = sa_get(sa, (int64_t)p->x[0] + k);
             s.qbeg = (int32_t)(p->info >> 32);
             s.score = s.len = slen;
             if (s.rbeg < l_pac && l_pac < s.rbeg + s.len) continue;   /* bns_intv2rid < 0: bridging */
@@ -277,9 +282,27 @@ static int read_chains(const bsw_chain_opt_t *opt, const int64_t *sa, int64_t l_
 
 /* Every read: mem_chain + mem_chain_flt -> seeds grouped by read / chain (bsw_fmi.h's output
  * layout).  Returns the number of seeds (written only while < seed_cap). */
+static int64_t mem_chain_src(const bsw_chain_opt_t *opt, const sa_src_t *sa, int64_t l_pac, const int32_t *read_len,
+                             int32_t n_reads, const bsw_bwtintv_t *mems, int32_t cap, const int32_t *n_mems,
+                             bsw_seed_t *seeds, int32_t *seed_read, int32_t *seed_chain, int64_t seed_cap);
 int64_t oracle_mem_chain(const bsw_chain_opt_t *opt, const int64_t *sa, int64_t l_pac, const int32_t *read_len,
                          int32_t n_reads, const bsw_bwtintv_t *mems, int32_t cap, const int32_t *n_mems,
                          bsw_seed_t *seeds, int32_t *seed_read, int32_t *seed_chain, int64_t seed_cap)
+{
+    const sa_src_t src = {sa, NULL};
+    return mem_chain_src(opt, &src, l_pac, read_len, n_reads, mems, cap, n_mems, seeds, seed_read, seed_chain, seed_cap);
+}
+/* the same with SA lookups through an oracle FM-index (fmi_ref.c; full or lean form) */
+int64_t oracle_mem_chain_fmi(const bsw_chain_opt_t *opt, const void *fmi, int64_t l_pac, const int32_t *read_len,
+                             int32_t n_reads, const bsw_bwtintv_t *mems, int32_t cap, const int32_t *n_mems,
+                             bsw_seed_t *seeds, int32_t *seed_read, int32_t *seed_chain, int64_t seed_cap)
+{
+    const sa_src_t src = {NULL, fmi};
+    return mem_chain_src(opt, &src, l_pac, read_len, n_reads, mems, cap, n_mems, seeds, seed_read, seed_chain, seed_cap);
+}
+static int64_t mem_chain_src(const bsw_chain_opt_t *opt, const sa_src_t *sa, int64_t l_pac, const int32_t *read_len,
+                             int32_t n_reads, const bsw_bwtintv_t *mems, int32_t cap, const int32_t *n_mems,
+                             bsw_seed_t *seeds, int32_t *seed_read, int32_t *seed_chain, int64_t seed_cap)
 {
     int64_t ns = 0;
     for (int32_t r = 0; r < n_reads; ++r) {

@@ -29,13 +29,21 @@
 
 typedef struct {
     int64_t n;            /* |T| = 2 * ref_len; T$ has n + 1 suffixes                          */
-    uint8_t *t;           /* T[0, n) codes 0..3                                                 */
-    int64_t *sa;          /* SA[0, n] (SA[0] = n, the '$' suffix)                               */
+    uint8_t *t;           /* T[0, n) codes 0..3  (NULL in the lean form)                        */
+    int64_t *sa;          /* SA[0, n] (SA[0] = n, the '$' suffix)  (NULL in the lean form)      */
     uint8_t *bwt;         /* BWT[0, n]: T[SA[r] - 1] or 4 for '$'                               */
-    int64_t *occ;         /* occ[4 * r + c] = #c in BWT[0, r), r in [0, n + 1]                  */
+    int64_t *occ;         /* occ[4 * r + c] = #c in BWT[0, r), r in [0, n + 1]  (full form)     */
     int64_t count[5];     /* count[c] = 1 + #{T[i] < c}                                         */
     int64_t sentinel;     /* r with SA[r] == 0 (BWT[r] = '$')                                   */
+    /* lean form (a genome-sized index in ~1.8 B per row instead of 42): occurrence checkpoints
+     * every LEAN_CP rows (cp[4 * b + c] = #c in BWT[0, b * LEAN_CP)) + a scan of at most 63 BWT
+     * bytes per query, and SA sampled every LEAN_SA rows resolved by LF walks (bwa's bwt_sa) */
+    int lean;
+    int64_t *cp;
+    int64_t *ssa;
 } fmi_ref_t;
+#define LEAN_CP 64
+#define LEAN_SA 32
 
 typedef struct { uint64_t x[3]; uint64_t info; } ref_intv_t;   /* bwa's bwtintv_t */
 
@@ -123,11 +131,97 @@ int oracle_fmi_build_with_sa(const uint8_t *ref, int64_t len, const int64_t *sa,
 
 void oracle_fmi_free(fmi_ref_t *f)
 {
-    free(f->t); free(f->sa); free(f->bwt); free(f->occ);
+    free(f->t); free(f->sa); free(f->bwt); free(f->occ); free(f->cp); free(f->ssa);
     memset(f, 0, sizeof(*f));
 }
 
-static int64_t occ(const fmi_ref_t *f, int c, int64_t r) { return f->occ[4 * r + c]; }
+static int64_t occ(const fmi_ref_t *f, int c, int64_t r)
+{
+    if (!f->lean) return f->occ[4 * r + c];
+    const int64_t b = r / LEAN_CP;
+    int64_t v = f->cp[4 * b + c];
+    for (int64_t i = b * LEAN_CP; i < r; ++i) v += f->bwt[i] == c;
+    return v;
+}
+
+/* The lean form from a caller-supplied suffix array of T$ (the bench's CPU leg at genome scale,
+ * where the full form's 42 B per row would need ~250 GB): BWT codes, occurrence checkpoints and
+ * the sampled SA are derived with `nthreads` threads; the SA array itself is not kept. */
+#include <pthread.h>
+typedef struct { fmi_ref_t *f; const uint8_t *ref; int64_t len; const int64_t *sa; int64_t r0, r1; int64_t cnt[4]; } lean_job_t;
+static void *lean_worker(void *pa)
+{
+    lean_job_t *j = (lean_job_t *)pa;
+    fmi_ref_t *f = j->f;
+    const int64_t n = f->n;
+    for (int64_t r = j->r0; r < j->r1; ++r) {
+        const int64_t p = j->sa[r];
+        uint8_t c = 4;
+        if (p > 0) {
+            const int64_t i = p - 1;                          /* T[i]: forward or reverse strand */
+            c = i < j->len ? j->ref[i] : (uint8_t)(3 - j->ref[n - 1 - i]);
+        }
+        f->bwt[r] = c;
+        if (r % LEAN_SA == 0) f->ssa[r / LEAN_SA] = p;
+    }
+    /* per-block counts of this range (blocks are whole: r0 is a multiple of LEAN_CP) */
+    for (int64_t b = j->r0 / LEAN_CP; b * LEAN_CP < j->r1; ++b) {
+        int64_t c4[4] = {0, 0, 0, 0};
+        const int64_t e = (b + 1) * LEAN_CP < j->r1 ? (b + 1) * LEAN_CP : j->r1;
+        for (int64_t r = b * LEAN_CP; r < e; ++r)
+            if (f->bwt[r] < 4) c4[f->bwt[r]]++;
+        for (int c = 0; c < 4; ++c) f->cp[4 * (b + 1) + c] = c4[c];   /* counts of block b, prefixed below */
+    }
+    return NULL;
+}
+int oracle_fmi_build_lean(const uint8_t *ref, int64_t len, const int64_t *sa, int nthreads, fmi_ref_t *f)
+{
+    memset(f, 0, sizeof(*f));
+    const int64_t n = 2 * len, N = n + 1, nb = N / LEAN_CP + 1;
+    f->n = n;
+    f->lean = 1;
+    f->bwt = (uint8_t *)malloc((size_t)N);
+    f->cp = (int64_t *)calloc((size_t)(4 * (nb + 1)), sizeof(int64_t));
+    f->ssa = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N / LEAN_SA + 1));
+    if (!f->bwt || !f->cp || !f->ssa) return -1;
+    int64_t tot[4] = {0, 0, 0, 0};
+    for (int64_t i = 0; i < len; ++i) {
+        if (ref[i] > 3) return -1;
+        tot[ref[i]]++;
+        tot[3 - ref[i]]++;                                    /* the reverse complement's base */
+    }
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    lean_job_t jobs[64];
+    pthread_t th[64];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (lean_job_t){f, ref, len, sa, (N * t / nthreads) / LEAN_CP * LEAN_CP,
+                               t + 1 == nthreads ? N : (N * (t + 1) / nthreads) / LEAN_CP * LEAN_CP, {0}};
+        pthread_create(&th[t], NULL, lean_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    for (int64_t b = 1; b <= nb; ++b)                          /* block counts -> prefix counts */
+        for (int c = 0; c < 4; ++c) f->cp[4 * b + c] += f->cp[4 * (b - 1) + c];
+    for (int64_t r = 0; r < N; ++r)
+        if (f->bwt[r] == 4) { f->sentinel = r; break; }
+    f->count[0] = 1;
+    for (int c = 0; c < 4; ++c) f->count[c + 1] = f->count[c] + tot[c];
+    return 0;
+}
+
+/* SA[r]: the array (full form) or bwa's bwt_sa -- LF steps back to a sampled row (lean form) */
+int64_t oracle_fmi_sa_at(const fmi_ref_t *f, int64_t r)
+{
+    if (!f->lean) return f->sa[r];
+    int64_t steps = 0;
+    while (r % LEAN_SA != 0) {
+        const int c = f->bwt[r];
+        if (c == 4) return steps;                             /* the '$' row: SA = 0 */
+        r = f->count[c] + occ(f, c, r);
+        ++steps;
+    }
+    return f->ssa[r / LEAN_SA] + steps;
+}
 
 /* 64-row occurrence blocks an extension touches (1 when rows k and k + s share one, else 2):
  * the algorithmic HBM bytes of the GPU kernel's block layout, counted for bench.py's roofline */
@@ -390,6 +484,14 @@ void oracle_collect_intv_mt(const fmi_ref_t *f, const oracle_mem_opt_t *opt, con
 int64_t oracle_fmi_n(const fmi_ref_t *f) { return f->n; }
 int64_t oracle_fmi_sentinel(const fmi_ref_t *f) { return f->sentinel; }
 void oracle_fmi_count(const fmi_ref_t *f, int64_t *c5) { memcpy(c5, f->count, sizeof(f->count)); }
-void oracle_fmi_sa(const fmi_ref_t *f, int64_t *sa) { memcpy(sa, f->sa, sizeof(int64_t) * (f->n + 1)); }
+void oracle_fmi_sa(const fmi_ref_t *f, int64_t *sa)
+{
+    if (!f->lean) { memcpy(sa, f->sa, sizeof(int64_t) * (f->n + 1)); return; }
+    for (int64_t r = 0; r <= f->n; ++r) sa[r] = oracle_fmi_sa_at(f, r);
+}
+void oracle_fmi_sa_rows(const fmi_ref_t *f, const int64_t *rows, int64_t m, int64_t *out)
+{
+    for (int64_t i = 0; i < m; ++i) out[i] = oracle_fmi_sa_at(f, rows[i]);
+}
 void oracle_fmi_bwt(const fmi_ref_t *f, uint8_t *bwt) { memcpy(bwt, f->bwt, (size_t)f->n + 1); }
 size_t oracle_fmi_sizeof(void) { return sizeof(fmi_ref_t); }

@@ -247,8 +247,10 @@ class FmiRef:
     """The oracle's FM-index of ref + reverse-complement(ref) (comparison-sorted suffix array,
     prefix-count occurrence table) and its SMEM passes."""
 
-    def __init__(self, ref, sa=None):
-        """sa: build from this suffix array of T$ instead of sorting (bench CPU leg only)"""
+    def __init__(self, ref, sa=None, lean=False, nthreads=1):
+        """sa: build from this suffix array of T$ instead of sorting (bench CPU leg only).
+        lean: the genome-scale form (oracle_fmi_build_lean, needs sa): occurrence checkpoints
+        every 64 rows and an SA sampled every 32 rows resolved by LF walks, ~1.8 B per row."""
         L = lib()
         P = ctypes.c_void_p
         L.oracle_fmi_sizeof.restype = ctypes.c_size_t
@@ -264,7 +266,13 @@ class FmiRef:
         L.oracle_collect_intv_mt.argtypes = [P, P, P, P, P, ctypes.c_int32, P, ctypes.c_int32, P, ctypes.c_int]
         self._buf = ctypes.create_string_buffer(L.oracle_fmi_sizeof())
         self.ref = np.ascontiguousarray(ref, dtype=np.uint8)
-        if sa is not None:
+        self.lean = bool(lean)
+        if lean:
+            L.oracle_fmi_build_lean.argtypes = [P, ctypes.c_int64, P, ctypes.c_int, P]
+            sa = np.ascontiguousarray(sa, dtype=np.int64)
+            assert len(sa) == 2 * len(self.ref) + 1
+            rc = L.oracle_fmi_build_lean(_ptr(self.ref), len(self.ref), _ptr(sa), int(nthreads), self._buf)
+        elif sa is not None:
             L.oracle_fmi_build_with_sa.argtypes = [P, ctypes.c_int64, P, P]
             sa = np.ascontiguousarray(sa, dtype=np.int64)
             assert len(sa) == 2 * len(self.ref) + 1
@@ -277,6 +285,14 @@ class FmiRef:
         self.sentinel = L.oracle_fmi_sentinel(self._buf)
         self.count = np.zeros(5, dtype=np.int64)
         L.oracle_fmi_count(self._buf, _ptr(self.count))
+
+    def sa_rows(self, rows):
+        """SA at the given rows (bwt_sa: LF walks in the lean form)"""
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        out = np.zeros(len(rows), dtype=np.int64)
+        lib().oracle_fmi_sa_rows.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+        lib().oracle_fmi_sa_rows(self._buf, _ptr(rows), len(rows), _ptr(out))
+        return out
 
     def sa(self):
         a = np.zeros(self.n + 1, dtype=np.int64)
@@ -335,15 +351,18 @@ def chain_opt(**kw):
 
 
 def mem_chain(sa, l_pac, read_len, mems, n_mems, opt=None):
-    """oracle_mem_chain over every read: (seeds SEED layout, seed_read, seed_chain) as bsw_fmi.h"""
+    """oracle_mem_chain over every read: (seeds SEED layout, seed_read, seed_chain) as bsw_fmi.h.
+    sa: the suffix array of T$ (numpy), or an FmiRef whose bwt_sa resolves the rows (lean form)."""
     import bsw as _bsw
     L = lib()
     P = ctypes.c_void_p
-    L.oracle_mem_chain.restype = ctypes.c_int64
-    L.oracle_mem_chain.argtypes = [P, P, ctypes.c_int64, P, ctypes.c_int32, P, ctypes.c_int32, P, P, P, P,
-                                   ctypes.c_int64]
+    fn = L.oracle_mem_chain_fmi if isinstance(sa, FmiRef) else L.oracle_mem_chain
+    fn.restype = ctypes.c_int64
+    fn.argtypes = [P, P, ctypes.c_int64, P, ctypes.c_int32, P, ctypes.c_int32, P, P, P, P, ctypes.c_int64]
     o = opt if opt is not None else chain_opt()
-    sa = np.ascontiguousarray(sa, dtype=np.int64)
+    src = sa._buf if isinstance(sa, FmiRef) else None
+    if src is None:
+        sa = np.ascontiguousarray(sa, dtype=np.int64)
     read_len = np.ascontiguousarray(read_len, dtype=np.int32)
     mems = np.ascontiguousarray(mems)
     n_mems = np.ascontiguousarray(n_mems, dtype=np.int32)
@@ -353,8 +372,8 @@ def mem_chain(sa, l_pac, read_len, mems, n_mems, opt=None):
         seeds = np.zeros(max(cnt, 1), dtype=_bsw.SEED_DTYPE)
         sr = np.zeros(max(cnt, 1), dtype=np.int32)
         sc = np.zeros(max(cnt, 1), dtype=np.int32)
-        need = L.oracle_mem_chain(ctypes.byref(o), _ptr(sa), l_pac, _ptr(read_len), n, _ptr(mems), cap, _ptr(n_mems),
-                                  _ptr(seeds), _ptr(sr), _ptr(sc), cnt)
+        need = fn(ctypes.byref(o), src if src is not None else _ptr(sa), l_pac, _ptr(read_len), n, _ptr(mems), cap,
+                  _ptr(n_mems), _ptr(seeds), _ptr(sr), _ptr(sc), cnt)
         if need <= cnt:
             return seeds[:need], sr[:need], sc[:need]
         cnt = need

@@ -167,6 +167,28 @@ def test_oracle_passes_2_and_3_fire(small_world):
     assert c_12.sum() > c_1.sum() and c_all.sum() > c_12.sum()
 
 
+@pytest.mark.parametrize("seed,n,L,msl", [(5, 3000, 100, 12), (7, 20000, 151, 19), (9, 60000, 151, 12)])
+def test_tied_intervals_are_identical(seed, n, L, msl):
+    """mem_collect_intv sorts intervals by info = qbeg << 32 | qend with klib's ks_introsort,
+    which leaves ties in an implementation order; here ties are ordered by (k, s, l).  That is no
+    parity gap: equal info means the same read substring, whose SA interval (k, s) and
+    reverse-complement row l are unique, so tied records are identical and every order of them
+    is the same sequence -- checked on repetitive references where ties do occur (pass-3
+    LAST-like seeds repeating a pass-1 / pass-2 span)."""
+    ref = repetitive_ref(n, seed)
+    o = oracle.FmiRef(ref)
+    reads, off, lens = sample_reads(ref, 400, L, seed + 1, p_sub=0.03)
+    out, cnt = o.collect_intv(reads, off, lens, cap=512, opt=oracle.mem_opt(min_seed_len=msl))
+    ties = 0
+    for i in range(len(lens)):
+        v = out[i, :cnt[i]]
+        same = v["info"][1:] == v["info"][:-1]
+        ties += int(same.sum())
+        for f in ("k", "l", "s"):
+            assert np.array_equal(v[f][1:][same], v[f][:-1][same]), (i, f)
+    assert ties > 0
+
+
 @pytest.mark.parametrize("seed,n", [(1, 5000), (3, 40000)])
 def test_host_builder_equals_oracle(seed, n):
     """the product's prefix-doubling suffix array / BWT / counts (host-only index, no GPU) ==
@@ -361,3 +383,113 @@ def test_index_self_check():
         f = bsw.Fmi(ref, flags=flags)
         assert f.check() == 0, flags
         f.close()
+
+
+@pytest.mark.parametrize("seed,n", [(3, 50_000), (4, 9_000)])
+def test_lean_oracle_equals_full(seed, n):
+    """the oracle's lean (genome-scale) index -- occurrence checkpoints every 64 rows, SA sampled
+    every 32 rows resolved by LF walks (bwa's bwt_sa) -- gives the full form's counts, every SA
+    row, the same intervals and the same chains"""
+    ref = repetitive_ref(n, seed)
+    o = oracle.FmiRef(ref)
+    sa = o.sa()
+    lean = oracle.FmiRef(ref, sa=sa, lean=True, nthreads=3)
+    assert lean.n == o.n and lean.sentinel == o.sentinel and list(lean.count) == list(o.count)
+    assert np.array_equal(lean.sa(), sa)
+    reads, off, lens = sample_reads(ref, 300, 151, seed + 1)
+    a, ca = o.collect_intv(reads, off, lens, cap=512)
+    b, cb = lean.collect_intv(reads, off, lens, cap=512, nthreads=2)
+    assert np.array_equal(ca, cb) and np.array_equal(a, b)
+    for x, y in zip(oracle.mem_chain(sa, len(ref), lens, a, ca), oracle.mem_chain(lean, len(ref), lens, a, ca)):
+        assert np.array_equal(x, y)
+
+
+def _text_check_intervals(T, reads, off, lens, mems, cnt, pos_of, n, max_rows=32):
+    """Every interval [k, k + s) (and its reverse-complement rows [l, l + s)) against the text:
+    the rows inside (up to max_rows of them) start an exact copy of the read's substring, the two
+    rows just outside do not -- so (k, s) and l are exactly the SA ranges of the substring and its
+    reverse complement (the SA itself is checked by bsw_fmi_check).  pos_of(rows) -> SA[rows]."""
+    rows, want, inside = [], [], []
+    for i in range(len(lens)):
+        rd = reads[off[i]:off[i] + lens[i]]
+        for v in mems[i, :cnt[i]]:
+            m, e = int(v["info"] >> 32), int(v["info"] & 0xffffffff)
+            p = rd[m:e].tobytes()
+            rc = (3 - rd[m:e][::-1]).astype(np.uint8).tobytes()
+            k, l, s = int(v["k"]), int(v["l"]), int(v["s"])
+            for base, pat in ((k, p), (l, rc)):
+                for r in list(range(base, base + min(s, max_rows))):
+                    rows.append(r), want.append(pat), inside.append(True)
+                for r in (base - 1, base + s):
+                    if 0 <= r <= n:
+                        rows.append(r), want.append(pat), inside.append(False)
+    pos = pos_of(np.array(rows, dtype=np.int64))
+    bad = 0
+    for r, p, w, ins in zip(rows, pos, want, inside):
+        got = T[p:p + len(w)].tobytes() if 0 <= p and p + len(w) <= len(T) else b""
+        bad += (got == w) != ins
+    return len(rows), bad
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_wide_index_at_genome_scale_text_and_oracle():
+    """BASELINE C4's index size class inside the GPU suite: a 2.2 Gb reference, whose two-strand
+    BWT has 4.4e9 rows (> 2^32: the wide 64-bit layout), built on the GPU and self-checked; 3,000
+    mutated PE reads seeded on the GPU with every interval checked against the text at its SA
+    rows; chains and mem_chain2aln regions equal to the oracle pipeline run on the product's
+    suffix-array rows (the oracle's own index would need ~180 GB at this size)."""
+    import bench
+    import hiprt
+    ref = bench.mem_reference(2200)
+    f = bsw.Fmi(ref)
+    info = f.info()
+    assert info.n + 1 > 2**32
+    assert f.check() == 0
+    reads, off, lens = bench.pe_reads(ref, 1500, seed=5)
+    cap = 256
+    mems, cnt = f.collect_intv(reads, off, lens, cap=cap)
+    assert (cnt <= cap).all()
+    T = np.concatenate([ref, (3 - ref[::-1])]).astype(np.uint8)
+
+    def pos_of(rows):
+        d_k = hiprt.DeviceBuffer.from_array(rows.astype(np.uint64))
+        d_p = hiprt.DeviceBuffer(len(rows) * 8)
+        f.sa_device(d_k.ptr, len(rows), d_p.ptr)
+        return d_p.download(np.zeros(len(rows), dtype=np.int64))
+    checked, bad = _text_check_intervals(T, reads, off, lens, mems, cnt, pos_of, info.n)
+    assert bad == 0 and checked > 3 * len(lens)
+    # chains + regions: the product's GPU pipeline vs the oracle on a compact copy of the SA rows
+    # the chains read (interval k -> k', the rows k + t * step laid out at k' + t * step)
+    copt = oracle.chain_opt()
+    mems_c, src, dst, base = mems.copy(), [], [], 0
+    for i in range(len(lens)):
+        for t in range(cnt[i]):
+            s = int(mems[i, t]["s"])
+            step = s // copt.max_occ if s > copt.max_occ else 1
+            take = np.arange(0, s, step)[:copt.max_occ]
+            mems_c["k"][i, t] = base
+            src.append(int(mems[i, t]["k"]) + take)
+            dst.append(base + take)
+            base += int(take[-1]) + 1 if len(take) else 0
+    sa_rows = np.zeros(max(base, 1), dtype=np.int64)
+    sa_rows[np.concatenate(dst)] = pos_of(np.concatenate(src))
+    seeds, sr, sc = oracle.mem_chain(sa_rows, len(ref), lens, mems_c, cnt, copt)
+    d_reads = hiprt.DeviceBuffer.from_array(reads)
+    (gs, gsr, gsc), (d_s, d_sr, d_sc), (d_off, d_len) = bsw.seed_and_chain(f, d_reads, off, lens, cap=cap)
+    assert np.array_equal(gsr, sr) and np.array_equal(gsc, sc) and np.array_equal(gs, seeds)
+    eng = bsw.Engine()
+    bsw.set_reference(eng, T)
+    opt = bsw.ext_opt(l_pac=len(ref))
+    ns = len(seeds)
+    d_out, d_ext = hiprt.DeviceBuffer(max(1, ns) * bsw.ALNREG_DTYPE.itemsize), hiprt.DeviceBuffer(max(1, ns) * 4)
+    bsw.chain2aln_resident(eng, d_reads.ptr, d_off.ptr, d_len.ptr, len(lens), d_s.ptr, d_sr.ptr, d_sc.ptr, ns,
+                           d_out.ptr, d_ext.ptr, opt)
+    out = d_out.download(np.zeros(ns, dtype=bsw.ALNREG_DTYPE))
+    ext = d_ext.download(np.zeros(ns, dtype=np.int32))
+    want, wext = oracle.chain2aln(oracle.make_params(), opt, T, reads, off, lens, seeds, sr, sc, nthreads=8)
+    assert np.array_equal(ext, wext)
+    for fld in bsw.ALNREG_DTYPE.names:
+        assert np.array_equal(out[fld], want[fld]), fld
+    eng.close()
+    f.close()

@@ -50,7 +50,7 @@ for step in "$@"; do
     segv)
         log=$O/segv_trace.log
         rm -rf "$O/segv_trace"
-        PERCALL_SEGV_LOG=$O/segv_diag.txt timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace \
+        PERCALL_SEGV_LOG=$O/segv_diag.txt PERCALL_MAPS_LOG=$O/segv_maps.txt timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace \
             --output-format csv -d "$O/segv_trace" -- bwa-mem2-arm_amd/lib/percall_bench 200000 8 1000 \
             > "$log" 2>&1; rc=$?
         [ -f "$O/segv_diag.txt" ] && { echo "FAULT diagnostics:"; head -40 "$O/segv_diag.txt"; }

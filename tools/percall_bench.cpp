@@ -4,15 +4,17 @@
 //   percall_bench [pairs_total] [threads] [sizes...]
 // For every call size: median single-caller latency (1 thread, 200 calls after warm-up) and the
 // aggregate rate of `threads` concurrent callers (each issuing calls back to back over its own
-// slice of the batch for ~0.5 s), once with cross-call coalescing (default) and once without
-// (BSW_OPT_COALESCE = 0); one JSON line on stdout.  Outputs are checked against a whole-batch
-// call (bit-identical required).
+// slice of the batch for 0.5 s after an untimed warm-up of every caller), with cross-call
+// coalescing (default) and without (BSW_OPT_COALESCE = 0) interleaved on / off / on / off, min
+// and max of each kept; one JSON line on stdout.  Outputs are checked against a whole-batch call
+// (bit-identical required).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <dlfcn.h>
 #include <execinfo.h>
 #include <signal.h>
@@ -104,54 +106,87 @@ int main(int argc, char **argv)
     if (const char *b = getenv("PERCALL_LINGER")) bsw_set_option(ctx, BSW_OPT_COALESCE_LINGER, atoi(b));
     std::vector<SeqPair> want = pairs;
     if (bsw_get_scores(ctx, want.data(), ref.data(), qer.data(), N, 100, 16) != BSW_OK) return 3;
-    printf("{\"tool\": \"percall_bench\", \"threads\": %d, \"pairs\": %d, \"curve\": [", T, N);
+    printf("{\"tool\": \"percall_bench\", \"threads\": %d, \"pairs\": %d, \"seconds_per_run\": 0.5, "
+           "\"order\": \"per size: 1-caller latency, then %d-caller runs interleaved coalescing on/off/on/off, each "
+           "after an untimed warm-up of every caller\", \"curve\": [", T, N, T);
     bool first = true;
     std::atomic<long> bad{0};
-    for (int co = 1; co >= 0; --co) {
-        bsw_set_option(ctx, BSW_OPT_COALESCE, co ? (getenv("PERCALL_COALESCE") ? atoi(getenv("PERCALL_COALESCE")) : 32768) : 0);
-        for (int32_t m : sizes) {
-            if (m > N / T) continue;
-            // one caller: median latency
-            std::vector<SeqPair> buf(pairs.begin(), pairs.begin() + m);
-            std::vector<double> lat;
-            for (int k = 0; k < 203; ++k) {
-                const int32_t a = (int32_t)(((int64_t)k * m) % (N - m + 1));
-                std::copy(pairs.begin() + a, pairs.begin() + a + m, buf.begin());
-                const auto t0 = Clock::now();
-                if (bsw_get_scores(ctx, buf.data(), ref.data(), qer.data(), m, 100, 16) != BSW_OK) return 4;
-                if (k >= 3) lat.push_back(secs(t0, Clock::now()));
-                for (int32_t i = 0; i < m; ++i) bad += memcmp(&buf[i].score, &want[a + i].score, 24) != 0;
-            }
-            std::sort(lat.begin(), lat.end());
-            const double med = lat[lat.size() / 2];
-            // T concurrent callers, each over its own contiguous slice, calls back to back
-            std::atomic<long> done{0};
-            std::atomic<bool> stop{false};
-            std::vector<std::thread> th;
-            const int32_t slice = N / T;
+    const int32_t co_on = getenv("PERCALL_COALESCE") ? atoi(getenv("PERCALL_COALESCE")) : 32768;
+    // T concurrent callers, each over its own contiguous slice, calls back to back for `secs_run`;
+    // returns M pairs / s
+    auto callers = [&](int32_t m, double secs_run) {
+        std::atomic<long> done{0};
+        std::vector<std::thread> th;
+        const int32_t slice = N / T;
+        const auto t0 = Clock::now();
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                std::vector<SeqPair> b(m);
+                for (int32_t k = 0;; ++k) {
+                    const int32_t a = t * slice + (int32_t)(((int64_t)k * m) % (slice - m + 1));
+                    std::copy(pairs.begin() + a, pairs.begin() + a + m, b.begin());
+                    if (bsw_get_scores(ctx, b.data(), ref.data(), qer.data(), m, 100, 16) != BSW_OK) { bad += 1000000; return; }
+                    for (int32_t i = 0; i < m; ++i) bad += memcmp(&b[i].score, &want[a + i].score, 24) != 0;
+                    done.fetch_add(m);
+                    if (secs(t0, Clock::now()) > secs_run) break;
+                }
+            });
+        for (auto &x : th) x.join();
+        return done.load() / secs(t0, Clock::now()) / 1e6;
+    };
+    for (int32_t m : sizes) {
+        if (m > N / T) continue;
+        // one caller: median latency (coalescing on: a lone caller leads its own batch at once)
+        bsw_set_option(ctx, BSW_OPT_COALESCE, co_on);
+        std::vector<SeqPair> buf(pairs.begin(), pairs.begin() + m);
+        std::vector<double> lat;
+        for (int k = 0; k < 203; ++k) {
+            const int32_t a = (int32_t)(((int64_t)k * m) % (N - m + 1));
+            std::copy(pairs.begin() + a, pairs.begin() + a + m, buf.begin());
             const auto t0 = Clock::now();
-            for (int t = 0; t < T; ++t)
-                th.emplace_back([&, t] {
-                    std::vector<SeqPair> b(m);
-                    for (int32_t k = 0; !stop.load(std::memory_order_relaxed); ++k) {
-                        const int32_t a = t * slice + (int32_t)(((int64_t)k * m) % (slice - m + 1));
-                        std::copy(pairs.begin() + a, pairs.begin() + a + m, b.begin());
-                        if (bsw_get_scores(ctx, b.data(), ref.data(), qer.data(), m, 100, 16) != BSW_OK) { bad += 1000000; return; }
-                        for (int32_t i = 0; i < m; ++i) bad += memcmp(&b[i].score, &want[a + i].score, 24) != 0;
-                        done.fetch_add(m);
-                        if (secs(t0, Clock::now()) > 0.5) break;
-                    }
-                });
-            for (auto &x : th) x.join();
-            const double dt = secs(t0, Clock::now());
-            printf("%s{\"pairs_per_call\": %d, \"coalescing\": %s, \"latency_ms_median\": %.3f, "
-                   "\"M_pairs_per_s_1_caller\": %.3f, \"M_pairs_per_s_%d_callers\": %.3f}",
-                   first ? "" : ", ", m, co ? "true" : "false", med * 1e3, m / med / 1e6, T, done.load() / dt / 1e6);
-            first = false;
-            fflush(stdout);
+            if (bsw_get_scores(ctx, buf.data(), ref.data(), qer.data(), m, 100, 16) != BSW_OK) return 4;
+            if (k >= 3) lat.push_back(secs(t0, Clock::now()));
+            for (int32_t i = 0; i < m; ++i) bad += memcmp(&buf[i].score, &want[a + i].score, 24) != 0;
         }
+        std::sort(lat.begin(), lat.end());
+        const double med = lat[lat.size() / 2];
+        // T callers, coalescing on / off interleaved A-B-A-B, each run after a warm-up of every
+        // caller (its slots, the coalescing leaders' buffers at this size)
+        std::vector<double> r[2];
+        for (int rep = 0; rep < 2; ++rep)
+            for (int co = 1; co >= 0; --co) {
+                bsw_set_option(ctx, BSW_OPT_COALESCE, co ? co_on : 0);
+                callers(m, 0.05);
+                r[co].push_back(callers(m, 0.5));
+            }
+        auto stat = [](std::vector<double> v) {
+            std::sort(v.begin(), v.end());
+            char o[256];
+            snprintf(o, sizeof o, "{\"median\": %.3f, \"min\": %.3f, \"max\": %.3f, \"runs\": [%.3f, %.3f]}",
+                     (v.front() + v.back()) / 2, v.front(), v.back(), v[0], v[1]);
+            return std::string(o);
+        };
+        printf("%s{\"pairs_per_call\": %d, \"latency_ms_median\": %.3f, \"M_pairs_per_s_1_caller\": %.3f, "
+               "\"M_pairs_per_s_%d_callers_coalescing\": %s, \"M_pairs_per_s_%d_callers_no_coalescing\": %s}",
+               first ? "" : ", ", m, med * 1e3, m / med / 1e6, T, stat(r[1]).c_str(), T, stat(r[0]).c_str());
+        first = false;
+        fflush(stdout);
     }
-    printf("], \"outputs_identical\": %s}\n", bad.load() == 0 ? "true" : "false");
+    bsw_set_option(ctx, BSW_OPT_COALESCE, co_on);
+    // PERCALL_MAPS_LOG=<file>: this process's mappings at the end of a clean run (to place the
+    // addresses of an earlier run's fault: the libraries' load order and sizes are the same, so
+    // their offsets from libbsw_hip.so's load base carry over; ASLR moves only the whole block)
+    if (const char *ml = getenv("PERCALL_MAPS_LOG"))
+        if (FILE *f = fopen(ml, "w")) {
+            put_addr(f, "bsw_get_scores", (void *)&bsw_get_scores);
+            if (FILE *m = fopen("/proc/self/maps", "r")) {
+                char line[512];
+                while (fgets(line, sizeof line, m)) fputs(line, f);
+                fclose(m);
+            }
+            fclose(f);
+        }
+    printf("],\"outputs_identical\": %s}\n", bad.load() == 0 ? "true" : "false");
     bsw_destroy(ctx);
     return bad.load() == 0 ? 0 : 5;
 }
