@@ -245,16 +245,92 @@ __device__ __forceinline__ uint32_t pack2(int v) { return ((uint32_t)v & 0xffffu
           [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [r0] "i"(R0)                             \
         : "vcc", "scc")
 
+// BSW_PC_JKEY (default 1): the FAST key from ONE scalar constant per group instead of two.  The
+// key halves H << 8 | j (H <= 255 in this kernel's regime) are built by v_perm from the group's
+// four column numbers as BYTES of one SGPR, J4 = {4G-1, 4G, 4G+1, 4G+2}, with two loop-invariant
+// VGPR selectors (gfx9 VOP3 reads one SGPR): one s_mov per group instead of two for the packed
+// {4G-1, 4G} / {4G+1, 4G+2} constants of v_lshl_or -- 24 fewer SALU on a C2 row.  The masked
+// bodies (out of line, ~9% of groups) load those packed constants themselves (two s_mov there).
+#ifndef BSW_PC_JKEY
+#define BSW_PC_JKEY 1
+#endif
+#define PC_GROUP_ASM_J                                                                   \
+    asm volatile(                                                                            \
+        "s_bitcmp1_b64 %[mfa], %[g]\n\t"                                                     \
+        "s_cbranch_scc0 5f\n\t"                                                              \
+        PC_CNT(0) PC_CNT(1)                                                                  \
+        PC_SCORES                                                                            \
+        PC_PH1("a", "%[ea]") PC_PH1("b", "%[eb]")                                            \
+        PC_FAST_CHAIN                                                                        \
+        "v_perm_b32 %[pa], %[ha], %[j4], %[ska]\n\t"                                         \
+        "v_pk_max_u16 %[key], %[key], %[pa]\n\t"                                             \
+        "v_perm_b32 %[pb], %[hb], %[j4], %[skb]\n\t"                                         \
+        "v_pk_max_u16 %[key], %[key], %[pb]\n"                                               \
+        "3:\n"                                                                               \
+        ".subsection 1\n"                                                                    \
+        "5:\n\t"                                                                             \
+        "s_bitcmp1_b64 %[men], %[g]\n\t"                                                     \
+        "s_cbranch_scc0 3b\n\t"                                                              \
+        "s_setprio 2\n\t"                                                                    \
+        PC_CNT(0)                                                                            \
+        "s_mov_b32 %[jja], %[ija]\n\t"               /* packed {4G-1, 4G}, {4G+1, 4G+2} */ \
+        "s_mov_b32 %[jjb], %[ijb]\n\t"                                                       \
+        "v_lshrrev_b32_e32 %[h1], 16, %[h1]\n\t"                                             \
+        PC_SCORES                                                                            \
+        "s_bitcmp1_b64 %[mle], %[g]\n\t"                                                     \
+        "s_cbranch_scc1 4f\n\t"                                                              \
+        PC_CNT(2)                                                                            \
+        PC_MASKED(PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"),                        \
+                  PC_MCELL("%[c1]", "%[c0]", "a", "WORD_1", "%[j1]"),                        \
+                  PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"),                        \
+                  PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"),                        \
+                  "v_perm_b32 %[pa], %[pa], %[j4], %[ska]\n\t",                              \
+                  "v_perm_b32 %[pb], %[pb], %[j4], %[skb]\n\t", "", "")                      \
+        "v_lshlrev_b32_e32 %[h1], 16, %[h1]\n\t"                                              \
+        "s_setprio 0\n\t"                                                                    \
+        "s_branch 3b\n"                                                                      \
+        "4:\n\t"                                                                             \
+        PC_CNT(3)                                                                            \
+        PC_MASKED(PC_RESET("%[h1]", "%[r0]") PC_MCELL("%[c0]", "%[h1]", "a", "WORD_0", "%[j0]"), \
+                  PC_RESET("%[c0]", "%[j1]") PC_MCELL("%[c1]", "%[c0]", "a", "WORD_1", "%[j1]"), \
+                  PC_RESET("%[c1]", "%[j2]") PC_MCELL("%[c2]", "%[c1]", "b", "WORD_0", "%[j2]"), \
+                  PC_RESET("%[c2]", "%[j3]") PC_MCELL("%[h1]", "%[c2]", "b", "WORD_1", "%[j3]"), \
+                  "v_perm_b32 %[pa], %[pa], %[j4], %[ska]\n\t",                              \
+                  "v_perm_b32 %[pb], %[pb], %[j4], %[skb]\n\t",                              \
+                  PC_LEFTMASK("a"), PC_LEFTMASK("b"))                                        \
+        "v_lshlrev_b32_e32 %[h1], 16, %[h1]\n\t"                                              \
+        "s_setprio 0\n\t"                                                                    \
+        "s_branch 3b\n"                                                                      \
+        ".subsection 0\n"                                                                    \
+        : [ha] "+v"(ha), [hb] "+v"(hb), [ea] "+v"(ea), [eb] "+v"(eb), [f] "+v"(f),           \
+          [h1] "+v"(h1), [key] "+v"(key), [y] "=&v"(y), [sa] "=&v"(sa), [sb] "=&v"(sb),     \
+          [ta] "=&v"(ta), [tb] "=&v"(tb), [xa] "=&v"(xa), [xb] "=&v"(xb), [c0] "=&v"(c0),    \
+          [c1] "=&v"(c1), [c2] "=&v"(c2), [pa] "=&v"(pa), [pb] "=&v"(pb), [fp] "=&v"(fp),   \
+          [jja] "=&s"(tja), [jjb] "=&s"(tjb)                                                 \
+          PC_CNT_OPS                                                                         \
+        : [q] "v"(q), [plo] "v"(plo), [phi] "v"(phi), [oe2] "s"(oe2), [ed2] "s"(ed2),        \
+          [ed] "s"(ed), [e0e] "s"(e0e), [ee2] "s"(ee2), [men] "s"(r.enter), [mfa] "s"(r.fast), [mle] "s"(r.left),           \
+          [endw] "v"(endw), [endm1w] "v"(endm1w),                                            \
+          [begm2w] "v"(begm2w), [endv] "v"(endv), [begv] "v"(begv), [g] "i"(G),             \
+          [j4] "s"(J4), [ska] "v"(bs.ka), [skb] "v"(bs.kb), [ija] "i"(JJA), [ijb] "i"(JJB),  \
+          [j0] "i"(4 * G), [j1] "i"(4 * G + 1),                                              \
+          [j2] "i"(4 * G + 2), [j3] "i"(4 * G + 3), [r0] "i"(R0)                             \
+        : "vcc", "scc")
+
+struct PcbSel { uint32_t ka, kb; };            // key selectors (VGPRs: v_perm takes one SGPR)
+
 // One 4-column group G (columns / slots 4G .. 4G+3) as ONE asm statement: skip / FAST /
 // MASKED (R: right edge only; L: also resets at beg) decided by scalar tests inside.
-template <int G>
+template <int G, bool JK>
 __device__ __forceinline__ void pc_group(uint32_t &ha, uint32_t &hb, uint32_t &ea, uint32_t &eb,
                                          uint32_t q, uint32_t plo, uint32_t phi, int &f, int &h1,
                                          uint32_t &key, uint32_t oe2, uint32_t ed2, int ed,
                                          const PcRow &r, uint32_t endw, uint32_t endm1w,
-                                         uint32_t begm2w, int endv, int begv, uint32_t (&ctr)[4])
+                                         uint32_t begm2w, int endv, int begv, const PcbSel &bs,
+                                         uint32_t (&ctr)[4])
 {
     (void)ctr;
+    (void)bs;
     // key slot s carries column j = s - 1: jj = {4G-1, 4G} and {4G+1, 4G+2}
     constexpr uint32_t JJA = ((uint32_t)(4 * G - 1) & 0xffffu) | ((uint32_t)(4 * G) << 16);
     constexpr uint32_t JJB = (uint32_t)(4 * G + 1) | ((uint32_t)(4 * G + 2) << 16);
@@ -266,6 +342,11 @@ __device__ __forceinline__ void pc_group(uint32_t &ha, uint32_t &hb, uint32_t &e
         // slot 0 holds the column-0 boundary, not a cell: its key half is 0 (c0 << 24 | 0)
         PC_GROUP_ASM("v_lshlrev_b32_e32 %[pa], 24, %[pa]\n\t",        /* pa = {H(0), H(1)} here */
                      "v_lshl_or_b32 %[pa], %[c0], 24, 0\n\t");
+    } else if constexpr (JK) {
+        constexpr uint32_t J4 = (uint32_t)(4 * G - 1) | ((uint32_t)(4 * G) << 8) | ((uint32_t)(4 * G + 1) << 16) |
+                                ((uint32_t)(4 * G + 2) << 24);
+        uint32_t tja, tjb;
+        PC_GROUP_ASM_J;
     } else {
         PC_GROUP_ASM("v_lshl_or_b32 %[pa], %[ha], 8, %[jja]\n\t",
                      "v_lshl_or_b32 %[pa], %[pa], 8, %[jja]\n\t");
@@ -367,7 +448,6 @@ constexpr uint32_t kSelK0 = 0x050C0C0Cu;       // group 0: {0, 0, 0, HB.b1} (slo
           [sa2] "s"(kSelA2), [sk0] "s"(kSelK0), [vka] "v"(bs.ka), [vkb] "v"(bs.kb)            \
         : "vcc", "scc")
 
-struct PcbSel { uint32_t ka, kb; };            // the key selectors (VGPRs: v_perm takes one SGPR)
 
 template <int G>
 __device__ __forceinline__ void pcb_group(uint32_t &hw, uint32_t &ew, uint32_t q, uint32_t plo, uint32_t phi,
@@ -406,8 +486,8 @@ __device__ __forceinline__ void pc_group_if(uint32_t (&hh)[(BY ? QMAX / 4 : QMAX
             pcb_group<G>(hh[G], ee[G], qs[G], plo, phi, f, h1, key, oe2, ed2, ed, r, endw, endm1w, begm2w, endv,
                          begv, bs, ctr);
         else
-            pc_group<G>(hh[2 * G], hh[2 * G + 1], ee[2 * G], ee[2 * G + 1], qs[G], plo, phi, f, h1, key, oe2, ed2,
-                        ed, r, endw, endm1w, begm2w, endv, begv, ctr);
+            pc_group<G, BSW_PC_JKEY && QMAX >= 128>(hh[2 * G], hh[2 * G + 1], ee[2 * G], ee[2 * G + 1], qs[G], plo, phi, f, h1, key, oe2, ed2,
+                        ed, r, endw, endm1w, begm2w, endv, begv, bs, ctr);
     }
 }
 
@@ -607,7 +687,11 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
     const uint32_t oe2 = (uint32_t)(kp.o_del + kp.e_del) * 0x10001u;
     const uint32_t ed2 = (uint32_t)kp.e_del * 0x10001u;
     uint32_t ctr[4] = {0, 0, 0, 0};                       // BSW_PC_STATS group-path counters
-    const PcbSel bs{kSelKa, kSelKb};
+    // key selectors in VGPRs: the byte planes' (BY) or the JKEY ones (int16 planes)
+    // (the JKEY selectors only where the two VGPRs cost no occupancy: QMAX >= 128 runs at two
+    // waves per SIMD either way; the 96 / 64 classes would drop from 3 / 4 waves)
+    PcbSel bs{BY ? kSelKa : 0x06010400u, BY ? kSelKb : 0x06030402u};
+    if constexpr (BY || (BSW_PC_JKEY && QMAX >= 128)) asm volatile("" : "+v"(bs.ka), "+v"(bs.kb));
 #ifdef BSW_PC_STATS
     uint32_t nrows = 0, nlast = 0, nue = 0;
 #endif

@@ -14,6 +14,7 @@
 #   segv            the round-3 traced 8-caller percall_bench (kernel + memory-copy trace) with the
 #                   fault handler armed (PERCALL_SEGV_LOG): one run, diagnostics kept if it faults
 #   percall:<args>  percall_bench <args> (commas for spaces), untraced
+#   ab:<lib>        same-box A/B: C2 line with lib/<lib> (base) vs the in-tree library, x3 alternating
 #   py:<file>       python -u <file> (a probe script under tools/)
 # (rounds 1-3 kept one file per gpurun call, tools/gpu_*.sh; they are in git history, baea391)
 set -o pipefail
@@ -60,6 +61,18 @@ for step in "$@"; do
         log=$O/percall.log
         timeout -k 10 300 bwa-mem2-arm_amd/lib/percall_bench $(sp "$arg") > "$log" 2>&1 || fail "$step" $? "$log"
         tail -1 "$log" | cut -c1-1500 ;;
+    ab)
+        # same-box A/B of the in-tree library (new) against lib/<arg> (base): C2 bench lines
+        # alternating base / new three times, value and DP kernel ms of each
+        log=$O/ab_$arg.log; : > "$log"
+        for k in 1 2 3; do
+            for v in base new; do
+                if [ $v = base ]; then L=$PWD/bwa-mem2-arm_amd/lib/$arg; else L=$PWD/bwa-mem2-arm_amd/lib/libbsw_hip.so; fi
+                BSW_HIP_LIB=$L timeout -k 10 200 python bench.py --no-cpu --no-host-path --steps 30 --warmup 3 \
+                    > "$O/ab_run.log" 2>&1 || fail "$step" $? "$O/ab_run.log"
+                python3 -c "import json;d=json.loads(open('$O/ab_run.log').read().strip().splitlines()[-1]);print('$v', d['value'], d['roofline']['launch_ms'])" | tee -a "$log"
+            done
+        done ;;
     py)
         log=$O/$(basename "$arg" .py).log
         timeout -k 10 600 python -u "$arg" > "$log" 2>&1 || fail "$step" $? "$log"
