@@ -10,7 +10,11 @@ One step = one bsw_get_scores_device() call over the whole resident batch (plan 
 DP kernel + results written back into the SeqPair records in HBM).  Inputs are resident in
 HBM before timing starts.  N GPUs: one process per GPU (torchrun), each with its own
 1M-pair shard (weak scaling, pairs are independent -> no data-path collective); the
-control plane (barriers, max-over-ranks timing) is torch.distributed/gloo.
+control plane (barriers, max-over-ranks timing) is torch.distributed/gloo.  At N > 1 the
+same line also carries `rccl_strong`: ONE fixed batch (--rccl-pairs, 4M) resident on GPU 0,
+scattered to the ranks' GPUs over an nccl (= RCCL) group, scored in place, outputs gathered
+back to GPU 0, all timed -- with rccl_world_size and the check that the gathered outputs are
+identical to the same batch scored on GPU 0 alone (BASELINE configs[4]'s batch scatter).
 
 Reported beside the metric:
   roofline     -- dominant kernel (pc_kernel<160> on C2), integer-VALU bound: algorithmic ops

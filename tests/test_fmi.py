@@ -493,3 +493,30 @@ def test_wide_index_at_genome_scale_text_and_oracle():
         assert np.array_equal(out[fld], want[fld]), fld
     eng.close()
     f.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gpu_builder_satellite_array():
+    """A repeat-dense reference for the GPU builder's tie resolution: 100 kb of a
+    perfect 171-bp tandem array (alpha-satellite-like) plus 20 kb of a perfect dinucleotide
+    repeat inside 2 Mb of random sequence.  Equal 27-base prefixes form ~171 tie groups of ~585
+    suffixes whose common prefixes run to the array's end; they are sorted on the host by suffix
+    comparison (bsw_fmi_build.hip).  Equal to the host prefix-doubling builder; the build time is
+    printed (a perfect multi-Mb array would scale as g log g x array length)."""
+    import time
+    rng = np.random.default_rng(17)
+    ref = rng.integers(0, 4, 2_000_000, dtype=np.uint8)
+    unit = rng.integers(0, 4, 171, dtype=np.uint8)
+    ref[500_000:600_000] = np.tile(unit, 100_000 // 171 + 1)[:100_000]
+    ref[1_200_000:1_220_000] = np.tile(np.array([0, 2], np.uint8), 10_000)
+    t = time.perf_counter()
+    g = bsw.Fmi(ref, flags=bsw.FMI_GPU_BUILD)
+    dt = time.perf_counter() - t
+    h = bsw.Fmi(ref, device=-1)
+    assert np.array_equal(g.sa(), h.sa())
+    assert g.check() == 0
+    print(f"GPU build of the 2 Mb satellite reference: {dt:.2f} s")
+    assert dt < 120
+    g.close()
+    h.close()

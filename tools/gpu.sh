@@ -15,6 +15,8 @@
 #                   fault handler armed (PERCALL_SEGV_LOG): one run, diagnostics kept if it faults
 #   percall:<args>  percall_bench <args> (commas for spaces), untraced
 #   ab:<lib>        same-box A/B: C2 line with lib/<lib> (base) vs the in-tree library, x3 alternating
+#   hptrace[:chunk] kernel + copy trace and per-chunk host timeline of 1M-pair host-buffer calls
+#   export:VAR=VAL  set an environment variable for the following steps (unset:VAR clears it)
 #   py:<file>       python -u <file> (a probe script under tools/)
 # (rounds 1-3 kept one file per gpurun call, tools/gpu_*.sh; they are in git history, baea391)
 set -o pipefail
@@ -73,6 +75,19 @@ for step in "$@"; do
                 python3 -c "import json;d=json.loads(open('$O/ab_run.log').read().strip().splitlines()[-1]);print('$v', d['value'], d['roofline']['launch_ms'])" | tee -a "$log"
             done
         done ;;
+    hptrace)
+        # the drop-in host path's timeline: per-chunk host times (BSW_DEBUG_HP) and a kernel +
+        # copy trace of a few 1M-pair bsw_get_scores calls (tools/host_path_once.py [chunk] [calls])
+        rm -rf "$O/hptrace"
+        BSW_DEBUG_HP=1 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+            -d "$O/hptrace" -- python3 tools/host_path_once.py ${arg:-262144} 4 > "$O/hptrace.log" 2>&1 \
+            || fail "$step" $? "$O/hptrace.log"
+        grep '^call' "$O/hptrace.log" ;;
+    export)
+        # export:VAR=VALUE for the steps after it (e.g. export:GPU_MAX_HW_QUEUES=8, export:BSW_HP_INLINE_ENQ=1)
+        export "${arg?}"; echo "exported $arg" ;;
+    unset)
+        unset "${arg?}"; echo "unset $arg" ;;
     py)
         log=$O/$(basename "$arg" .py).log
         timeout -k 10 600 python -u "$arg" > "$log" 2>&1 || fail "$step" $? "$log"
