@@ -195,26 +195,24 @@ def traffic_dominant(prefix: str):
 
 def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
     """oracle/bsw_sse41.c (the reference's SSE4.1 getScores16 design restated) on a bounded
-    sample of the same batch, median of 3 after a warm-up.  Thread counts tried: every core of
-    the affinity set (`cores`), the cgroup CPU quota (the box's real CPU share, which can be far
-    below the affinity set) and 16; `value` is the BEST of them with `cores` = the count that
-    gave it, the others beside it, plus the 1-thread SSE4.1 and scalar ksw_extend2 rates
-    (BASELINE.md / north_star: core count stated)."""
+    sample of the same batch, median of 3 after a warm-up.  Thread counts tried: the reference's
+    own sweep 1 / 2 / 4 / 8 / 16 (benchmark_threading.sh:96-119, median of 3) and the cgroup CPU
+    quota (the box's real CPU share, which can be far below the affinity set; the affinity set
+    itself only when no quota caps it -- oversubscribing the quota measures nothing); `value` is
+    the BEST of them with `cores` = the count that gave it, the sweep beside it, plus the 1-thread
+    SSE4.1 and scalar ksw_extend2 rates (BASELINE.md / north_star: core count stated)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # CPU baseline leg only (test infrastructure)
     P = oracle.make_params()
     host = host_cpu_info()
     quota = host.get("cgroup_cpu_quota")
-    counts = [cores]
-    if quota and int(math.ceil(quota)) < cores:
-        counts.append(int(math.ceil(quota)))
-    if 16 < cores and 16 not in counts:
-        counts.append(16)
+    cap = min(cores, int(math.ceil(quota))) if quota else cores
+    counts = sorted({c for c in (1, 2, 4, 8, 16) if c <= cap} | {cap})
     rates = {}
     best = None
     for c in counts:
         # ~12.5K pairs per thread (>= 0.1 s per run at ~0.1 M pairs/s/thread), at most the batch
-        S = min(len(pairs), max(200_000, 12_500 * c))
+        S = min(len(pairs), max(50_000, 12_500 * c))
         out = pairs[:S].copy()
         r = S / _timed(lambda: oracle.sse41_get_scores16(P, out, ref, qer, w, c), 3) / 1e6
         rates[c] = r
@@ -245,8 +243,8 @@ def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
                               if phys else None),
         "sample": f"first {S} pairs of the rank-0 C2 batch; oracle/bsw_sse41.c (SSE4.1, 8 x int16 "
                   f"lanes, restated upstream getScores16 design, not the upstream binary), {bc} threads "
-                  f"(best of {sorted(counts)} threads: affinity set {cores}, cgroup quota {quota}), "
-                  f"median of 3 after 1 warm-up",
+                  f"(best of {counts} threads: the reference's 1/2/4/8/16 sweep and the cgroup quota "
+                  f"{quota}; affinity set {cores}), median of 3 after 1 warm-up each",
         "host": host,
         "sse41_by_threads": {str(c): round(r, 4) for c, r in sorted(rates.items())},
         "sse41_1thread": round(sse_1t, 4), "scalar_ksw_extend2_1thread": round(scalar_1t, 4),

@@ -49,6 +49,11 @@ struct FmiDevT {                     // kernel view of the resident index (U = r
     const uint8_t *text;
     const U *sa;
     const U *isa;
+    // k-mer interval table (null / kt = 0: off): the exact (k, l, s) of every string of 1 .. kt
+    // bases, level j at ktab + (4^j - 4) / 3, code = the bases as a base-4 number (first base most
+    // significant); 16 B per entry (ktab_get)
+    const uint4 *ktab;
+    int kt;
 };
 
 // text-mode interval entries keep the occurrence's text position in k; their end carries this
@@ -153,6 +158,30 @@ __device__ __forceinline__ IvT<U> set_intv(const FmiDevT<U> &f, int c)
     return IvT<U>{k, l, k1 - k};
 }
 
+// k-mer table entries: x, y, z = the low 32 bits of k, l, s; w = their bits 32..39 (wide index)
+__device__ __forceinline__ uint64_t ktab_off(int len) { return ((1ull << (2 * len)) - 4) / 3; }
+template <class U>
+__device__ __forceinline__ uint4 ktab_pack(IvT<U> v)
+{
+    if constexpr (sizeof(U) == 8)
+        return uint4{(uint32_t)v.k, (uint32_t)v.l, (uint32_t)v.s,
+                     (uint32_t)((v.k >> 32) & 0xff) | (uint32_t)((v.l >> 32) & 0xff) << 8 |
+                         (uint32_t)((v.s >> 32) & 0xff) << 16};
+    else
+        return uint4{v.k, v.l, v.s, 0u};
+}
+// the interval of the len-base string with base-4 code `code` (1 <= len <= f.kt)
+template <class U>
+__device__ __forceinline__ IvT<U> ktab_get(const FmiDevT<U> &f, int len, uint64_t code)
+{
+    const uint4 e = f.ktab[ktab_off(len) + code];
+    if constexpr (sizeof(U) == 8)
+        return IvT<U>{(uint64_t)e.x | (uint64_t)(e.w & 0xff) << 32, (uint64_t)e.y | (uint64_t)((e.w >> 8) & 0xff) << 32,
+                      (uint64_t)e.z | (uint64_t)((e.w >> 16) & 0xff) << 32};
+    else
+        return IvT<U>{e.x, e.y, e.z};
+}
+
 // 4 bytes at p (any alignment) from aligned dword loads; p .. p + 7 must be readable
 __device__ __forceinline__ uint32_t load4u(const uint8_t *p)
 {
@@ -186,6 +215,70 @@ __device__ __forceinline__ IvT<U> text_intv(const FmiDevT<U> &f, U p, int len)
 
 // ---------------------------------------------------------------- device: per-read passes
 
+#ifndef BSW_SMEM_KPF
+#define BSW_SMEM_KPF 1           // 0: the forward walks issue each table load when they need it
+#endif
+
+// The first 16 bases of q[x, len) in registers, and a two-deep pipeline of k-mer table loads over
+// its N-free prefix: a forward walk's first steps (one per base, each waiting on its own load)
+// then wait on a load issued two steps earlier -- the table loads depend on the read alone.  The
+// read's bases come from registers too, since waiting on a byte load of the read would also wait
+// for every older load (the memory counter is in order).
+template <class U>
+struct KPre {
+    uint32_t pw;                 // q[x + t] & 3 in bits 31 - 2t .. 30 - 2t
+    uint32_t nm;                 // bit t: q[x + t] is N, or x + t >= len
+    int P;                       // lengths 1 .. P are table-served: N-free, <= kt
+    int m;                       // the length the next take() returns
+    uint4 e0, e1;                // entries of lengths m, m + 1
+    __device__ __forceinline__ int base(int t) const { return (nm >> t & 1) ? 4 : (int)(pw >> (30 - 2 * t) & 3); }
+    __device__ __forceinline__ uint4 load(const FmiDevT<U> &f, int len) const
+    {
+        return len <= P ? f.ktab[ktab_off(len) + (pw >> (32 - 2 * len))] : uint4{0, 0, 0, 0};
+    }
+    __device__ __forceinline__ void init(const FmiDevT<U> &f, const uint8_t *q, int x, int len)
+    {
+        const int nb = min(16, len - x);                         // >= 1
+        const uintptr_t a = (uintptr_t)(q + x);
+        const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const int nd = (int)(sh + nb + 3) >> 2;                  // aligned dwords holding a read byte
+        uint32_t d[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) d[k] = k < nd ? w[k] : 0xFFFFFFFFu;   // never past a read byte's page
+        pw = 0;
+        nm = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t r = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);   // q[x + 4j, + 4)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int t = 4 * j + b;
+                const uint32_t c = r >> (8 * b) & 0xff;
+                nm |= (uint32_t)(t >= nb || c > 3) << t;
+                pw |= (c & 3) << (30 - 2 * t);
+            }
+        }
+        P = min(f.kt, (int)__builtin_ctz(nm | 0x10000u));
+        m = 2;
+        e0 = load(f, 2);
+        e1 = load(f, 3);
+    }
+    // the interval of q[x, x + m) (m <= P), then m + 1
+    __device__ __forceinline__ IvT<U> take(const FmiDevT<U> &f)
+    {
+        const uint4 e = e0;
+        e0 = e1;
+        e1 = load(f, m + 2);
+        ++m;
+        if constexpr (sizeof(U) == 8)
+            return IvT<U>{(uint64_t)e.x | (uint64_t)(e.w & 0xff) << 32, (uint64_t)e.y | (uint64_t)((e.w >> 8) & 0xff) << 32,
+                          (uint64_t)e.z | (uint64_t)((e.w >> 16) & 0xff) << 32};
+        else
+            return IvT<U>{e.x, e.y, e.z};
+    }
+};
+
 template <class U>
 struct alignas(16) EntT {            // one interval-vector entry: (k, l, s) and the match end
     U k, l, s, e;
@@ -218,8 +311,17 @@ __device__ __forceinline__ void push_out(Lane<U> &L, IvT<U> v, uint32_t start, u
 
 // bwt_smem1a with max_intv = 0 (bwt_smem1): SMEMs overlapping x with occurrence >= min_intv;
 // those of length >= keep_len go to the output.  Returns the next x.
+//
+// prune (the re-seeding pass, whose return value is unused): every interval the backward sweep
+// could output is a substring q[b, e) with >= min_intv occurrences that contains x, so its suffix
+// q[x, e) and its prefix q[b, x] have >= min_intv occurrences too (occurrences only shrink as a
+// string grows): e <= e_max, the forward reach the forward phase has just found, and b >= b_min,
+// the backward reach of the single base q[x].  When e_max - b_min < keep_len nothing can be
+// output and the sweep (~8x the forward phase's block loads on a genome: every entry extended
+// until its count drops) is skipped -- outputs identical by construction (re-seeding of unique
+// SMEMs on a large genome almost never finds a >= 19-base repeat).
 template <class U>
-__device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int keep_len)
+__device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int keep_len, bool prune = false)
 {
     const uint8_t *q = L.q;
     const int len = L.len;
@@ -232,6 +334,15 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
     U ikend = (U)(x + 1);
     int nc = 0, i;
     const bool text = f.text && min_intv <= 1;
+#if BSW_SMEM_KPF
+    KPre<U> pre;
+    pre.init(f, q, x, len);
+    uint64_t win = (uint64_t)pre.pw << 32;              // q[x, x + 16), q[x] in bits 63:62 (the sweep)
+#else
+    // q[x, i) as a base-4 code (table lookups while i + 1 - x <= kt) and as a 2-bit window with
+    // q[x] in bits 63:62 (the backward sweep's table lookups)
+    uint64_t code = (uint64_t)qx, win = (uint64_t)qx << 62;
+#endif
     for (i = x + 1; i < len; ++i) {                      // forward search
         if (text && ik.s == 1) {
             // one occurrence left: every further step keeps s = 1 while the read matches the
@@ -250,9 +361,17 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
             i = e;
             break;
         }
+#if BSW_SMEM_KPF
+        const int qi = i - x < 16 ? pre.base(i - x) : q[i];
+        if (qi < 4) {
+            const IvT<U> ok = i + 1 - x <= pre.P ? pre.take(f) : forward_ext(f, ik, qi);
+#else
         const int qi = q[i];
         if (qi < 4) {
-            const IvT<U> ok = forward_ext(f, ik, qi);
+            code = code << 2 | (uint64_t)qi;
+            if (i - x < 32) win |= (uint64_t)qi << (62 - 2 * (i - x));
+            const IvT<U> ok = i + 1 - x <= f.kt ? ktab_get(f, i + 1 - x, code) : forward_ext(f, ik, qi);
+#endif
             if (ok.s != ik.s) {
                 if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
                 else L.overflow = 1;
@@ -275,6 +394,24 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
     nc = min(nc, L.scap);
     // upstream reverses curr (longest matches first); here prev is read back to front once
     const int ret = (int)((uint32_t)curr[(size_t)(nc - 1) * st].e & ~kTextFlag);
+    if (prune && ret - x < keep_len) {
+        // b_min: extend q[x] to the left while it keeps >= min_intv occurrences; stop as soon as
+        // the bound reaches keep_len (then the sweep must run)
+        IvT<U> bk = set_intv(f, qx);
+        int b = x;
+        uint64_t bcode = (uint64_t)qx;                   // q[b, x] as a base-4 code
+        while (b > 0 && ret - b < keep_len) {
+            const int c = q[b - 1];
+            if (c > 3) break;
+            const int m = x + 2 - b;                     // length of q[b - 1, x]
+            bcode |= (uint64_t)c << (2 * (m - 1));
+            const IvT<U> ok = m <= f.kt ? ktab_get(f, m, bcode) : backward_ext(f, bk, c);
+            if (ok.s < min_intv) break;
+            bk = ok;
+            --b;
+        }
+        if (ret - b < keep_len) return ret;
+    }
     { EntT<U> *t = curr; curr = prev; prev = t; }
     int np = nc;
     bool rev = true;
@@ -282,6 +419,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
     uint32_t last_start = 0;
     for (i = x - 1; i >= -1; --i) {                      // backward search
         const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+        win = win >> 2 | (uint64_t)(c & 3) << 62;      // q[i, i + 32)
         nc = 0;
         U last_cs = 0;
         // the entries' extensions are independent loads: compute kBackUnroll of them before
@@ -290,8 +428,11 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
         auto ext_of = [&](const EntT<U> &pv) -> IvT<U> {
             IvT<U> ok = {0, 0, 0};
             if (c >= 0) {
+                const int m = (int)((uint32_t)pv.e & ~kTextFlag) - i;   // length of q[i, pe)
                 if ((uint32_t)pv.e & kTextFlag) {           // one occurrence: the base before it
                     if (pv.k > 0 && f.text[pv.k - 1] == (uint8_t)c) ok = IvT<U>{pv.k - 1, 0, 1};
+                } else if (m <= f.kt) {                     // a short string: its table entry
+                    ok = ktab_get(f, m, win >> (64 - 2 * m));
                 } else {
                     ok = backward_ext(f, IvT<U>{pv.k, pv.l, pv.s}, c);
                 }
@@ -354,6 +495,12 @@ __device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U> &L, int x, int min_le
     const int qx = q[x];
     if (qx > 3) return x + 1;
     IvT<U> ik = set_intv(f, qx);
+#if BSW_SMEM_KPF
+    KPre<U> pre;
+    pre.init(f, q, x, L.len);
+#else
+    uint64_t code = (uint64_t)qx;                        // q[x, i) as a base-4 code
+#endif
     for (int i = x + 1; i < L.len; ++i) {
         if (f.text && ik.s == 1 && max_intv > 1) {
             // one occurrence: the walk returns at i* = max(i, x + min_len) (every s is 0 or 1 <
@@ -370,9 +517,16 @@ __device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U> &L, int x, int min_le
                 push_out(L, text_intv(f, p, is + 1 - x), (uint32_t)x, (uint32_t)(is + 1));
             return is + 1;
         }
+#if BSW_SMEM_KPF
+        const int qi = i - x < 16 ? pre.base(i - x) : q[i];
+        if (qi < 4) {
+            const IvT<U> ok = i + 1 - x <= pre.P ? pre.take(f) : forward_ext(f, ik, qi);
+#else
         const int qi = q[i];
         if (qi < 4) {
-            const IvT<U> ok = forward_ext(f, ik, qi);
+            code = code << 2 | (uint64_t)qi;
+            const IvT<U> ok = i + 1 - x <= f.kt ? ktab_get(f, i + 1 - x, code) : forward_ext(f, ik, qi);
+#endif
             if (ok.s < max_intv && i - x >= min_len) {
                 if (ok.s > 0) push_out(L, ok, (uint32_t)x, (uint32_t)(i + 1));
                 return i + 1;
@@ -432,7 +586,7 @@ __device__ int smem_read(const FmiDevT<U> &f, const MemOpt &opt, const uint8_t *
         const bsw_bwtintv_t p = L.out[k];
         const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
         if (end - start < opt.split_len || p.x[2] > (uint64_t)opt.split_width) continue;
-        smem1(f, L, (start + end) >> 1, (U)(p.x[2] + 1), opt.min_seed_len);
+        smem1(f, L, (start + end) >> 1, (U)(p.x[2] + 1), opt.min_seed_len, true);
     }
     // pass 3: LAST-like seeds
     if (opt.max_mem_intv > 0) {
@@ -483,6 +637,32 @@ __global__ BSW_SMEM_LB void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
     if (t >= n) return;
     const int e = smem_read(f, opt, reads, read_off, read_len, n0, n, t, scratch, scap, mems, cap, n_mems);
     if (e) atomicOr(err, e);
+}
+
+// one level of the k-mer interval table: level 1 from the counts, level j > 1 by extending every
+// level-(j - 1) entry backward by its first base (a string's interval is unique, so this equals
+// what the walks compute step by step); grid-stride (an AQL grid is 32-bit)
+template <class U>
+__global__ void ktab_kernel(const FmiDevT<U> f, int j, uint4 *__restrict__ tab)
+{
+    const uint64_t cnt = 1ull << (2 * j), o = ktab_off(j);
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += (uint64_t)gridDim.x * blockDim.x) {
+        IvT<U> v;
+        if (j == 1) {
+            v = set_intv(f, (int)c);
+        } else {
+            const uint64_t rest = c & ((1ull << (2 * (j - 1))) - 1);
+            const uint4 e = tab[ktab_off(j - 1) + rest];
+            IvT<U> p;
+            if constexpr (sizeof(U) == 8)
+                p = IvT<U>{(uint64_t)e.x | (uint64_t)(e.w & 0xff) << 32, (uint64_t)e.y | (uint64_t)((e.w >> 8) & 0xff) << 32,
+                           (uint64_t)e.z | (uint64_t)((e.w >> 16) & 0xff) << 32};
+            else
+                p = IvT<U>{e.x, e.y, e.z};
+            v = backward_ext(f, p, (int)(c >> (2 * (j - 1))));
+        }
+        tab[o + c] = ktab_pack(v);
+    }
 }
 
 template <class S>
@@ -585,6 +765,8 @@ struct bsw_fmi {
     uint8_t *d_bwt = nullptr;                 // GPU-built index: BWT codes (copy_bwt)
     uint8_t *d_text = nullptr;                // text mode: T + 64 bytes of 0xFF padding
     void *d_isa = nullptr;                    // text mode: SA^-1 (uint32_t or uint64_t)
+    uint4 *d_ktab = nullptr;                  // k-mer interval table (levels 1 .. kt)
+    int kt = 0;
     std::vector<uint32_t> sa;                 // host-built index: host copies (tests, bwt_sa)
     std::vector<FmiBlock> h_blk;              // host-only index (device < 0): the occurrence blocks
     std::vector<uint8_t> bwt;
@@ -723,6 +905,41 @@ int attach_text(bsw_fmi_t *f, const uint8_t *ref, int64_t len)
     return BSW_OK;
 }
 
+// The k-mer interval table's depth: floor(log4 |T|) - 1 levels (strings that short still occur
+// ~4+ times, so the walks would spend their loads on them), at most 13 (1.4 GB of 16-B entries);
+// BSW_FMI_KTAB=<levels> overrides (0: off)
+int ktab_levels(int64_t n)
+{
+    int lg = 0;
+    while (lg < 31 && ((int64_t)1 << (2 * (lg + 1))) <= n) ++lg;
+    int kt = std::min(13, lg - 1);
+    if (const char *e = getenv("BSW_FMI_KTAB")) kt = std::min(14, atoi(e));
+    return std::max(0, kt);
+}
+
+template <class U>
+int build_ktab(bsw_fmi_t *f, FmiDevT<U> &dv)
+{
+    const int kt = ktab_levels(f->n);
+    if (kt <= 0) return BSW_OK;
+    const size_t ents = (size_t)(((1ull << (2 * (kt + 1))) - 4) / 3);   // levels 1 .. kt
+    int rc = hip_rc(hipMalloc(&f->d_ktab, ents * sizeof(uint4)));
+    if (rc) return rc;
+    for (int j = 1; j <= kt && !rc; ++j) {
+        const uint64_t cnt = 1ull << (2 * j);
+        const unsigned grid = (unsigned)std::min<uint64_t>(1u << 16, (cnt + 255) / 256);
+        hipLaunchKernelGGL(ktab_kernel<U>, dim3(grid), dim3(256), 0, f->stream, dv, j, f->d_ktab);
+        rc = hip_rc(hipGetLastError());
+    }
+    if (!rc) rc = hip_rc(hipStreamSynchronize(f->stream));
+    if (rc) return rc;
+    dv.ktab = f->d_ktab;
+    dv.kt = kt;
+    f->kt = kt;
+    f->dev_bytes += (int64_t)(ents * sizeof(uint4));
+    return BSW_OK;
+}
+
 int finish_device_index(bsw_fmi_t *f)
 {
     int rc = BSW_OK;
@@ -790,6 +1007,7 @@ int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, b
         f->build_s = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
         int r2 = finish_device_index(f);
         if (!r2 && text) r2 = attach_text(f, ref, ref_len);
+        if (!r2) r2 = wide ? build_ktab(f, f->dv64) : build_ktab(f, f->dv32);
         if (r2) { bsw_fmi_destroy(f); return r2; }
         f->build_s = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
         *out = f;
@@ -847,7 +1065,7 @@ int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, b
         (rc = hip_rc(hipMemcpy(f->d_sa, f->sa.data(), (size_t)N * sizeof(uint32_t), hipMemcpyHostToDevice))) == BSW_OK &&
         (rc = finish_device_index(f)) == BSW_OK) {
         f->dev_bytes = (int64_t)(nb * sizeof(FmiBlock) + (size_t)N * sizeof(uint32_t));
-        if (!text || (rc = attach_text(f, ref, ref_len)) == BSW_OK) {
+        if ((!text || (rc = attach_text(f, ref, ref_len)) == BSW_OK) && (rc = build_ktab(f, f->dv32)) == BSW_OK) {
             *out = f;
             return BSW_OK;
         }
@@ -870,6 +1088,7 @@ void bsw_fmi_destroy(bsw_fmi_t *f)
     if (f->d_bwt) (void)hipFree(f->d_bwt);
     if (f->d_text) (void)hipFree(f->d_text);
     if (f->d_isa) (void)hipFree(f->d_isa);
+    if (f->d_ktab) (void)hipFree(f->d_ktab);
     if (f->d_err) (void)hipFree(f->d_err);
     if (f->d_scratch) (void)hipFree(f->d_scratch);
     if (f->ev0) (void)hipEventDestroy(f->ev0);

@@ -45,6 +45,7 @@ GQ_OP2(pmax, "v_pk_max_i16")
 GQ_OP2(pmin, "v_pk_min_i16")
 GQ_OP2(padd, "v_pk_add_u16")
 GQ_OP2(psub, "v_pk_sub_i16")
+GQ_OP2(pmaxu, "v_pk_max_u16")
 #undef GQ_OP2
 
 // {a.lo, max(a.lo, a.hi)}: two-column inclusive prefix inside one register
@@ -245,8 +246,12 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
     // and the key).  RM: some live pair's band ends before qlen, so writes stop at slot end and E(end)
     // = 0 (A.7 stale columns); without it every pair's end is qlen and slots past qlen are never
     // read, so the row writes unmasked and finds H(i, qlen - 1) at a fixed place.
-    auto row = [&](auto LMc, auto RMc) {
-        constexpr bool LM = decltype(LMc)::value, RM = decltype(RMc)::value;
+    // K8 (every pair of the wave has H <= h0 + min(qlen, tlen) <= 255): the row-max key as two
+    // 16-bit halves H << 8 | j per register (one v_perm + one v_pk_max_u16) instead of two 32-bit
+    // keys H << 16 | j (two v_perm + two v_max); folded to one 32-bit key before the group
+    // reduction, same last-column tie rule
+    auto row = [&](auto LMc, auto RMc, auto K8c) {
+        constexpr bool LM = decltype(LMc)::value, RM = decltype(RMc)::value, K8 = decltype(K8c)::value;
         const uint2 prn = s_prof[min((int)tb8[min(i + 1, tlen - 1)], 7)];
         const int beg = max(0, i - wl);
         const int end = min(min(endc, i + wl + 1), qlen);
@@ -324,12 +329,16 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
                 hsel = qr == r ? hcur[r] : hsel;
             }
             const uint32_t hm = LM ? (hcur[r] & lt[r] & ~lm[r]) : (hcur[r] & lt[r]);
-            key = max(key, max(__builtin_amdgcn_perm(hm, jj[r], 0x05040100u),     // H.lo << 16 | j
-                               __builtin_amdgcn_perm(hm, jj[r], 0x07060302u)));   // H.hi << 16 | j+1
+            if constexpr (K8)
+                key = pmaxu(key, __builtin_amdgcn_perm(hm, jj[r], 0x06020400u));    // {H << 8 | j} x 2
+            else
+                key = max(key, max(__builtin_amdgcn_perm(hm, jj[r], 0x05040100u),     // H.lo << 16 | j
+                                   __builtin_amdgcn_perm(hm, jj[r], 0x07060302u)));   // H.hi << 16 | j+1
         }
         if constexpr (!RM) hq_c = qr >= 0 ? (hsel >> qsh) & 0xffffu : 0u;
+        if constexpr (K8) key = max(key & 0xffffu, key >> 16);
         const uint32_t kmax = grp_max_u32<GS>(key);
-        const int m = (int)(kmax >> 16), mj = (int)(kmax & 0xffffu);
+        const int m = (int)(kmax >> (K8 ? 8 : 16)), mj = (int)(kmax & (K8 ? 0xffu : 0xffffu));
         int hq = (int)grp_max_u32<GS>(hq_c);                              // H >= 0 in [beg, end)
         hq = end - 1 < beg ? h1b : hq;                                // empty row: h1 = h1b
         // A.4: j == qlen (gscore, max_ie) -- selects, no exec-masked blocks
@@ -363,16 +372,26 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
         endc = min(lp1 + 2, qlen);
         alive = alive && !stop;
     };
-    for (;; ++i) {
-        const bool live = alive && i < tlen;
-        if (!__builtin_amdgcn_ballot_w64(live)) break;
-        // wave-uniform row forms (the masks only where some live pair needs them)
-        const bool need_lm = __builtin_amdgcn_ballot_w64(live && i - wl > 0) != 0;
-        const bool need_rm = __builtin_amdgcn_ballot_w64(live && min(min(endc, i + wl + 1), qlen) != qlen) != 0;
-        if (!live) continue;
-        if (need_rm) row(std::true_type{}, std::true_type{});
-        else if (need_lm) row(std::true_type{}, std::false_type{});
-        else row(std::false_type{}, std::false_type{});
+    const bool k8 = __builtin_amdgcn_ballot_w64(alive && h0 + min(qlen, tlen) > 255) == 0;
+    auto rows = [&](auto K8c) {
+        for (;; ++i) {
+            const bool live = alive && i < tlen;
+            if (!__builtin_amdgcn_ballot_w64(live)) break;
+            // wave-uniform row forms (the masks only where some live pair needs them)
+            const bool need_lm = __builtin_amdgcn_ballot_w64(live && i - wl > 0) != 0;
+            const bool need_rm = __builtin_amdgcn_ballot_w64(live && min(min(endc, i + wl + 1), qlen) != qlen) != 0;
+            if (!live) continue;
+            if (need_rm) row(std::true_type{}, std::true_type{}, K8c);
+            else if (need_lm) row(std::true_type{}, std::false_type{}, K8c);
+            else row(std::false_type{}, std::false_type{}, K8c);
+        }
+    };
+    if constexpr (GS == 16) {         // (the quad form keeps one path: its registers are the limit)
+        if (k8) rows(std::true_type{});
+        else rows(std::false_type{});
+    } else {
+        (void)k8;
+        rows(std::false_type{});
     }
     if (idx >= 0 && gl == 0) {
         if (out24) {

@@ -1164,47 +1164,12 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         pend_n[k] = 0;
         return BSW_OK;
     };
-    double stage_ms = 0;
-    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;     // per-chunk host timeline (A/B tooling)
-    auto ms_since = [&](std::chrono::steady_clock::time_point t) {
-        return std::chrono::duration<double, std::milli>(t - t_start).count();
-    };
-    rc = [&]() -> int {
-        BSW_TRY(hipSetDevice(dc.device));
-        int k = 0;
-        int32_t seq = 0;
-        const int32_t nblk = (int32_t)bs.size();
-        const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
-        // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
-        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
-        for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 2)) {
-            // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
-            int64_t bytes = 0;
-            for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
-                const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
-                if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
-                bytes += x;
-            }
-            // (a small remainder stays its own chunk: folded into the last full chunk it added a
-            // third, nearly empty generation of waves to that launch -- 262144 pairs are exactly
-            // two generations at two waves per SIMD -- and the call got ~1 ms slower; as its own
-            // launch it runs beside the last chunk on another queue.  Measured, DESIGN.md §6)
-            const int32_t a = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a;
-            const auto tw = now();
-            int r = finish(k);                          // slot k's last chunk
-            if (r) return r;
-            if (!slots[k]) {
-                slots[k] = dc.acquire(r);
-                if (r) return r;
-            }
-            Slot &s = *slots[k];
-            StagedChunk c;
-            const auto t0 = now();
-            if ((r = stage_chunk(s, pairs + a, ref, qer, m, bs.data() + b, nb, two_bit, c))) return r;
-            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
-            if (dbg)
-                fprintf(stderr, "hp chunk %d: %d pairs  finish-wait %.3f..%.3f  stage %.3f..%.3f ms\n", (int)seq, (int)m,
-                        ms_since(tw), ms_since(t0), ms_since(t0), ms_since(now()));
+    // the device side of one staged chunk -- H2D of the slot's staging buffer, unpack kernels,
+    // plan / sort -- then its launcher job.  On a failure the job still goes to the launcher,
+    // which skips its DP and releases finish(k) with the error
+    auto enqueue = [&](int k, int32_t seq, const StagedChunk &c, int32_t m) -> int {
+        Slot &s = *slots[k];
+        const int r = [&]() -> int {
             BSW_TRY(grow(s.d_stage, s.cap_dstage, c.bytes));
             BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.bytes, hipMemcpyHostToDevice, s.stream));
             const uint8_t *d_r = s.d_stage + c.ref_off, *d_q = s.d_stage + c.qer_off;
@@ -1254,13 +1219,114 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
             pc.d_ref = d_r - c.r_base;
             pc.d_qer = d_q - c.q_base;
             pc.n = m; pc.w = w; pc.cell_bits = cell_bits; pc.stream = s.stream;
-            if ((r = run_plan(kp, s, pc))) return r;
-            pend_at[k] = a; pend_n[k] = m; pend_mode[k] = c.mode; pend_seq[k] = seq;
-            {
-                std::lock_guard<std::mutex> g(L.mu);
-                L.q.push_back(Launcher::Job{k, seq, c.mode});
+            return run_plan(kp, s, pc);
+        }();
+        {
+            std::lock_guard<std::mutex> g(L.mu);
+            if (r && !L.rc) L.rc = r;
+            L.q.push_back(Launcher::Job{k, seq, c.mode});
+        }
+        L.cv.notify_all();
+        return r;
+    };
+    // Calls of several chunks hand each staged chunk to an enqueuer thread, so the calling thread
+    // stages the next chunk at once: the enqueue of a chunk (H2D, unpack, plan, sort -- ~0.9 ms
+    // of runtime calls per 256K-pair chunk in the kernel + copy trace) otherwise sat between two
+    // stagings and made the next chunk's DP start after the current one had drained
+    // (profiles/r04/hostpath_trace_*.txt).  One-chunk calls enqueue inline (no thread hand-off).
+    struct EnqJob { int k; int32_t seq; StagedChunk c; int32_t m; };
+    struct Enqueuer {
+        std::mutex mu;
+        std::condition_variable cv;
+        std::deque<EnqJob> q;
+        bool stop = false;
+    } E;
+    const int32_t nblk0 = (int32_t)bs.size();
+    const int32_t first_blk = std::min(std::max<int32_t>(1, chunk / kStageBlk),
+                                       nblk0 <= 32 ? nblk0 : std::max<int32_t>(16, nblk0 / 32));
+    const bool async = nblk0 > first_blk && getenv("BSW_HP_INLINE_ENQ") == nullptr;
+    std::thread enqueuer;
+    if (async)
+        enqueuer = std::thread([&] {
+            const bool dev_ok = hipSetDevice(dc.device) == hipSuccess;
+            for (;;) {
+                EnqJob job;
+                {
+                    std::unique_lock<std::mutex> lk(E.mu);
+                    E.cv.wait(lk, [&] { return E.stop || !E.q.empty(); });
+                    if (E.q.empty()) return;
+                    job = E.q.front();
+                    E.q.pop_front();
+                }
+                if (!dev_ok) {
+                    std::lock_guard<std::mutex> g(L.mu);
+                    if (!L.rc) L.rc = BSW_E_HIP;
+                    L.q.push_back(Launcher::Job{job.k, job.seq, job.c.mode});
+                    L.cv.notify_all();
+                    continue;
+                }
+                (void)enqueue(job.k, job.seq, job.c, job.m);
             }
-            L.cv.notify_all();
+        });
+    auto stop_enqueuer = [&] {
+        {
+            std::lock_guard<std::mutex> g(E.mu);
+            E.stop = true;
+        }
+        E.cv.notify_all();
+        if (enqueuer.joinable()) enqueuer.join();
+    };
+    double stage_ms = 0;
+    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;     // per-chunk host timeline (A/B tooling)
+    auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(t - t_start).count();
+    };
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        int k = 0;
+        int32_t seq = 0;
+        const int32_t nblk = (int32_t)bs.size();
+        const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
+        // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
+        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
+        for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 2)) {
+            // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
+            int64_t bytes = 0;
+            for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
+                const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
+                if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
+                bytes += x;
+            }
+            // (a small remainder stays its own chunk: folded into the last full chunk it added a
+            // third, nearly empty generation of waves to that launch -- 262144 pairs are exactly
+            // two generations at two waves per SIMD -- and the call got ~1 ms slower; as its own
+            // launch it runs beside the last chunk on another queue.  Measured, DESIGN.md §6)
+            const int32_t a = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a;
+            const auto tw = now();
+            int r = finish(k);                          // slot k's last chunk
+            if (r) return r;
+            if (!slots[k]) {
+                slots[k] = dc.acquire(r);
+                if (r) return r;
+            }
+            Slot &s = *slots[k];
+            StagedChunk c;
+            const auto t0 = now();
+            if ((r = stage_chunk(s, pairs + a, ref, qer, m, bs.data() + b, nb, two_bit, c))) return r;
+            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
+            if (dbg)
+                fprintf(stderr, "hp chunk %d: %d pairs  finish-wait %.3f..%.3f  stage %.3f..%.3f ms\n", (int)seq, (int)m,
+                        ms_since(tw), ms_since(t0), ms_since(t0), ms_since(now()));
+            pend_at[k] = a; pend_n[k] = m; pend_mode[k] = c.mode; pend_seq[k] = seq;
+            if (async) {
+                {
+                    std::lock_guard<std::mutex> g(E.mu);
+                    E.q.push_back(EnqJob{k, seq, c, m});
+                }
+                E.cv.notify_all();
+            } else if ((r = enqueue(k, seq, c, m))) {
+                return r;
+            }
         }
         for (int j = 0; j < nslots; ++j) {
             const int r = finish(j);
@@ -1269,6 +1335,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         if (dbg) fprintf(stderr, "hp drained at %.3f ms\n", ms_since(now()));
         return BSW_OK;
     }();
+    stop_enqueuer();                                    // drains its queue first (every job reaches the launcher)
     stop_launcher();                                    // drains the queue first (it exits only when empty)
     agg.stage_ms = (float)stage_ms;
     agg.host_ms = (float)std::chrono::duration<double, std::milli>(now() - t_start).count();

@@ -232,6 +232,19 @@ void oracle_fmi_counters(uint64_t *out, int reset)
     out[1] = __atomic_load_n(&g_block_loads, __ATOMIC_RELAXED);
     if (reset) { g_ext_calls = 0; g_block_loads = 0; }
 }
+/* the same split by seeding phase (0 pass-1 forward, 1 pass-1 backward sweep, 2 / 3 pass-2
+ * forward / backward, 4 pass 3): [phase][0] extensions, [1] those of an interval with s >= 2 (the
+ * GPU kernel's text mode serves s = 1 from the text), [2] block loads of the s >= 2 ones */
+static __thread int g_phase;
+static uint64_t g_ph[5][3];
+void oracle_fmi_phase_counters(uint64_t *out15, int reset)
+{
+    for (int p = 0; p < 5; ++p)
+        for (int k = 0; k < 3; ++k) {
+            out15[3 * p + k] = __atomic_load_n(&g_ph[p][k], __ATOMIC_RELAXED);
+            if (reset) g_ph[p][k] = 0;
+        }
+}
 
 /* bwa-mem2 FMI_search::backwardExt: interval (k, l, s) of string X -> that of aX */
 static void backward_ext(const fmi_ref_t *f, const uint64_t in[3], int a, uint64_t out[3])
@@ -240,6 +253,11 @@ static void backward_ext(const fmi_ref_t *f, const uint64_t in[3], int a, uint64
     int64_t sp = (int64_t)in[0], ep = (int64_t)in[0] + (int64_t)in[2];
     __atomic_fetch_add(&g_ext_calls, 1, __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_block_loads, (sp >> 6) == (ep >> 6) ? 1 : 2, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_ph[g_phase][0], 1, __ATOMIC_RELAXED);
+    if (in[2] >= 2) {
+        __atomic_fetch_add(&g_ph[g_phase][1], 1, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&g_ph[g_phase][2], (sp >> 6) == (ep >> 6) ? 1 : 2, __ATOMIC_RELAXED);
+    }
     for (int b = 0; b < 4; ++b) {
         k[b] = f->count[b] + occ(f, b, sp);
         s[b] = occ(f, b, ep) - occ(f, b, sp);
@@ -320,6 +338,7 @@ static int smem1a(const fmi_ref_t *f, int len, const uint8_t *q, int x, int min_
         }
     }
     if (i == len) ipush(curr, &ik);
+    g_phase |= 1;
     ireverse(curr);
     ret = (int)(uint32_t)curr->a[0].info;
     swap = curr; curr = prev; prev = swap;
@@ -344,6 +363,7 @@ static int smem1a(const fmi_ref_t *f, int len, const uint8_t *q, int x, int min_
         swap = curr; curr = prev; prev = swap;
     }
     ireverse(mem);
+    g_phase &= ~1;
     return ret;
 }
 
@@ -397,6 +417,7 @@ int oracle_collect_intv(const fmi_ref_t *f, const oracle_mem_opt_t *opt, const u
     int i, k, x = 0, old_n;
     int split_len = (int)(opt->min_seed_len * opt->split_factor + .499);
     ivec_t mem = {0, 0, 0}, mem1 = {0, 0, 0}, t0 = {0, 0, 0}, t1 = {0, 0, 0};
+    g_phase = 0;
     while (x < len) {                                         /* first pass: SMEMs */
         if (seq[x] < 4) {
             x = smem1a(f, len, seq, x, 1, 0, &mem1, &t0, &t1);
@@ -410,6 +431,7 @@ int oracle_collect_intv(const fmi_ref_t *f, const oracle_mem_opt_t *opt, const u
         }
     }
     old_n = (int)mem.n;                                       /* second pass: re-seeding */
+    g_phase = 2;
     for (k = 0; k < old_n; ++k) {
         ref_intv_t p = mem.a[k];
         int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
@@ -419,6 +441,7 @@ int oracle_collect_intv(const fmi_ref_t *f, const oracle_mem_opt_t *opt, const u
             if ((int)((uint32_t)mem1.a[i].info - (mem1.a[i].info >> 32)) >= opt->min_seed_len)
                 ipush(&mem, &mem1.a[i]);
     }
+    g_phase = 4;
     if (opt->max_mem_intv > 0) {                              /* third pass: LAST-like */
         x = 0;
         while (x < len) {

@@ -269,6 +269,26 @@ def test_gpu_collect_intv_edges(flags):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("levels", [0, 1, 5, 12])
+@pytest.mark.parametrize("flags", [None, bsw.FMI_GPU_BUILD | bsw.FMI_WIDE], ids=["narrow", "wide"])
+def test_gpu_kmer_table_depths_equal_oracle(levels, flags, monkeypatch):
+    """The k-mer interval table (BSW_FMI_KTAB levels; 0 = off, 12 = far past log4 |T| on this
+    reference, so most deep entries are empty intervals) serves the short strings of every walk:
+    pass-1 / pass-2 forward, the backward sweeps, the re-seeding bound, pass 3.  Outputs == the
+    oracle at every depth, narrow and wide, with long runs and an N-rich read set."""
+    monkeypatch.setenv("BSW_FMI_KTAB", str(levels))
+    ref = _long_runs_ref(60_000, 11)
+    reads, off, lens = sample_reads(ref, 2500, 151, 13, p_n=0.01)
+    o = oracle.FmiRef(ref)
+    f = bsw.Fmi(ref, flags=flags)
+    for opt in (dict(), dict(min_seed_len=11, split_width=50), dict(max_mem_intv=0)):
+        o_out, o_cnt = o.collect_intv(reads, off, lens, cap=512, opt=oracle.mem_opt(**opt), nthreads=8)
+        g_out, g_cnt = f.collect_intv(reads, off, lens, cap=512, opt=bsw.mem_opt(**opt))
+        _compare(o_out, o_cnt, g_out, g_cnt)
+    f.close()
+
+
+@pytest.mark.gpu
 def test_gpu_device_api_and_sa_lookup():
     import hiprt
     ref = np.random.default_rng(6).integers(0, 4, 100_000, dtype=np.uint8)
