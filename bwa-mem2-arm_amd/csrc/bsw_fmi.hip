@@ -913,7 +913,7 @@ int ktab_levels(int64_t n)
     int lg = 0;
     while (lg < 31 && ((int64_t)1 << (2 * (lg + 1))) <= n) ++lg;
     int kt = std::min(13, lg - 1);
-    if (const char *e = getenv("BSW_FMI_KTAB")) kt = std::min(14, atoi(e));
+    if (const char *e = getenv("BSW_FMI_KTAB")) kt = std::min(15, atoi(e));
     return std::max(0, kt);
 }
 
