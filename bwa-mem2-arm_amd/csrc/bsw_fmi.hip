@@ -906,13 +906,14 @@ int attach_text(bsw_fmi_t *f, const uint8_t *ref, int64_t len)
 }
 
 // The k-mer interval table's depth: floor(log4 |T|) - 1 levels (strings that short still occur
-// ~4+ times, so the walks would spend their loads on them), at most 13 (1.4 GB of 16-B entries);
-// BSW_FMI_KTAB=<levels> overrides (0: off)
+// ~4+ times, so the walks would spend their loads on them), at most 15 (22.9 GB of 16-B entries,
+// a 3 Gb genome's depth; 13 / 14 / 15 levels measured 314 / 290 / 283 ms of SMEM kernel per 10M
+// C4 reads, profiles/r04/ab_smem_ktab.txt); BSW_FMI_KTAB=<levels> overrides (0: off)
 int ktab_levels(int64_t n)
 {
     int lg = 0;
     while (lg < 31 && ((int64_t)1 << (2 * (lg + 1))) <= n) ++lg;
-    int kt = std::min(13, lg - 1);
+    int kt = std::min(15, lg - 1);
     if (const char *e = getenv("BSW_FMI_KTAB")) kt = std::min(15, atoi(e));
     return std::max(0, kt);
 }

@@ -27,7 +27,9 @@ mkdir -p "$O"
 export TMPDIR=/tmp
 fail() { echo "step $1 FAILED (rc $2); log tail:"; tail -30 "$3"; exit 1; }
 sp() { echo "${1//,/ }"; }
+n=0
 for step in "$@"; do
+    n=$((n + 1))
     kind=${step%%:*}; arg=""; [[ "$step" == *:* ]] && arg=${step#*:}
     t0=$(date +%s)
     case "$kind" in
@@ -42,7 +44,7 @@ for step in "$@"; do
         timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 || fail "$step" $? "$log"
         tail -3 "$log" ;;
     bench)
-        log=$O/bench${arg:+_$(echo "$arg" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-60)}.log
+        log=$O/bench${arg:+_$(echo "$arg" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-60)}_$n.log
         timeout -k 10 600 python bench.py $(sp "$arg") > "$log" 2>&1 || fail "$step" $? "$log"
         tail -1 "$log" | cut -c1-1500 ;;
     prof)
@@ -60,7 +62,7 @@ for step in "$@"; do
         [ $rc -eq 0 ] || fail "$step" $rc "$log"
         grep '^{' "$log" | cut -c1-600 ;;
     percall)
-        log=$O/percall.log
+        log=$O/percall_$n.log
         timeout -k 10 300 bwa-mem2-arm_amd/lib/percall_bench $(sp "$arg") > "$log" 2>&1 || fail "$step" $? "$log"
         tail -1 "$log" | cut -c1-1500 ;;
     ab)
