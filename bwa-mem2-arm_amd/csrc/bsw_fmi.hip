@@ -284,11 +284,37 @@ struct alignas(16) EntT {            // one interval-vector entry: (k, l, s) and
     U k, l, s, e;
 };
 
+// Interval-vector entries in HBM scratch: EntT<U> as is (16 B narrow, 32 B wide), or for the wide
+// index the packed 16-B EntP when k, l < 2^40, s < 2^32 and ends < 2^15 (every realistic genome:
+// a 3 Gb two-strand text has 6e9 rows and single-base counts ~1.8e9; the host checks and falls
+// back to EntT).  The sweeps write and re-read ~20 KB of entries per 150 bp read at 3 Gb (PMC:
+// 20 GB of HBM writes per 1M-read launch), so halving the wide entry halves that traffic.
+struct alignas(16) EntP {
+    uint32_t k, l, s, w;     // w: k bits 32..39, l bits 32..39, e (15 bits + the text flag)
+};
 template <class U>
+__device__ __forceinline__ void ent_put(EntT<U> *p, const EntT<U> &e) { *p = e; }
+template <class U>
+__device__ __forceinline__ EntT<U> ent_get(const EntT<U> *p) { return *p; }
+__device__ __forceinline__ void ent_put(EntP *p, const EntT<uint64_t> &e)
+{
+    const uint32_t ee = (uint32_t)e.e;
+    *reinterpret_cast<uint4 *>(p) = uint4{(uint32_t)e.k, (uint32_t)e.l, (uint32_t)e.s,
+                                          (uint32_t)(e.k >> 32 & 0xff) | (uint32_t)(e.l >> 32 & 0xff) << 8 |
+                                              (ee & 0x7fffu) << 16 | (ee >> 31) << 31};
+}
+__device__ __forceinline__ EntT<uint64_t> ent_get(const EntP *p)
+{
+    const uint4 v = *reinterpret_cast<const uint4 *>(p);
+    return EntT<uint64_t>{(uint64_t)v.x | (uint64_t)(v.w & 0xff) << 32, (uint64_t)v.y | (uint64_t)(v.w >> 8 & 0xff) << 32,
+                          (uint64_t)v.z, (uint64_t)((v.w >> 16 & 0x7fffu) | (v.w >> 31) << 31)};
+}
+
+template <class U, class S = EntT<U>>
 struct Lane {
     const uint8_t *q;
     int len;
-    EntT<U> *sa, *sb;        // scratch vectors, element j at [j * stride]
+    S *sa, *sb;              // scratch vectors, element j at [j * stride]
     size_t stride;
     int scap;                // scratch entries per vector
     bsw_bwtintv_t *out;      // this read's output slots
@@ -297,8 +323,8 @@ struct Lane {
     int overflow;            // scratch overflow (cannot happen for scap >= len + 1)
 };
 
-template <class U>
-__device__ __forceinline__ void push_out(Lane<U> &L, IvT<U> v, uint32_t start, uint32_t end)
+template <class U, class S>
+__device__ __forceinline__ void push_out(Lane<U, S> &L, IvT<U> v, uint32_t start, uint32_t end)
 {
     if (L.nout < L.cap) {
         bsw_bwtintv_t o;
@@ -320,15 +346,15 @@ __device__ __forceinline__ void push_out(Lane<U> &L, IvT<U> v, uint32_t start, u
 // output and the sweep (~8x the forward phase's block loads on a genome: every entry extended
 // until its count drops) is skipped -- outputs identical by construction (re-seeding of unique
 // SMEMs on a large genome almost never finds a >= 19-base repeat).
-template <class U>
-__device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int keep_len, bool prune = false)
+template <class U, class S>
+__device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int keep_len, bool prune = false)
 {
     const uint8_t *q = L.q;
     const int len = L.len;
     const int qx = q[x];
     if (qx > 3) return x + 1;
     if (min_intv < 1) min_intv = 1;
-    EntT<U> *curr = L.sa, *prev = L.sb;
+    S *curr = L.sa, *prev = L.sb;
     const size_t st = L.stride;
     IvT<U> ik = set_intv(f, qx);
     U ikend = (U)(x + 1);
@@ -354,7 +380,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
             ik.k = p;
             ikend = (U)((uint32_t)e | kTextFlag);
             if (e < len) {
-                if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
+                if (nc < L.scap) ent_put(curr + (size_t)nc * st, EntT<U>{ik.k, ik.l, ik.s, ikend});
                 else L.overflow = 1;
                 ++nc;
             }
@@ -373,27 +399,27 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
             const IvT<U> ok = i + 1 - x <= f.kt ? ktab_get(f, i + 1 - x, code) : forward_ext(f, ik, qi);
 #endif
             if (ok.s != ik.s) {
-                if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
+                if (nc < L.scap) ent_put(curr + (size_t)nc * st, EntT<U>{ik.k, ik.l, ik.s, ikend});
                 else L.overflow = 1;
                 ++nc;
                 if (ok.s < min_intv) break;
             }
             ik = ok; ikend = (U)(i + 1);
         } else {
-            if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
+            if (nc < L.scap) ent_put(curr + (size_t)nc * st, EntT<U>{ik.k, ik.l, ik.s, ikend});
             else L.overflow = 1;
             ++nc;
             break;
         }
     }
     if (i == len) {
-        if (nc < L.scap) curr[(size_t)nc * st] = EntT<U>{ik.k, ik.l, ik.s, ikend};
+        if (nc < L.scap) ent_put(curr + (size_t)nc * st, EntT<U>{ik.k, ik.l, ik.s, ikend});
         else L.overflow = 1;
         ++nc;
     }
     nc = min(nc, L.scap);
     // upstream reverses curr (longest matches first); here prev is read back to front once
-    const int ret = (int)((uint32_t)curr[(size_t)(nc - 1) * st].e & ~kTextFlag);
+    const int ret = (int)((uint32_t)ent_get(curr + (size_t)(nc - 1) * st).e & ~kTextFlag);
     if (prune && ret - x < keep_len) {
         // b_min: extend q[x] to the left while it keeps >= min_intv occurrences; stop as soon as
         // the bound reaches keep_len (then the sweep must run)
@@ -412,7 +438,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
         }
         if (ret - b < keep_len) return ret;
     }
-    { EntT<U> *t = curr; curr = prev; prev = t; }
+    { S *t = curr; curr = prev; prev = t; }
     int np = nc;
     bool rev = true;
     int nmem = 0;
@@ -445,7 +471,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
 #pragma unroll
           for (int u = 0; u < kBackUnroll; ++u) {
               const int j = min(j0 + u, np - 1);
-              pvs[u] = prev[(size_t)(rev ? np - 1 - j : j) * st];
+              pvs[u] = ent_get(prev + (size_t)(rev ? np - 1 - j : j) * st);
           }
 #pragma unroll
           for (int u = 0; u < kBackUnroll; ++u) oks[u] = ext_of(pvs[u]);
@@ -472,7 +498,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
                 const bool to_text = f.text && ok.s == 1;
                 const U k2 = tm ? ok.k : (to_text ? f.sa[ok.k] : ok.k);
                 if (nc < L.scap)
-                    curr[(size_t)nc * st] = EntT<U>{k2, ok.l, ok.s, (U)(pe | ((tm || to_text) ? kTextFlag : 0u))};
+                    ent_put(curr + (size_t)nc * st, EntT<U>{k2, ok.l, ok.s, (U)(pe | ((tm || to_text) ? kTextFlag : 0u))});
                 else L.overflow = 1;
                 ++nc;
                 last_cs = ok.s;
@@ -482,14 +508,14 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U> &L, int x, U min_intv, int kee
         if (nc == 0) break;
         np = min(nc, L.scap);
         rev = false;
-        { EntT<U> *t = curr; curr = prev; prev = t; }
+        { S *t = curr; curr = prev; prev = t; }
     }
     return ret;
 }
 
 // bwt_seed_strategy1
-template <class U>
-__device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U> &L, int x, int min_len, U max_intv)
+template <class U, class S>
+__device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U, S> &L, int x, int min_len, U max_intv)
 {
     const uint8_t *q = L.q;
     const int qx = q[x];
@@ -552,14 +578,14 @@ __device__ __forceinline__ bool iv_less(const bsw_bwtintv_t &a, const bsw_bwtint
 // writes them: a per-lane state machine doing one extension per iteration (so that a wave's time
 // is its busiest lane's work instead of the sum of per-phase maxima) measured 1.4x SLOWER (31.9
 // vs 22.1 ms on 1M reads x 16 Mb) -- the bookkeeping transitions cost whole iterations.
-template <class U>
+template <class U, class S>
 __device__ int smem_read(const FmiDevT<U> &f, const MemOpt &opt, const uint8_t *__restrict__ reads,
                          const int64_t *__restrict__ read_off, const int32_t *__restrict__ read_len, int32_t n0,
-                         int32_t n, int t, EntT<U> *__restrict__ scratch, int32_t scap,
+                         int32_t n, int t, S *__restrict__ scratch, int32_t scap,
                          bsw_bwtintv_t *__restrict__ mems, int32_t cap, int32_t *__restrict__ n_mems)
 {
     const int r = n0 + t;                                    // read index
-    Lane<U> L;
+    Lane<U, S> L;
     L.q = reads + read_off[r];
     L.len = read_len[r];
     L.stride = (size_t)n;
@@ -616,7 +642,7 @@ __device__ int smem_read(const FmiDevT<U> &f, const MemOpt &opt, const uint8_t *
 #endif
 constexpr int kSmemBlock = BSW_SMEM_BLOCK;          // threads per workgroup of the SMEM kernel
 
-template <class U>
+template <class U, class S>
 #ifndef BSW_SMEM_WAVES           // experiment builds: a minimum of waves per SIMD for the walk
 #define BSW_SMEM_WAVES 0         // (0 = the compiler's choice: 4 wide / 6 narrow)
 #endif
@@ -629,7 +655,7 @@ __global__ BSW_SMEM_LB void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
                                                   const uint8_t *__restrict__ reads,
                                                   const int64_t *__restrict__ read_off,
                                                   const int32_t *__restrict__ read_len, int32_t n0, int32_t n,
-                                                  EntT<U> *__restrict__ scratch, int32_t scap,
+                                                  S *__restrict__ scratch, int32_t scap,
                                                   bsw_bwtintv_t *__restrict__ mems, int32_t cap,
                                                   int32_t *__restrict__ n_mems, int32_t *__restrict__ err)
 {
@@ -802,9 +828,18 @@ int launch_collect(bsw_fmi_t *f, const FmiDevT<U> &dv, const MemOpt &mo, const u
                    int32_t *d_cnt, hipStream_t s)
 {
     const int32_t scap = max_len + 1;
+    // the wide index's packed 16-B entries when every value fits (EntP); else EntT<U>
+    bool packed = false;
+    if constexpr (sizeof(U) == 8) {
+        uint64_t smax = 0;
+        for (int c = 0; c < 4; ++c) smax = std::max<uint64_t>(smax, (uint64_t)(f->count[c + 1] - f->count[c]));
+        packed = smax < (1ull << 32) && (uint64_t)f->n + 2 < (1ull << 40) && max_len < 32767 &&
+                 getenv("BSW_SMEM_WIDE_ENT") == nullptr;
+    }
+    const size_t esz = packed ? sizeof(EntP) : sizeof(EntT<U>);
     // chunk so the two scratch vectors stay within 16 GB (of 288 GB: one launch for up to ~3M
-    // 151-bp reads with 16-byte entries, ~1.5M with the wide index's 32-byte ones)
-    const size_t per_read = (size_t)2 * scap * sizeof(EntT<U>);
+    // 151-bp reads with 16-byte entries)
+    const size_t per_read = (size_t)2 * scap * esz;
     const int32_t chunk = (int32_t)std::max<size_t>(64, std::min<size_t>((size_t)n, ((size_t)16 << 30) / per_read));
     const size_t need = per_read * (size_t)std::min(chunk, n);
     if (need > f->scratch_bytes) {
@@ -818,9 +853,18 @@ int launch_collect(bsw_fmi_t *f, const FmiDevT<U> &dv, const MemOpt &mo, const u
     (void)hipEventRecord(f->ev0, s);
     for (int32_t n0 = 0; n0 < n; n0 += chunk) {
         const int32_t m = std::min(chunk, n - n0);
-        hipLaunchKernelGGL(smem_kernel<U>, dim3((unsigned)((m + kSmemBlock - 1) / kSmemBlock)), dim3(kSmemBlock), 0, s,
-                           dv, mo, d_reads, d_off,
-                           d_len, n0, m, (EntT<U> *)f->d_scratch, scap, d_mems, cap, d_cnt, f->d_err);
+        const dim3 grid((unsigned)((m + kSmemBlock - 1) / kSmemBlock));
+        if constexpr (sizeof(U) == 8) {
+            if (packed)
+                hipLaunchKernelGGL((smem_kernel<U, EntP>), grid, dim3(kSmemBlock), 0, s, dv, mo, d_reads, d_off, d_len, n0,
+                                   m, (EntP *)f->d_scratch, scap, d_mems, cap, d_cnt, f->d_err);
+            else
+                hipLaunchKernelGGL((smem_kernel<U, EntT<U>>), grid, dim3(kSmemBlock), 0, s, dv, mo, d_reads, d_off, d_len,
+                                   n0, m, (EntT<U> *)f->d_scratch, scap, d_mems, cap, d_cnt, f->d_err);
+        } else {
+            hipLaunchKernelGGL((smem_kernel<U, EntT<U>>), grid, dim3(kSmemBlock), 0, s, dv, mo, d_reads, d_off, d_len, n0,
+                               m, (EntT<U> *)f->d_scratch, scap, d_mems, cap, d_cnt, f->d_err);
+        }
         if (hipGetLastError() != hipSuccess) return BSW_E_HIP;
     }
     (void)hipEventRecord(f->ev1, s);

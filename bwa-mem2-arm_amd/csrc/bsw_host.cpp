@@ -181,6 +181,9 @@ struct PlanCall {
     int32_t n = 0, w = 0;
     int cell_bits = 16;
     hipStream_t stream = nullptr;
+    hipStream_t dp_stream = nullptr;    // the DP kernels' stream when not `stream` (host pipeline:
+                                        //   everything else of a chunk runs on the helper stream)
+    hipStream_t plan_stream = nullptr;  // plan + sort stream when not the slot's pstream
     // row-group kernel contract as the host checked it: gq_maxq >= 0 = every pair fits (longest
     // query gq_maxq, longest target gq_maxt); -2 = not checked (the kernel flags misfits, run_dp
     // falls back to the planned path); -1 = some pair does not fit (planned path at once)
@@ -236,7 +239,13 @@ struct Slot {
     bsw_stats_t stats{};
     hipEvent_t evm = nullptr;           // class-count readback of the last run_plan
     hipStream_t pstream = nullptr;      // high-priority stream of run_plan
+    // host pipeline (host_shard): a stream confined to a few reserved CUs for everything of a
+    // chunk but its DP (copies, unpack / plan / sort kernels, outputs' gather and readback) and one
+    // over the other CUs for the DP -- so the next chunk's preparation never waits for wave slots
+    // behind the current chunk's DP workgroups (null: not created / masking unavailable)
+    hipStream_t hstream = nullptr, dstream = nullptr;
     hipEvent_t evh = nullptr;           // inputs ready on the call's stream (pstream waits)
+    hipEvent_t evd = nullptr;           // host pipeline: a chunk's DP done (its outputs' readback waits)
     PlanCall plan;                      // arguments of the last run_plan (run_dp's input)
     int fast = 0;                       // last run_plan launched the row-group kernel: 2 = host-
                                         //   checked batch, 1 = kernel-checked (flag read back)
@@ -311,7 +320,10 @@ struct DeviceCtx {
         if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->evm) (void)hipEventDestroy(s->evm);
         if (s->evh) (void)hipEventDestroy(s->evh);
+        if (s->evd) (void)hipEventDestroy(s->evd);
         if (s->pstream) (void)hipStreamDestroy(s->pstream);
+        if (s->hstream) (void)hipStreamDestroy(s->hstream);
+        if (s->dstream) (void)hipStreamDestroy(s->dstream);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         if (s->stream) (void)hipStreamDestroy(s->stream);
         for (int k = 0; k < Slot::kSide; ++k) {
@@ -349,7 +361,8 @@ struct DeviceCtx {
     {
         if (rc) {
             (void)hipSetDevice(s->device);
-            for (hipStream_t st : {s->stream, s->pstream, s->run_stream, s->side[0], s->side[1], s->side[2]})
+            for (hipStream_t st : {s->stream, s->pstream, s->hstream, s->dstream, s->run_stream, s->side[0], s->side[1],
+                                   s->side[2]})
                 if (st) (void)hipStreamSynchronize(st);
         }
         std::lock_guard<std::mutex> g(mu);
@@ -448,6 +461,57 @@ static hipError_t grow_sort(Slot &s, int32_t n)
 //   run_dp   : wait for that readback, enqueue the DP kernels and the readback of their
 //              range-guard word into h_meta[kMetaErr]
 // finish_stats() waits for the rest and turns a tripped guard into BSW_E_RANGE.
+// the slot's high-priority stream (created on first use)
+static int ensure_pstream(Slot &s)
+{
+    if (!s.pstream) {
+        int lo = 0, hi = 0;
+        BSW_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        BSW_TRY(hipStreamCreateWithPriority(&s.pstream, hipStreamNonBlocking, hi));
+        BSW_TRY(hipEventCreateWithFlags(&s.evh, hipEventDisableTiming));
+    }
+    return BSW_OK;
+}
+
+// The host pipeline's CU split (experiment knob, off by default): BSW_HP_RESERVE_CUS = n > 0 CUs,
+// spread evenly over the device (one per XCD for 8 on a 256-CU MI355X), serve the helper stream and
+// the rest the DP stream.  Measured (profiles/r04/hostpath_ab_r4j.txt): no better than the
+// high-priority helper stream for 1M-pair calls (70.8 / 73.4 vs 75.7 M/s on one box), and the
+// per-slot masked queues cost concurrent small calls a third of their rate (8 x 1K without
+// coalescing 6.4-7.4 vs 9-10 M/s): every masked stream is a hardware queue of its own.
+static int reserve_cus()
+{
+    static const int v = [] {
+        const char *e = getenv("BSW_HP_RESERVE_CUS");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    return v;
+}
+static void ensure_cu_streams(Slot &s)
+{
+    if (s.hstream || reserve_cus() == 0) return;
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, s.device) != hipSuccess) return;
+    const int ncu = pr.multiProcessorCount, nr = reserve_cus();
+    if (ncu < 2 * nr || ncu > 1024) return;
+    uint32_t hm[32] = {}, dm[32] = {};
+    const int nw = (ncu + 31) / 32;
+    for (int c = 0; c < ncu; ++c) dm[c / 32] |= 1u << (c % 32);
+    for (int r = 0; r < nr; ++r) {
+        const int c = r * (ncu / nr);
+        hm[c / 32] |= 1u << (c % 32);
+        dm[c / 32] &= ~(1u << (c % 32));
+    }
+    hipStream_t h = nullptr, d = nullptr;
+    if (hipExtStreamCreateWithCUMask(&h, (uint32_t)nw, hm) != hipSuccess) return;
+    if (hipExtStreamCreateWithCUMask(&d, (uint32_t)nw, dm) != hipSuccess) {
+        (void)hipStreamDestroy(h);
+        return;
+    }
+    s.hstream = h;
+    s.dstream = d;
+}
+
 static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
 {
     s.stats = bsw_stats_t{};
@@ -467,17 +531,26 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
         const bool checked = pc.gq_maxq >= 0;
         const int cols = checked ? gq_cols_for(pc.gq_maxq, gs) : (gs == 16 ? 10 : 40);
         int32_t *d_err = s.d_meta + kMetaErr;
+        // the DP stream when the call has one (host pipeline: the helper stream holds few CUs)
+        hipStream_t fs = pc.stream;
+        if (pc.dp_stream && pc.dp_stream != pc.stream) {
+            if (int r = ensure_pstream(s)) return r;           // (creates evh)
+            BSW_TRY(hipEventRecord(s.evh, pc.stream));
+            BSW_TRY(hipStreamWaitEvent(pc.dp_stream, s.evh, 0));
+            fs = pc.dp_stream;
+            s.run_stream = fs;
+        }
         if (!pc.d_out24)                       // (the staged path's input kernel zeroed them)
-            BSW_TRY(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), pc.stream));
-        BSW_TRY(hipEventRecord(s.ev0, pc.stream));
+            BSW_TRY(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), fs));
+        BSW_TRY(hipEventRecord(s.ev0, fs));
         BSW_TRY(launch_gq_kernel(gs, cols, kp, pc.w, pc.d_pairs, nullptr, n, pc.d_ref, pc.d_qer,
                                  d_err, checked ? nullptr : s.d_meta + kMetaFlag, checked ? pc.d_out24 : nullptr,
-                                 pc.stream));
-        BSW_TRY(hipEventRecord(s.ev1, pc.stream));
-        BSW_TRY(hipMemcpyAsync(s.h_meta + kMetaErr, d_err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, pc.stream));
+                                 fs));
+        BSW_TRY(hipEventRecord(s.ev1, fs));
+        BSW_TRY(hipMemcpyAsync(s.h_meta + kMetaErr, d_err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, fs));
         if (!checked) {
             if (!s.evm) BSW_TRY(hipEventCreateWithFlags(&s.evm, hipEventDisableTiming));
-            BSW_TRY(hipEventRecord(s.evm, pc.stream));
+            BSW_TRY(hipEventRecord(s.evm, fs));
         }
         s.stats.n_launches = 1;
         s.stats.n_i16 = n;
@@ -489,15 +562,12 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     // event): while other chunks' DP kernels fill the GPU, their few blocks are dispatched
     // first instead of queuing behind thousands of DP workgroups (it delays the next chunk's
     // DP launch otherwise: 1-3 ms per chunk in the host pipeline's trace)
-    if (!s.pstream) {
-        int lo = 0, hi = 0;
-        BSW_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        BSW_TRY(hipStreamCreateWithPriority(&s.pstream, hipStreamNonBlocking, hi));
-        BSW_TRY(hipEventCreateWithFlags(&s.evh, hipEventDisableTiming));
+    if (int r = ensure_pstream(s)) return r;
+    hipStream_t stream = pc.plan_stream ? pc.plan_stream : s.pstream;
+    if (pc.stream != stream) {
+        BSW_TRY(hipEventRecord(s.evh, pc.stream));
+        BSW_TRY(hipStreamWaitEvent(stream, s.evh, 0));
     }
-    BSW_TRY(hipEventRecord(s.evh, pc.stream));
-    BSW_TRY(hipStreamWaitEvent(s.pstream, s.evh, 0));
-    hipStream_t stream = s.pstream;
     BSW_TRY(grow_sort(s, n));
     BSW_TRY(hipMemsetAsync(s.d_meta, 0, kMetaWords * sizeof(int32_t), stream));
     int32_t *d_counts = s.d_meta, *d_maxq = s.d_meta + kMetaMaxq;
@@ -531,7 +601,7 @@ static int run_dp(const KParams &kp, Slot &s)
 {
     const PlanCall &pc = s.plan;
     if (pc.n == 0) return BSW_OK;
-    hipStream_t stream = pc.stream;
+    hipStream_t stream = pc.dp_stream && !s.fast ? pc.dp_stream : pc.stream;
     const int32_t w = pc.w;
     const int cell_bits = pc.cell_bits;
     SeqPair *d_pairs = pc.d_pairs;
@@ -641,6 +711,7 @@ static int run_dp(const KParams &kp, Slot &s)
     // the DP kernels' range guard (a pair routed to a class that cannot hold it) -> host,
     // after every DP launch of this batch
     BSW_TRY(hipMemcpyAsync(s.h_meta + kMetaErr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    s.run_stream = stream;
     s.timed = true;
     return BSW_OK;
 }
@@ -1092,6 +1163,10 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     int32_t pend_seq[nslots] = {-1, -1, -1};
     int pend_mode[nslots] = {};
     bsw_stats_t agg{};
+    // Everything but the DP kernels runs on the slot's high-priority stream: the next chunk's
+    // copies, unpack / plan / sort kernels and the outputs' readback are dispatched ahead of the
+    // queued DP workgroups instead of behind them (BSW_HP_ONE_STREAM=1: all on the slot's stream)
+    const bool hp_split = getenv("BSW_HP_ONE_STREAM") == nullptr;
     // launcher thread: chunk seq numbers in order; launched[k] = last seq whose DP is enqueued
     struct Launcher {
         std::mutex mu;
@@ -1120,15 +1195,28 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
             }
             Slot &p = *slots[job.first];
             if (!r) r = run_dp(kp, p);
+            // the outputs' gather and readback go on the high-priority stream once the DP (and its
+            // guard readback) is done: on the DP stream they would queue behind the next chunks'
+            // DP workgroups (a 1.4 ms copy in the trace)
+            hipStream_t os = p.run_stream;
+            hipStream_t hs = p.plan.plan_stream;       // the chunk's helper stream (hp_split)
+            if (!r && hp_split && hs && p.run_stream != hs) {
+                if (!p.evd && hipEventCreateWithFlags(&p.evd, hipEventDisableTiming) != hipSuccess) r = BSW_E_HIP;
+                if (!r && (hipEventRecord(p.evd, p.run_stream) != hipSuccess ||
+                           hipStreamWaitEvent(hs, p.evd, 0) != hipSuccess))
+                    r = BSW_E_HIP;
+                os = hs;
+                p.run_stream = hs;                     // finish_stats waits here: after the DP's stream
+            }
             if (!r && job.mode == kStage2bit) {        // outputs only: 24 B per pair
                 const int32_t m = p.plan.n;
-                hipLaunchKernelGGL(gather_outputs_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, p.stream,
+                hipLaunchKernelGGL(gather_outputs_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, os,
                                    p.plan.d_pairs, (int32_t *)p.d_stage, m);
                 if (hipGetLastError() != hipSuccess ||
-                    hipMemcpyAsync(p.h_stage, p.d_stage, (size_t)m * 24, hipMemcpyDeviceToHost, p.stream) != hipSuccess)
+                    hipMemcpyAsync(p.h_stage, p.d_stage, (size_t)m * 24, hipMemcpyDeviceToHost, os) != hipSuccess)
                     r = BSW_E_HIP;
             } else if (!r && hipMemcpyAsync(p.h_stage, p.plan.d_pairs, (size_t)p.plan.n * sizeof(SeqPair),
-                                            hipMemcpyDeviceToHost, p.stream) != hipSuccess) {
+                                            hipMemcpyDeviceToHost, os) != hipSuccess) {
                 r = BSW_E_HIP;
             }
             {
@@ -1170,28 +1258,33 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     auto enqueue = [&](int k, int32_t seq, const StagedChunk &c, int32_t m) -> int {
         Slot &s = *slots[k];
         const int r = [&]() -> int {
+            if (hp_split) {
+                if (int e = ensure_pstream(s)) return e;
+                ensure_cu_streams(s);
+            }
+            hipStream_t hs = hp_split ? (s.hstream ? s.hstream : s.pstream) : s.stream;
             BSW_TRY(grow(s.d_stage, s.cap_dstage, c.bytes));
-            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.bytes, hipMemcpyHostToDevice, s.stream));
+            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.bytes, hipMemcpyHostToDevice, hs));
             const uint8_t *d_r = s.d_stage + c.ref_off, *d_q = s.d_stage + c.qer_off;
             SeqPair *d_p = (SeqPair *)(s.d_stage + c.pair_off);
             if (c.mode == kStage2bit) {     // 2-bit codes -> bytes, exceptions patched, records expanded
                 BSW_TRY(grow(s.d_ref, s.cap_ref, c.rb + 4));
                 BSW_TRY(grow(s.d_qer, s.cap_qer, c.qb + 4));
                 BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)m));
-                BSW_TRY(hipMemsetAsync(s.d_ref + c.rb, 0, 4, s.stream));
-                BSW_TRY(hipMemsetAsync(s.d_qer + c.qb, 0, 4, s.stream));
+                BSW_TRY(hipMemsetAsync(s.d_ref + c.rb, 0, 4, hs));
+                BSW_TRY(hipMemsetAsync(s.d_qer + c.qb, 0, 4, hs));
                 const int64_t tr = ((int64_t)c.rb + 15) / 16, tq = ((int64_t)c.qb + 15) / 16;
                 if (tr > 0)
-                    hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, s.stream,
+                    hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, hs,
                                        d_r, s.d_ref, (int64_t)c.rb);
                 if (tq > 0)
-                    hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, s.stream,
+                    hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, hs,
                                        d_q, s.d_qer, (int64_t)c.qb);
                 const int32_t ne = c.n_exr + c.n_exq;
                 if (ne > 0)
-                    hipLaunchKernelGGL(patch_codes_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s.stream,
+                    hipLaunchKernelGGL(patch_codes_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, hs,
                                        (const uint32_t *)(s.d_stage + c.exc_off), c.n_exr, ne, s.d_ref, s.d_qer);
-                hipLaunchKernelGGL(expand_pairs_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s.stream,
+                hipLaunchKernelGGL(expand_pairs_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, hs,
                                    (const PairIn *)(s.d_stage + c.pair_off), s.d_pairs, m);
                 BSW_TRY(hipGetLastError());
                 d_r = s.d_ref;
@@ -1200,14 +1293,14 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
             } else if (c.packed) {          // nibbles -> one byte per base in the slot's buffers
                 BSW_TRY(grow(s.d_ref, s.cap_ref, c.rb + 4));
                 BSW_TRY(grow(s.d_qer, s.cap_qer, c.qb + 4));
-                BSW_TRY(hipMemsetAsync(s.d_ref + c.rb, 0, 4, s.stream));
-                BSW_TRY(hipMemsetAsync(s.d_qer + c.qb, 0, 4, s.stream));
+                BSW_TRY(hipMemsetAsync(s.d_ref + c.rb, 0, 4, hs));
+                BSW_TRY(hipMemsetAsync(s.d_qer + c.qb, 0, 4, hs));
                 const int64_t tr = ((int64_t)c.rb + 7) / 8, tq = ((int64_t)c.qb + 7) / 8;
                 if (tr > 0)
-                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, s.stream,
+                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, hs,
                                        d_r, s.d_ref, (int64_t)c.rb);
                 if (tq > 0)
-                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, s.stream,
+                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, hs,
                                        d_q, s.d_qer, (int64_t)c.qb);
                 BSW_TRY(hipGetLastError());
                 d_r = s.d_ref;
@@ -1218,7 +1311,11 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
             // kernels index ref / qer by idr / idq: shift the bases so staged byte 0 is r_base / q_base
             pc.d_ref = d_r - c.r_base;
             pc.d_qer = d_q - c.q_base;
-            pc.n = m; pc.w = w; pc.cell_bits = cell_bits; pc.stream = s.stream;
+            pc.n = m; pc.w = w; pc.cell_bits = cell_bits; pc.stream = hs;
+            if (hp_split) {
+                pc.dp_stream = s.dstream ? s.dstream : s.stream;
+                pc.plan_stream = hs;
+            }
             return run_plan(kp, s, pc);
         }();
         {
@@ -1343,7 +1440,8 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         if (!slots[k]) continue;
         if (rc) {                                       // nothing in flight on a returned slot
             (void)hipStreamSynchronize(slots[k]->stream);
-            if (slots[k]->pstream) (void)hipStreamSynchronize(slots[k]->pstream);
+            for (hipStream_t st : {slots[k]->pstream, slots[k]->hstream, slots[k]->dstream})
+                if (st) (void)hipStreamSynchronize(st);
         }
         dc.give_back(std::move(slots[k]));
     }

@@ -1,14 +1,19 @@
 """Summarise rocprofv3 CSV output (kernel trace + PMC passes) for the lane kernel.
 
-usage: python tools/pmc_summary.py gpurun_out/prof [profiles/<round>]
+usage: python tools/pmc_summary.py gpurun_out/prof [profiles/<round>] [--only=kernel,...]
+(--only: merge just those kernels into pmc_latest.json -- e.g. a C4 profile's smem_kernel without
+its small extension launches replacing the C2 line's pc_kernel<160>)
 Writes <dest>/kernel_stats.csv (copied), <dest>/pmc_summary.json and profiles/pmc_latest.json
 (read by bench.py for roofline.traffic).
 """
 import csv, glob, json, os, shutil, sys
 from collections import defaultdict
 
-src = sys.argv[1]
-dest = sys.argv[2] if len(sys.argv) > 2 else None
+args = [a for a in sys.argv[1:] if not a.startswith('--only=')]
+only = [a.split('=', 1)[1].split(',') for a in sys.argv[1:] if a.startswith('--only=')]
+only = only[0] if only else None   # --only=k1,k2: merge just these kernels into pmc_latest.json
+src = args[0]
+dest = args[1] if len(args) > 1 else None
 
 def newest(pattern):
     """Per directory only the newest run's file: gpurun merges every call's output into the same
@@ -83,11 +88,12 @@ if dest:
     with open(os.path.join(dest, 'pmc_summary.json'), 'w') as fh:
         json.dump(summary, fh, indent=1)
     # profiles/pmc_latest.json: merged over workloads (bench.py reads each kernel's traffic)
-    latest = os.path.join(os.path.dirname(dest.rstrip('/')), 'pmc_latest.json')
+    latest = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'pmc_latest.json')
     merged = {}
     if os.path.exists(latest):
         with open(latest) as fh:
             merged = json.load(fh)
-    merged.update({k: v for k, v in summary.items() if 'hbm_bytes_per_launch' in v or k not in merged})
+    merged.update({k: v for k, v in summary.items()
+                   if (only is None and ('hbm_bytes_per_launch' in v or k not in merged)) or (only and k in only)})
     with open(latest, 'w') as fh:
         json.dump(merged, fh, indent=1)
