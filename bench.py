@@ -254,7 +254,7 @@ def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
 
 
 def coalesce_opt(eng):
-    return getattr(eng, "coalesce_setting", 32768)
+    return getattr(eng, "coalesce_setting", 8192)
 
 
 def host_path_rates(eng, pairs, ref, qer, w, cell_bits, want, curve_sizes=(1_000, 10_000, 100_000)):

@@ -388,7 +388,7 @@ struct bsw_ctx {
     int32_t host_chunk = 262144;        // BSW_OPT_HOST_CHUNK: pairs per host-buffer pipeline chunk
     int host_pack = 2;                  // BSW_OPT_HOST_PACK: 2-bit (2) or nibble (4) staging
     int64_t split_min = 131072;         // BSW_OPT_SPLIT_MIN: smaller calls go whole to one device
-    int32_t coalesce = 32768;           // BSW_OPT_COALESCE: calls of <= this many pairs coalesce
+    int32_t coalesce = 8192;            // BSW_OPT_COALESCE: calls of <= this many pairs coalesce
     std::atomic<unsigned> rr{0};        // tie-break rotation of the one-device pick
     ~bsw_ctx()
     {
@@ -1268,24 +1268,20 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
             const uint8_t *d_r = s.d_stage + c.ref_off, *d_q = s.d_stage + c.qer_off;
             SeqPair *d_p = (SeqPair *)(s.d_stage + c.pair_off);
             if (c.mode == kStage2bit) {     // 2-bit codes -> bytes, exceptions patched, records expanded
-                BSW_TRY(grow(s.d_ref, s.cap_ref, c.rb + 4));
-                BSW_TRY(grow(s.d_qer, s.cap_qer, c.qb + 4));
+                // one launch (stage_in_kernel: both unpacks, the exception patches, the records and
+                // the pad zeroing) instead of six: a chunk's enqueue is launch-bound on the host
+                // (~60 us per launch while the pool packs the next chunk, HIP API trace
+                // profiles/r04/hostpath_api_trace.txt)
+                BSW_TRY(grow(s.d_ref, s.cap_ref, c.rb + 16));
+                BSW_TRY(grow(s.d_qer, s.cap_qer, c.qb + 16));
                 BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)m));
-                BSW_TRY(hipMemsetAsync(s.d_ref + c.rb, 0, 4, hs));
-                BSW_TRY(hipMemsetAsync(s.d_qer + c.qb, 0, 4, hs));
                 const int64_t tr = ((int64_t)c.rb + 15) / 16, tq = ((int64_t)c.qb + 15) / 16;
-                if (tr > 0)
-                    hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, hs,
-                                       d_r, s.d_ref, (int64_t)c.rb);
-                if (tq > 0)
-                    hipLaunchKernelGGL(unpack2_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, hs,
-                                       d_q, s.d_qer, (int64_t)c.qb);
-                const int32_t ne = c.n_exr + c.n_exq;
-                if (ne > 0)
-                    hipLaunchKernelGGL(patch_codes_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, hs,
-                                       (const uint32_t *)(s.d_stage + c.exc_off), c.n_exr, ne, s.d_ref, s.d_qer);
-                hipLaunchKernelGGL(expand_pairs_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, hs,
-                                   (const PairIn *)(s.d_stage + c.pair_off), s.d_pairs, m);
+                const int64_t nthr = tr + tq + m;
+                hipLaunchKernelGGL(stage_in_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, hs,
+                                   s.d_stage + c.ref_off, (int64_t)c.rb, s.d_stage + c.qer_off, (int64_t)c.qb,
+                                   (const uint32_t *)(s.d_stage + c.exc_off), c.n_exr, c.n_exr + c.n_exq,
+                                   (const PairIn *)(s.d_stage + c.pair_off), m, s.d_ref, s.d_qer, s.d_pairs,
+                                   (int32_t *)nullptr);
                 BSW_TRY(hipGetLastError());
                 d_r = s.d_ref;
                 d_q = s.d_qer;

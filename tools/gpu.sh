@@ -16,6 +16,7 @@
 #   percall:<args>  percall_bench <args> (commas for spaces), untraced
 #   ab:<lib>        same-box A/B: C2 line with lib/<lib> (base) vs the in-tree library, x3 alternating
 #   hptrace[:chunk] kernel + copy trace and per-chunk host timeline of 1M-pair host-buffer calls
+#   hpapi[:chunk]   the same plus the HIP runtime API trace
 #   export:VAR=VAL  set an environment variable for the following steps (unset:VAR clears it)
 #   py:<file>       python -u <file> (a probe script under tools/)
 # (rounds 1-3 kept one file per gpurun call, tools/gpu_*.sh; they are in git history, baea391)
@@ -85,6 +86,13 @@ for step in "$@"; do
             -d "$O/hptrace" -- python3 tools/host_path_once.py ${arg:-262144} 4 > "$O/hptrace.log" 2>&1 \
             || fail "$step" $? "$O/hptrace.log"
         grep '^call' "$O/hptrace.log" ;;
+    hpapi)
+        # hptrace plus the HIP runtime API trace (per-thread host timeline of every runtime call)
+        rm -rf "$O/hpapi"
+        BSW_DEBUG_HP=1 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace --output-format csv \
+            -d "$O/hpapi" -- python3 tools/host_path_once.py ${arg:-262144} 4 > "$O/hpapi.log" 2>&1 \
+            || fail "$step" $? "$O/hpapi.log"
+        grep '^call' "$O/hpapi.log" ;;
     export)
         # export:VAR=VALUE for the steps after it (e.g. export:GPU_MAX_HW_QUEUES=8, export:BSW_HP_INLINE_ENQ=1)
         export "${arg?}"; echo "exported $arg" ;;

@@ -111,7 +111,7 @@ int main(int argc, char **argv)
            "after an untimed warm-up of every caller\", \"curve\": [", T, N, T);
     bool first = true;
     std::atomic<long> bad{0};
-    const int32_t co_on = getenv("PERCALL_COALESCE") ? atoi(getenv("PERCALL_COALESCE")) : 32768;
+    const int32_t co_on = getenv("PERCALL_COALESCE") ? atoi(getenv("PERCALL_COALESCE")) : 8192;   // the library default
     // T concurrent callers, each over its own contiguous slice, calls back to back for `secs_run`;
     // returns M pairs / s
     auto callers = [&](int32_t m, double secs_run) {
