@@ -588,6 +588,8 @@ __device__ int smem_read(const FmiDevT<U> &f, const MemOpt &opt, const uint8_t *
     Lane<U, S> L;
     L.q = reads + read_off[r];
     L.len = read_len[r];
+    // [slot][read]: a wave's lanes at the same slot touch one contiguous run (a [read][slot] layout,
+    // each read's vectors contiguous, measured 13% slower at 3 Gb: profiles/r04/hostpath_ab_r4m.txt)
     L.stride = (size_t)n;
     L.sa = scratch + t;
     L.sb = scratch + (size_t)scap * n + t;
