@@ -284,6 +284,7 @@ struct DeviceCtx {
     std::mutex agg_mu;
     std::condition_variable agg_cv;
     std::deque<AggReq *> agg_q;
+    int64_t agg_qn = 0;                 // pairs queued in agg_q
     int agg_leaders = 0;
     int agg_leaders_max = 4;            // BSW_OPT_COALESCE_LEADERS
     int agg_linger_us = 0;              // BSW_OPT_COALESCE_LINGER (experiment knob: no gain measured)
@@ -1468,6 +1469,7 @@ struct AggReq {
     bool done = false;
 };
 constexpr int32_t kAggMaxPairs = 262144;        // pairs per coalesced batch
+constexpr int64_t kAggLingerPairs = 4096;       // a lingering leader starts once this many are queued
 
 struct AggSeg {                                 // one call inside a coalesced batch
     AggReq *r;
@@ -1683,18 +1685,20 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
     AggReq me{pairs, ref, qer, n, w, cell_bits, kp.end_bonus};
     std::unique_lock<std::mutex> lk(dc.agg_mu);
     dc.agg_q.push_back(&me);
+    dc.agg_qn += n;
+    if (dc.agg_linger_us > 0) dc.agg_cv.notify_all();      // a lingering leader counts the queue
     while (!me.done) {
         if (dc.agg_leaders < dc.agg_leaders_max && !dc.agg_q.empty()) {
             // lead: every queued call with the front call's (w, cell_bits, end_bonus), FIFO
             const bool busy = dc.agg_leaders > 0;     // another batch in flight on this device
-            if (busy && dc.agg_linger_us > 0) {
-                // the device is busy anyway: give the callers whose batches just finished a moment to
-                // queue their next calls, so this batch carries them too.  The wait holds this
-                // leader's place, and every finishing batch's notify ends it early.  Measured
-                // (DESIGN.md §5): 30 us looked +50% at 8 callers x 1K in one A/B and was noise in
-                // an interleaved x5 (1K 13.0 vs 12.5 M/s, 10K 35.1 vs 37.2): off by default
+            if (busy && dc.agg_linger_us > 0 && dc.agg_qn < kAggLingerPairs) {
+                // the device is busy anyway: hold this leader's place until the queue holds
+                // kAggLingerPairs pairs (the next calls of the callers whose batches just finished)
+                // or linger_us passes -- a row-group batch costs ~0.3 ms whether it carries 1K or 4K
+                // pairs, so fuller batches are the small-call throughput
                 ++dc.agg_leaders;
-                dc.agg_cv.wait_for(lk, std::chrono::microseconds(dc.agg_linger_us));
+                dc.agg_cv.wait_for(lk, std::chrono::microseconds(dc.agg_linger_us),
+                                   [&] { return me.done || dc.agg_qn >= kAggLingerPairs; });
                 --dc.agg_leaders;
                 if (me.done) break;
                 if (dc.agg_q.empty()) continue;       // another leader took every queued call
@@ -1710,6 +1714,7 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
                 if (r->w == fw && r->cell_bits == fcb && r->eb == feb && (G.empty() || tot + r->n <= kAggMaxPairs)) {
                     G.push_back(r);
                     tot += r->n;
+                    dc.agg_qn -= r->n;
                     it = dc.agg_q.erase(it);
                 } else {
                     ++it;
