@@ -285,6 +285,8 @@ struct DeviceCtx {
     std::condition_variable agg_cv;
     std::deque<AggReq *> agg_q;
     int64_t agg_qn = 0;                 // pairs queued in agg_q
+    int64_t agg_run = 0;                // pairs in the batches on the device
+    int agg_nrun = 0;                   // batches on the device
     int agg_leaders = 0;
     int agg_leaders_max = 4;            // BSW_OPT_COALESCE_LEADERS
     int agg_linger_us = 0;              // BSW_OPT_COALESCE_LINGER (experiment knob: no gain measured)
@@ -1691,14 +1693,19 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
         if (dc.agg_leaders < dc.agg_leaders_max && !dc.agg_q.empty()) {
             // lead: every queued call with the front call's (w, cell_bits, end_bonus), FIFO
             const bool busy = dc.agg_leaders > 0;     // another batch in flight on this device
-            if (busy && dc.agg_linger_us > 0 && dc.agg_qn < kAggLingerPairs) {
+            // linger only behind two or more running batches: with fewer concurrent callers the
+            // batches must overlap instead (a lingering second caller serialised two callers'
+            // batches: 2 x 1K 4.0 vs 6.8 M/s, profiles/r04/percall_linger_r4q.txt)
+            if (dc.agg_nrun >= 2 && dc.agg_linger_us > 0 && dc.agg_qn < kAggLingerPairs) {
                 // the device is busy anyway: hold this leader's place until the queue holds
-                // kAggLingerPairs pairs (the next calls of the callers whose batches just finished)
-                // or linger_us passes -- a row-group batch costs ~0.3 ms whether it carries 1K or 4K
-                // pairs, so fuller batches are the small-call throughput
+                // kAggLingerPairs pairs (the next calls of the callers whose batches just finished),
+                // the device goes idle, or linger_us passes -- a row-group batch costs ~0.3 ms
+                // whether it carries 1K or 4K pairs, so fuller batches are the small-call
+                // throughput
                 ++dc.agg_leaders;
-                dc.agg_cv.wait_for(lk, std::chrono::microseconds(dc.agg_linger_us),
-                                   [&] { return me.done || dc.agg_qn >= kAggLingerPairs; });
+                dc.agg_cv.wait_for(lk, std::chrono::microseconds(dc.agg_linger_us), [&] {
+                    return me.done || dc.agg_qn >= kAggLingerPairs || dc.agg_nrun < 2;
+                });
                 --dc.agg_leaders;
                 if (me.done) break;
                 if (dc.agg_q.empty()) continue;       // another leader took every queued call
@@ -1720,11 +1727,15 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
                     ++it;
                 }
             }
+            dc.agg_run += tot;
+            ++dc.agg_nrun;
             lk.unlock();
             KParams gk = kp;
             gk.end_bonus = feb;
             run_group(gk, dc, G, chunk, two_bit, busy);
             lk.lock();
+            dc.agg_run -= tot;
+            --dc.agg_nrun;
             --dc.agg_leaders;
             for (AggReq *r : G) r->done = true;
             dc.agg_cv.notify_all();
