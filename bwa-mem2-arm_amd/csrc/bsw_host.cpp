@@ -287,9 +287,11 @@ struct DeviceCtx {
     int64_t agg_qn = 0;                 // pairs queued in agg_q
     int64_t agg_run = 0;                // pairs in the batches on the device
     int agg_nrun = 0;                   // batches on the device
+    int agg_inside = 0;                 // callers inside coalesced_call
+    int agg_lingering = 0;              // leaders waiting for a deeper queue
     int agg_leaders = 0;
     int agg_leaders_max = 4;            // BSW_OPT_COALESCE_LEADERS
-    int agg_linger_us = 0;              // BSW_OPT_COALESCE_LINGER (experiment knob: no gain measured)
+    int agg_linger_us = 0;              // BSW_OPT_COALESCE_LINGER (off: a trade-off by caller count)
     std::mutex mu;
     std::vector<std::unique_ptr<Slot>> free_slots;
     uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
@@ -1688,24 +1690,29 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
     std::unique_lock<std::mutex> lk(dc.agg_mu);
     dc.agg_q.push_back(&me);
     dc.agg_qn += n;
-    if (dc.agg_linger_us > 0) dc.agg_cv.notify_all();      // a lingering leader counts the queue
+    ++dc.agg_inside;
+    if (dc.agg_lingering > 0) dc.agg_cv.notify_all();      // a lingering leader counts the queue
     while (!me.done) {
         if (dc.agg_leaders < dc.agg_leaders_max && !dc.agg_q.empty()) {
             // lead: every queued call with the front call's (w, cell_bits, end_bonus), FIFO
             const bool busy = dc.agg_leaders > 0;     // another batch in flight on this device
-            // linger only behind two or more running batches: with fewer concurrent callers the
-            // batches must overlap instead (a lingering second caller serialised two callers'
-            // batches: 2 x 1K 4.0 vs 6.8 M/s, profiles/r04/percall_linger_r4q.txt)
-            if (dc.agg_nrun >= 2 && dc.agg_linger_us > 0 && dc.agg_qn < kAggLingerPairs) {
+            // linger only when there are more callers than leader slots (batching is then the only
+            // way to serve them all) and two or more batches run: with fewer callers the batches
+            // must overlap instead -- a lingering leader serialised 2 callers (1K: 4.0 vs 6.8 M/s)
+            // and cost 4 callers a quarter (profiles/r04/percall_linger_r4{q,r}.txt)
+            if (dc.agg_inside > dc.agg_leaders_max && dc.agg_nrun >= 2 && dc.agg_linger_us > 0 &&
+                dc.agg_qn < kAggLingerPairs) {
                 // the device is busy anyway: hold this leader's place until the queue holds
                 // kAggLingerPairs pairs (the next calls of the callers whose batches just finished),
                 // the device goes idle, or linger_us passes -- a row-group batch costs ~0.3 ms
                 // whether it carries 1K or 4K pairs, so fuller batches are the small-call
                 // throughput
                 ++dc.agg_leaders;
+                ++dc.agg_lingering;
                 dc.agg_cv.wait_for(lk, std::chrono::microseconds(dc.agg_linger_us), [&] {
                     return me.done || dc.agg_qn >= kAggLingerPairs || dc.agg_nrun < 2;
                 });
+                --dc.agg_lingering;
                 --dc.agg_leaders;
                 if (me.done) break;
                 if (dc.agg_q.empty()) continue;       // another leader took every queued call
@@ -1743,6 +1750,7 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
             dc.agg_cv.wait(lk);
         }
     }
+    --dc.agg_inside;
     if (st) *st = me.st;
     return me.rc;
 }

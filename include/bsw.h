@@ -179,12 +179,13 @@ enum {
                                  group kernel (default 0 = never: measured slower at 10K-pair
                                  calls x 8 callers; an experiment knob).  Outputs
                                  are identical either way                                       */
-    BSW_OPT_COALESCE_LINGER = 16, /* microseconds (0..100000, default 0) a coalescing leader that
-                                 starts while another batch is in flight on its device waits for
-                                 more queued calls before taking the queue: concurrent callers'
-                                 next calls then ride in the same batch.  A lone caller never
-                                 waits.  An experiment knob: no gain measured.
-                                 Outputs are identical either way                                */
+    BSW_OPT_COALESCE_LINGER = 16, /* microseconds (0..100000, default 0): with more concurrent
+                                 callers than BSW_OPT_COALESCE_LEADERS and two or more batches
+                                 running, a new leader waits up to this long for 4096 queued pairs
+                                 (or for fewer than two running batches) before taking the queue,
+                                 so batches fill up.  Measured at 150: 8 callers +16-25% at 1K-4K
+                                 pairs per call, 4 / 16 callers mixed, hence off by
+                                 default.  A lone caller never waits.  Outputs are identical     */
     BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
 };
