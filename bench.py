@@ -565,7 +565,9 @@ def rccl_group(world):
     path is exercised on a one-GPU box too."""
     import datetime
     import torch.distributed as dist
-    to = datetime.timedelta(seconds=300)
+    # a collective that never completes (a rank that failed before it) ends the job at this
+    # timeout; 120 s bounds what a broken leg costs the driver's scaling run
+    to = datetime.timedelta(seconds=120)
     if world > 1:
         return dist.new_group(backend="nccl", timeout=to)
     if not dist.is_initialized():
@@ -1210,7 +1212,11 @@ def main_mem(args, rank, local, world, c1: bool):
     eng = bsw.Engine(device=local)
     bsw.set_reference(eng, T)
     opt = bsw.ext_opt(w=args.w, l_pac=len(ref))
-    mopt, copt = bsw.mem_opt(), bsw.chain_opt()
+    # BSW_BENCH_MEMOPT="max_mem_intv=0,split_factor=1000": seeding-option experiments (which pass
+    # costs what); the line's config then says so -- never a headline setting
+    mo_kw = {k: (float(v) if k == "split_factor" else int(v)) for k, v in
+             (x.split("=") for x in os.environ.get("BSW_BENCH_MEMOPT", "").split(",") if x)}
+    mopt, copt = bsw.mem_opt(**mo_kw), bsw.chain_opt()
     cap = 256 if n <= 2_000_000 else 64                  # interval slots per read (HBM: n * cap * 32 B)
     d_reads = hiprt.DeviceBuffer.from_array(reads)
     d_off, d_len = hiprt.DeviceBuffer.from_array(off), hiprt.DeviceBuffer.from_array(lens)
@@ -1284,7 +1290,8 @@ def main_mem(args, rank, local, world, c1: bool):
                                 f"C4 front end: {n} PE 150 bp reads/GPU vs a {args.ref_mb} Mb random reference") +
                                " -- FM-index SMEM seeding -> SA + mem_chain + mem_chain_flt -> mem_chain2aln, all on "
                                "the GPU, index / reads / two-strand text resident in HBM",
-                   "reads_per_gpu": n, "ref_bases": int(len(ref)), "parallelism": f"shard{world} (independent reads)"},
+                   "reads_per_gpu": n, "ref_bases": int(len(ref)), "parallelism": f"shard{world} (independent reads)",
+                   **({"seeding_options_EXPERIMENT": mo_kw} if mo_kw else {})},
         "reads_per_s_M": round(reads_s, 3),
         "extensions_per_s_M": round(n_ext_all / dt_max / 1e6, 3),
         "stage_ms": {"smem": round(float(pm[0]), 3), "chain": round(float(pm[1]), 3),
