@@ -1159,14 +1159,20 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     std::vector<BlkStat> bs;
     if (!prepass(pairs, n, bs)) return BSW_E_RANGE;
     if (chunk <= 0) chunk = n;
-    constexpr int nslots = 3;  // slots are taken as chunks start (a one-chunk call takes one)
+    // slots are taken as chunks start (a one-chunk call takes one); BSW_HP_SLOTS (2..6, default 3)
+    // is an experiment knob: chunk k + nslots stages only once chunk k's outputs are back
+    constexpr int kMaxSlots = 6;
+    static const int nslots = [] {
+        const char *e = getenv("BSW_HP_SLOTS");
+        return e ? std::min(6, std::max(2, atoi(e))) : 3;
+    }();
     int rc = BSW_OK;
-    std::unique_ptr<Slot> slots[nslots];
+    std::unique_ptr<Slot> slots[kMaxSlots];
     slots[0] = dc.acquire(rc);
     if (rc) return rc;
-    int32_t pend_at[nslots] = {}, pend_n[nslots] = {};  // chunk in flight per slot
-    int32_t pend_seq[nslots] = {-1, -1, -1};
-    int pend_mode[nslots] = {};
+    int32_t pend_at[kMaxSlots] = {}, pend_n[kMaxSlots] = {};  // chunk in flight per slot
+    int32_t pend_seq[kMaxSlots] = {-1, -1, -1, -1, -1, -1};
+    int pend_mode[kMaxSlots] = {};
     bsw_stats_t agg{};
     // Everything but the DP kernels runs on the slot's high-priority stream: the next chunk's
     // copies, unpack / plan / sort kernels and the outputs' readback are dispatched ahead of the
@@ -1178,7 +1184,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         std::condition_variable cv;
         struct Job { int first; int32_t second; int mode; };
         std::deque<Job> q;                        // (slot, seq, staging mode)
-        int32_t launched[nslots] = {-1, -1, -1};
+        int32_t launched[kMaxSlots] = {-1, -1, -1, -1, -1, -1};
         bool stop = false;
         int rc = BSW_OK;
     } L;
