@@ -430,7 +430,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
             const int c = q[b - 1];
             if (c > 3) break;
             const int m = x + 2 - b;                     // length of q[b - 1, x]
-            bcode |= (uint64_t)c << (2 * (m - 1));
+            if (m <= f.kt) bcode |= (uint64_t)c << (2 * (m - 1));   // (kt <= 15: the shift stays < 64)
             const IvT<U> ok = m <= f.kt ? ktab_get(f, m, bcode) : backward_ext(f, bk, c);
             if (ok.s < min_intv) break;
             bk = ok;
