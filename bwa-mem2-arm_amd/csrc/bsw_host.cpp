@@ -1395,7 +1395,10 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         const int32_t nblk = (int32_t)bs.size();
         const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
         // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
-        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
+        // the first chunk: 16 blocks (64K pairs) or 1/32 of the call; BSW_HP_FIRST_BLK (experiment
+        // knob) overrides the 16
+        static const int32_t kFirst = getenv("BSW_HP_FIRST_BLK") ? std::max(1, atoi(getenv("BSW_HP_FIRST_BLK"))) : 16;
+        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(kFirst, nblk / 32));
         for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 2)) {
             // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
             int64_t bytes = 0;
