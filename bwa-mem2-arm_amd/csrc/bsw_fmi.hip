@@ -969,6 +969,9 @@ int build_ktab(bsw_fmi_t *f, FmiDevT<U> &dv)
 {
     const int kt = ktab_levels(f->n);
     if (kt <= 0) return BSW_OK;
+    // ktab_pack keeps k, l and s in 40 bits: an index whose rows pass that runs without the table
+    // (every walk then extends base by base), as launch_collect's packed-entry guard does
+    if (sizeof(U) == 8 && (uint64_t)f->n + 2 >= (1ull << 40)) return BSW_OK;
     const size_t ents = (size_t)(((1ull << (2 * (kt + 1))) - 4) / 3);   // levels 1 .. kt
     int rc = hip_rc(hipMalloc(&f->d_ktab, ents * sizeof(uint4)));
     if (rc) return rc;

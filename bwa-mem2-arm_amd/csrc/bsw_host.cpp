@@ -259,10 +259,22 @@ static int hip_rc(hipError_t e)
 }
 #define BSW_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return ::bsw::hip_rc(_e); } while (0)
 
+// BSW_OPT_TEST_FAIL_ALLOC: this many upcoming buffer growths fail as out of memory (tests of the
+// host-buffer call's recovery, bsw.h); process-wide, 0 in production
+static std::atomic<int> g_fail_alloc{0};
+static bool inject_nomem()
+{
+    int v = g_fail_alloc.load(std::memory_order_relaxed);
+    while (v > 0)
+        if (g_fail_alloc.compare_exchange_weak(v, v - 1)) return true;
+    return false;
+}
+
 template <class T>
 static hipError_t grow(T *&p, size_t &cap, size_t need)   // cap counts elements (bytes for void)
 {
     if (need <= cap) return hipSuccess;
+    if (inject_nomem()) return hipErrorOutOfMemory;
     // 25% headroom: the pipeline's chunks vary (ramp, a merged remainder up to 1.25x) and slots
     // rotate between them, so exact-fit growth reallocated on many calls (hipFree syncs the device)
     const size_t n = std::max(need + need / 4, cap * 3 / 2);
@@ -358,6 +370,18 @@ struct DeviceCtx {
         if ((rc = hip_rc(hipMalloc((void **)&s->d_meta, kMetaWords * sizeof(int32_t))))) return nullptr;
         if ((rc = hip_rc(hipHostMalloc((void **)&s->h_meta, kMetaWords * sizeof(int32_t), 0)))) return nullptr;
         return s;
+    }
+    // free every cached slot (streams, events, device and pinned buffers): the first step of a
+    // failed call's recovery (scores_eb), so its rerun allocates afresh.  Slots other calls hold
+    // are untouched; they come back to the pool as usual
+    void trim()
+    {
+        std::vector<std::unique_ptr<Slot>> v;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            v.swap(free_slots);
+        }
+        for (auto &s : v) release_slot(s.get());
     }
     // rc != 0: the call failed part-way and may have left work queued on the slot's streams
     // (or the caller's stream it ran on) that still reads or writes the slot's buffers -- drain
@@ -1349,8 +1373,12 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         bool stop = false;
     } E;
     const int32_t nblk0 = (int32_t)bs.size();
+    // the first chunk: 16 blocks (64K pairs) or 1/32 of the call; BSW_HP_FIRST_BLK (experiment
+    // knob) overrides the 16.  The same size decides whether the call runs as several chunks
+    // (enqueuer thread) and cuts the chunks below
+    static const int32_t kFirst = getenv("BSW_HP_FIRST_BLK") ? std::max(1, atoi(getenv("BSW_HP_FIRST_BLK"))) : 16;
     const int32_t first_blk = std::min(std::max<int32_t>(1, chunk / kStageBlk),
-                                       nblk0 <= 32 ? nblk0 : std::max<int32_t>(16, nblk0 / 32));
+                                       nblk0 <= 32 ? nblk0 : std::max<int32_t>(kFirst, nblk0 / 32));
     const bool async = nblk0 > first_blk && getenv("BSW_HP_INLINE_ENQ") == nullptr;
     std::thread enqueuer;
     if (async)
@@ -1395,10 +1423,7 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         const int32_t nblk = (int32_t)bs.size();
         const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
         // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
-        // the first chunk: 16 blocks (64K pairs) or 1/32 of the call; BSW_HP_FIRST_BLK (experiment
-        // knob) overrides the 16
-        static const int32_t kFirst = getenv("BSW_HP_FIRST_BLK") ? std::max(1, atoi(getenv("BSW_HP_FIRST_BLK"))) : 16;
-        int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(kFirst, nblk / 32));
+        int32_t cur = first_blk;
         for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 2)) {
             // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
             int64_t bytes = 0;
@@ -2099,6 +2124,48 @@ static int one_device(bsw_ctx_t *ctx, int64_t n)
     return best;
 }
 
+// Recovery of a host-buffer range whose run on device d0 failed with BSW_E_NOMEM / BSW_E_HIP
+// (bsw.h, bsw_get_scores): 1. again on d0 after its cached slots are freed, 2. on each other
+// device of the context, 3. in halves (down to one 4096-pair staging block), each half the same
+// way.  No coalescing here: the range runs as a call of its own.  Outputs are identical to an
+// undisturbed call -- pairs are independent, and a failed run writes no input field (staged
+// records go back as outputs only or as the caller's own bytes).  `how` gets the deepest step
+// used.  Upstream plans to degrade on engine errors instead of aborting the run
+// (PHASE2_IMPLEMENTATION_SUMMARY.md:210-225); there is no CPU path to degrade to here.
+static bool recoverable(int rc) { return rc == BSW_E_NOMEM || rc == BSW_E_HIP; }
+
+static int recover_range(bsw_ctx_t *ctx, const KParams &kp, int d0, SeqPair *pairs, const uint8_t *ref,
+                         const uint8_t *qer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *st, int &how)
+{
+    const int nd = (int)ctx->devs.size();
+    int rc = BSW_E_HIP;
+    for (int k = 0; k < nd; ++k) {
+        const int d = (d0 + k) % nd;
+        DeviceCtx &dc = *ctx->devs[d];
+        dc.trim();
+        {
+            Inflight g(dc);
+            rc = host_shard(kp, dc, pairs, ref, qer, n, w, cell_bits, ctx->host_chunk, ctx->host_pack == 2, st);
+        }
+        if (rc == BSW_OK) {
+            how = std::max(how, k == 0 ? 1 : 2);
+            return BSW_OK;
+        }
+        if (!recoverable(rc)) return rc;
+    }
+    if (n <= kStageBlk) return rc;
+    const int32_t h = std::max<int32_t>(kStageBlk, (n / 2) & ~(kStageBlk - 1));
+    bsw_stats_t a{}, b{};
+    if ((rc = recover_range(ctx, kp, d0, pairs, ref, qer, h, w, cell_bits, &a, how))) return rc;
+    if ((rc = recover_range(ctx, kp, (d0 + 1) % nd, pairs + h, ref, qer, n - h, w, cell_bits, &b, how))) return rc;
+    how = std::max(how, 3);
+    *st = a;
+    st->kernel_ms += b.kernel_ms; st->stage_ms += b.stage_ms; st->host_ms += b.host_ms;
+    st->n_i16 += b.n_i16; st->n_u8 += b.n_u8; st->n_wide += b.n_wide; st->n_packed += b.n_packed;
+    st->n_launches += b.n_launches; st->n_wave += b.n_wave; st->n_group += b.n_group;
+    return BSW_OK;
+}
+
 int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *seqBufRef,
               const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits, bsw_stats_t *out)
 {
@@ -2121,14 +2188,19 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
                 return BSW_E_RANGE;
     std::vector<int> rcs(nd, BSW_OK);
     std::vector<bsw_stats_t> st(nd);
+    std::vector<int> how(nd, 0);
     if (nd == 1) {
-        Inflight g(*ctx->devs[one]);
-        if (n <= ctx->coalesce)             // kt_for-sized: coalesce with concurrent callers
-            rcs[0] = coalesced_call(kp, *ctx->devs[one], pairs, seqBufRef, seqBufQer, n, w, cell_bits,
+        {
+            Inflight g(*ctx->devs[one]);
+            if (n <= ctx->coalesce)             // kt_for-sized: coalesce with concurrent callers
+                rcs[0] = coalesced_call(kp, *ctx->devs[one], pairs, seqBufRef, seqBufQer, n, w, cell_bits,
+                                        ctx->host_chunk, ctx->host_pack == 2, &st[0]);
+            else
+                rcs[0] = host_shard(kp, *ctx->devs[one], pairs, seqBufRef, seqBufQer, n, w, cell_bits,
                                     ctx->host_chunk, ctx->host_pack == 2, &st[0]);
-        else
-            rcs[0] = host_shard(kp, *ctx->devs[one], pairs, seqBufRef, seqBufQer, n, w, cell_bits,
-                                ctx->host_chunk, ctx->host_pack == 2, &st[0]);
+        }
+        if (recoverable(rcs[0]))
+            rcs[0] = recover_range(ctx, kp, one, pairs, seqBufRef, seqBufQer, n, w, cell_bits, &st[0], how[0]);
     } else {
         // contiguous pair ranges of equal estimated work (static band cells)
         const std::vector<int32_t> cut = split_by_cells(pairs, n, w, nd);
@@ -2136,9 +2208,14 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
         for (int d = 0; d < nd; ++d) {
             const int32_t a = cut[d], b = cut[d + 1];
             th.emplace_back([&, d, a, b] {
-                Inflight g(*ctx->devs[d]);
-                rcs[d] = host_shard(kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a, w,
-                                    cell_bits, ctx->host_chunk, ctx->host_pack == 2, &st[d]);
+                {
+                    Inflight g(*ctx->devs[d]);
+                    rcs[d] = host_shard(kp, *ctx->devs[d], pairs + a, seqBufRef, seqBufQer, b - a, w,
+                                        cell_bits, ctx->host_chunk, ctx->host_pack == 2, &st[d]);
+                }
+                if (recoverable(rcs[d]))
+                    rcs[d] = recover_range(ctx, kp, d, pairs + a, seqBufRef, seqBufQer, b - a, w, cell_bits, &st[d],
+                                           how[d]);
             });
         }
         for (auto &t : th) t.join();
@@ -2152,6 +2229,7 @@ int scores_eb(bsw_ctx_t *ctx, int32_t end_bonus, SeqPair *pairs, const uint8_t *
         agg.n_wave += st[d].n_wave; agg.n_group += st[d].n_group;
         agg.stage_ms = std::max(agg.stage_ms, st[d].stage_ms);
         agg.host_ms = std::max(agg.host_ms, st[d].host_ms);
+        agg.recovery = std::max(agg.recovery, how[d]);
     }
     agg.n_devices = nd;
     *out = agg;
@@ -2654,6 +2732,10 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
         }
         return BSW_OK;
     case BSW_OPT_TEST_MISROUTE: if (!b01) return BSW_E_INVAL; ctx->kp.misroute = (int8_t)value; return BSW_OK;
+    case BSW_OPT_TEST_FAIL_ALLOC:
+        if (value < 0 || value > 1000000) return BSW_E_INVAL;
+        bsw::g_fail_alloc.store((int)value);
+        return BSW_OK;
     default: return BSW_E_INVAL;
     }
 }

@@ -40,10 +40,14 @@
 
 namespace bsw {
 
-constexpr int kPcChunkDw = 17;
+constexpr int kPcChunkDw = 17;           // dwords per lane per 64-row target chunk (as lane kernel)
 #ifdef BSW_PC_STATS
 __device__ unsigned long long g_pc_stats[8];
-#endif           // dwords per lane per 64-row target chunk (as lane kernel)
+// per-wave schedule record (tools/pc_times.py): start / end (s_memrealtime, 100 MHz), XCC id and
+// HW_ID (CU / SIMD / SE), rows run -- the launch's occupancy over time, ramp-up and tail
+constexpr int kPcTimesMax = 1 << 16;
+__device__ unsigned long long g_pc_times[kPcTimesMax][4];
+#endif
 
 struct PcRow {                           // per-row uniform (SGPR) group sets, bit G = group G
     uint64_t enter;                      // groups touching slots [min beg, max end]
@@ -587,6 +591,9 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
                                                     int32_t *__restrict__ err)
 {
     constexpr int NG = QMAX / 4;        // groups = query words (4 codes each)
+#ifdef BSW_PC_STATS
+    const unsigned long long t_wave0 = wall_clock64();
+#endif
     __shared__ uint32_t s_tgt[WPB][2][kPcChunkDw][64];   // 8.7 KB per wave
     __shared__ uint2 s_prof[8];                           // per-row score profiles, by target code
     if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
@@ -820,6 +827,16 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
             atomicAdd(&g_pc_stats[6], 1ull);
             atomicAdd(&g_pc_stats[7], (unsigned long long)nu);
         }
+        const unsigned wid = blockIdx.x * WPB + (threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0 && wid < (unsigned)kPcTimesMax) {
+            unsigned xcc, hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            g_pc_times[wid][0] = t_wave0;
+            g_pc_times[wid][1] = wall_clock64();
+            g_pc_times[wid][2] = ((unsigned long long)xcc << 32) | hw;
+            g_pc_times[wid][3] = rows;
+        }
     }
 #endif
     if (valid) {
@@ -842,6 +859,13 @@ extern "C" int bsw_pc_stats(unsigned long long *out, int reset)
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_pc_stats), z, sizeof(z)) != hipSuccess) return -5;
     }
     return 0;
+}
+// the per-wave schedule records of the last launch (n waves, 4 x u64 each)
+extern "C" int bsw_pc_times(unsigned long long *out, int n)
+{
+    n = n < kPcTimesMax ? n : kPcTimesMax;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pc_times), (size_t)n * 32) != hipSuccess) return -5;
+    return n;
 }
 #endif
 

@@ -47,6 +47,7 @@ OPT_COALESCE_LEADERS = 12
 OPT_GROUP_KERNEL = 13
 OPT_MID_BATCH = 14
 OPT_TEST_MISROUTE = 100
+OPT_TEST_FAIL_ALLOC = 101
 
 # include/bsw_ext.h structs
 SEED_DTYPE = np.dtype([("rbeg", np.int64), ("qbeg", np.int32), ("len", np.int32)])
@@ -75,7 +76,8 @@ class Stats(ctypes.Structure):
                 ("n_u8", ctypes.c_int32), ("n_wide", ctypes.c_int32),
                 ("n_launches", ctypes.c_int32), ("n_packed", ctypes.c_int32),
                 ("stage_ms", ctypes.c_float), ("host_ms", ctypes.c_float), ("n_wave", ctypes.c_int32),
-                ("n_devices", ctypes.c_int32), ("n_group", ctypes.c_int32)]
+                ("n_devices", ctypes.c_int32), ("n_group", ctypes.c_int32),
+                ("recovery", ctypes.c_int32)]
 
 
 def default_params(a=1, b=4, o_del=6, e_del=1, o_ins=6, e_ins=1, zdrop=100, end_bonus=5,
@@ -200,7 +202,7 @@ class Engine:
     _OPTS = {"kernel8": OPT_KERNEL8, "fork": OPT_FORK, "sortkey": OPT_SORTKEY, "glob_band": OPT_GLOB_BAND,
              "ext_chunk": OPT_EXT_CHUNK, "host_chunk": OPT_HOST_CHUNK, "long": OPT_LONG, "host_pack": OPT_HOST_PACK,
              "small_batch": OPT_SMALL_BATCH, "split_min": OPT_SPLIT_MIN, "coalesce": OPT_COALESCE, "coalesce_leaders": OPT_COALESCE_LEADERS, "group_kernel": OPT_GROUP_KERNEL, "mid_batch": OPT_MID_BATCH, "busy_min": 15, "coalesce_linger": 16,
-             "test_misroute": OPT_TEST_MISROUTE}
+             "test_misroute": OPT_TEST_MISROUTE, "test_fail_alloc": OPT_TEST_FAIL_ALLOC}
 
     def set_option(self, name, value: int):
         """bsw_set_option by name (kernel8, fork, sortkey, glob_band, ext_chunk, host_chunk, test_misroute)

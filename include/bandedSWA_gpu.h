@@ -121,6 +121,8 @@ private:
         snprintf(path, sizeof(path), "%s.%06u.bswb", record_, k);
         check(bswb_write(path, &params_, w, cell_bits, 1, pairs, n, ref, rb, qer, qb), "BSW_RECORD");
     }
+    // reached only after the engine's own recovery (bsw.h, bsw_get_scores: a failed device run is
+    // rerun on fresh buffers, on the context's other devices, then in halves) has also failed
     static void check(int rc, const char *what)
     {
         if (rc != BSW_OK) {

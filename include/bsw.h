@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BSW_ABI_VERSION 6
+#define BSW_ABI_VERSION 7
 
 enum {
     BSW_OK = 0,
@@ -82,7 +82,14 @@ void bsw_destroy(bsw_ctx_t *ctx);
 
 /* Blocking host-buffer call (drop-in for getScores16 / getScores8).
  * cell_bits: 16 -> int16 cells; 8 -> uint8 cells for pairs whose scores provably fit
- * (h0 + max(mat) * min(len1, len2) <= 255), int16 for the rest (overflow fallback). */
+ * (h0 + max(mat) * min(len1, len2) <= 255), int16 for the rest (overflow fallback).
+ * Recovery (ABI version 7): when a device run fails with BSW_E_NOMEM or BSW_E_HIP the call is
+ * run again before any error is returned -- once on the same device after its cached slots
+ * (streams + buffers) are freed, then on each other device of the context, then in halves
+ * (recursively, down to 4096 pairs), each half the same way.  Outputs are identical (pairs are
+ * independent; a failed run writes no input field).  bsw_last_stats().recovery says which step
+ * completed the call.  Upstream's plan for engine errors is to degrade, not abort
+ * (PHASE2_IMPLEMENTATION_SUMMARY.md:210-225); there is still no CPU path. */
 int  bsw_get_scores(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef,
                     const uint8_t *seqBufQer, int32_t n, int32_t w, int cell_bits);
 
@@ -112,6 +119,11 @@ typedef struct bsw_stats_t {
                                    (1, or all of them when split; ABI version 5)         */
     int32_t n_group;            /* of n_i16: pairs run on the small-batch row-group kernel
                                    (16 lanes per pair; ABI version 6)                    */
+    int32_t recovery;           /* host-buffer calls: how a call whose first run failed with
+                                   BSW_E_NOMEM / BSW_E_HIP was completed (ABI version 7):
+                                   0 = no failure, 1 = rerun on its device after the cached
+                                   slots were freed, 2 = rerun on another device of the
+                                   context, 3 = rerun in halves (see bsw_get_scores)      */
 } bsw_stats_t;
 int  bsw_last_stats(bsw_ctx_t *ctx, bsw_stats_t *out);
 
@@ -186,8 +198,12 @@ enum {
                                  so batches fill up.  Measured at 150: 8 callers +16-25% at 1K-4K
                                  pairs per call, 4 / 16 callers mixed, hence off by
                                  default.  A lone caller never waits.  Outputs are identical     */
-    BSW_OPT_TEST_MISROUTE = 100 /* tests only: 1 = every pair to the QMAX=32 lane class, so
+    BSW_OPT_TEST_MISROUTE = 100, /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
+    BSW_OPT_TEST_FAIL_ALLOC = 101 /* tests only: the next `value` (0..1000000) device buffer
+                                 allocations of the engine's host-buffer path fail with
+                                 hipErrorOutOfMemory (process-wide count), so the recovery of
+                                 bsw_get_scores can be exercised                               */
 };
 int  bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value);
 

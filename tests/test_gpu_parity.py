@@ -471,6 +471,44 @@ def test_group_kernel_golden(golden, quad):
         e.close()
 
 
+@pytest.mark.parametrize("w", [5, 100])
+def test_group_kernel_score_255_boundary(w):
+    """The row-group kernel's 8-bit row-max key (bsw_gq.hip, K8: H << 8 | j in 16 bits) holds only
+    when every live pair of the wave has h0 + min(qlen, tlen) <= 255.  Identical query / target
+    pairs with h0 = 255 - qlen drive H to exactly 255 on the diagonal; waves of four pairs (16
+    lanes each) mix them with pairs at h0 + qlen = 256 (the wave then runs the 16-bit key) and
+    with near-identical ones, in every position of the wave.  Host and device entry points, both
+    routed to the 16-lane form, equal the oracle."""
+    rng = np.random.default_rng(255 + w)
+    items = []
+    for k in range(64):
+        qlen = int(rng.choice([40, 100, 149, 150, 159, 160]))
+        q = rng.integers(0, 4, qlen).astype(np.uint8)
+        t = np.concatenate([q, rng.integers(0, 4, int(rng.integers(0, 140))).astype(np.uint8)])
+        over = (k // 4) % 3          # wave k // 4: all at 255 / one at 256 / all at 256
+        h0 = 255 - qlen + (1 if over == 2 or (over == 1 and k % 4 == (k // 12) % 4) else 0)
+        if k % 5 == 4:               # a mismatch somewhere: H stays below the bound
+            j = int(rng.integers(0, qlen))
+            q = q.copy()
+            q[j] = (q[j] + 1) & 3
+        items.append((t, q, h0))
+    pairs, ref, qer = bswgen.assemble(items)
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+    assert (want["score"] == 255).sum() >= 8 and (want["score"] == 256).sum() >= 8
+    e = bsw.Engine()
+    for cell_bits in (16, 8):
+        got = pairs.copy()
+        e.get_scores(got, ref, qer, w, cell_bits)
+        _assert_same(want, got, f"gq 255/256 host w={w} cell_bits={cell_bits}")
+        assert e.last_stats().n_group == len(pairs)
+    dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (pairs.copy(), ref, qer))
+    e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, len(pairs), w, 16)
+    _assert_same(want, dp.download(np.empty_like(pairs)), f"gq 255/256 device w={w}")
+    assert e.last_stats().n_group == len(pairs)
+    e.close()
+
+
 def test_group_kernel_fallback_device():
     """Device entry point, small batch with a few pairs outside the row-group contract (query past
     160, int16-unsafe h0): the kernel flags them and the whole batch reruns on the planned path."""
