@@ -365,9 +365,16 @@ def main():
                          "fixed batch of --total-pairs split over the ranks by band cells, host buffers "
                          "in, PCIe both ways inside the timed region (C5)")
     ap.add_argument("--total-pairs", type=int, default=10_000_000, help="strong: pairs in the whole batch")
-    ap.add_argument("--rccl-pairs", type=int, default=4_000_000,
+    ap.add_argument("--rccl-chunks", type=int, default=4,
+                    help="RCCL C2 leg: pieces per rank (chunk k + 1 scatters while chunk k is scored)")
+    ap.add_argument("--rccl-pairs", type=int, default=10_000_000,
                     help="default C2 line at N > 1: pairs of the strong-scaling RCCL leg reported beside the weak "
                          "value (one batch on GPU 0, RCCL scatter -> score -> RCCL gather); 0 = off")
+    ap.add_argument("--c5-reads", type=int, default=10_000_000,
+                    help="default C2 line at N > 1: PE reads of the C5 sub-object (BASELINE configs[4]: the read "
+                         "set resident on GPU 0, RCCL read scatter, the whole GPU front end on every rank, records "
+                         "gathered); 0 = off")
+    ap.add_argument("--c5-ref-mb", type=int, default=3000, help="C5 sub-object: reference size (Mb)")
     ap.add_argument("--transport", default="host", choices=("host", "rccl"),
                     help="strong: host (default) -- every rank holds its range in host memory and the call "
                          "stages it over its own PCIe link; rccl -- the whole batch resident on GPU 0, scattered "
@@ -447,15 +454,24 @@ def main():
     res = np.empty_like(pairs)
     d_pairs.download(res)
     # N > 1: the strong-scaling RCCL leg beside the weak value (every rank takes part)
-    rccl = None
-    if world > 1 and args.rccl_pairs > 0:
-        if args.distinct_gpus < world:
-            rccl = {"skipped": f"{world} ranks share {args.distinct_gpus} GPU(s) (--rehearse): RCCL needs one GPU per rank"}
-        else:
+    # N > 1: the strong-scaling RCCL legs beside the weak value (every rank takes part): the C2 batch
+    # scatter and C5 (BASELINE configs[4]: the PE read set over the whole front end).  Each leg's
+    # ranks agree over gloo before and after their RCCL phases, so a failing rank makes the leg
+    # report an error on every rank instead of leaving the others blocked in a collective
+    rccl = c5 = None
+    if world > 1:
+        share = f"{world} ranks share {args.distinct_gpus} GPU(s) (--rehearse): RCCL needs one GPU per rank"
+        def leg(fn, *a, **k):
             try:
-                rccl = rccl_c2_leg(args, rank, local, world, args.rccl_pairs, steps=10, warmup=2, eng=eng)
-            except Exception as e:  # noqa: BLE001  (the weak line still prints)
-                rccl = {"error": repr(e)[:400]}
+                return fn(*a, **k)
+            except Exception as e:  # noqa: BLE001  (symmetric failures: every rank lands here)
+                return {"error": repr(e)[:400]}
+        if args.rccl_pairs > 0:
+            rccl = {"skipped": share} if args.distinct_gpus < world else \
+                leg(rccl_c2_leg, args, rank, local, world, args.rccl_pairs, steps=10, warmup=2, eng=eng)
+        if args.c5_reads > 0:
+            c5 = {"skipped": share} if args.distinct_gpus < world else \
+                leg(rccl_c5_leg, args, rank, local, world, args.c5_reads, args.c5_ref_mb, steps=5, warmup=1)
     if rank != 0:
         return
     total_pairs = args.pairs * world * args.steps
@@ -520,6 +536,9 @@ def main():
         out["rehearsal"] = f"{world} ranks on {args.distinct_gpus} GPU(s): not a scaling measurement"
     if rccl is not None:
         out["rccl_strong"] = rccl
+    if c5 is not None:
+        out["c5"] = dict(c5, workload=f"C5 (BASELINE configs[4]): {args.c5_reads} PE 150 bp reads vs a "
+                                      f"{args.c5_ref_mb} Mb random reference, RCCL read scatter over {world} GPUs")
     if world == 1 and not args.no_host_path:
         hp = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res)
         out["abi_inclusive_value"] = hp.pop("value")
@@ -582,13 +601,17 @@ def rccl_group(world):
 
 def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump=""):
     """Strong scaling over RCCL (BASELINE configs[4]'s batch scatter): ONE batch of
-    `total` C2 pairs generated on rank 0 and resident on GPU 0 as one packed shard buffer per rank
-    (shards.BatchScatter: contiguous ranges of equal static band cells, records rebased to their
-    own windows), SCATTERED to the ranks' GPUs by RCCL, scored in place on every GPU
-    (bsw_get_scores_device on pointers into the received buffer), the 24 output bytes per pair
-    GATHERED back to GPU 0 by RCCL -- all three inside the timed region (barrier + device sync on
-    both sides, max over ranks).  Rank 0 then runs the whole batch alone on GPU 0 (the one-GPU
+    `total` C2 pairs generated on rank 0 and resident on GPU 0 in the engine's 2-bit wire form
+    (shards.BatchScatter: contiguous ranges of equal static band cells, each cut into
+    --rccl-chunks pieces packed by bsw_pack_batch, ~134 B per pair), SCATTERED chunk by chunk to the
+    ranks' GPUs by RCCL (every chunk's scatter issued at once), each piece scored in place as soon
+    as it lands (bsw_get_scores_packed_device on its own stream and thread, so pieces overlap on
+    the device), the 24 output bytes per pair GATHERED back to GPU 0 by RCCL chunk by chunk -- all
+    inside the timed region (barrier + device sync on both sides, max over ranks).  Rank 0 then
+    runs the whole batch alone on GPU 0 (bsw_get_scores_device on the resident batch: the one-GPU
     time of the same job, and the check that the gathered outputs are identical to it).
+    A rank whose scoring fails keeps taking part in every collective and the ranks agree on the
+    outcome over gloo afterwards (one rank must not leave the others blocked in RCCL).
     Returns the leg's dict on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
@@ -596,21 +619,28 @@ def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump="
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     g = rccl_group(world)
+    meta_g = dist.group.WORLD if world > 1 else None
     cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
     t0 = time.perf_counter()
     pairs = ref = qer = None
+    err = None
     if rank == 0:
-        pairs, ref, qer = bsw.synth_batch(total, cfg=cfg)
-    bs = shards.BatchScatter(rank, world, g, dev, pairs, ref, qer, w=args.w)
+        try:
+            pairs, ref, qer = bsw.synth_batch(total, cfg=cfg)
+        except Exception as e:  # noqa: BLE001
+            err = e
+    if not agree(err is None, world):
+        return {"error": f"batch generation failed: {err!r}"[:400]} if rank == 0 else None
+    bs = shards.BatchScatter(rank, world, g, dev, pairs, ref, qer, w=args.w, meta_group=meta_g,
+                             chunks=args.rccl_chunks)
     setup_s = time.perf_counter() - t0
     own = eng is None
     if own:
         eng = bsw.Engine(device=local)
 
-    def score(recv, row):
-        po, ro, qo = shards.offsets(row)
-        base = recv.data_ptr()
-        eng.get_scores_device(base + po, base + ro, base + qo, int(row[0]), args.w, args.cell_bits)
+    def score(c, recv, row, out):
+        eng.get_scores_packed_device(recv.data_ptr(), bsw.Packed.from_row(row), args.w, args.cell_bits,
+                                     out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
 
     for _ in range(warmup):
         bs.step(score)
@@ -623,12 +653,16 @@ def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump="
     barrier(world)
     dt = time.perf_counter() - t
     dt_max = allreduce_max(dt, world)
+    ok = bs.agree_ok()
     phase = {k: allreduce_max(float(np.mean(v)), world) for k, v in bs.ms.items()}
     rws = dist.get_world_size(g)
     if rank != 0:
         if own:
             eng.close()
         return None
+    if not ok:
+        return {"error": f"a rank's scoring failed: {bs.error!r}"[:400] if bs.error else "a rank's scoring failed",
+                "rccl_world_size": rws}
     res = bs.merged()
     if dump:
         np.save(dump, res)
@@ -651,15 +685,17 @@ def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump="
     return {
         "value": round(total * steps / dt_max / 1e6, 3), "unit": UNIT, "scaling": "strong",
         "ms_per_step": round(ms, 3), "steps": steps, "warmup": warmup,
-        "total_pairs": total, "pairs_rank0": bs.n_me, "shard_buffer_bytes": bs.S,
+        "total_pairs": total, "pairs_rank0": bs.n_me, "chunks": bs.chunks,
+        "wire_bytes_per_pair": round(bs.wire_bytes / total, 1), "shard_buffer_bytes": bs.S,
         "rccl_world_size": rws, "backend": dist.get_backend(g),
         "phase_ms_max_over_ranks": {k: round(v, 3) for k, v in phase.items()},
         "single_gpu_ms": round(one_ms, 3), "single_gpu_value": round(total / (one_ms * 1e-3) / 1e6, 3),
         "strong_speedup_vs_single_gpu": round(one_ms / ms, 3),
         "outputs_identical_to_single_gpu": bool(same),
         "setup_s": round(setup_s, 2),
-        "step": "RCCL scatter of the packed shard buffers from GPU 0 -> bsw_get_scores_device in place on "
-                "every GPU -> RCCL gather of 24 output bytes per pair to GPU 0 (all timed)",
+        "step": "RCCL scatter of every chunk's 2-bit wire-form pieces from GPU 0 (issued at once) -> "
+                "bsw_get_scores_packed_device on each piece as it lands (own stream per chunk) -> RCCL "
+                "gather of 24 output bytes per pair to GPU 0 per chunk (all timed)",
     }
 
 
@@ -669,6 +705,8 @@ def main_strong_rccl(args, rank, local, world):
     leg = rccl_c2_leg(args, rank, local, world, args.total_pairs, args.steps, args.warmup, dump=args.dump)
     if rank != 0:
         return
+    if "value" not in leg:
+        raise SystemExit(f"bench.py: the RCCL leg failed: {leg}")
     cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
     N = args.total_pairs
     out_j = {
@@ -752,38 +790,64 @@ class MemFrontEnd:
         return np.ascontiguousarray(rec[:ns].cpu().numpy()).view(shards.REC_DTYPE).reshape(-1)
 
 
-def main_mem_strong_rccl(args, rank, local, world):
-    """C5 as BASELINE configs[4] words it, on the full front end: ONE set of --reads PE reads
+def agree(ok: bool, world: int) -> bool:
+    """gloo all-reduce of a success flag: True only when every rank's `ok` is (ranks decide
+    together whether to enter the next RCCL phase, so none is left blocked in a collective)"""
+    if world == 1:
+        return ok
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([0 if ok else 1], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item()) == 0
+
+
+def rccl_c5_leg(args, rank, local, world, n_reads, ref_mb, steps, warmup, dump="", blocks_only=False):
+    """C5 as BASELINE configs[4] words it, on the full front end: ONE set of n_reads PE reads
     generated on rank 0 and resident on GPU 0, cut into contiguous read ranges and SCATTERED to the
     ranks' GPUs by RCCL (shards.ReadScatter); every rank runs SMEM seeding -> chaining ->
-    mem_chain2aln on its shard against its own index of the --ref-mb reference (built on its GPU
+    mem_chain2aln on its shard against its own index of the ref_mb reference (built on its GPU
     before timing); every seed's record (seed, read, chain, region, extended flag: 68 B) is
     GATHERED back to GPU 0 by RCCL.  Scatter, front end and gather are timed (barrier + sync on
     both sides, max over ranks).  Rank 0 then runs the whole read set alone on GPU 0: the one-GPU
-    time of the same job and the check that the gathered records are identical to it."""
+    time of the same job and the check that the gathered records are identical to it.  Ranks
+    agree over gloo before the first RCCL collective (a rank whose setup failed makes every rank
+    skip the leg) and after the timed steps (a failed front end is held, never left hanging).
+    Returns the leg's dict on rank 0 (an "error" entry if it failed), None elsewhere."""
     import torch
+    import torch.distributed as dist
     import shards
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    g = rccl_group(world)
     t0 = time.perf_counter()
-    log = lambda m: print(f"[bench c4mem-rccl rank {rank}] {m} ({time.perf_counter() - t0:.1f} s)",  # noqa: E731
+    log = lambda m: print(f"[bench c5 rank {rank}] {m} ({time.perf_counter() - t0:.1f} s)",  # noqa: E731
                           file=sys.stderr, flush=True)
-    ref = mem_reference(args.ref_mb)
-    reads = off = lens = None
-    if rank == 0:
-        reads, off, lens = pe_reads(ref, max(1, args.reads // 2), seed=42)
-    rs = shards.ReadScatter(rank, world, g, dev, reads, off, lens)
+    err = None
+    try:
+        ref = mem_reference(ref_mb)
+        reads = off = lens = None
+        if rank == 0:
+            reads, off, lens = pe_reads(ref, max(1, n_reads // 2), seed=42)
+        gen_s = time.perf_counter() - t0
+        t = time.perf_counter()
+        fmi = bsw.Fmi(ref, device=local, flags=(bsw.FMI_NO_TEXT if blocks_only else None))
+        build_s = time.perf_counter() - t
+        eng = bsw.Engine(device=local)
+        T = np.concatenate([ref, (3 - ref[::-1])]).astype(np.uint8)
+        bsw.set_reference(eng, T)
+        del T
+        l_pac = len(ref)
+    except Exception as e:  # noqa: BLE001
+        err = e
+    meta_g = dist.group.WORLD if world > 1 else None
+    if not agree(err is None, world):
+        return {"error": f"setup failed on a rank: {err!r}"[:400] if err else "setup failed on another rank"} \
+            if rank == 0 else None
+    g = rccl_group(world)
+    rs = shards.ReadScatter(rank, world, g, dev, reads, off, lens, meta_group=meta_g)
     N = int(rs.meta[:, 0].sum())
-    gen_s = time.perf_counter() - t0
-    log(f"{N} reads, {rs.n_me} on this rank")
-    t = time.perf_counter()
-    fmi = bsw.Fmi(ref, device=local, flags=(bsw.FMI_NO_TEXT if args.fmi_blocks_only else None))
-    build_s = time.perf_counter() - t
-    T = np.concatenate([ref, (3 - ref[::-1])]).astype(np.uint8)
-    eng = bsw.Engine(device=local)
-    bsw.set_reference(eng, T)
-    opt = bsw.ext_opt(w=args.w, l_pac=len(ref))
+    log(f"{N} reads, {rs.n_me} on this rank; index built in {build_s:.1f} s")
+    opt = bsw.ext_opt(w=args.w, l_pac=l_pac)
     cap = 256 if N <= 2_000_000 else 64                  # as one GPU would run the whole set (main_mem)
     fe = MemFrontEnd(fmi, eng, opt, rs.n_me, cap, dev, max(16, 4 * rs.n_me))
     o_reads, o_off, o_len = rs.layout()
@@ -798,31 +862,41 @@ def main_mem_strong_rccl(args, rank, local, world):
     score.n_ext = 0
     # sizing pass (untimed): the seed count fixes the gathered record capacity
     rs.scatter()
-    ns0 = score(rs.recv, rs.meta[rank], None) if rs.n_me > 0 else 0
+    try:
+        ns0 = score(rs.recv, rs.meta[rank], None) if rs.n_me > 0 else 0
+    except Exception as e:  # noqa: BLE001
+        err, ns0 = e, 0
     rs.size(ns0 + 16)
-    log(f"index built in {build_s:.1f} s; {ns0} seeds on this rank")
-    for _ in range(args.warmup):
+    if not agree(err is None, world):
+        fmi.close()
+        return {"error": f"sizing pass failed on a rank: {err!r}"[:400] if err else "sizing failed on another rank"} \
+            if rank == 0 else None
+    for _ in range(warmup):
         rs.step(score)
     for k in rs.ms:
         rs.ms[k].clear()
     score.n_ext = 0
     barrier(world)
     t = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         rs.step(score)
     barrier(world)
     dt = time.perf_counter() - t
     dt_max = allreduce_max(dt, world)
+    ok = rs.agree_ok()
     n_ext_all = allreduce_sum(score.n_ext, world)
     phase = {k: allreduce_max(float(np.mean(v)), world) for k, v in rs.ms.items()}
-    import torch.distributed as dist
     rws = dist.get_world_size(g)
     if rank != 0:
         fmi.close()
-        return
+        return None
+    if not ok:
+        fmi.close()
+        return {"error": f"a rank's front end failed: {rs.error!r}"[:400] if rs.error else "a rank's front end failed",
+                "rccl_world_size": rws}
     got = rs.merged()
-    if args.dump:
-        np.save(args.dump, got)
+    if dump:
+        np.save(dump, got)
     # the whole read set on GPU 0 alone (its own buffers; same index and engine)
     d_r = torch.from_numpy(reads).to(dev)
     d_o = torch.from_numpy(off.astype(np.int64)).to(dev)
@@ -837,11 +911,39 @@ def main_mem_strong_rccl(args, rank, local, world):
     want = one_fe.records(ns1)
     same = bool(len(want) == len(got) and np.array_equal(want.view(np.uint8), got.view(np.uint8)))
     fmi.close()
-    ms = dt_max / args.steps * 1e3
+    ms = dt_max / steps * 1e3
     one_ms = statistics.median(one[1:]) * 1e3
+    return {
+        "value": round(n_ext_all / dt_max / 1e6, 3), "unit": UNIT, "scaling": "strong",
+        "ms_per_step": round(ms, 3), "steps": steps, "warmup": warmup,
+        "reads_per_s_M": round(N * steps / dt_max / 1e6, 3),
+        "total_reads": N, "reads_rank0": rs.n_me, "ref_bases": int(l_pac),
+        "rccl_world_size": rws, "backend": dist.get_backend(g), "shard_buffer_bytes": rs.S,
+        "record_bytes_per_seed": shards.REC_DTYPE.itemsize, "record_capacity": rs.cap,
+        "phase_ms_max_over_ranks": {k: round(v, 3) for k, v in phase.items()},
+        "seeds": int(len(got)),
+        "single_gpu_ms": round(one_ms, 3), "strong_speedup_vs_single_gpu": round(one_ms / ms, 3),
+        "outputs_identical_to_single_gpu": same,
+        "index_build_s": round(build_s, 2), "synth_gen_s": round(gen_s, 2),
+        "step": "RCCL scatter of the PE read shards from GPU 0 -> every rank: SMEM seeding -> SA + mem_chain + "
+                "mem_chain_flt -> mem_chain2aln on its own GPU-resident index -> RCCL gather of the per-seed "
+                "records to GPU 0 (all timed)",
+    }
+
+
+def main_mem_strong_rccl(args, rank, local, world):
+    """C5 as its own line (--workload c4mem --scaling strong --transport rccl): rccl_c5_leg over
+    --reads PE reads vs a --ref-mb reference; value = extensions / max-over-ranks step time."""
+    leg = rccl_c5_leg(args, rank, local, world, args.reads, args.ref_mb, args.steps, args.warmup, dump=args.dump,
+                      blocks_only=args.fmi_blocks_only)
+    if rank != 0:
+        return
+    if "value" not in leg:
+        raise SystemExit(f"bench.py: the C5 leg failed: {leg}")
+    N = leg["total_reads"]
     out_j = {
-        "metric": METRIC, "value": round(n_ext_all / dt_max / 1e6, 3), "unit": UNIT, "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "metric": METRIC, "value": leg.pop("value"), "unit": UNIT, "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": leg.pop("ms_per_step"), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int16",
         "data": "synthetic PE reads (bench.pe_reads) from a bsw_synth.c random reference",
         "config": {"workload": f"C5 strong scaling, RCCL read scatter: one set of {N} PE 150 bp reads resident on "
@@ -849,17 +951,16 @@ def main_mem_strong_rccl(args, rank, local, world):
                                f"scattered with RCCL over xGMI; every rank: FM-index SMEM seeding -> SA + mem_chain "
                                f"+ mem_chain_flt -> mem_chain2aln on its own GPU-resident index; per-seed records "
                                f"gathered to GPU 0 with RCCL, inside the timed region",
-                   "total_reads": N, "reads_rank0": rs.n_me, "ref_bases": int(len(ref)),
+                   "total_reads": N, "reads_rank0": leg["reads_rank0"], "ref_bases": leg["ref_bases"],
                    "parallelism": f"split{world} (contiguous read ranges; RCCL scatter + gather)",
                    "distinct_gpus": args.distinct_gpus},
-        "reads_per_s_M": round(N * args.steps / dt_max / 1e6, 3),
-        "rccl": {"rccl_world_size": rws, "backend": dist.get_backend(g), "shard_buffer_bytes": rs.S,
-                 "record_bytes_per_seed": shards.REC_DTYPE.itemsize, "record_capacity": rs.cap,
-                 "phase_ms_max_over_ranks": {k: round(v, 3) for k, v in phase.items()}},
-        "seeds": int(len(got)),
-        "single_gpu_ms": round(one_ms, 3), "strong_speedup_vs_single_gpu": round(one_ms / ms, 3),
-        "outputs_identical_to_single_gpu": same,
-        "index_build_s": round(build_s, 2), "synth_gen_s": round(gen_s, 2),
+        "reads_per_s_M": leg["reads_per_s_M"],
+        "rccl": {k: leg[k] for k in ("rccl_world_size", "backend", "shard_buffer_bytes", "record_bytes_per_seed",
+                                     "record_capacity", "phase_ms_max_over_ranks")},
+        "seeds": leg["seeds"],
+        "single_gpu_ms": leg["single_gpu_ms"], "strong_speedup_vs_single_gpu": leg["strong_speedup_vs_single_gpu"],
+        "outputs_identical_to_single_gpu": leg["outputs_identical_to_single_gpu"],
+        "index_build_s": leg["index_build_s"], "synth_gen_s": leg["synth_gen_s"],
     }
     print(json.dumps(out_j), flush=True)
 

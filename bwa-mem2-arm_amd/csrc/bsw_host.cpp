@@ -2338,6 +2338,54 @@ int bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_ref
     return rc;
 }
 
+// The packed wire form (bsw_pack_batch) scored in place: one stage_in_kernel (2-bit unpack of both
+// extents, exception patches, 20-B records -> SeqPair, pads zeroed), the device pipeline, then the
+// 24 output bytes per pair compacted into d_out -- the path of a batch that arrived over RCCL
+int bsw_get_scores_packed_device(bsw_ctx_t *ctx, const void *d_packed, const bsw_packed_t *desc, int32_t w,
+                                 int cell_bits, int32_t *d_out, void *stream)
+{
+    if (!ctx || !desc) return BSW_E_INVAL;
+    const bsw_packed_t d = *desc;
+    if (d.n < 0 || w < 0 || (cell_bits != 8 && cell_bits != 16)) return BSW_E_INVAL;
+    if (d.n == 0) return BSW_OK;
+    if (!d_packed || !d_out || d.ref_bytes < 0 || d.qer_bytes < 0 || d.n_exc_ref < 0 || d.n_exc_qer < 0 ||
+        d.ref_bytes >= ((int64_t)1 << 28) || d.qer_bytes >= ((int64_t)1 << 28) ||
+        ((d.rec_off | d.ref_off | d.qer_off | d.exc_off) & 3) != 0)
+        return BSW_E_INVAL;
+    bsw::DeviceCtx &dc = *ctx->devs[0];
+    int rc = BSW_OK;
+    auto slot = dc.acquire(rc);
+    if (!slot) return rc;
+    bsw::Slot &s = *slot;
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        hipStream_t st = stream ? (hipStream_t)stream : s.stream;
+        BSW_TRY(bsw::grow(s.d_ref, s.cap_ref, (size_t)d.ref_bytes + 16));
+        BSW_TRY(bsw::grow(s.d_qer, s.cap_qer, (size_t)d.qer_bytes + 16));
+        BSW_TRY(bsw::grow(s.d_pairs, s.cap_pairs, (size_t)d.n));
+        const uint8_t *b = (const uint8_t *)d_packed;
+        const int64_t tr = (d.ref_bytes + 15) / 16, tq = (d.qer_bytes + 15) / 16;
+        const int64_t nthr = tr + tq + d.n;
+        hipLaunchKernelGGL(bsw::stage_in_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st,
+                           b + d.ref_off, d.ref_bytes, b + d.qer_off, d.qer_bytes, (const uint32_t *)(b + d.exc_off),
+                           d.n_exc_ref, d.n_exc_ref + d.n_exc_qer, (const bsw::PairIn *)(b + d.rec_off), d.n,
+                           s.d_ref, s.d_qer, s.d_pairs, (int32_t *)nullptr);
+        BSW_TRY(hipGetLastError());
+        int r = bsw::run_device(ctx->kp, s, s.d_pairs, s.d_ref, s.d_qer, d.n, w, cell_bits, st);
+        if (r) return r;
+        if ((r = bsw::finish_stats(s))) return r;
+        hipLaunchKernelGGL(bsw::gather_outputs_kernel, dim3((unsigned)((d.n + 255) / 256)), dim3(256), 0, st,
+                           s.d_pairs, d_out, d.n);
+        BSW_TRY(hipGetLastError());
+        BSW_TRY(hipStreamSynchronize(st));
+        std::lock_guard<std::mutex> g(ctx->stats_mu);
+        ctx->last = s.stats;
+        return BSW_OK;
+    }();
+    dc.give_back(std::move(slot), rc);
+    return rc;
+}
+
 int bsw_ksw_align2_device(bsw_ctx_t *ctx, const SeqPair *d_pairs, const uint8_t *d_ref,
                           const uint8_t *d_qer, int32_t n, bsw_kswr_t *d_aln, void *stream)
 {

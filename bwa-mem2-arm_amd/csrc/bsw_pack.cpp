@@ -6,6 +6,8 @@
 #include <immintrin.h>
 #include <cstdint>
 #include <cstddef>
+#include <algorithm>
+#include <cstring>
 #include <vector>
 #include "bsw_internal.h"
 
@@ -140,3 +142,65 @@ void pack_2bit(uint8_t *dst, const uint8_t *src, size_t nbytes, uint32_t pos0, s
 }
 
 }  // namespace bsw
+
+// bsw_pack_batch (bsw.h): the 2-bit wire form of a batch, host-only
+extern "C" int bsw_pack_batch(const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t n, void *dst,
+                              int64_t cap, bsw_packed_t *desc)
+{
+    if (!desc || n < 0 || (n > 0 && !pairs) || cap < 0) return BSW_E_INVAL;
+    int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        const SeqPair &p = pairs[i];
+        if (p.len1 < 0 || p.len2 < 0 || p.len1 > BSW_MAX_LEN || p.len2 > BSW_MAX_LEN || p.idr < 0 || p.idq < 0)
+            return BSW_E_RANGE;
+        if (p.len1 > 0) { r_lo = std::min<int64_t>(r_lo, p.idr); r_hi = std::max<int64_t>(r_hi, (int64_t)p.idr + p.len1); }
+        if (p.len2 > 0) { q_lo = std::min<int64_t>(q_lo, p.idq); q_hi = std::max<int64_t>(q_hi, (int64_t)p.idq + p.len2); }
+    }
+    if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+    if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+    const int64_t rb = r_hi - r_lo, qb = q_hi - q_lo;
+    if (rb >= ((int64_t)1 << 28) || qb >= ((int64_t)1 << 28)) return BSW_E_RANGE;
+    if ((rb > 0 && !ref) || (qb > 0 && !qer)) return BSW_E_INVAL;
+    auto count_exc = [](const uint8_t *s, int64_t len) {
+        int64_t c = 0;
+        for (int64_t k = 0; k < len; ++k) c += (s[k] & 0xfc) != 0;
+        return c;
+    };
+    const int64_t er = count_exc(ref + r_lo, rb), eq = count_exc(qer + q_lo, qb);
+    auto a256 = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    bsw_packed_t d{};
+    d.n = n;
+    d.n_exc_ref = (int32_t)er;
+    d.n_exc_qer = (int32_t)eq;
+    d.ref_bytes = rb;
+    d.qer_bytes = qb;
+    d.rec_off = 0;
+    d.ref_off = a256((int64_t)n * 20);
+    d.qer_off = a256(d.ref_off + (rb + 3) / 4 + 4);
+    d.exc_off = a256(d.qer_off + (qb + 3) / 4 + 4);
+    d.total_bytes = a256(d.exc_off + 4 * (er + eq));
+    *desc = d;
+    if (!dst) return BSW_OK;
+    if (cap < d.total_bytes) return BSW_E_INVAL;
+    uint8_t *h = (uint8_t *)dst;
+    int32_t *rec = (int32_t *)(h + d.rec_off);
+    for (int32_t i = 0; i < n; ++i) {
+        const SeqPair &p = pairs[i];
+        rec[5 * (int64_t)i + 0] = p.len1 > 0 ? (int32_t)(p.idr - r_lo) : 0;
+        rec[5 * (int64_t)i + 1] = p.len2 > 0 ? (int32_t)(p.idq - q_lo) : 0;
+        rec[5 * (int64_t)i + 2] = p.len1;
+        rec[5 * (int64_t)i + 3] = p.len2;
+        rec[5 * (int64_t)i + 4] = p.h0;
+    }
+    std::vector<uint32_t> exr, exq;
+    memset(h + d.ref_off, 0, (size_t)(d.qer_off - d.ref_off));
+    memset(h + d.qer_off, 0, (size_t)(d.exc_off - d.qer_off));
+    bsw::pack_2bit(h + d.ref_off, ref + r_lo, (size_t)rb, 0u, exr);
+    bsw::pack_2bit(h + d.qer_off, qer + q_lo, (size_t)qb, 0u, exq);
+    if ((int64_t)exr.size() != er || (int64_t)exq.size() != eq) return BSW_E_INVAL;   // (cannot happen)
+    uint32_t *ex = (uint32_t *)(h + d.exc_off);
+    if (er) memcpy(ex, exr.data(), 4 * (size_t)er);
+    if (eq) memcpy(ex + er, exq.data(), 4 * (size_t)eq);
+    memset(h + d.exc_off + 4 * (er + eq), 0, (size_t)(d.total_bytes - d.exc_off - 4 * (er + eq)));
+    return BSW_OK;
+}

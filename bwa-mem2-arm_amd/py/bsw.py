@@ -28,6 +28,7 @@ assert SEQPAIR_DTYPE.itemsize == 56
 # Every symbol include/bsw.h declares (tests check the library exports all of them).
 ABI_SYMBOLS = ("bsw_params_default", "bsw_create", "bsw_create_on", "bsw_destroy", "bsw_get_scores",
                "bsw_get_scores_device", "bsw_last_stats", "bsw_strerror", "bsw_abi_version",
+               "bsw_pack_batch", "bsw_get_scores_packed_device",
                "bsw_ext_opt_default", "bsw_extend_seeds", "bsw_ext_last_stats",
                "bswb_write", "bswb_read_header", "bswb_read",
                "bsw_ksw_align2", "bsw_ksw_align2_device", "bsw_mate_last_stats",
@@ -160,7 +161,10 @@ def hip_lib():
         L.bsw_mem_chain_device.argtypes = [P, P, P, ctypes.c_int32, P, ctypes.c_int32, P, P, P, P, ctypes.c_int64,
                                            P, P]
         L.bsw_mem_chain_device.restype = ctypes.c_int
+        L.bsw_pack_batch.argtypes = [P, P, P, ctypes.c_int32, P, ctypes.c_int64, P]
+        L.bsw_get_scores_packed_device.argtypes = [P, P, P, ctypes.c_int32, ctypes.c_int, P, P]
         for f in ("bsw_create", "bsw_create_on", "bsw_get_scores", "bsw_get_scores_device", "bsw_last_stats",
+                  "bsw_pack_batch", "bsw_get_scores_packed_device",
                   "bsw_abi_version", "bsw_extend_seeds", "bsw_ext_last_stats", "bswb_write",
                   "bswb_read_header", "bswb_read", "bsw_ksw_align2", "bsw_ksw_align2_device",
                   "bsw_mate_last_stats", "bsw_ksw_global2", "bsw_ksw_global2_device", "bsw_global_last_stats",
@@ -237,10 +241,51 @@ class Engine:
                                                ctypes.c_void_p(d_ref), ctypes.c_void_p(d_qer),
                                                n, w, cell_bits, ctypes.c_void_p(stream)))
 
+    def get_scores_packed_device(self, d_packed: int, desc: "Packed", w: int, cell_bits: int, d_out: int,
+                                 stream: int = 0):
+        """bsw_get_scores_packed_device: a packed batch (bsw_pack_batch) resident at d_packed;
+        the 6 output int32 per pair go to d_out."""
+        _check(hip_lib().bsw_get_scores_packed_device(self._ctx, ctypes.c_void_p(d_packed), ctypes.byref(desc), w,
+                                                      cell_bits, ctypes.c_void_p(d_out), ctypes.c_void_p(stream)))
+
     def last_stats(self) -> Stats:
         s = Stats()
         _check(hip_lib().bsw_last_stats(self._ctx, ctypes.byref(s)))
         return s
+
+
+class Packed(ctypes.Structure):
+    """bsw_packed_t: descriptor of a batch in the 2-bit wire form (bsw_pack_batch)"""
+    _fields_ = [("n", ctypes.c_int32), ("n_exc_ref", ctypes.c_int32), ("n_exc_qer", ctypes.c_int32),
+                ("pad_", ctypes.c_int32), ("ref_bytes", ctypes.c_int64), ("qer_bytes", ctypes.c_int64),
+                ("rec_off", ctypes.c_int64), ("ref_off", ctypes.c_int64), ("qer_off", ctypes.c_int64),
+                ("exc_off", ctypes.c_int64), ("total_bytes", ctypes.c_int64)]
+    FIELDS = ("n", "n_exc_ref", "n_exc_qer", "ref_bytes", "qer_bytes", "rec_off", "ref_off", "qer_off", "exc_off",
+              "total_bytes")
+
+    def to_row(self) -> np.ndarray:
+        return np.array([getattr(self, f) for f in self.FIELDS], dtype=np.int64)
+
+    @classmethod
+    def from_row(cls, row) -> "Packed":
+        d = cls()
+        for f, v in zip(cls.FIELDS, row):
+            setattr(d, f, int(v))
+        return d
+
+
+def pack_batch(pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray, pad_to: int = 0):
+    """bsw_pack_batch: (uint8 buffer, Packed) -- the 2-bit wire form of pairs over ref / qer,
+    zero-padded to pad_to bytes when that is larger (host-only, no device needed)."""
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    qer = np.ascontiguousarray(qer, dtype=np.uint8)
+    d = Packed()
+    L = hip_lib()
+    _check(L.bsw_pack_batch(_ptr(pairs), _ptr(ref), _ptr(qer), len(pairs), None, 0, ctypes.byref(d)))
+    buf = np.zeros(max(int(d.total_bytes), int(pad_to), 64), dtype=np.uint8)
+    _check(L.bsw_pack_batch(_ptr(pairs), _ptr(ref), _ptr(qer), len(pairs), _ptr(buf), len(buf), ctypes.byref(d)))
+    return buf, d
 
 
 def split_by_cells(pairs: np.ndarray, w: int, parts: int) -> np.ndarray:

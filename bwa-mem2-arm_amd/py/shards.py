@@ -1,16 +1,18 @@
 """Batch scatter / gather over ranks -- BASELINE configs[4]'s "batch scatter" of SeqPair batches.
 
 One batch (SeqPair records + the two byte buffers they index, upstream's layout) is cut into
-contiguous pair ranges of equal static band cells (bsw_split_by_cells).  Each
-range becomes ONE byte buffer
+contiguous pair ranges of equal static band cells (bsw_split_by_cells), one per
+rank, and each range into `chunks` contiguous pieces.  Every piece travels in the engine's 2-bit
+wire form (bsw_pack_batch, include/bsw.h: 20-B input records, 2-bit codes of the piece's byte
+extents, an exception word per non-ACGT byte -- ~133 B per C2 pair instead of 56 + 450), one
+scatter per chunk index, so chunk k + 1 moves while chunk k is scored; the rank scores each
+received piece in place (bsw_get_scores_packed_device: one unpack kernel, then the device
+pipeline) and its 24 output bytes per pair come back by one gather per chunk.  numpy here:
+bench.py moves the buffers as torch tensors between the GPUs (backend "nccl" = RCCL over xGMI),
+tests/test_dist.py as CPU tensors over gloo (with unpack_packed standing in for the device).
 
-    [SeqPair x n | ref bytes | qer bytes | zero padding]
-
-with idr / idq rebased to the range's own byte extents, every buffer padded to the largest, so a
-single scatter moves every rank's shard and the rank computes on it in place (bsw_get_scores_device
-on pointers into the buffer).  Outputs come back as 6 int32 per pair (score, tle, gtle, qle,
-gscore, max_off) by one gather.  numpy here: bench.py moves the buffers as torch tensors between
-the GPUs (backend "nccl" = RCCL over xGMI), tests/test_dist.py as CPU tensors over gloo."""
+(Round 4 moved whole 56-B records + 1 byte per base in one unchunked scatter: pack_shards /
+unpack_shard below, kept for the byte-layout tests.)"""
 
 import numpy as np
 
@@ -194,7 +196,15 @@ class ReadScatter:
         self.recv = torch.zeros(self.S, dtype=torch.uint8, device=device)
         self.cnt = torch.zeros(1, dtype=torch.int64, device=device)
         self.rec = None
+        self.error = None
         self.ms = {"scatter": [], "front_end": [], "gather": []}
+
+    def agree_ok(self) -> bool:
+        """collective over meta_group: True when no rank's score() failed"""
+        t = self._torch.tensor([0 if self.error is None else 1], dtype=self._torch.int64)
+        if self.world > 1:
+            self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX, group=self.meta_group)
+        return int(t.item()) == 0
 
     def layout(self):
         """(reads, off, lens) byte offsets of this rank's shard inside recv"""
@@ -223,13 +233,20 @@ class ReadScatter:
         self._sync()
 
     def step(self, score):
+        """one timed step; a score() failure (or more seeds than the capacity) is held in
+        self.error and this rank sends 0 records, so every rank still takes part in the gathers
+        (agree_ok() afterwards tells all ranks)"""
         import time
         t0 = time.perf_counter()
         self.scatter()
         t1 = time.perf_counter()
-        ns = score(self.recv, self.meta[self.rank], self.rec) if self.n_me > 0 else 0
-        if ns > self.cap:
-            raise RuntimeError(f"rank {self.rank}: {ns} seeds past the record capacity {self.cap}")
+        try:
+            ns = score(self.recv, self.meta[self.rank], self.rec) if self.n_me > 0 else 0
+            if ns > self.cap:
+                raise RuntimeError(f"rank {self.rank}: {ns} seeds past the record capacity {self.cap}")
+        except Exception as e:  # noqa: BLE001
+            self.error = self.error or e
+            ns = 0
         self.cnt.fill_(ns)
         t2 = time.perf_counter()
         if self.group is not None:
@@ -248,78 +265,207 @@ class ReadScatter:
         return merge_records([x.cpu().numpy() for x in self.g_rec], [int(x.item()) for x in self.g_cnt], self.cut)
 
 
+def unpack_packed(buf: np.ndarray, desc_row):
+    """numpy inverse of bsw_pack_batch (test stand-in for the device unpack): (pairs, ref, qer)
+    with idr / idq indexing the unpacked extents, outputs zeroed"""
+    d = bsw.Packed.from_row(desc_row)
+    n = d.n
+    rec = buf[d.rec_off:d.rec_off + 20 * n].view(np.int32).reshape(n, 5)
+    pairs = np.zeros(n, dtype=bsw.SEQPAIR_DTYPE)
+    for k, f in enumerate(("idr", "idq", "len1", "len2", "h0")):
+        pairs[f] = rec[:, k]
+
+    def codes(off, nb, exc):
+        b = buf[off:off + (nb + 3) // 4]
+        out = np.stack([(b >> (2 * k)) & 3 for k in range(4)], axis=1).reshape(-1)[:nb].astype(np.uint8)
+        out[(exc >> 4).astype(np.int64)] = (exc & 15).astype(np.uint8)
+        return out
+
+    exc = buf[d.exc_off:d.exc_off + 4 * (d.n_exc_ref + d.n_exc_qer)].view(np.uint32)
+    ref = codes(d.ref_off, d.ref_bytes, exc[:d.n_exc_ref])
+    qer = codes(d.qer_off, d.qer_bytes, exc[d.n_exc_ref:])
+    return pairs, ref, qer
+
+
+def chunk_cut(n: int, chunks: int) -> np.ndarray:
+    """contiguous pieces of one rank's range (equal pair counts)"""
+    return np.array([n * k // chunks for k in range(chunks + 1)], dtype=np.int64)
+
+
+def pack_chunks(pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray, cut, chunks: int):
+    """rank 0's packing (untimed): per rank r and chunk c the wire form of rank r's piece c.
+    Returns (bufs[r][c] uint8 arrays, desc [world, chunks, 10] int64, size [chunks]: the padded
+    buffer size of chunk index c, the max over ranks, a multiple of 256)."""
+    world = len(cut) - 1
+    bufs = [[None] * chunks for _ in range(world)]
+    desc = np.zeros((world, chunks, len(bsw.Packed.FIELDS)), dtype=np.int64)
+    for r in range(world):
+        lo, hi = int(cut[r]), int(cut[r + 1])
+        cc = chunk_cut(hi - lo, chunks)
+        for c in range(chunks):
+            b, d = bsw.pack_batch(np.ascontiguousarray(pairs[lo + cc[c]:lo + cc[c + 1]]), ref, qer)
+            bufs[r][c] = b
+            desc[r, c] = d.to_row()
+    size = np.array([max(256, (max(len(bufs[r][c]) for r in range(world)) + 255) & ~255) for c in range(chunks)],
+                    dtype=np.int64)
+    return bufs, desc, size
+
+
 class BatchScatter:
     """One fixed SeqPair batch held by rank 0, scored by every rank: the strong-scaling leg of
     bench.py (BASELINE configs[4]'s "RCCL-over-xGMI batch scatter") and of tests/test_dist.py.
 
-    Construction (collective, untimed): rank 0 cuts the batch by static band cells, packs one
-    buffer per rank (pack_shards) and keeps them on `device` (GPU 0 in bench.py); the per-rank
-    meta goes to every rank over `meta_group` (gloo).  step(score) (collective, timed by the
-    caller): `dist.scatter` of the shard buffers over `group` (backend "nccl" = RCCL in bench.py,
-    gloo on CPU in the tests), `score(recv, meta_row)` on the received buffer in place (the
-    caller's engine: bsw_get_scores_device on pointers into it, or the SSE4.1 restatement on
-    numpy views), the 6 output int32 per pair copied out of the scored records, `dist.gather` of
-    those blocks back to rank 0.  With group=None (one rank) a copy stands in for the scatter.
+    Construction (collective, untimed): rank 0 cuts the batch by static band cells, each rank's
+    range into `chunks` pieces, and packs every piece in the wire form (pack_chunks), keeping the
+    buffers on `device` (GPU 0 in bench.py); the descriptors go to every rank over `meta_group`
+    (gloo).  step(score) (collective, timed by the caller):
+      - every chunk's `dist.scatter` is issued at once (async, in chunk order, over `group`: backend
+        "nccl" = RCCL in bench.py, gloo in the tests);
+      - one thread per chunk waits for its scatter (on its own stream in bench.py, so the wait is
+        a device-side dependency) and calls score(c, recv[c], desc_row, out[c]) -- the engine's
+        bsw_get_scores_packed_device in bench.py, the numpy unpack + SSE4.1 restatement in the
+        tests -- which writes the piece's 6 output int32 per pair into out[c]; pieces of
+        different chunks therefore overlap on the device (no per-chunk drain);
+      - gathers of out[c] to rank 0, one per chunk, issued in chunk order as pieces finish.
+    With group=None (one rank) copies stand in for the collectives.  A score() failure is held
+    (self.error) while the collectives go on symmetrically -- one rank must not leave the others
+    blocked in a collective -- and agree_ok() reports it to every rank afterwards.
     merged() on rank 0: the whole batch's records with the gathered outputs written in."""
 
-    def __init__(self, rank, world, group, device, pairs=None, ref=None, qer=None, w=100, meta_group=None):
+    def __init__(self, rank, world, group, device, pairs=None, ref=None, qer=None, w=100, meta_group=None,
+                 chunks=4):
         import torch
         import torch.distributed as dist
         self.rank, self.world, self.group, self.device = rank, world, group, device
         self._torch, self._dist = torch, dist
-        meta_t = torch.zeros((world, 3), dtype=torch.int64)
+        self.meta_group = meta_group
         self.src = None
         self.pairs = self.cut = None
+        # chunk count: at least `chunks`, and enough that every piece's byte extents stay inside
+        # the wire form's 2^28-byte bound (with a 2x margin): decided on rank 0, broadcast
+        ch = torch.tensor([max(1, chunks)], dtype=torch.int64)
         if rank == 0:
             self.pairs = pairs
             self.cut = bsw.split_by_cells(pairs, w, world)
-            bufs, meta = pack_shards(pairs, ref, qer, self.cut)
-            meta_t.copy_(torch.from_numpy(meta))
-            self.src = [torch.from_numpy(bufs[k]).to(device) for k in range(world)]
+            for r in range(world):
+                p = pairs[int(self.cut[r]):int(self.cut[r + 1])]
+                for idx, ln in (("idr", "len1"), ("idq", "len2")):
+                    m = p[ln] > 0
+                    if m.any():
+                        ext = int((p[idx][m].astype(np.int64) + p[ln][m]).max() - p[idx][m].min())
+                        ch[0] = max(int(ch[0]), -(-ext // (1 << 27)))
+        if world > 1:
+            dist.broadcast(ch, src=0, group=meta_group)
+        chunks = self.chunks = int(ch.item())
+        nf = len(bsw.Packed.FIELDS)
+        meta_t = torch.zeros((world, chunks, nf + 1), dtype=torch.int64)
+        if rank == 0:
+            bufs, desc, size = pack_chunks(pairs, ref, qer, self.cut, chunks)
+            meta_t[:, :, :nf] = torch.from_numpy(desc)
+            meta_t[:, :, nf] = torch.from_numpy(np.broadcast_to(size, (world, chunks)).copy())
+            self.src = []
+            for c in range(chunks):
+                row = []
+                for r in range(world):
+                    t = torch.zeros(int(size[c]), dtype=torch.uint8)
+                    t[:len(bufs[r][c])] = torch.from_numpy(bufs[r][c])
+                    row.append(t.to(device))
+                self.src.append(row)
             del bufs
         if world > 1:
             dist.broadcast(meta_t, src=0, group=meta_group)
-        self.meta = meta_t.numpy().copy()
-        self.S = buffer_bytes(self.meta)
-        self.n_me = int(self.meta[rank, 0])
-        self.nmax = max(1, int(self.meta[:, 0].max()))
-        self.recv = torch.zeros(self.S, dtype=torch.uint8, device=device)
-        self.out_me = torch.zeros((self.nmax, 6), dtype=torch.int32, device=device)
-        self.gathered = ([torch.zeros((self.nmax, 6), dtype=torch.int32, device=device) for _ in range(world)]
-                         if rank == 0 else None)
-        self.ms = {"scatter": [], "score": [], "gather": []}
+        meta = meta_t.numpy().copy()
+        self.desc = meta[:, :, :nf]
+        self.size = meta[0, :, nf]
+        self.n_me = int(self.desc[rank, :, 0].sum())
+        self.nmax = [max(1, int(self.desc[:, c, 0].max())) for c in range(chunks)]
+        self.S = int(self.size.sum())                  # wire bytes per rank (padded)
+        self.wire_bytes = int(self.desc[:, :, -1].sum())   # total packed bytes of the batch
+        self.recv = [torch.zeros(int(self.size[c]), dtype=torch.uint8, device=device) for c in range(chunks)]
+        self.out = [torch.zeros((self.nmax[c], 6), dtype=torch.int32, device=device) for c in range(chunks)]
+        self.gathered = ([[torch.zeros((self.nmax[c], 6), dtype=torch.int32, device=device) for _ in range(world)]
+                          for c in range(chunks)] if rank == 0 else None)
+        # one stream per chunk (the scoring thread's current stream: its scatter's wait and the
+        # engine call are ordered on it)
+        self.streams = ([torch.cuda.Stream(device=device) for _ in range(chunks)] if device.type == "cuda"
+                        else None)
+        self.error = None
+        self.ms = {"scatter_first": [], "score_all": [], "gather_last": []}
 
     def _sync(self):
-        if self.recv.is_cuda:
-            self._torch.cuda.synchronize(self.recv.device)
+        if self.recv[0].is_cuda:
+            self._torch.cuda.synchronize(self.recv[0].device)
+
+    def _score_chunk(self, c, work, score, done):
+        import contextlib
+        ctx = (self._torch.cuda.stream(self.streams[c]) if self.streams is not None
+               else contextlib.nullcontext())
+        try:
+            with ctx:
+                if work is not None:
+                    work.wait()
+                if self.desc[self.rank, c, 0] > 0:
+                    score(c, self.recv[c], self.desc[self.rank, c], self.out[c])
+        except Exception as e:  # noqa: BLE001  (held: the collectives must go on on every rank)
+            self.error = self.error or e
+        finally:
+            done[c] = __import__("time").perf_counter()
 
     def step(self, score):
+        import threading
         import time
         dist = self._dist
         t0 = time.perf_counter()
         if self.group is not None:
-            dist.scatter(self.recv, self.src if self.rank == 0 else None, src=0, group=self.group)
+            works = [dist.scatter(self.recv[c], self.src[c] if self.rank == 0 else None, src=0, group=self.group,
+                                  async_op=True) for c in range(self.chunks)]
         else:
-            self.recv.copy_(self.src[0])
-        self._sync()                    # the engine runs on its own stream: the shard must be in
-        t1 = time.perf_counter()
-        n = self.n_me
-        if n > 0:
-            score(self.recv, self.meta[self.rank])
-            po = offsets(self.meta[self.rank])[0]
-            self.out_me[:n] = self.recv[po:po + 56 * n].view(self._torch.int32).view(n, 14)[:, OUT_COLS]
+            for c in range(self.chunks):
+                self.recv[c].copy_(self.src[c][0])
+            works = [None] * self.chunks
+        done = [0.0] * self.chunks
+        th = [threading.Thread(target=self._score_chunk, args=(c, works[c], score, done))
+              for c in range(self.chunks)]
+        for t in th:
+            t.start()
+        gw = []
+        for c, t in enumerate(th):
+            t.join()
+            if self.group is not None:
+                gw.append(dist.gather(self.out[c], self.gathered[c] if self.rank == 0 else None, dst=0,
+                                      group=self.group, async_op=True))
         t2 = time.perf_counter()
-        if self.group is not None:
-            dist.gather(self.out_me, self.gathered, dst=0, group=self.group)
+        for g in gw:
+            g.wait()
         self._sync()
         t3 = time.perf_counter()
-        for k, a, b in (("scatter", t0, t1), ("score", t1, t2), ("gather", t2, t3)):
-            self.ms[k].append((b - a) * 1e3)
+        self.ms["scatter_first"].append((done[0] - t0) * 1e3)
+        self.ms["score_all"].append((t2 - t0) * 1e3)
+        self.ms["gather_last"].append((t3 - t2) * 1e3)
+
+    def agree_ok(self) -> bool:
+        """collective over meta_group: True when no rank's score() failed"""
+        torch = self._torch
+        t = torch.tensor([0 if self.error is None else 1], dtype=torch.int64)
+        if self.world > 1:
+            self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX, group=self.meta_group)
+        return int(t.item()) == 0
+
+    def outputs_of(self, c, r):
+        """rank 0: the gathered [n, 6] outputs of rank r's chunk c (numpy)"""
+        n = int(self.desc[r, c, 0])
+        src = self.gathered[c][r] if self.group is not None else self.out[c]
+        return src[:n].cpu().numpy()
 
     def merged(self) -> np.ndarray:
         """rank 0: a copy of the batch with every rank's gathered outputs written in"""
-        outs = ([x.cpu().numpy() for x in self.gathered] if self.group is not None
-                else [self.out_me.cpu().numpy()])
         res = self.pairs.copy()
-        merge_outputs(res, outs, self.cut)
+        v = res.view(np.int32).reshape(-1, 14)
+        for r in range(self.world):
+            lo, hi = int(self.cut[r]), int(self.cut[r + 1])
+            cc = chunk_cut(hi - lo, self.chunks)
+            for c in range(self.chunks):
+                a, b = lo + int(cc[c]), lo + int(cc[c + 1])
+                if b > a:
+                    v[a:b, OUT_COLS] = self.outputs_of(c, r)
         return res

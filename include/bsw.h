@@ -101,6 +101,35 @@ int  bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_re
                            const uint8_t *d_qer, int32_t n, int32_t w, int cell_bits,
                            void *stream);
 
+/* 2-bit wire form of a SeqPair batch (ABI version 7): the host pipeline's staging format made a
+ * transport format, ~133 bytes per C2 pair instead of 56 + 450 -- what a batch scatter moves
+ * between GPUs (bench.py's RCCL legs).  One buffer, offsets 256-aligned:
+ *   [rec: n x 20 B {idr, idq, len1, len2, h0} | ref: 2-bit codes of the batch's ref extent + 4 pad
+ *    | qer: the same for its qer extent | exc: one uint32 pos << 4 | code per byte outside 0..3
+ *    (ref ones first, then qer ones, ascending)]
+ * idr / idq are rebased to the extents (empty sequences: 0).  Extents must stay below 2^28 bytes
+ * (exception positions are 28 bits): larger batches are packed in pieces. */
+typedef struct bsw_packed_t {
+    int32_t n;                            /* pairs                                        */
+    int32_t n_exc_ref, n_exc_qer;         /* exception words of each extent               */
+    int32_t pad_;
+    int64_t ref_bytes, qer_bytes;         /* extent lengths (unpacked bytes)              */
+    int64_t rec_off, ref_off, qer_off, exc_off, total_bytes;
+} bsw_packed_t;
+/* Host-only.  Fills *desc for pairs[0, n) over seqBufRef / seqBufQer; with dst == NULL only sizes
+ * it (desc->total_bytes), else writes the packed batch into dst (cap bytes, >= total_bytes).
+ * BSW_E_RANGE: a bad pair (negative or > BSW_MAX_LEN length, negative offset) or an extent past
+ * 2^28 bytes. */
+int  bsw_pack_batch(const SeqPair *pairs, const uint8_t *seqBufRef, const uint8_t *seqBufQer, int32_t n,
+                    void *dst, int64_t cap, bsw_packed_t *desc);
+/* Device-resident scoring of a packed batch on the context's first device: d_packed is the
+ * buffer bsw_pack_batch wrote (desc its descriptor), now in HBM; the six outputs of pair p are
+ * written to d_out[6p .. 6p+5] (score, tle, gtle, qle, gscore, max_off: 24 B per pair, the
+ * gather's payload).  Unpack (one kernel), plan / sort / DP as bsw_get_scores_device, outputs
+ * compacted.  Runs on `stream` (NULL: the context's own) and returns when d_out is written. */
+int  bsw_get_scores_packed_device(bsw_ctx_t *ctx, const void *d_packed, const bsw_packed_t *desc,
+                                  int32_t w, int cell_bits, int32_t *d_out, void *stream);
+
 /* Per-call statistics of the last bsw_get_scores_device / bsw_get_scores on this
  * thread: the hot kernel's event-timed duration (ms) and the pairs routed per kernel. */
 typedef struct bsw_stats_t {

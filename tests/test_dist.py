@@ -81,12 +81,16 @@ def test_synth_shards_tile_global_batch():
     assert np.array_equal(np.concatenate([a["h0"], b["h0"]]), full["h0"])
 
 
-def _scatter_worker(rank, world, port, n, q):
+def _scatter_worker(rank, world, port, n, q, chunks, fail_rank):
     """bench.py's strong-scaling RCCL leg (rccl_c2_leg / --transport rccl) on CPU tensors over
-    gloo, through the same orchestration code (shards.BatchScatter): rank 0 packs the whole
-    batch, scatters one padded buffer per rank, every rank scores its shard in place (the SSE4.1
-    restatement stands in for the GPU here), the 6 outputs per pair are gathered back to rank 0
-    and merged; two steps, so the buffers are reused as in the timed loop."""
+    gloo, through the same orchestration code (shards.BatchScatter): rank 0 cuts the batch by band
+    cells and packs every rank's range in `chunks` pieces of the 2-bit wire form (bsw_pack_batch),
+    every chunk is scattered (async, all at once), each rank scores its pieces in place on one
+    thread per chunk (numpy unpack + the SSE4.1 restatement stand in for the GPU), the 6 outputs
+    per pair are gathered back to rank 0 chunk by chunk and merged; two steps, so the buffers are
+    reused as in the timed loop.  fail_rank >= 0: that rank's score raises on chunk 0 of the
+    second step -- every rank must still finish the step's collectives and then agree the leg
+    failed."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -97,34 +101,48 @@ def _scatter_worker(rank, world, port, n, q):
         pairs, ref, qer = bsw.synth_batch(n)
         pairs["len2"][::97] = 0                       # empty queries / targets inside a shard
         pairs["len1"][5::89] = 0
-    bs = shards.BatchScatter(rank, world, dist.group.WORLD, torch.device("cpu"), pairs, ref, qer, w=100)
+        qer[11::503] = 4                              # N bases: exception words of the wire form
+        ref[3::701] = 4
+    bs = shards.BatchScatter(rank, world, dist.group.WORLD, torch.device("cpu"), pairs, ref, qer, w=100,
+                             meta_group=dist.group.WORLD, chunks=chunks)
+    calls = []
 
-    def score(recv, row):
-        p, r, qq = shards.unpack_shard(recv.numpy(), row)
+    def score(c, recv, row, out):
+        calls.append(c)
+        if rank == fail_rank and len(calls) > chunks and c == 0:
+            raise RuntimeError("injected")
+        p, r, qq = shards.unpack_packed(recv.numpy(), row)
         oracle.sse41_get_scores16(oracle.make_params(), p, r, qq, 100, 1)
+        out[:len(p)] = torch.from_numpy(shards.outputs(p))
 
     for _ in range(2):
         bs.step(score)
+    ok = bs.agree_ok()
     if rank == 0:
-        res = bs.merged()
-        want = pairs.copy()
-        oracle.get_scores(oracle.make_params(), want, ref, qer, 100)
-        q.put(all(np.array_equal(res[f], want[f]) for f in bsw.OUT_FIELDS) and
-              all(np.array_equal(res[f], pairs[f]) for f in ("idr", "idq", "len1", "len2", "h0")) and
-              all(len(v) == 2 for v in bs.ms.values()) and
-              int(bs.meta[:, 0].sum()) == n)
+        if fail_rank >= 0:
+            q.put(not ok)
+        else:
+            res = bs.merged()
+            want = pairs.copy()
+            oracle.get_scores(oracle.make_params(), want, ref, qer, 100)
+            q.put(ok and
+                  all(np.array_equal(res[f], want[f]) for f in bsw.OUT_FIELDS) and
+                  all(np.array_equal(res[f], pairs[f]) for f in ("idr", "idq", "len1", "len2", "h0")) and
+                  all(len(v) == 2 for v in bs.ms.values()) and
+                  int(bs.desc[:, :, 0].sum()) == n and bs.wire_bytes < n * 150)
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3])
-def test_scatter_gather_shards_equal_single_process(world):
+@pytest.mark.parametrize("world,chunks,fail_rank", [(2, 1, -1), (2, 4, -1), (3, 3, -1), (3, 2, 1)])
+def test_scatter_gather_shards_equal_single_process(world, chunks, fail_rank):
     n = 1500
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, n, q, chunks, fail_rank))
+             for r in range(world)]
     for p in procs:
         p.start()
     ok = q.get(timeout=240)
@@ -132,6 +150,47 @@ def test_scatter_gather_shards_equal_single_process(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert ok
+
+
+def test_packed_wire_form_roundtrip():
+    """bsw_pack_batch (host-only) and its numpy inverse: records rebased to the extents, codes
+    (incl. N and other non-ACGT bytes as exception words) and outputs of the oracle identical"""
+    import shards
+    pairs, ref, qer = bsw.synth_batch(3000)
+    qer[5::97] = 4
+    ref[7::131] = 4
+    ref[9::1009] = 7                                   # any code outside 0..3 survives
+    pairs["len1"][::50] = 0
+    for lo, hi in ((0, 3000), (17, 1234), (2999, 3000), (5, 5)):
+        sub = np.ascontiguousarray(pairs[lo:hi])
+        buf, d = bsw.pack_batch(sub, ref, qer)
+        assert d.n == hi - lo and d.total_bytes % 256 == 0 and d.total_bytes <= len(buf)
+        p, r, qq = shards.unpack_packed(buf, d.to_row())
+        for i in range(len(sub)):
+            a, b = sub[i], p[i]
+            assert (a["len1"], a["len2"], a["h0"]) == (b["len1"], b["len2"], b["h0"])
+            assert np.array_equal(ref[a["idr"]:a["idr"] + a["len1"]], r[b["idr"]:b["idr"] + b["len1"]])
+            assert np.array_equal(qer[a["idq"]:a["idq"] + a["len2"]], qq[b["idq"]:b["idq"] + b["len2"]])
+        if hi - lo > 1000:
+            assert d.n_exc_ref > 0 and d.n_exc_qer > 0
+            assert d.total_bytes < (hi - lo) * 160        # vs 56 + 450 bytes per pair unpacked
+            w1, w2 = sub.copy(), p.copy()
+            oracle.get_scores(oracle.make_params(), w1, ref, qer, 100)
+            oracle.get_scores(oracle.make_params(), w2, r, qq, 100)
+            for f in bsw.OUT_FIELDS:
+                assert np.array_equal(w1[f], w2[f])
+
+
+def test_packed_wire_form_errors():
+    pairs, ref, qer = bsw.synth_batch(10)
+    bad = pairs.copy()
+    bad["len1"][3] = -1
+    with pytest.raises(bsw.BswError):
+        bsw.pack_batch(bad, ref, qer)
+    big = pairs[:2].copy()
+    big["idr"][1] = (1 << 28)                           # extent past 2^28 bytes
+    with pytest.raises(bsw.BswError):
+        bsw.pack_batch(big, np.zeros((1 << 28) + 400, np.uint8), qer)
 
 
 def _read_scatter_worker(rank, world, port, nreads, q):

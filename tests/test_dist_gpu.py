@@ -100,15 +100,15 @@ def test_ranks_c4_pe_workload_equal_oracle(tmp_path, workload):
 
 @pytest.mark.gpu
 def test_rccl_transport_one_rank_equal_oracle(tmp_path):
-    """bench.py --scaling strong --transport rccl with one rank: the batch packed into its shard
-    buffer (shards.py), resident on GPU 0 as a torch tensor, scored in place through
-    bsw_get_scores_device on pointers into that tensor, the outputs read back through the same
-    torch views the RCCL gather moves.  (RCCL itself needs one GPU per rank: the N > 1 scatter /
+    """bench.py --scaling strong --transport rccl with one rank: the batch packed in the 2-bit wire
+    form (bsw_pack_batch, three pieces), resident on GPU 0 as torch tensors, scattered by a one-rank
+    RCCL communicator, each piece scored in place through bsw_get_scores_packed_device on its own
+    stream and thread, the outputs gathered back through the same torch tensors RCCL moves.  (RCCL itself needs one GPU per rank: the N > 1 scatter /
     gather logic is covered over gloo by tests/test_dist.py; the 8-GPU run is the driver's.)"""
     n = 150_000
     dump = str(tmp_path / "rccl.npy")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--scaling", "strong", "--transport", "rccl",
-           "--total-pairs", str(n), "--steps", "2", "--warmup", "1", "--dump", dump]
+           "--total-pairs", str(n), "--rccl-chunks", "3", "--steps", "2", "--warmup", "1", "--dump", dump]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
@@ -116,6 +116,8 @@ def test_rccl_transport_one_rank_equal_oracle(tmp_path):
     # a one-rank RCCL communicator carried the scatter / gather (backend nccl = RCCL on ROCm)
     assert line["rccl"]["rccl_world_size"] == 1 and line["rccl"]["backend"] == "nccl"
     assert line["rccl"]["outputs_identical_to_single_gpu"] is True
+    # the 2-bit wire form (bsw_pack_batch), three pieces per rank scattered / scored / gathered
+    assert line["rccl"]["chunks"] == 3 and line["rccl"]["wire_bytes_per_pair"] < 150
     got = np.load(dump)
     full, ref, qer = bsw.synth_batch(n)
     want = full.copy()

@@ -509,6 +509,35 @@ def test_group_kernel_score_255_boundary(w):
     e.close()
 
 
+@pytest.mark.parametrize("n", [0, 1, 700, 40_000])
+def test_packed_device_equal_oracle(n):
+    """bsw_get_scores_packed_device: a batch in the 2-bit wire form (bsw_pack_batch: 20-B records,
+    2-bit codes, exception words for N and other non-ACGT bytes) uploaded as one buffer, unpacked
+    on the device and scored; the 24 output bytes per pair equal the oracle.  Small batches take
+    the row-group kernel, 40K pairs the planned path; mixed shapes include long queries and
+    int16-unsafe h0 (several kernel classes)."""
+    pairs, ref, qer = bswgen.random_pairs(max(n, 1), seed=600 + n, qlen=(0, 300), tlen=(0, 400), h0=(0, 300))
+    pairs = pairs[:n]
+    qer[7::61] = 4
+    ref[3::89] = 4
+    if n > 100:
+        pairs["h0"][::37] = 32000
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    buf, d = bsw.pack_batch(pairs, ref, qer)
+    db = hiprt.DeviceBuffer.from_array(buf)
+    out = np.full((max(n, 1), 6), -7, dtype=np.int32)
+    dout = hiprt.DeviceBuffer.from_array(out)
+    e = bsw.Engine()
+    for cell_bits in (16, 8):
+        e.get_scores_packed_device(db.ptr, d, 100, cell_bits, dout.ptr)
+        got = dout.download(np.empty_like(out))[:n]
+        for k, f in enumerate(bsw.OUT_FIELDS):
+            bad = int((got[:, k] != want[f]).sum())
+            assert bad == 0, f"packed n={n} cell_bits={cell_bits}: {f} differs in {bad} pairs"
+    e.close()
+
+
 def test_group_kernel_fallback_device():
     """Device entry point, small batch with a few pairs outside the row-group contract (query past
     160, int16-unsafe h0): the kernel flags them and the whole batch reruns on the planned path."""
