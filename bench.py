@@ -11,7 +11,8 @@ DP kernel + results written back into the SeqPair records in HBM).  Inputs are r
 HBM before timing starts.  N GPUs: one process per GPU (torchrun), each with its own
 1M-pair shard (weak scaling, pairs are independent -> no data-path collective); the
 control plane (barriers, max-over-ranks timing) is torch.distributed/gloo.  At N > 1 the
-same line also carries `rccl_strong`: ONE fixed batch (--rccl-pairs, 4M) resident on GPU 0,
+same line also carries `rccl_strong`: ONE fixed batch (--rccl-pairs, 6M: SeqPair's int32 idr
+addresses at most ~7M C2 windows of 300 bytes) resident on GPU 0 in the 2-bit wire form,
 scattered to the ranks' GPUs over an nccl (= RCCL) group, scored in place, outputs gathered
 back to GPU 0, all timed -- with rccl_world_size and the check that the gathered outputs are
 identical to the same batch scored on GPU 0 alone (BASELINE configs[4]'s batch scatter).
@@ -367,7 +368,7 @@ def main():
     ap.add_argument("--total-pairs", type=int, default=10_000_000, help="strong: pairs in the whole batch")
     ap.add_argument("--rccl-chunks", type=int, default=4,
                     help="RCCL C2 leg: pieces per rank (chunk k + 1 scatters while chunk k is scored)")
-    ap.add_argument("--rccl-pairs", type=int, default=10_000_000,
+    ap.add_argument("--rccl-pairs", type=int, default=6_000_000,
                     help="default C2 line at N > 1: pairs of the strong-scaling RCCL leg reported beside the weak "
                          "value (one batch on GPU 0, RCCL scatter -> score -> RCCL gather); 0 = off")
     ap.add_argument("--c5-reads", type=int, default=10_000_000,
@@ -544,7 +545,7 @@ def main():
         out["abi_inclusive_value"] = hp.pop("value")
         out["abi_inclusive"] = dict(hp, unit=UNIT, note="bsw_get_scores on pageable host buffers: staging "
                                     "(2-bit codes, 20-B input records) + H2D + plan/sort/DP + D2H of the outputs, "
-                                    "chunked pipeline over three slots")
+                                    "chunked pipeline over four slots")
         # the same curve from C++ kt_for-style threads through the C ABI (tools/percall_bench.cpp:
         # no Python between calls), with and without cross-call coalescing
         import subprocess
@@ -1433,16 +1434,20 @@ def main_mem(args, rank, local, world, c1: bool):
         t = time.perf_counter()
         cpu_front(S1, 1)
         dt_1 = time.perf_counter() - t
+        oracle.FmiRef.counters(reset=True)
         t = time.perf_counter()
         w_seeds, w_sr, w_sc, want, wext = cpu_front(S, nt)
         dt_cpu = time.perf_counter() - t
+        n_bext, n_blocks = oracle.FmiRef.counters()
         k = int(np.searchsorted(sr, S))
         same = bool(len(w_seeds) == k and np.array_equal(w_sr, sr[:k]) and np.array_equal(w_sc, sc[:k]) and
                     np.array_equal(wext, ext[:k]) and all(np.array_equal(want[f], out[:k][f])
                                                           for f in bsw.ALNREG_DTYPE.names))
         rps = S / dt_cpu / 1e6
         out_j["cpu_baseline"] = {
-            "value": round(rps, 5) if c1 else None, "unit": "M reads/s", "cores": nt, "kind": "port",
+            "value": round(rps, 5) if c1 else None, "unit": "M reads/s", "cores": nt, "kind": "oracle",
+            "kind_note": "the scalar oracle pipeline (oracle/*.c restatements of bwa's algorithms, written for "
+                         "checking, not speed) -- NOT the reference's optimized CPU path; see reference_published",
             "reads_per_s_M": round(rps, 5), "reads_per_s_M_1thread": round(S1 / dt_1 / 1e6, 5),
             "sample": f"first {S} reads; oracle/fmi_ref.c collect_intv + oracle/chain_ref.c mem_chain/mem_chain_flt + "
                       f"oracle/ext_ref.c chain2aln (scalar ksw_extend2) on {nt} threads (collect and chain2aln "
@@ -1459,6 +1464,32 @@ def main_mem(args, rank, local, world, c1: bool):
             rate = n_cpu / dt_cpu / 1e6
             out_j["cpu_baseline"].update(value=round(rate, 5), unit=UNIT)
         out_j["cpu_baseline"].update(per_core_rate=round(rate / nt, 6), node_extrapolated=node_extrapolation(rate, nt))
+        # the SMEM kernel's HBM roofline: algorithmic bytes = the reference algorithm's occurrence-
+        # block loads (bwa-mem2 CP_OCC: one 64-B block per backward extension, two when the interval
+        # spans blocks; counted by the oracle's walk on this sample) x 64 B per read, plus the read
+        # bytes; achieved = those bytes for every read of the step / the SMEM kernel time of the step
+        # (the GPU's k-mer table and text mode skip part of these loads: achieved may pass traffic)
+        alg_per_read = n_blocks * 64.0 / S + float(np.mean(lens))
+        smem_s = fmi.last_kernel_ms() * 1e-3
+        pmc = traffic_per_launch("smem_kernel")
+        ach = alg_per_read * n / smem_s / 1e9
+        out_j["roofline"] = {
+            "bound": "hbm", "kernel": "smem_kernel", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
+            "frac": round(ach / 8000.0, 4),
+            "traffic": pmc, "traffic_note": "HBM bytes per launch of smem_kernel from the committed PMC pass "
+                                            "(profiles/pmc_latest.json; FETCH_SIZE raw: 64-B random requests)",
+            "algorithmic": f"{alg_per_read:.0f} B per read ({n_blocks / S:.1f} occurrence-block loads x 64 B "
+                           f"+ the read) x {n} reads per step", "launch_ms_per_step": round(smem_s * 1e3, 3),
+            "backward_extensions_per_read": round(n_bext / S, 1)}
+    if not c1:
+        # the reference's own published bwa-mem2 rate (another machine and another dataset, SAM output
+        # included): beside the oracle leg, never as the baseline of a ratio
+        out_j["reference_published"] = {
+            "value": 0.130378, "unit": "M reads/s", "threads": 16,
+            "machine": "AWS Graviton4 c8g.4xlarge (16 vCPUs, Neoverse-V2)",
+            "dataset": "human chr22 (~50 MB reference), 1M x 150 bp reads; bwa-mem2 mem end to end incl. SAM",
+            "source": "/root/reference/GRAVITON4_BENCHMARK_RESULTS.md:21-30",
+            "note": "another machine and another dataset: quoted for scale, not a measured ratio"}
     fmi.close()
     print(json.dumps(out_j), flush=True)
 

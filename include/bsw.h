@@ -179,7 +179,7 @@ enum {
     BSW_OPT_HOST_CHUNK = 6,   /* bsw_get_scores: largest pipeline chunk in pairs (default
                                  262144, rounded down to whole 4096-pair blocks, at least one):
                                  a host-buffer call is staged, copied and computed chunk by
-                                 chunk over up to three streams so copies overlap the DP
+                                 chunk over up to four slots so copies overlap the DP
                                  kernels; calls of <= 128K pairs run as one chunk            */
     BSW_OPT_HOST_PACK = 8,    /* bsw_get_scores staging of contiguous sequence buffers: 2 = 2-bit
                                  codes + exception words for bytes outside 0..3, 20-B input
