@@ -466,6 +466,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.mid_batch = 32768;
     kp.group_kernel = 1;
     kp.busy_min = 0;                 // measured slower at every setting: off
+    kp.lds_pad = getenv("BSW_PC_LDS_PAD") ? std::max(0, atoi(getenv("BSW_PC_LDS_PAD"))) : 0;   // experiment knob
 }
 
 // keys / keys2 / vals / order (radix-sort buffers) grow together
@@ -1171,11 +1172,17 @@ static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, int mode)
 // chunk k's kernels only after chunk k + 1 was staged: ~1.4 ms of idle GPU per chunk in the
 // rocprofv3 timeline).  Chunks ramp from ~n/32 pairs up to `chunk` so the first kernels start
 // early.  Outputs are identical to one unchunked call (pairs are independent).
-static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref,
+static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref,
                       const uint8_t *qer, int32_t n, int32_t w, int cell_bits, int32_t chunk, bool two_bit,
                       bsw_stats_t *st)
 {
     if (n == 0) return BSW_OK;
+    // the chunks' DP kernels run with LDS padding that caps their waves per CU, so the next chunk's
+    // helper kernels (unpack, plan, sort, gather, copies) find free wave slots instead of queuing
+    // ~1 ms behind DP waves (kernel + copy trace): BSW_HP_LDS_PAD bytes (experiment)
+    static const int hp_pad = getenv("BSW_HP_LDS_PAD") ? std::max(0, atoi(getenv("BSW_HP_LDS_PAD"))) : -1;
+    KParams kp = kp0;
+    if (hp_pad >= 0) kp.lds_pad = hp_pad;
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto t_start = now();
     // the whole prepass (validation + per-block byte extents) before chunk 0: validating only chunk

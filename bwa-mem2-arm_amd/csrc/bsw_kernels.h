@@ -43,6 +43,9 @@ struct KParams {
     int32_t small_batch;        // host: calls / chunks of at most this many pairs run every
                                 //   qualifying pair on the wave kernel (latency, not
                                 //   throughput, bounds them; BSW_OPT_SMALL_BATCH, 0 = off)
+    int32_t lds_pad;            // host: dynamic LDS bytes per packed-column workgroup (0 = none).
+                                //   LDS caps the DP waves per CU, so a host-pipeline chunk's DP
+                                //   leaves wave slots for the next chunk's helper kernels
 };
 
 // qlen limit of the register-resident kernel instantiations.

@@ -874,15 +874,14 @@ static void launch_pc_q(const KParams &kp, int32_t w, SeqPair *pairs, const int3
                         const uint8_t *ref, const uint8_t *qer, int32_t *err, hipStream_t s)
 {
     const unsigned grid = (unsigned)((n + 63) / 64);
-    // one wave per workgroup: a finished wave's slot and LDS are reused at once
-#ifndef BSW_PC_LDS_PAD          // experiment builds only: dynamic LDS per workgroup caps waves per CU
-#define BSW_PC_LDS_PAD 0
-#endif
+    // one wave per workgroup: a finished wave's slot and LDS are reused at once;
+    // kp.lds_pad: dynamic LDS per workgroup, which caps the waves per CU (host pipeline, §5)
+    const unsigned pad = (unsigned)max(kp.lds_pad, 0);
     if (kp.kern8 == 2)                 // byte planes (BSW_OPT_KERNEL8 = 2)
-        hipLaunchKernelGGL((pc_kernel<QMAX, 1, true>), dim3(grid), dim3(64), BSW_PC_LDS_PAD, s, kp, w, pairs, order, n,
+        hipLaunchKernelGGL((pc_kernel<QMAX, 1, true>), dim3(grid), dim3(64), pad, s, kp, w, pairs, order, n,
                            ref, qer, err);
     else
-        hipLaunchKernelGGL((pc_kernel<QMAX, 1, false>), dim3(grid), dim3(64), BSW_PC_LDS_PAD, s, kp, w, pairs, order,
+        hipLaunchKernelGGL((pc_kernel<QMAX, 1, false>), dim3(grid), dim3(64), pad, s, kp, w, pairs, order,
                            n, ref, qer, err);
 }
 
