@@ -117,11 +117,15 @@ __global__ void glob_plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, c
 
 // ------------------------------------------------------------------ traceback (both kernels)
 // zw: this wave's matrix; upstream's loop from (tlen - 1, min(tlen + w, qlen) - 1).
+// Narrow window (tb_dw > 0, column kernel): row i holds the tb_dw dwords from column
+// max(i + doff, 0) rounded down; a step outside them appends the job to retry (count retry[0]).
 __device__ void glob_traceback(const uint32_t *__restrict__ zw, int cap_dw, int wmax, int lane, int qlen,
                                int tlen, int w, uint32_t *__restrict__ out, int stride,
-                               int32_t *__restrict__ nout)
+                               int32_t *__restrict__ nout, int tb_dw = 0, int doff = 0,
+                               int32_t *__restrict__ retry = nullptr, int idx = 0)
 {
     if (qlen >= 1 && tlen >= 1 && qlen < tlen - w) { *nout = -2; return; }
+    const int rowdw = tb_dw > 0 ? tb_dw : cap_dw;
     int i = tlen - 1, k = min(i + w + 1, qlen) - 1, which = 0, n = 0;
     uint32_t cur = 0;                                      // last op, not yet stored
     auto push = [&](uint32_t op, uint32_t len) {
@@ -131,8 +135,18 @@ __device__ void glob_traceback(const uint32_t *__restrict__ zw, int cap_dw, int 
         ++n;
     };
     while (i >= 0 && k >= 0) {
-        const int dlo = max(i - wmax, 0) >> 3;
-        const uint32_t word = zw[((int64_t)i * cap_dw + ((k >> 3) - dlo)) * 64 + lane];
+        int sl;
+        if (tb_dw > 0) {
+            sl = (k >> 3) - (max(i + doff, 0) >> 3);
+            if ((unsigned)sl >= (unsigned)tb_dw) {           // the path left the corridor
+                retry[1 + atomicAdd(retry, 1)] = idx;
+                *nout = -3;
+                return;
+            }
+        } else {
+            sl = (k >> 3) - (max(i - wmax, 0) >> 3);
+        }
+        const uint32_t word = zw[((int64_t)i * rowdw + sl) * 64 + lane];
         const uint32_t nib = (word >> ((k & 7) * 4)) & 15u;
         which = which == 0 ? (int)(nib & 3u) : which == 1 ? (int)((nib >> 2) & 1u) : ((nib & 8u) ? 2 : 0);
         if (which == 0) { push(0, 1); --i; --k; }
@@ -209,18 +223,25 @@ struct GRow {                       // per-row uniform bounds (SGPRs)
     int lo, hi;                     // columns any lane touches: [min beg, max end + 1)
     int fb, fe;                     // columns every active lane has in band: [max beg, min end)
     int dlo, cap_dw;                // traceback window of this row
+    int tb_dw;                      // > 0: narrow per-lane corridor window of tb_dw dwords
 };
 
 template <int G, int QMAX>
 __device__ __forceinline__ void glob_group_at(uint32_t (&R)[QMAX], const uint32_t (&q8)[QMAX / 8], uint2 pr,
                                               int &h1, int &f, const GCx &c, int beg, int end, const GRow &r,
-                                              uint32_t *__restrict__ zrow, int lane)
+                                              uint32_t *__restrict__ zrow, int lane, int tlo)
 {
     if (8 * G + 8 <= r.lo || 8 * G >= r.hi) return;       // uniform
     uint32_t word;
     if (8 * G >= r.fb && 8 * G + 8 <= r.fe) word = glob_group<G, QMAX, false>(R, q8, pr, h1, f, c, beg, end);
     else word = glob_group<G, QMAX, true>(R, q8, pr, h1, f, c, beg, end);
-    if (zrow && G - r.dlo < r.cap_dw) zrow[(G - r.dlo) * 64 + lane] = word;
+    if (zrow) {
+        if (r.tb_dw > 0) {                                  // narrow: this lane's corridor dwords only
+            if ((unsigned)(G - tlo) < (unsigned)r.tb_dw) zrow[(G - tlo) * 64 + lane] = word;
+        } else if (G - r.dlo < r.cap_dw) {
+            zrow[(G - r.dlo) * 64 + lane] = word;
+        }
+    }
     // keep the scheduler from interleaving groups: each group's temporaries die here, so the
     // row (QMAX packed {h, e} registers) plus one group's working set fits 2 waves per SIMD
     __builtin_amdgcn_sched_barrier(0);
@@ -229,9 +250,10 @@ __device__ __forceinline__ void glob_group_at(uint32_t (&R)[QMAX], const uint32_
 template <int QMAX, int... G>
 __device__ __forceinline__ void glob_row(std::integer_sequence<int, G...>, uint32_t (&R)[QMAX],
                                          const uint32_t (&q8)[QMAX / 8], uint2 pr, int &h1, int &f, const GCx &c,
-                                         int beg, int end, const GRow &r, uint32_t *__restrict__ zrow, int lane)
+                                         int beg, int end, const GRow &r, uint32_t *__restrict__ zrow, int lane,
+                                         int tlo)
 {
-    (glob_group_at<G, QMAX>(R, q8, pr, h1, f, c, beg, end, r, zrow, lane), ...);
+    (glob_group_at<G, QMAX>(R, q8, pr, h1, f, c, beg, end, r, zrow, lane, tlo), ...);
 }
 
 template <int QMAX>
@@ -239,7 +261,7 @@ __global__ __launch_bounds__(64, 2) void glob_lane_kernel(
     const GlobParams gp, SeqPair *__restrict__ pairs, const int32_t *__restrict__ order, int32_t n,
     const uint8_t *__restrict__ ref, const uint8_t *__restrict__ qer, uint32_t *__restrict__ z, int64_t zstride,
     int32_t cap_dw, uint32_t *__restrict__ cigar, int32_t stride, int32_t *__restrict__ n_cigar,
-    unsigned long long *__restrict__ cells)
+    unsigned long long *__restrict__ cells, int32_t tb_dw, int32_t *__restrict__ retry)
 {
     constexpr int NG = QMAX / 8;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -290,6 +312,15 @@ __global__ __launch_bounds__(64, 2) void glob_lane_kernel(
         R[j] = ((uint32_t)h & 0xffffu) | ((uint32_t)kGNeg << 16);
     }
     int score = qlen == 0 ? 0 : (qlen <= w ? -(gp.o_ins + gp.e_ins * qlen) : kGMinusInf);
+    // Narrow traceback window (tb_dw > 0): the path from (0, 0) to (tlen - 1, qlen - 1) runs along the
+    // diagonals between 0 and qlen - tlen; each row keeps only the tb_dw dwords from column
+    // i + min(0, qlen - tlen) - xs, xs the widest slack whose corridor (|qlen - tlen| + 2 xs + 1
+    // columns, any alignment) fits them.  A job with no room (xs < 0) or whose path leaves the
+    // corridor goes to retry (the host reruns it with the full band window).  ~3x fewer matrix bytes.
+    const int dlt = qlen - tlen;
+    const int xs = tb_dw > 0 ? (8 * tb_dw - 8 - abs(dlt)) / 2 : 0;
+    const int doff = min(0, dlt) - xs;
+    const int rowdw = tb_dw > 0 ? tb_dw : cap_dw;
     const GCx cx{gp.e_del, gp.oe_del, gp.e_ins, gp.oe_ins};
     unsigned long long ncell = 0;
     uint32_t tnext = (live && tlen > 0) ? ref[p.idr] : 4u;
@@ -310,11 +341,12 @@ __global__ __launch_bounds__(64, 2) void glob_lane_kernel(
         r.fe = __builtin_amdgcn_readfirstlane(wave_min(act ? end : INT_MAX));
         r.dlo = r.lo >> 3;
         r.cap_dw = cap_dw;
+        r.tb_dw = tb_dw;
         const int bnd = -(gp.o_del + gp.e_del * (i + 1));
         int h1 = (act && beg == 0) ? bnd : kGNeg;
         int f = kGNeg;
         glob_row<QMAX>(std::make_integer_sequence<int, NG>{}, R, q8, pr, h1, f, cx, beg, end, r,
-                       zw ? zw + (int64_t)i * cap_dw * 64 : nullptr, lane);
+                       zw ? zw + (int64_t)i * rowdw * 64 : nullptr, lane, max(i + doff, 0) >> 3);
         if (act) {
             ncell += (unsigned long long)max(end - beg, 0);
             if (end == qlen) score = beg < end ? h1 : (beg == 0 ? bnd : kGMinusInf);
@@ -324,7 +356,14 @@ __global__ __launch_bounds__(64, 2) void glob_lane_kernel(
     if (lane == 0 && cells) atomicAdd(cells, ncell);
     if (!live) return;
     pairs[idx].score = score;
-    if (zw) glob_traceback(zw, cap_dw, wmax, lane, qlen, tlen, w, cigar + (int64_t)idx * stride, stride, n_cigar + idx);
+    if (!zw) return;
+    if (tb_dw > 0 && xs < 0 && !(qlen >= 1 && tlen >= 1 && qlen < tlen - w)) {
+        retry[1 + atomicAdd(retry, 1)] = idx;               // corridor wider than the window
+        n_cigar[idx] = -3;
+        return;
+    }
+    glob_traceback(zw, cap_dw, wmax, lane, qlen, tlen, w, cigar + (int64_t)idx * stride, stride, n_cigar + idx,
+                   tb_dw, doff, retry, idx);
 }
 
 // ------------------------------------------------------------------ band-coordinate kernel
@@ -627,18 +666,19 @@ template <int QMAX>
 static void launch_lane_q(const GlobParams &gp, SeqPair *pairs, const int32_t *order, int32_t n,
                           const uint8_t *ref, const uint8_t *qer, uint32_t *z, int64_t zstride, int32_t cap_dw,
                           uint32_t *cigar, int32_t stride, int32_t *n_cigar, unsigned long long *cells,
-                          hipStream_t s)
+                          hipStream_t s, int32_t tb_dw, int32_t *retry)
 {
     hipLaunchKernelGGL(glob_lane_kernel<QMAX>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, gp, pairs,
-                       order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells);
+                       order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, tb_dw, retry);
 }
 
 hipError_t launch_glob_class(int cls, const GlobParams &gp, SeqPair *pairs, const int32_t *order, int32_t n,
                              const uint8_t *ref, const uint8_t *qer, uint32_t *z, int64_t zstride,
                              int32_t cap_dw, int2 *ehs, uint32_t *cigar, int32_t stride, int32_t *n_cigar,
-                             unsigned long long *cells, hipStream_t s)
+                             unsigned long long *cells, hipStream_t s, int32_t tb_dw, int32_t *retry)
 {
     if (n <= 0) return hipSuccess;
+    if (tb_dw > 0 && (!retry || !z || cls < kGlobLane0 || cls >= kGlobWideClass)) return hipErrorInvalidValue;
     switch (cls) {
 #define GB(C, BW)                                                                                           \
     case C:                                                                                                 \
@@ -647,11 +687,11 @@ hipError_t launch_glob_class(int cls, const GlobParams &gp, SeqPair *pairs, cons
         break;
     GB(0, 32) GB(1, 48) GB(2, 64) GB(3, 80) GB(4, 96)
 #undef GB
-    case kGlobLane0 + 0: launch_lane_q<32>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
-    case kGlobLane0 + 1: launch_lane_q<64>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
-    case kGlobLane0 + 2: launch_lane_q<96>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
-    case kGlobLane0 + 3: launch_lane_q<128>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
-    case kGlobLane0 + 4: launch_lane_q<160>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s); break;
+    case kGlobLane0 + 0: launch_lane_q<32>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s, tb_dw, retry); break;
+    case kGlobLane0 + 1: launch_lane_q<64>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s, tb_dw, retry); break;
+    case kGlobLane0 + 2: launch_lane_q<96>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s, tb_dw, retry); break;
+    case kGlobLane0 + 3: launch_lane_q<128>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s, tb_dw, retry); break;
+    case kGlobLane0 + 4: launch_lane_q<160>(gp, pairs, order, n, ref, qer, z, zstride, cap_dw, cigar, stride, n_cigar, cells, s, tb_dw, retry); break;
     case kGlobWideClass:
         hipLaunchKernelGGL(glob_wide_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gp, pairs, order,
                            n, ref, qer, z, zstride, cap_dw, ehs, cigar, stride, n_cigar, cells);

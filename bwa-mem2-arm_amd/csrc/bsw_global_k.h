@@ -53,9 +53,12 @@ hipError_t launch_glob_plan(const SeqPair *pairs, int32_t n, const GlobParams &g
 // DP + traceback of class cls over jobs order[0, n).  z: traceback matrix, zstride uint32 per
 // wave (>= max tlen * cap_dw * 64), null for scores only; ehs: int32 row scratch of the wide
 // class, (max qlen + 1) * n int2.
+// tb_dw > 0 (column classes only): narrow traceback window -- each lane stores per row only tb_dw
+// dwords around its diagonal corridor (glob_lane_kernel); jobs whose path leaves it are appended
+// to retry[1..] (count in retry[0]) for a full-window rerun.  Row stride of z: tb_dw or cap_dw.
 hipError_t launch_glob_class(int cls, const GlobParams &gp, SeqPair *pairs, const int32_t *order, int32_t n,
                              const uint8_t *ref, const uint8_t *qer, uint32_t *z, int64_t zstride,
                              int32_t cap_dw, int2 *ehs, uint32_t *cigar, int32_t stride, int32_t *n_cigar,
-                             unsigned long long *cells, hipStream_t s);
+                             unsigned long long *cells, hipStream_t s, int32_t tb_dw = 0, int32_t *retry = nullptr);
 
 }  // namespace bsw

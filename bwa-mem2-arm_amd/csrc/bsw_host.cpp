@@ -224,6 +224,7 @@ struct Slot {
     int32_t *d_gmeta = nullptr, *h_gmeta = nullptr;
     uint32_t *d_gcig = nullptr; size_t cap_gcig = 0;
     int32_t *d_gncig = nullptr; size_t cap_gncig = 0;
+    int32_t *d_gretry = nullptr; size_t cap_gretry = 0;   // narrow-window traceback retries: count, list
     // device extension pipeline (bsw_ext_dev.hip)
     SeqPair *d_xpairs = nullptr, *d_xsub = nullptr; size_t cap_xpairs = 0, cap_xsub = 0;
     uint8_t *d_xq = nullptr, *d_xt = nullptr; size_t cap_xq = 0, cap_xt = 0;
@@ -327,6 +328,7 @@ struct DeviceCtx {
         (void)hipFree(s->d_mcells); (void)hipFree(s->d_mpairs); (void)hipFree(s->d_maln);
         if (s->h_mmeta) (void)hipHostFree(s->h_mmeta);
         (void)hipFree(s->d_gz); (void)hipFree(s->d_gmeta); (void)hipFree(s->d_gcig); (void)hipFree(s->d_gncig);
+        (void)hipFree(s->d_gretry);
         if (s->h_gmeta) (void)hipHostFree(s->h_gmeta);
         (void)hipFree(s->d_xpairs); (void)hipFree(s->d_xsub); (void)hipFree(s->d_xq); (void)hipFree(s->d_xt);
         (void)hipFree(s->d_xst);
@@ -1930,6 +1932,11 @@ static int glob_device(const GlobParams &gp, Slot &s, SeqPair *d_pairs, const ui
     }
     if (m[kGMetaErr]) return BSW_E_RANGE;
     const bool want = d_cigar && stride > 0;
+    // column classes keep only a narrow corridor of the traceback matrix (glob_lane_kernel: 3 dwords
+    // per row instead of the band's ~10 at bwa-shaped w); jobs whose path leaves it rerun below with
+    // the full band window.  BSW_GLOB_TB_DW (experiment): dwords per row, 0 = full window always
+    static const int tb_env = getenv("BSW_GLOB_TB_DW") ? std::max(0, atoi(getenv("BSW_GLOB_TB_DW"))) : 3;
+    if (want) BSW_TRY(grow(s.d_gretry, s.cap_gretry, (size_t)n + 1));
     BSW_TRY(hipEventRecord(s.ev0, st));
     int32_t off = 0;
     for (int c = 0; c < kGlobClasses; ++c) {
@@ -1937,21 +1944,41 @@ static int glob_device(const GlobParams &gp, Slot &s, SeqPair *d_pairs, const ui
         if (cnt <= 0) continue;
         const int tm = m[kGMetaTmax + c], wm = m[kGMetaWmax + c], qm = m[kGMetaQmax + c];
         const int cap_dw = glob_cap_dw(c, qm, wm);
-        const int64_t zstride = (int64_t)std::max(tm, 1) * cap_dw * 64;
-        int32_t chunk = cnt;
-        if (want) {
-            const int64_t waves = std::max<int64_t>(1, kGlobZCapWords / zstride);
-            chunk = (int32_t)std::min<int64_t>(cnt, waves * 64);
-            BSW_TRY(grow(s.d_gz, s.cap_gz, (size_t)((chunk + 63) / 64) * (size_t)zstride));
-        }
-        if (c == kGlobWideClass) BSW_TRY(grow(s.d_scratch, s.cap_scratch, (size_t)(qm + 1) * (size_t)chunk));
-        for (int32_t a = 0; a < cnt; a += chunk) {
-            const int32_t b = std::min(cnt, a + chunk);
-            BSW_TRY(launch_glob_class(c, gp, d_pairs, s.d_order + off + a, b - a, d_ref, d_qer,
-                                      want ? s.d_gz : nullptr, zstride, cap_dw, s.d_scratch, d_cigar, stride,
-                                      d_ncig, s.d_mcells, st));
-            stats->n_launches++;
-            if (want) stats->z_bytes += (int64_t)((b - a + 63) / 64) * zstride * 4;
+        const bool col = c >= kGlobLane0 && c < kGlobWideClass;
+        const int tb = (want && col && tb_env > 0 && tb_env < cap_dw) ? tb_env : 0;
+        // one pass over the class (narrow window when tb > 0), then the retry list with the full window
+        for (int pass = 0; pass < (tb > 0 ? 2 : 1); ++pass) {
+            const int ptb = pass == 0 ? tb : 0;
+            int32_t pcnt = cnt;
+            const int32_t *ord = s.d_order + off;
+            if (pass == 1) {                                // the jobs the narrow window could not serve
+                int32_t nr = 0;
+                BSW_TRY(hipMemcpyAsync(&nr, s.d_gretry, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+                BSW_TRY(hipStreamSynchronize(st));
+                stats->n_tb_retry += nr;
+                if (nr <= 0) break;
+                pcnt = nr;
+                ord = s.d_gretry + 1;
+            } else if (ptb > 0) {
+                BSW_TRY(hipMemsetAsync(s.d_gretry, 0, sizeof(int32_t), st));
+            }
+            const int64_t zstride = (int64_t)std::max(tm, 1) * (ptb > 0 ? ptb : cap_dw) * 64;
+            int32_t chunk = pcnt;
+            if (want) {
+                const int64_t waves = std::max<int64_t>(1, kGlobZCapWords / zstride);
+                chunk = (int32_t)std::min<int64_t>(pcnt, waves * 64);
+                BSW_TRY(grow(s.d_gz, s.cap_gz, (size_t)((chunk + 63) / 64) * (size_t)zstride));
+            }
+            if (c == kGlobWideClass) BSW_TRY(grow(s.d_scratch, s.cap_scratch, (size_t)(qm + 1) * (size_t)chunk));
+            for (int32_t a = 0; a < pcnt; a += chunk) {
+                const int32_t b = std::min(pcnt, a + chunk);
+                BSW_TRY(launch_glob_class(c, gp, d_pairs, ord + a, b - a, d_ref, d_qer,
+                                          want ? s.d_gz : nullptr, zstride, cap_dw, s.d_scratch, d_cigar, stride,
+                                          d_ncig, pass == 0 ? s.d_mcells : nullptr, st, ptb,
+                                          ptb > 0 ? s.d_gretry : nullptr));
+                stats->n_launches++;
+                if (want) stats->z_bytes += (int64_t)((b - a + 63) / 64) * zstride * 4;
+            }
         }
         if (c == kGlobWideClass) stats->n_wide += cnt;
         else stats->n_lane += cnt;

@@ -427,7 +427,7 @@ def mate_last_stats(engine) -> MateStats:
 class GlobalStats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_float), ("n_jobs", ctypes.c_int32), ("n_lane", ctypes.c_int32),
                 ("n_wide", ctypes.c_int32), ("n_launches", ctypes.c_int32), ("cells", ctypes.c_int64),
-                ("z_bytes", ctypes.c_int64)]
+                ("z_bytes", ctypes.c_int64), ("n_tb_retry", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
 def ksw_global2(engine, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray, stride: int = 64):

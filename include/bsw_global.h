@@ -52,6 +52,10 @@ typedef struct bsw_global_stats_t {
     int32_t n_launches;
     int64_t cells;              /* band cells computed (sum over jobs of row band widths)      */
     int64_t z_bytes;            /* traceback-matrix bytes written (nibble per cell, per wave)   */
+    int32_t n_tb_retry;         /* column-kernel jobs whose traceback left the narrow corridor
+                                   window (or whose corridor does not fit it) and were rerun with
+                                   the full band window (ABI version 7)                        */
+    int32_t pad_;
 } bsw_global_stats_t;
 int bsw_global_last_stats(bsw_ctx_t *ctx, bsw_global_stats_t *out);
 

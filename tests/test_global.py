@@ -191,6 +191,10 @@ def test_gpu_random_jobs_match_oracle(scoring, routing):
     got = bsw.ksw_global2(eng, pairs, ref, qer, stride=96)
     _check(want, got, f"random jobs {scoring}")
     assert np.array_equal(pairs["score"], want[0])
+    if routing == "column":
+        # unrelated random pairs: many paths leave the column kernel's narrow traceback corridor and
+        # take the full-window rerun -- both paths exercised, outputs equal the oracle above
+        assert bsw.global_last_stats(eng).n_tb_retry > 0
     eng.close()
 
 
@@ -206,6 +210,9 @@ def test_gpu_bwa_shaped_jobs_match_oracle(read_len, routing):
     st = bsw.global_last_stats(eng)
     assert st.n_jobs == len(pairs) and (st.n_wide > 0) == (read_len > 160)   # 250 bp: w ~ 60 -> wide
     assert st.n_lane + st.n_wide == len(pairs)
+    if routing == "column" and read_len <= 160:
+        # bwa-shaped jobs: the narrow corridor (3 dwords per row) serves nearly every traceback
+        assert st.n_tb_retry < 0.05 * len(pairs), st.n_tb_retry
     eng.close()
 
 
