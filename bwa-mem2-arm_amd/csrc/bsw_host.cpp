@@ -2657,7 +2657,7 @@ int bsw_ksw_global2(bsw_ctx_t *ctx, SeqPair *pairs, const uint8_t *seqBufRef, co
     for (const auto &x : st) {
         agg.kernel_ms = std::max(agg.kernel_ms, x.kernel_ms);
         agg.n_jobs += x.n_jobs; agg.n_lane += x.n_lane; agg.n_wide += x.n_wide; agg.n_launches += x.n_launches;
-        agg.cells += x.cells; agg.z_bytes += x.z_bytes;
+        agg.cells += x.cells; agg.z_bytes += x.z_bytes; agg.n_tb_retry += x.n_tb_retry;
     }
     std::lock_guard<std::mutex> g(ctx->stats_mu);
     ctx->glob_last = agg;
