@@ -1623,7 +1623,10 @@ def main_global(args, rank, local, world):
         "config": {"workload": f"global + CIGAR: {args.jobs} jobs/GPU resident in HBM, 150 bp read vs its "
                                f"reference span, w by bwa_gen_cigar2 (opt->w 100), CIGAR stride {stride}",
                    "jobs_per_gpu": args.jobs, "parallelism": f"shard{world} (independent jobs)",
-                   "n_lane": st.n_lane, "n_wide": st.n_wide, "n_launches": st.n_launches},
+                   "n_lane": st.n_lane, "n_wide": st.n_wide, "n_launches": st.n_launches,
+                   "traceback_window": ("full band" if os.environ.get("BSW_GLOB_TB_DW") == "0" else
+                                        f"narrow corridor, {os.environ.get('BSW_GLOB_TB_DW', '3')} dwords per row"),
+                   "n_tb_retry": st.n_tb_retry, "z_bytes_per_step": st.z_bytes},
         "roofline": {"bound": "valu", "achieved": round(st.cells * OPS_PER_CELL / (kms * 1e-3) / 1e12, 3),
                      "peak": round(VALU_PEAK_TOPS, 1), "unit": "TOP/s",
                      "frac": round(st.cells * OPS_PER_CELL / (kms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
