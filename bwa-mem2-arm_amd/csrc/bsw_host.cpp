@@ -151,7 +151,19 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, const 
             keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
                       ((uint32_t)(1 - rel) << 19) | ((uint32_t)(2047 - min(tlen, 2047)) << 8) |
                       (uint32_t)(255 - min(max(p.h0, 0), 255));
-        else
+        else if (keymode >= 3) {
+            // compact 16-bit keys (experiment, BSW_KEYMODE): class | qlen desc inside the class's
+            // 32-column bucket | related | identities desc | h0 desc, coarsened to fit 16 bits
+            const int ub = (c < kWideClass) ? 32 * ((c % kNumLaneClasses) + 1) : 255;
+            const int qd = max(0, ub - qlen);
+            const uint32_t hd = (uint32_t)(255 - min(max(p.h0, 0), 255));
+            const uint32_t k16 = keymode == 3
+                ? ((uint32_t)c << 12) | ((uint32_t)min(15, qd >> 1) << 8) | ((uint32_t)(1 - rel) << 7) |
+                      ((uint32_t)(31 - min(mt, 31)) << 2) | (hd >> 6)
+                : ((uint32_t)c << 12) | ((uint32_t)min(31, qd) << 7) | ((uint32_t)(1 - rel) << 6) |
+                      ((uint32_t)(31 - min(mt, 31)) << 1) | (hd >> 7);
+            keys[i] = k16 << 16;
+        } else
             keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
                       ((uint32_t)(1 - rel) << 19) | ((uint32_t)(63 - min(tlen >> 5, 63)) << 13) |
                       ((uint32_t)(31 - min(mt, 31)) << 8) | (uint32_t)(255 - min(max(p.h0, 0), 255));
@@ -460,7 +472,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.pk_ok = ok ? 1 : 0;
     // routing / scheduling defaults; bsw_set_option changes them per context
     kp.kern8 = 1;
-    kp.keymode = 2;
+    kp.keymode = getenv("BSW_KEYMODE") ? (int8_t)atoi(getenv("BSW_KEYMODE")) : 2;   // (env: experiments)
     kp.misroute = 0;
     kp.fork = 1;
     kp.long_route = 1;
