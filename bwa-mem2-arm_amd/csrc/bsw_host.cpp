@@ -858,11 +858,7 @@ __global__ void patch_codes_kernel(const uint32_t *__restrict__ exc, int32_t n_r
     (t < n_r ? ref : qer)[e >> 4] = (uint8_t)(e & 15u);
 }
 
-// the kernels' input fields of a SeqPair, staged without the caller bookkeeping and outputs
-struct PairIn {
-    int32_t idr, idq, len1, len2, h0;
-};
-static_assert(sizeof(PairIn) == 20, "PairIn");
+// (PairIn: the kernels' input fields of a SeqPair, bsw_kernels.h)
 
 __global__ void expand_pairs_kernel(const PairIn *__restrict__ in, SeqPair *__restrict__ out, int32_t n)
 {
@@ -954,18 +950,20 @@ constexpr int32_t kStageBlk = 4096;           // pairs per block (a chunk is who
 struct BlkStat {
     int64_t r_lo, r_hi, q_lo, q_hi, r_sum, q_sum;
     bool bad;
+    bool fast;                  // every pair fits the packed-column kernel (host_shard_fast)
 };
 
 // blocks [b0, b1) of bs (sized for every block of the n pairs); false if any pair there is invalid
 static bool prepass_range(const SeqPair *pairs, int32_t n, std::vector<BlkStat> &bs, int32_t b0, int32_t b1)
 {
     auto blk = [&](int32_t b) {
-        BlkStat t{INT64_MAX, 0, INT64_MAX, 0, 0, 0, false};
+        BlkStat t{INT64_MAX, 0, INT64_MAX, 0, 0, 0, false, true};
         const int32_t e = std::min(n, (b + 1) * kStageBlk);
         for (int32_t i = b * kStageBlk; i < e; ++i) {
             const SeqPair &p = pairs[i];
             t.bad |= p.len1 < 0 || p.len2 < 0 || p.len1 > BSW_MAX_LEN || p.len2 > BSW_MAX_LEN || p.idr < 0 ||
                      p.idq < 0;
+            t.fast &= p.len2 < 160 && p.h0 >= 0 && p.h0 + std::min(std::max(p.len1, 0), std::max(p.len2, 0)) <= 255;
             if (p.len1 > 0) { t.r_lo = std::min<int64_t>(t.r_lo, p.idr); t.r_hi = std::max<int64_t>(t.r_hi, (int64_t)p.idr + p.len1); t.r_sum += p.len1; }
             if (p.len2 > 0) { t.q_lo = std::min<int64_t>(t.q_lo, p.idq); t.q_hi = std::max<int64_t>(t.q_hi, (int64_t)p.idq + p.len2); t.q_sum += p.len2; }
         }
@@ -1177,6 +1175,225 @@ static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, int mode)
     }
 }
 
+// ---------------------------------------------------------------- host pipeline, fast path
+// A host-buffer call whose every pair fits the packed-column kernel (bwa-style scoring, qlen <
+// 160, h0 + min(len1, len2) <= 255) and whose chunks' byte extents are contiguous (the upstream
+// layout) runs with NO device helper kernel: per chunk the host computes each pair's schedule key
+// (plan_kernel's key of that class, from the same bytes: fast_keys), sorts the chunk by it (a
+// parallel stable LSD radix over the key bytes that vary), stages the records in that order as
+// 20-B PairIn with nibble offsets and the byte extents as nibbles; the device runs one H2D, one
+// pc_kernel<160, nibbles> reading the staged chunk in place and writing 24 B of outputs per pair,
+// and one D2H.  Why: in the general pipeline every chunk's unpack / plan / sort / gather kernels
+// wait ~0.3-1.6 ms for wave slots behind the previous chunk's DP waves (kernel + copy trace,
+// profiles/r05/hostpath_trace_timeline.txt), so consecutive chunks' DP kernels could not overlap
+// (9.6 ms of chunk DP for 6.85 ms of work).  Outputs are identical (pairs are independent; the
+// order only schedules).  BSW_HP_FAST=0 turns the path off (A/B).
+struct FastChunk {
+    int32_t a = 0, m = 0;                    // pairs [a, a + m) of the call
+    size_t ref_off = 0, qer_off = 0, out_off = 0, h2d = 0, dev = 0;
+    int64_t r_lo = 0, q_lo = 0;
+};
+
+// stable LSD radix of idx[0, m) by keys[idx[.]] over the key bytes that vary; tmp: scratch of m
+static void radix_order(const uint32_t *keys, int32_t m, int32_t *idx, int32_t *tmp)
+{
+    for (int32_t i = 0; i < m; ++i) idx[i] = i;
+    if (m <= 1) return;
+    uint32_t vor = 0, vand = ~0u;
+    for (int32_t i = 0; i < m; ++i) { vor |= keys[i]; vand &= keys[i]; }
+    const uint32_t vary = vor ^ vand;
+    const int nt = (int)std::min<int64_t>(HostPool::workers() + 1, std::max<int64_t>(1, m >> 14));
+    std::vector<int32_t> hist((size_t)nt * 256);
+    for (int d = 0; d < 4; ++d) {
+        if (((vary >> (8 * d)) & 0xffu) == 0) continue;
+        const int sh = 8 * d;
+        auto lo = [&](int t) { return (int32_t)((int64_t)m * t / nt); };
+        HostPool::get().parallel_for(nt, [&](int t) {
+            int32_t *h = hist.data() + (size_t)t * 256;
+            std::fill(h, h + 256, 0);
+            for (int32_t i = lo(t); i < lo(t + 1); ++i) ++h[(keys[idx[i]] >> sh) & 0xffu];
+        });
+        int32_t run = 0;                                       // offsets: digit-major, then piece
+        for (int b = 0; b < 256; ++b)
+            for (int t = 0; t < nt; ++t) {
+                const int32_t c = hist[(size_t)t * 256 + b];
+                hist[(size_t)t * 256 + b] = run;
+                run += c;
+            }
+        HostPool::get().parallel_for(nt, [&](int t) {
+            int32_t *h = hist.data() + (size_t)t * 256;
+            for (int32_t i = lo(t); i < lo(t + 1); ++i) tmp[h[(keys[idx[i]] >> sh) & 0xffu]++] = idx[i];
+        });
+        std::copy(tmp, tmp + m, idx);
+    }
+}
+
+static int stage_fast(Slot &s, const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t m,
+                      const BlkStat *bs, int32_t nblk, FastChunk &c, std::vector<uint32_t> &keys,
+                      std::vector<int32_t> &perm, std::vector<int32_t> &tmp)
+{
+    int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+    for (int32_t b = 0; b < nblk; ++b) {
+        r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
+        q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi);
+    }
+    if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+    if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+    const size_t rb = (size_t)(r_hi - r_lo), qb = (size_t)(q_hi - q_lo);
+    c.m = m;
+    c.r_lo = r_lo; c.q_lo = q_lo;
+    c.ref_off = align256((size_t)m * sizeof(PairIn));
+    c.qer_off = align256(c.ref_off + (rb + 1) / 2 + 8);
+    c.h2d = c.qer_off + (qb + 1) / 2 + 8;
+    c.out_off = align256(c.h2d);
+    c.dev = c.out_off + (size_t)m * 24;
+    const size_t hb = std::max(c.h2d, (size_t)m * 24);
+    if (hb > s.cap_stage) {
+        const size_t cap = std::max(hb + hb / 4, s.cap_stage * 3 / 2);
+        if (s.h_stage) (void)hipHostFree(s.h_stage);
+        s.h_stage = nullptr; s.cap_stage = 0;
+        BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));
+        s.cap_stage = cap;
+    }
+    keys.resize((size_t)m);
+    perm.resize((size_t)m);
+    tmp.resize((size_t)m);
+    uint8_t *h = (uint8_t *)s.h_stage;
+    // keys (pieces of 8K pairs) and both nibble packs (pieces of ~4 MB) as one pool job list
+    const int nk = (int)std::max<int64_t>(1, m >> 13), nr = (int)std::max<size_t>(1, rb >> 22),
+              nq = (int)std::max<size_t>(1, qb >> 22);
+    auto even = [](size_t total, int k, int parts) {
+        return k == parts ? total : (total * (size_t)k / (size_t)parts) & ~(size_t)31;
+    };
+    HostPool::get().parallel_for(nk + nr + nq, [&](int t) {
+        if (t < nk) {
+            const int32_t a0 = (int32_t)((int64_t)m * t / nk), a1 = (int32_t)((int64_t)m * (t + 1) / nk);
+            fast_keys(pairs + a0, a1 - a0, ref, qer, keys.data() + a0);
+        } else if (t < nk + nr) {
+            const size_t a0 = even(rb, t - nk, nr), a1 = even(rb, t - nk + 1, nr);
+            pack_nibbles(h + c.ref_off + a0 / 2, ref + r_lo + a0, a1 - a0);
+        } else {
+            const size_t a0 = even(qb, t - nk - nr, nq), a1 = even(qb, t - nk - nr + 1, nq);
+            pack_nibbles(h + c.qer_off + a0 / 2, qer + q_lo + a0, a1 - a0);
+        }
+    });
+    memset(h + c.ref_off + (rb + 1) / 2, 0, 8);
+    memset(h + c.qer_off + (qb + 1) / 2, 0, 8);
+    radix_order(keys.data(), m, perm.data(), tmp.data());
+    PairIn *rec = (PairIn *)h;
+    const int nw = (int)std::max<int64_t>(1, m >> 14);
+    HostPool::get().parallel_for(nw, [&](int t) {
+        for (int32_t k = (int32_t)((int64_t)m * t / nw); k < (int32_t)((int64_t)m * (t + 1) / nw); ++k) {
+            const SeqPair &p = pairs[perm[k]];
+            rec[k] = PairIn{p.len1 > 0 ? (int32_t)(p.idr - r_lo) : 0, p.len2 > 0 ? (int32_t)(p.idq - q_lo) : 0,
+                            p.len1, p.len2, p.h0};
+        }
+    });
+    return BSW_OK;
+}
+
+// the fast path's chunks as block ranges [first, second): the general pipeline's schedule (a first
+// chunk of 16 blocks or 1/32 of the call, doubling up to `chunk` pairs, at most 512 MB of bytes)
+static std::vector<std::pair<int32_t, int32_t>> fast_chunks(const std::vector<BlkStat> &bs, int32_t n, int32_t chunk)
+{
+    (void)n;
+    std::vector<std::pair<int32_t, int32_t>> out;
+    const int32_t nblk = (int32_t)bs.size();
+    const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
+    int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
+    for (int32_t b = 0, nb = 0; b < nblk; b += nb, cur = std::min(cap_blk, cur * 2)) {
+        int64_t bytes = 0;
+        for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
+            const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
+            if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
+            bytes += x;
+        }
+        out.emplace_back(b, b + nb);
+    }
+    return out;
+}
+
+static int host_shard_fast(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref, const uint8_t *qer,
+                           int32_t n, int32_t w, int32_t chunk, const std::vector<BlkStat> &bs, bsw_stats_t *st)
+{
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t_start = now();
+    constexpr int kSlots = 4;
+    std::unique_ptr<Slot> slots[kSlots];
+    FastChunk fc[kSlots];
+    bool pend[kSlots] = {};
+    std::vector<uint32_t> keys[kSlots];
+    std::vector<int32_t> perm[kSlots], tmp[kSlots];
+    bsw_stats_t agg{};
+    double stage_ms = 0;
+    int rc = BSW_OK;
+    auto finish = [&](int k) -> int {
+        if (!pend[k]) return BSW_OK;
+        pend[k] = false;
+        Slot &s = *slots[k];
+        BSW_TRY(hipStreamSynchronize(s.stream));
+        float ms = 0.f;
+        BSW_TRY(hipEventElapsedTime(&ms, s.ev0, s.ev1));
+        agg.kernel_ms += ms;
+        if (s.h_meta[kMetaErr] != 0) return BSW_E_RANGE;
+        const int32_t *o = (const int32_t *)s.h_stage;
+        const int32_t m = fc[k].m, a = fc[k].a;
+        const int32_t *pm = perm[k].data();
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(HostPool::workers() + 1, m >> 15));
+        HostPool::get().parallel_for(nt, [&](int t) {
+            for (int32_t j = (int32_t)((int64_t)m * t / nt); j < (int32_t)((int64_t)m * (t + 1) / nt); ++j) {
+                const int32_t *q = o + 6 * (int64_t)j;
+                SeqPair &p = pairs[a + pm[j]];
+                p.score = q[0]; p.tle = q[1]; p.gtle = q[2]; p.qle = q[3]; p.gscore = q[4]; p.max_off = q[5];
+            }
+        });
+        agg.n_packed += m; agg.n_i16 += m; agg.n_launches += 1;
+        return BSW_OK;
+    };
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        int k = 0;
+        for (const auto &ch : fast_chunks(bs, n, chunk)) {
+            const int32_t b = ch.first, nb = ch.second - ch.first;
+            const int32_t a = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a;
+            if (int r = finish(k)) return r;
+            if (!slots[k]) {
+                int r = BSW_OK;
+                slots[k] = dc.acquire(r);
+                if (r) return r;
+            }
+            Slot &s = *slots[k];
+            const auto t0 = now();
+            if (int r = stage_fast(s, pairs + a, ref, qer, m, bs.data() + b, nb, fc[k], keys[k], perm[k], tmp[k]))
+                return r;
+            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
+            fc[k].a = a;
+            const FastChunk &c = fc[k];
+            BSW_TRY(grow(s.d_stage, s.cap_dstage, c.dev));
+            int32_t *d_err = s.d_meta + kMetaErr;
+            BSW_TRY(hipMemsetAsync(d_err, 0, sizeof(int32_t), s.stream));
+            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.h2d, hipMemcpyHostToDevice, s.stream));
+            BSW_TRY(hipEventRecord(s.ev0, s.stream));
+            BSW_TRY(launch_pc_nib_kernel(kp, w, (const PairIn *)s.d_stage, m, s.d_stage + c.ref_off,
+                                         s.d_stage + c.qer_off, (int32_t *)(s.d_stage + c.out_off), d_err, s.stream));
+            BSW_TRY(hipEventRecord(s.ev1, s.stream));
+            BSW_TRY(hipMemcpyAsync(s.h_stage, s.d_stage + c.out_off, (size_t)m * 24, hipMemcpyDeviceToHost, s.stream));
+            BSW_TRY(hipMemcpyAsync(s.h_meta + kMetaErr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
+            pend[k] = true;
+            k = (k + 1) % kSlots;
+        }
+        for (int j = 0; j < kSlots; ++j)
+            if (int r = finish(j)) return r;
+        return BSW_OK;
+    }();
+    for (int j = 0; j < kSlots; ++j)
+        if (slots[j]) dc.give_back(std::move(slots[j]), rc);
+    agg.stage_ms = (float)stage_ms;
+    agg.host_ms = (float)std::chrono::duration<double, std::milli>(now() - t_start).count();
+    if (rc == BSW_OK && st) *st = agg;
+    return rc;
+}
+
 // One device's share of a host-buffer call: a pipeline of chunks over up to three slots.
 // Per chunk: stage into the slot's pinned buffer (records + nibble-packed sequences, host
 // pool) -> one H2D -> unpack -> plan / sort -> DP kernels -> D2H of the records.  The calling
@@ -1204,6 +1421,28 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
     std::vector<BlkStat> bs;
     if (!prepass(pairs, n, bs)) return BSW_E_RANGE;
     if (chunk <= 0) chunk = n;
+    // the fast path (no device helper kernels) when every pair fits the packed-column kernel and the
+    // call is past the small-batch kernels' sizes (those are latency-bound: the row-group kernel)
+    static const bool fast_on = getenv("BSW_HP_FAST") == nullptr || atoi(getenv("BSW_HP_FAST")) != 0;
+    if (fast_on && kp0.pk_ok && kp0.kern8 == 1 && !kp0.misroute && kp0.maxsc == 1 && n > kp0.small_batch &&
+        n > kp0.mid_batch && two_bit) {
+        bool ok = true;
+        for (const BlkStat &b : bs) ok = ok && b.fast;
+        // every chunk's byte extents must be contiguous (the upstream layout; permuted batches take the
+        // general path, which gathers) and addressable as int32 nibble offsets
+        for (const auto &ch : fast_chunks(bs, n, chunk)) {
+            int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
+            for (int32_t b = ch.first; b < ch.second; ++b) {
+                r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi); r_sum += bs[b].r_sum;
+                q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi); q_sum += bs[b].q_sum;
+            }
+            if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+            if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+            ok = ok && (r_hi - r_lo) <= r_sum + r_sum / 4 + 4096 && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096 &&
+                 (r_hi - r_lo) < ((int64_t)1 << 30) && (q_hi - q_lo) < ((int64_t)1 << 30);
+        }
+        if (ok) return host_shard_fast(kp, dc, pairs, ref, qer, n, w, chunk, bs, st);
+    }
     // slots are taken as chunks start (a one-chunk call takes one); chunk k + nslots stages only
     // once chunk k's outputs are back.  4 since round 4: with the helper stream the fourth slot
     // lets the next chunk stage a DP generation earlier (same box, alternating: 84.7 / 87.7 vs

@@ -41,4 +41,9 @@ int chain_rounds_device(bsw_ctx_t *ctx, const bsw_ext_opt_t *opt, const uint8_t 
 // 2-bit codes + exception words (pos0 + k) << 4 | (src[k] & 15) for bytes outside 0..3
 void pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes);
 void pack_2bit(uint8_t *dst, const uint8_t *src, size_t nbytes, uint32_t pos0, std::vector<uint32_t> &exc);
+// host pipeline fast path (bsw_host.cpp host_shard_fast): plan_kernel's schedule key of the
+// packed-column class for pairs [0, n) -- (255 - qlen) << 20 | (1 - related) << 19 |
+// (63 - tlen / 32) << 13 | (31 - seed identities) << 8 | (255 - h0), identities as the device's
+// seed_matches (best of 13 shifts of query[10, 40) against target[4 + s, 34 + s))
+void fast_keys(const SeqPair *pairs, int32_t n, const uint8_t *ref, const uint8_t *qer, uint32_t *keys);
 }  // namespace bsw

@@ -48,6 +48,13 @@ struct KParams {
                                 //   leaves wave slots for the next chunk's helper kernels
 };
 
+// The kernels' input fields of a SeqPair (staged without the caller bookkeeping and outputs):
+// 20 B per pair in the host pipeline's staging buffers and the packed wire form (bsw.h).
+struct PairIn {
+    int32_t idr, idq, len1, len2, h0;
+};
+static_assert(sizeof(PairIn) == 20, "PairIn");
+
 // qlen limit of the register-resident kernel instantiations.
 constexpr int kLaneQmax[] = {32, 64, 96, 128, 160};
 constexpr int kLaneQmaxMax = 160;
@@ -63,6 +70,14 @@ hipError_t launch_lane_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *p
 hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
                             const int32_t *order, int32_t n, const uint8_t *ref,
                             const uint8_t *qer, int32_t *err, hipStream_t s);
+
+// The same kernel (QMAX 160) over a host-staged chunk read in place (the host
+// pipeline's fast path): recs[k] = pair k's input fields (pairs already in schedule order, no
+// `order`), idr / idq = NIBBLE indices into ref4 / qer4 (two codes per byte, low nibble first;
+// both 4-byte aligned), outputs as 6 x int32 per pair into out24[6k ..].  Same eligibility as
+// launch_pc_kernel (qlen < 160, h0 + min(len1, len2) <= 255, kp.pk_ok).
+hipError_t launch_pc_nib_kernel(const KParams &kp, int32_t w, const PairIn *recs, int32_t n, const uint8_t *ref4,
+                                const uint8_t *qer4, int32_t *out24, int32_t *err, hipStream_t s);
 
 // Wave-per-alignment band kernel (bsw_wv.hip): one SeqPair per wavefront, the row spread over
 // the 64 lanes as a sliding window of 64 * cols absolute columns (cols = 4, 8 or 16).  Needs

@@ -141,6 +141,53 @@ void pack_2bit(uint8_t *dst, const uint8_t *src, size_t nbytes, uint32_t pos0, s
     else pack_2bit_sse2(dst, src, nbytes, pos0, exc);
 }
 
+// seed identities (plan_kernel's seed_matches, bsw_host.cpp): best over shifts s = 0..12 of the
+// matches of query[10, 40) with target[4 + s, 34 + s); 31 when the pair is too short to test
+static int seed_matches_scalar(const uint8_t *q, int qlen, const uint8_t *r, int tlen)
+{
+    if (qlen < 40 || tlen < 46) return 31;
+    int best = 0;
+    for (int s = 0; s <= 12; ++s) {
+        int c = 0;
+        for (int j = 0; j < 30; ++j) c += q[10 + j] == r[4 + j + s];
+        best = c > best ? c : best;
+    }
+    return best;
+}
+
+// AVX2: the 30 query bytes in one register, each shift one unaligned load + compare + popcount.
+// Reads target bytes [4, 48): only when tlen >= 48 (the scalar form otherwise)
+__attribute__((target("avx2,popcnt"))) static int seed_matches_avx2(const uint8_t *q, int qlen, const uint8_t *r,
+                                                                    int tlen)
+{
+    if (qlen < 42 || tlen < 48) return seed_matches_scalar(q, qlen, r, tlen);
+    const __m256i qv = _mm256_loadu_si256((const __m256i *)(q + 10));
+    int best = 0;
+    for (int s = 0; s <= 12; ++s) {
+        const __m256i rv = _mm256_loadu_si256((const __m256i *)(r + 4 + s));
+        const uint32_t m = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(qv, rv)) & 0x3fffffffu;
+        const int c = __builtin_popcount(m);
+        best = c > best ? c : best;
+    }
+    return best;
+}
+
+void fast_keys(const SeqPair *pairs, int32_t n, const uint8_t *ref, const uint8_t *qer, uint32_t *keys)
+{
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    for (int32_t i = 0; i < n; ++i) {
+        const SeqPair &p = pairs[i];
+        const int qlen = p.len2 > 0 ? p.len2 : 0, tlen = p.len1 > 0 ? p.len1 : 0;
+        const uint8_t *q = qer + (qlen > 0 ? p.idq : 0), *r = ref + (tlen > 0 ? p.idr : 0);
+        const int mt = avx2 ? seed_matches_avx2(q, qlen, r, tlen) : seed_matches_scalar(q, qlen, r, tlen);
+        const int rel = mt > 18;
+        const int h0 = p.h0 < 0 ? 0 : (p.h0 > 255 ? 255 : p.h0);
+        keys[i] = ((uint32_t)(255 - (qlen < 255 ? qlen : 255)) << 20) | ((uint32_t)(1 - rel) << 19) |
+                  ((uint32_t)(63 - ((tlen >> 5) < 63 ? (tlen >> 5) : 63)) << 13) |
+                  ((uint32_t)(31 - (mt < 31 ? mt : 31)) << 8) | (uint32_t)(255 - h0);
+    }
+}
+
 }  // namespace bsw
 
 // bsw_pack_batch (bsw.h): the 2-bit wire form of a batch, host-only

@@ -327,6 +327,37 @@ def test_host_pipeline_chunks(chunk):
     e.close()
 
 
+@pytest.mark.parametrize("chunk", [4096, 65536, 262144])
+def test_host_fast_path_equal_oracle(chunk, c2_full):
+    """The host pipeline's fast path (bsw_host.cpp host_shard_fast: the host computes the schedule
+    keys, sorts each chunk, stages records + nibbles; one pc_kernel<160, nibbles> per chunk reads
+    them in place, no device helper kernels): contiguous C2 batches with extra N bases, empty
+    sequences and the 8-bit regime's edge h0 values, in 1 to ~75 chunks; outputs equal the oracle
+    and only the six output fields change."""
+    pairs, ref, qer, _ = c2_full
+    n = 300_000
+    p = pairs[:n].copy()
+    r, q = ref.copy(), qer.copy()
+    q[13::997] = 4                                   # more N (and a non-ACGT code) than C2 has
+    r[5::1201] = 4
+    r[7::50_003] = 6
+    p["len2"][::5001] = 0                            # empty queries / targets
+    p["len1"][3::7001] = 0
+    qs = p["len2"] > 0
+    p["h0"][qs & (np.arange(n) % 13 == 0)] = 255 - np.minimum(p["len2"], p["len1"])[qs & (np.arange(n) % 13 == 0)]
+    want = p.copy()
+    oracle.get_scores(_oparams(), want, r, q, 100, nthreads=16)
+    e = bsw.Engine(host_chunk=chunk)
+    got = p.copy()
+    e.get_scores(got, r, q, 100)
+    _assert_same(want, got, f"fast path chunk {chunk}")
+    for f in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid"):
+        assert np.array_equal(got[f], p[f])
+    st = e.last_stats()
+    assert st.n_packed == n and st.n_group == 0 and st.n_launches >= 1
+    e.close()
+
+
 @pytest.mark.parametrize("bad_at", [10, 150_000, 199_999])
 def test_host_pipeline_invalid_pair_writes_nothing(bad_at):
     """The pipeline validates the first chunk's blocks, starts it, and validates the rest before
