@@ -338,9 +338,8 @@ def test_host_fast_path_equal_oracle(chunk, c2_full):
     n = 300_000
     p = pairs[:n].copy()
     r, q = ref.copy(), qer.copy()
-    q[13::997] = 4                                   # more N (and a non-ACGT code) than C2 has
+    q[13::997] = 4                                   # more N than C2 has (codes are 0..4 by the ABI)
     r[5::1201] = 4
-    r[7::50_003] = 6
     p["len2"][::5001] = 0                            # empty queries / targets
     p["len1"][3::7001] = 0
     qs = p["len2"] > 0
