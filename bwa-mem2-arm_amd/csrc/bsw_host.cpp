@@ -1190,48 +1190,67 @@ static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, int mode)
 // order only schedules).  BSW_HP_FAST=0 turns the path off (A/B).
 struct FastChunk {
     int32_t a = 0, m = 0;                    // pairs [a, a + m) of the call
-    size_t ref_off = 0, qer_off = 0, out_off = 0, h2d = 0, dev = 0;
+    size_t perm_off = 0, ref_off = 0, qer_off = 0, err_off = 0, out_off = 0, h2d = 0, dev = 0;
     int64_t r_lo = 0, q_lo = 0;
+    std::chrono::steady_clock::time_point t0;   // (BSW_DEBUG_HP timeline)
 };
 
-// stable LSD radix of idx[0, m) by keys[idx[.]] over the key bytes that vary; tmp: scratch of m
-static void radix_order(const uint32_t *keys, int32_t m, int32_t *idx, int32_t *tmp)
+// The schedule order of a chunk, on ONE thread (it runs beside the pool staging the next chunk):
+// perm[k] = the pair in slot k, by ascending key, stable.  Only the key bits that vary in the
+// chunk count (compacted by pext): one counting pass when they fit 16 bits (C2: related +
+// identities + h0 = 14 bits), else an LSD radix of 8-bit digits over (key << 32 | pair) words.
+static void sort_order(const uint32_t *keys, int32_t m, int32_t *perm, std::vector<uint64_t> &kv,
+                       std::vector<uint64_t> &tmp)
 {
-    for (int32_t i = 0; i < m; ++i) idx[i] = i;
-    if (m <= 1) return;
+    if (m <= 1) {
+        if (m == 1) perm[0] = 0;
+        return;
+    }
     uint32_t vor = 0, vand = ~0u;
     for (int32_t i = 0; i < m; ++i) { vor |= keys[i]; vand &= keys[i]; }
     const uint32_t vary = vor ^ vand;
-    const int nt = (int)std::min<int64_t>(HostPool::workers() + 1, std::max<int64_t>(1, m >> 14));
-    std::vector<int32_t> hist((size_t)nt * 256);
-    for (int d = 0; d < 4; ++d) {
-        if (((vary >> (8 * d)) & 0xffu) == 0) continue;
-        const int sh = 8 * d;
-        auto lo = [&](int t) { return (int32_t)((int64_t)m * t / nt); };
-        HostPool::get().parallel_for(nt, [&](int t) {
-            int32_t *h = hist.data() + (size_t)t * 256;
-            std::fill(h, h + 256, 0);
-            for (int32_t i = lo(t); i < lo(t + 1); ++i) ++h[(keys[idx[i]] >> sh) & 0xffu];
-        });
-        int32_t run = 0;                                       // offsets: digit-major, then piece
-        for (int b = 0; b < 256; ++b)
-            for (int t = 0; t < nt; ++t) {
-                const int32_t c = hist[(size_t)t * 256 + b];
-                hist[(size_t)t * 256 + b] = run;
-                run += c;
-            }
-        HostPool::get().parallel_for(nt, [&](int t) {
-            int32_t *h = hist.data() + (size_t)t * 256;
-            for (int32_t i = lo(t); i < lo(t + 1); ++i) tmp[h[(keys[idx[i]] >> sh) & 0xffu]++] = idx[i];
-        });
-        std::copy(tmp, tmp + m, idx);
+    const int bits = __builtin_popcount(vary);
+    kv.resize((size_t)m);
+    compact_keys(keys, 0, m, vary, kv.data());
+    if (bits <= 16) {
+        std::vector<int32_t> cnt((size_t)1 << bits, 0);
+        for (int32_t i = 0; i < m; ++i) ++cnt[kv[i] >> 32];
+        int32_t run = 0;
+        for (auto &c : cnt) {
+            const int32_t x = c;
+            c = run;
+            run += x;
+        }
+        for (int32_t i = 0; i < m; ++i) perm[cnt[kv[i] >> 32]++] = (int32_t)(uint32_t)kv[i];
+        return;
     }
+    tmp.resize((size_t)m);
+    uint64_t *src = kv.data(), *dst = tmp.data();
+    int32_t hist[256];
+    for (int d = 0; 8 * d < bits; ++d) {
+        const int sh = 32 + 8 * d;
+        std::fill(hist, hist + 256, 0);
+        for (int32_t i = 0; i < m; ++i) ++hist[(src[i] >> sh) & 0xffu];
+        int32_t run = 0;
+        for (int x = 0; x < 256; ++x) {
+            const int32_t c = hist[x];
+            hist[x] = run;
+            run += c;
+        }
+        for (int32_t i = 0; i < m; ++i) dst[hist[(src[i] >> sh) & 0xffu]++] = src[i];
+        std::swap(src, dst);
+    }
+    for (int32_t i = 0; i < m; ++i) perm[i] = (int32_t)(uint32_t)src[i];
 }
 
+// Stage one chunk (records in the caller's order as PairIn with nibble offsets, schedule keys,
+// both byte extents as nibbles) with the host pool.  `side` runs on the calling thread while the
+// pool works (the previous chunk's sort and launch).
 static int stage_fast(Slot &s, const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t m,
                       const BlkStat *bs, int32_t nblk, FastChunk &c, std::vector<uint32_t> &keys,
-                      std::vector<int32_t> &perm, std::vector<int32_t> &tmp)
+                      const std::function<void()> &side)
 {
+    c.t0 = std::chrono::steady_clock::now();
     int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
     for (int32_t b = 0; b < nblk; ++b) {
         r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
@@ -1242,12 +1261,17 @@ static int stage_fast(Slot &s, const SeqPair *pairs, const uint8_t *ref, const u
     const size_t rb = (size_t)(r_hi - r_lo), qb = (size_t)(q_hi - q_lo);
     c.m = m;
     c.r_lo = r_lo; c.q_lo = q_lo;
-    c.ref_off = align256((size_t)m * sizeof(PairIn));
+    c.perm_off = align256((size_t)m * sizeof(PairIn));
+    c.ref_off = align256(c.perm_off + (size_t)m * 4);
     c.qer_off = align256(c.ref_off + (rb + 1) / 2 + 8);
-    c.h2d = c.qer_off + (qb + 1) / 2 + 8;
-    c.out_off = align256(c.h2d);
+    // the range-guard word travels inside the H2D (zeroed by the host) and the D2H (beside the
+    // outputs): a memset or a 4-byte readback is a blit kernel that waits for wave slots behind
+    // the previous chunk's DP waves, and holds its stream meanwhile (trace)
+    c.err_off = align256(c.qer_off + (qb + 1) / 2 + 8);
+    c.h2d = c.err_off + 256;
+    c.out_off = c.err_off + 256;
     c.dev = c.out_off + (size_t)m * 24;
-    const size_t hb = std::max(c.h2d, (size_t)m * 24);
+    const size_t hb = std::max(c.h2d, (size_t)256 + (size_t)m * 24);
     if (hb > s.cap_stage) {
         const size_t cap = std::max(hb + hb / 4, s.cap_stage * 3 / 2);
         if (s.h_stage) (void)hipHostFree(s.h_stage);
@@ -1256,19 +1280,29 @@ static int stage_fast(Slot &s, const SeqPair *pairs, const uint8_t *ref, const u
         s.cap_stage = cap;
     }
     keys.resize((size_t)m);
-    perm.resize((size_t)m);
-    tmp.resize((size_t)m);
     uint8_t *h = (uint8_t *)s.h_stage;
-    // keys (pieces of 8K pairs) and both nibble packs (pieces of ~4 MB) as one pool job list
+    PairIn *rec = (PairIn *)h;
+    // task 0 (the calling thread): `side`; then records + keys (pieces of 8K pairs) and both nibble
+    // packs (pieces of ~4 MB) as one pool job list
     const int nk = (int)std::max<int64_t>(1, m >> 13), nr = (int)std::max<size_t>(1, rb >> 22),
               nq = (int)std::max<size_t>(1, qb >> 22);
     auto even = [](size_t total, int k, int parts) {
         return k == parts ? total : (total * (size_t)k / (size_t)parts) & ~(size_t)31;
     };
-    HostPool::get().parallel_for(nk + nr + nq, [&](int t) {
+    HostPool::get().parallel_for(1 + nk + nr + nq, [&](int t) {
+        if (t == 0) {
+            side();
+            return;
+        }
+        --t;
         if (t < nk) {
             const int32_t a0 = (int32_t)((int64_t)m * t / nk), a1 = (int32_t)((int64_t)m * (t + 1) / nk);
             fast_keys(pairs + a0, a1 - a0, ref, qer, keys.data() + a0);
+            for (int32_t i = a0; i < a1; ++i) {
+                const SeqPair &p = pairs[i];
+                rec[i] = PairIn{p.len1 > 0 ? (int32_t)(p.idr - r_lo) : 0, p.len2 > 0 ? (int32_t)(p.idq - q_lo) : 0,
+                                p.len1, p.len2, p.h0};
+            }
         } else if (t < nk + nr) {
             const size_t a0 = even(rb, t - nk, nr), a1 = even(rb, t - nk + 1, nr);
             pack_nibbles(h + c.ref_off + a0 / 2, ref + r_lo + a0, a1 - a0);
@@ -1279,16 +1313,10 @@ static int stage_fast(Slot &s, const SeqPair *pairs, const uint8_t *ref, const u
     });
     memset(h + c.ref_off + (rb + 1) / 2, 0, 8);
     memset(h + c.qer_off + (qb + 1) / 2, 0, 8);
-    radix_order(keys.data(), m, perm.data(), tmp.data());
-    PairIn *rec = (PairIn *)h;
-    const int nw = (int)std::max<int64_t>(1, m >> 14);
-    HostPool::get().parallel_for(nw, [&](int t) {
-        for (int32_t k = (int32_t)((int64_t)m * t / nw); k < (int32_t)((int64_t)m * (t + 1) / nw); ++k) {
-            const SeqPair &p = pairs[perm[k]];
-            rec[k] = PairIn{p.len1 > 0 ? (int32_t)(p.idr - r_lo) : 0, p.len2 > 0 ? (int32_t)(p.idq - q_lo) : 0,
-                            p.len1, p.len2, p.h0};
-        }
-    });
+    memset(h + c.err_off, 0, 256);
+    if (getenv("BSW_DEBUG_HP"))
+        fprintf(stderr, "fast stage %d pairs: %.3f ms\n", (int)m,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c.t0).count());
     return BSW_OK;
 }
 
@@ -1301,7 +1329,11 @@ static std::vector<std::pair<int32_t, int32_t>> fast_chunks(const std::vector<Bl
     const int32_t nblk = (int32_t)bs.size();
     const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
     int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
+    const int32_t first = cur;
     for (int32_t b = 0, nb = 0; b < nblk; b += nb, cur = std::min(cap_blk, cur * 2)) {
+        // ramp down again toward the end: the last chunk's H2D + kernel (one wave lifetime at
+        // least) are the call's tail once the host has staged everything (chunks' kernels overlap)
+        cur = std::min(cur, std::max(first, (nblk - b) / 2));
         int64_t bytes = 0;
         for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
             const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
@@ -1323,32 +1355,67 @@ static int host_shard_fast(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, con
     FastChunk fc[kSlots];
     bool pend[kSlots] = {};
     std::vector<uint32_t> keys[kSlots];
-    std::vector<int32_t> perm[kSlots], tmp[kSlots];
+    std::vector<uint64_t> kv[kSlots], tmp[kSlots];
+    // (a slot is reused only after finish(): its chunk was launched one step after staging, so a
+    // staged-but-unlaunched chunk never sits in the slot being restaged -- kSlots >= 2)
     bsw_stats_t agg{};
     double stage_ms = 0;
     int rc = BSW_OK;
+    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;
     auto finish = [&](int k) -> int {
         if (!pend[k]) return BSW_OK;
         pend[k] = false;
         Slot &s = *slots[k];
+        const auto tw = now();
+        // the readbacks are queued only now: copies of all streams pass one copy engine in order,
+        // so a D2H queued right behind its kernel held every later chunk's H2D until that kernel
+        // ended (kernel + copy trace: chunks fully serialised)
+        BSW_TRY(hipMemcpyAsync(s.h_stage, s.d_stage + fc[k].err_off, 256 + (size_t)fc[k].m * 24,
+                               hipMemcpyDeviceToHost, s.stream));
         BSW_TRY(hipStreamSynchronize(s.stream));
         float ms = 0.f;
         BSW_TRY(hipEventElapsedTime(&ms, s.ev0, s.ev1));
         agg.kernel_ms += ms;
-        if (s.h_meta[kMetaErr] != 0) return BSW_E_RANGE;
-        const int32_t *o = (const int32_t *)s.h_stage;
+        if (dbg)
+            fprintf(stderr, "fast finish slot %d: waited %.3f ms at %.3f, kernel %.3f ms\n", k,
+                    std::chrono::duration<double, std::milli>(now() - tw).count(),
+                    std::chrono::duration<double, std::milli>(tw - t_start).count(), ms);
+        if (((const int32_t *)s.h_stage)[0] != 0) return BSW_E_RANGE;
+        const int32_t *o = (const int32_t *)((const uint8_t *)s.h_stage + 256);   // outputs, caller's order
         const int32_t m = fc[k].m, a = fc[k].a;
-        const int32_t *pm = perm[k].data();
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(HostPool::workers() + 1, m >> 15));
         HostPool::get().parallel_for(nt, [&](int t) {
             for (int32_t j = (int32_t)((int64_t)m * t / nt); j < (int32_t)((int64_t)m * (t + 1) / nt); ++j) {
                 const int32_t *q = o + 6 * (int64_t)j;
-                SeqPair &p = pairs[a + pm[j]];
+                SeqPair &p = pairs[a + j];
                 p.score = q[0]; p.tle = q[1]; p.gtle = q[2]; p.qle = q[3]; p.gscore = q[4]; p.max_off = q[5];
             }
         });
         agg.n_packed += m; agg.n_i16 += m; agg.n_launches += 1;
         return BSW_OK;
+    };
+    // chunk c's sort and launch run on the calling thread while the pool stages chunk c + 1
+    // (stage_fast's side task): the sort is off the staging path, at one chunk of latency
+    int prev = -1;                                   // slot holding a staged chunk not yet launched
+    int side_rc = BSW_OK;
+    auto launch = [&](int k) {
+        if (k < 0 || side_rc) return;
+        side_rc = [&]() -> int {
+            Slot &s = *slots[k];
+            const FastChunk &c = fc[k];
+            uint8_t *h = (uint8_t *)s.h_stage;
+            sort_order(keys[k].data(), c.m, (int32_t *)(h + c.perm_off), kv[k], tmp[k]);
+            BSW_TRY(grow(s.d_stage, s.cap_dstage, c.dev));
+            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.h2d, hipMemcpyHostToDevice, s.stream));
+            BSW_TRY(hipEventRecord(s.ev0, s.stream));
+            BSW_TRY(launch_pc_nib_kernel(kp, w, (const PairIn *)s.d_stage, (const int32_t *)(s.d_stage + c.perm_off),
+                                         c.m, s.d_stage + c.ref_off, s.d_stage + c.qer_off,
+                                         (int32_t *)(s.d_stage + c.out_off), (int32_t *)(s.d_stage + c.err_off),
+                                         s.stream));
+            BSW_TRY(hipEventRecord(s.ev1, s.stream));
+            pend[k] = true;
+            return BSW_OK;
+        }();
     };
     rc = [&]() -> int {
         BSW_TRY(hipSetDevice(dc.device));
@@ -1362,26 +1429,19 @@ static int host_shard_fast(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, con
                 slots[k] = dc.acquire(r);
                 if (r) return r;
             }
-            Slot &s = *slots[k];
+            const int p = prev;
             const auto t0 = now();
-            if (int r = stage_fast(s, pairs + a, ref, qer, m, bs.data() + b, nb, fc[k], keys[k], perm[k], tmp[k]))
+            if (int r = stage_fast(*slots[k], pairs + a, ref, qer, m, bs.data() + b, nb, fc[k], keys[k],
+                                   [&] { launch(p); }))
                 return r;
+            if (side_rc) return side_rc;
             stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
             fc[k].a = a;
-            const FastChunk &c = fc[k];
-            BSW_TRY(grow(s.d_stage, s.cap_dstage, c.dev));
-            int32_t *d_err = s.d_meta + kMetaErr;
-            BSW_TRY(hipMemsetAsync(d_err, 0, sizeof(int32_t), s.stream));
-            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.h2d, hipMemcpyHostToDevice, s.stream));
-            BSW_TRY(hipEventRecord(s.ev0, s.stream));
-            BSW_TRY(launch_pc_nib_kernel(kp, w, (const PairIn *)s.d_stage, m, s.d_stage + c.ref_off,
-                                         s.d_stage + c.qer_off, (int32_t *)(s.d_stage + c.out_off), d_err, s.stream));
-            BSW_TRY(hipEventRecord(s.ev1, s.stream));
-            BSW_TRY(hipMemcpyAsync(s.h_stage, s.d_stage + c.out_off, (size_t)m * 24, hipMemcpyDeviceToHost, s.stream));
-            BSW_TRY(hipMemcpyAsync(s.h_meta + kMetaErr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
-            pend[k] = true;
+            prev = k;
             k = (k + 1) % kSlots;
         }
+        launch(prev);
+        if (side_rc) return side_rc;
         for (int j = 0; j < kSlots; ++j)
             if (int r = finish(j)) return r;
         return BSW_OK;

@@ -46,4 +46,6 @@ void pack_2bit(uint8_t *dst, const uint8_t *src, size_t nbytes, uint32_t pos0, s
 // (63 - tlen / 32) << 13 | (31 - seed identities) << 8 | (255 - h0), identities as the device's
 // seed_matches (best of 13 shifts of query[10, 40) against target[4 + s, 34 + s))
 void fast_keys(const SeqPair *pairs, int32_t n, const uint8_t *ref, const uint8_t *qer, uint32_t *keys);
+// kv[i] = (the bits of keys[i] selected by `vary`, compacted: pext) << 32 | i, for i in [a0, a1)
+void compact_keys(const uint32_t *keys, int32_t a0, int32_t a1, uint32_t vary, uint64_t *kv);
 }  // namespace bsw

@@ -72,12 +72,13 @@ hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pai
                             const uint8_t *qer, int32_t *err, hipStream_t s);
 
 // The same kernel (QMAX 160) over a host-staged chunk read in place (the host
-// pipeline's fast path): recs[k] = pair k's input fields (pairs already in schedule order, no
-// `order`), idr / idq = NIBBLE indices into ref4 / qer4 (two codes per byte, low nibble first;
-// both 4-byte aligned), outputs as 6 x int32 per pair into out24[6k ..].  Same eligibility as
-// launch_pc_kernel (qlen < 160, h0 + min(len1, len2) <= 255, kp.pk_ok).
-hipError_t launch_pc_nib_kernel(const KParams &kp, int32_t w, const PairIn *recs, int32_t n, const uint8_t *ref4,
-                                const uint8_t *qer4, int32_t *out24, int32_t *err, hipStream_t s);
+// pipeline's fast path): lane slot k runs pair order[k] (the host's schedule order), reading its
+// input fields recs[order[k]] -- idr / idq = NIBBLE indices into ref4 / qer4 (two codes per byte,
+// low nibble first; both 4-byte aligned) -- and writing its outputs as 6 x int32 to
+// out24[6 order[k] ..].  Same eligibility as launch_pc_kernel (qlen < 160, h0 + min(len1, len2)
+// <= 255, kp.pk_ok).
+hipError_t launch_pc_nib_kernel(const KParams &kp, int32_t w, const PairIn *recs, const int32_t *order, int32_t n,
+                                const uint8_t *ref4, const uint8_t *qer4, int32_t *out24, int32_t *err, hipStream_t s);
 
 // Wave-per-alignment band kernel (bsw_wv.hip): one SeqPair per wavefront, the row spread over
 // the 64 lanes as a sliding window of 64 * cols absolute columns (cols = 4, 8 or 16).  Needs

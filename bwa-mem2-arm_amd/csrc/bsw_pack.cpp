@@ -188,6 +188,23 @@ void fast_keys(const SeqPair *pairs, int32_t n, const uint8_t *ref, const uint8_
     }
 }
 
+__attribute__((target("bmi2"))) static void compact_bmi2(const uint32_t *keys, int32_t a0, int32_t a1, uint32_t vary,
+                                                         uint64_t *kv)
+{
+    for (int32_t i = a0; i < a1; ++i) kv[i] = ((uint64_t)_pext_u32(keys[i], vary) << 32) | (uint32_t)i;
+}
+
+void compact_keys(const uint32_t *keys, int32_t a0, int32_t a1, uint32_t vary, uint64_t *kv)
+{
+    static const bool bmi2 = __builtin_cpu_supports("bmi2");
+    if (bmi2) { compact_bmi2(keys, a0, a1, vary, kv); return; }
+    for (int32_t i = a0; i < a1; ++i) {
+        uint32_t ck = 0;
+        for (uint32_t v = vary, o = 0; v; v &= v - 1, ++o) ck |= ((keys[i] >> __builtin_ctz(v)) & 1u) << o;
+        kv[i] = ((uint64_t)ck << 32) | (uint32_t)i;
+    }
+}
+
 }  // namespace bsw
 
 // bsw_pack_batch (bsw.h): the 2-bit wire form of a batch, host-only

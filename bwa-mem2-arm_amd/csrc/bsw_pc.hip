@@ -608,12 +608,12 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
     __syncthreads();
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = gid < n;
-    const int idx = valid ? (NIB ? gid : (order ? order[gid] : gid)) : 0;
+    const int idx = valid ? (order ? order[gid] : gid) : 0;
     SeqPair *sp = pairs + idx;
     int idr = 0, idq = 0, tlen = 0, qlen = 0, h0 = 0;
     if (valid) {
         if constexpr (NIB) {
-            const PairIn r = recs[gid];
+            const PairIn r = recs[idx];
             idr = r.idr; idq = r.idq; tlen = r.len1; qlen = r.len2; h0 = r.h0;
         } else {
             idr = sp->idr; idq = sp->idq; tlen = sp->len1; qlen = sp->len2; h0 = sp->h0;
@@ -878,7 +878,7 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
 #endif
     if (valid) {
         if constexpr (NIB) {
-            int32_t *o = out24 + 6 * (int64_t)gid;
+            int32_t *o = out24 + 6 * (int64_t)idx;
             o[0] = best; o[1] = best_i + 1; o[2] = max_ie + 1; o[3] = best_j + 1; o[4] = gsc; o[5] = moff;
         } else {
             sp->score = best;
@@ -927,14 +927,14 @@ static void launch_pc_q(const KParams &kp, int32_t w, SeqPair *pairs, const int3
                            n, ref, qer, err);
 }
 
-hipError_t launch_pc_nib_kernel(const KParams &kp, int32_t w, const PairIn *recs, int32_t n, const uint8_t *ref4,
-                                const uint8_t *qer4, int32_t *out24, int32_t *err, hipStream_t s)
+hipError_t launch_pc_nib_kernel(const KParams &kp, int32_t w, const PairIn *recs, const int32_t *order, int32_t n,
+                                const uint8_t *ref4, const uint8_t *qer4, int32_t *out24, int32_t *err, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
     if (((uintptr_t)ref4 | (uintptr_t)qer4) & 3) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((n + 63) / 64);
     hipLaunchKernelGGL((pc_kernel<160, 1, false, true>), dim3(grid), dim3(64), (unsigned)max(kp.lds_pad, 0), s, kp, w,
-                       (SeqPair *)nullptr, (const int32_t *)nullptr, n, ref4, qer4, err, recs, out24);
+                       (SeqPair *)nullptr, order, n, ref4, qer4, err, recs, out24);
     return hipGetLastError();
 }
 
