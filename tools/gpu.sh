@@ -99,7 +99,7 @@ for step in "$@"; do
     unset)
         unset "${arg?}"; echo "unset $arg" ;;
     py)
-        log=$O/$(basename "$arg" .py).log
+        log=$O/$(basename "$arg" .py)_$n.log
         timeout -k 10 600 python -u "$arg" > "$log" 2>&1 || fail "$step" $? "$log"
         tail -5 "$log" ;;
     *) echo "unknown step $step"; exit 2 ;;

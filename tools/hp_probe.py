@@ -31,6 +31,6 @@ for k in range(calls + 2):
         ms.append((time.perf_counter() - t) * 1e3)
 same = all(np.array_equal(buf[f], want[f]) for f in bsw.OUT_FIELDS)
 med = statistics.median(ms)
-print(f"pads hp={os.environ.get('BSW_HP_LDS_PAD', '-')} pc={os.environ.get('BSW_PC_LDS_PAD', '-')}: host call median "
+print(f"fast={os.environ.get('BSW_HP_FAST', '-')} pads hp={os.environ.get('BSW_HP_LDS_PAD', '-')} pc={os.environ.get('BSW_PC_LDS_PAD', '-')}: host call median "
       f"{med:.2f} ms (min {min(ms):.2f}) = {1e3 / med:.1f} M/s; resident DP kernel {statistics.median(km[2:]):.3f} ms; "
-      f"outputs identical {same}", flush=True)
+      f"outputs identical {same}; calls {[round(x, 2) for x in ms]}", flush=True)
