@@ -1454,7 +1454,7 @@ static int host_shard_fast(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, con
     return rc;
 }
 
-// One device's share of a host-buffer call: a pipeline of chunks over up to three slots.
+// One device's share of a host-buffer call: a pipeline of chunks over the device's slots (four by default).
 // Per chunk: stage into the slot's pinned buffer (records + nibble-packed sequences, host
 // pool) -> one H2D -> unpack -> plan / sort -> DP kernels -> D2H of the records.  The calling
 // thread only stages and enqueues copies and plans; a launcher thread enqueues each chunk's DP

@@ -237,6 +237,23 @@ void oracle_fmi_counters(uint64_t *out, int reset)
  * GPU kernel's text mode serves s = 1 from the text), [2] block loads of the s >= 2 ones */
 static __thread int g_phase;
 static uint64_t g_ph[5][3];
+/* analysis counters (tools/smem_phase_counts.py), per phase, over the extensions the GPU kernel
+ * walks through occurrence blocks -- s >= 2 and a result string longer than kt (shorter ones come
+ * from its k-mer table): [0] all of them, [1] those of an interval with exactly s = 2, [2] those
+ * of [1] that keep s = 2 (both occurrences agree on the next base: what a two-position text mode
+ * would serve) */
+static __thread int g_len;
+static int g_kt;
+static uint64_t g_s2[5][3];
+void oracle_fmi_s2_counters(uint64_t *out15, int reset, int kt)
+{
+    for (int p = 0; p < 5; ++p)
+        for (int k = 0; k < 3; ++k) {
+            out15[3 * p + k] = __atomic_load_n(&g_s2[p][k], __ATOMIC_RELAXED);
+            if (reset) g_s2[p][k] = 0;
+        }
+    g_kt = kt;
+}
 void oracle_fmi_phase_counters(uint64_t *out15, int reset)
 {
     for (int p = 0; p < 5; ++p)
@@ -267,6 +284,11 @@ static void backward_ext(const fmi_ref_t *f, const uint64_t in[3], int a, uint64
     l[2] = l[3] + s[3];
     l[1] = l[2] + s[2];
     l[0] = l[1] + s[1];
+    if (in[2] >= 2 && g_len > g_kt) {
+        __atomic_fetch_add(&g_s2[g_phase][0], 1, __ATOMIC_RELAXED);
+        if (in[2] == 2) __atomic_fetch_add(&g_s2[g_phase][1], 1, __ATOMIC_RELAXED);
+        if (in[2] == 2 && s[a] == 2) __atomic_fetch_add(&g_s2[g_phase][2], 1, __ATOMIC_RELAXED);
+    }
     out[0] = (uint64_t)k[a]; out[1] = (uint64_t)l[a]; out[2] = (uint64_t)s[a];
 }
 
@@ -326,6 +348,7 @@ static int smem1a(const fmi_ref_t *f, int len, const uint8_t *q, int x, int min_
             break;
         } else if (q[i] < 4) {
             c = 3 - q[i];
+            g_len = i + 1 - x;
             ext_fwd(f, &ik, c, &ok);
             if (ok.x[2] != ik.x[2]) {
                 ipush(curr, &ik);
@@ -346,6 +369,7 @@ static int smem1a(const fmi_ref_t *f, int len, const uint8_t *q, int x, int min_
         c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
         for (j = 0, curr->n = 0; j < prev->n; ++j) {
             ref_intv_t *p = &prev->a[j];
+            g_len = (int)(uint32_t)p->info - i;
             if (c >= 0 && ik.x[2] >= max_intv) ext_back(f, p, c, &ok);
             if (c < 0 || ik.x[2] < max_intv || ok.x[2] < (uint64_t)min_intv) {
                 if (curr->n == 0) {
@@ -379,6 +403,7 @@ static int seed_strategy1(const fmi_ref_t *f, int len, const uint8_t *q, int x, 
     for (i = x + 1; i < len; ++i) {
         if (q[i] < 4) {
             c = 3 - q[i];
+            g_len = i + 1 - x;
             ext_fwd(f, &ik, c, &ok);
             if (ok.x[2] < (uint64_t)max_intv && i - x >= min_len) {
                 *mem = ok;
