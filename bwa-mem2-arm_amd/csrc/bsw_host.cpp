@@ -1187,7 +1187,7 @@ static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, int mode)
 // wait ~0.3-1.6 ms for wave slots behind the previous chunk's DP waves (kernel + copy trace,
 // profiles/r05/hostpath_trace_timeline.txt), so consecutive chunks' DP kernels could not overlap
 // (9.6 ms of chunk DP for 6.85 ms of work).  Outputs are identical (pairs are independent; the
-// order only schedules).  BSW_HP_FAST=0 turns the path off (A/B).
+// order only schedules).  Off by default (measured slower); BSW_HP_FAST=1 turns it on.
 struct FastChunk {
     int32_t a = 0, m = 0;                    // pairs [a, a + m) of the call
     size_t perm_off = 0, ref_off = 0, qer_off = 0, err_off = 0, out_off = 0, h2d = 0, dev = 0;
@@ -1346,7 +1346,8 @@ static std::vector<std::pair<int32_t, int32_t>> fast_chunks(const std::vector<Bl
 }
 
 static int host_shard_fast(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref, const uint8_t *qer,
-                           int32_t n, int32_t w, int32_t chunk, const std::vector<BlkStat> &bs, bsw_stats_t *st)
+                           int32_t n, int32_t w, int cell_bits, int32_t chunk, const std::vector<BlkStat> &bs,
+                           bsw_stats_t *st)
 {
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto t_start = now();
@@ -1391,7 +1392,8 @@ static int host_shard_fast(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, con
                 p.score = q[0]; p.tle = q[1]; p.gtle = q[2]; p.qle = q[3]; p.gscore = q[4]; p.max_off = q[5];
             }
         });
-        agg.n_packed += m; agg.n_i16 += m; agg.n_launches += 1;
+        agg.n_packed += m; agg.n_launches += 1;
+        (cell_bits == 8 ? agg.n_u8 : agg.n_i16) += m;     // as run_dp counts the packed classes
         return BSW_OK;
     };
     // chunk c's sort and launch run on the calling thread while the pool stages chunk c + 1
@@ -1483,7 +1485,11 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
     if (chunk <= 0) chunk = n;
     // the fast path (no device helper kernels) when every pair fits the packed-column kernel and the
     // call is past the small-batch kernels' sizes (those are latency-bound: the row-group kernel)
-    static const bool fast_on = getenv("BSW_HP_FAST") == nullptr || atoi(getenv("BSW_HP_FAST")) != 0;
+    // opt-in (BSW_HP_FAST=1, read per call): same box, interleaved, the general pipeline ran 1M-pair
+    // calls in 12.1 ms and this path in 14.9 ms (profiles/r05/hostpath_fast_ab.txt: the host sort +
+    // nibble staging of each chunk is slower than the device plan / sort it replaces)
+    const char *fe = getenv("BSW_HP_FAST");
+    const bool fast_on = fe != nullptr && atoi(fe) != 0;
     if (fast_on && kp0.pk_ok && kp0.kern8 == 1 && !kp0.misroute && kp0.maxsc == 1 && n > kp0.small_batch &&
         n > kp0.mid_batch && two_bit) {
         bool ok = true;
@@ -1501,7 +1507,7 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
             ok = ok && (r_hi - r_lo) <= r_sum + r_sum / 4 + 4096 && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096 &&
                  (r_hi - r_lo) < ((int64_t)1 << 30) && (q_hi - q_lo) < ((int64_t)1 << 30);
         }
-        if (ok) return host_shard_fast(kp, dc, pairs, ref, qer, n, w, chunk, bs, st);
+        if (ok) return host_shard_fast(kp, dc, pairs, ref, qer, n, w, cell_bits, chunk, bs, st);
     }
     // slots are taken as chunks start (a one-chunk call takes one); chunk k + nslots stages only
     // once chunk k's outputs are back.  4 since round 4: with the helper stream the fourth slot

@@ -328,12 +328,13 @@ def test_host_pipeline_chunks(chunk):
 
 
 @pytest.mark.parametrize("chunk", [4096, 65536, 262144])
-def test_host_fast_path_equal_oracle(chunk, c2_full):
+def test_host_fast_path_equal_oracle(chunk, c2_full, monkeypatch):
     """The host pipeline's fast path (bsw_host.cpp host_shard_fast: the host computes the schedule
     keys, sorts each chunk, stages records + nibbles; one pc_kernel<160, nibbles> per chunk reads
     them in place, no device helper kernels): contiguous C2 batches with extra N bases, empty
     sequences and the 8-bit regime's edge h0 values, in 1 to ~75 chunks; outputs equal the oracle
-    and only the six output fields change."""
+    and only the six output fields change.  The path is opt-in (BSW_HP_FAST=1, read per call)."""
+    monkeypatch.setenv("BSW_HP_FAST", "1")
     pairs, ref, qer, _ = c2_full
     n = 300_000
     p = pairs[:n].copy()

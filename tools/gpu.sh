@@ -6,6 +6,7 @@
 # Steps:
 #   tests           the whole -m gpu suite, one process, per-test timeout
 #   tests:<expr>    the -m gpu tests matching -k <expr>
+#   testsall        the whole -m gpu suite without -x (every failure listed; a GPU fault still ends it)
 #   smoke           __graft_entry__.smoke()
 #   bench           the default bench line (driver form: python bench.py)
 #   bench:<args>    bench.py with extra arguments (commas for spaces: bench:--workload,c1)
@@ -38,6 +39,11 @@ for step in "$@"; do
         log=$O/gpu_tests${arg:+_$arg}.log
         k=(); [ -n "$arg" ] && k=(-k "$arg")
         timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${k[@]}" \
+            > "$log" 2>&1 || fail "$step" $? "$log"
+        tail -1 "$log" ;;
+    testsall)
+        log=$O/gpu_tests_all.log
+        timeout -k 10 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
             > "$log" 2>&1 || fail "$step" $? "$log"
         tail -1 "$log" ;;
     smoke)
