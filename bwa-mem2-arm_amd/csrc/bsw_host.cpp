@@ -220,6 +220,7 @@ struct Slot {
     int32_t *d_meta = nullptr;          // counts[kMetaCounts], maxq_wide, err
     int32_t *h_meta = nullptr;          // pinned mirror
     int2 *d_scratch = nullptr; size_t cap_scratch = 0;
+    int32_t *d_pq = nullptr; size_t cap_pq = 0;   // persistent DP kernel: head, ready, abort words
     // host-buffer pipeline: pinned staging of one chunk and its device copy
     void *h_stage = nullptr; size_t cap_stage = 0;
     uint8_t *d_stage = nullptr; size_t cap_dstage = 0;
@@ -322,18 +323,32 @@ struct DeviceCtx {
     uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
     int64_t refres_len = -1;
     std::shared_mutex refmu;            // extension calls hold it shared while they use d_refres
+    // persistent host pipeline (host_shard_pq): one call at a time per device, on a CU-masked pair
+    // of streams -- the DP grid on all but pq_nres CUs, the chunks' helper kernels on those
+    std::mutex pq_mu;
+    hipStream_t pq_h = nullptr, pq_d = nullptr;
+    int pq_nres = 0, pq_ncu = 0;
+    bool pq_failed = false;             // stream creation failed once: the general pipeline
+    hipEvent_t pq_ev[8] = {}, pq_t0 = nullptr, pq_t1 = nullptr, pq_init = nullptr;
+    void *pq_hout = nullptr; size_t pq_hout_cap = 0;   // pinned: the call's 24-B outputs
 
     ~DeviceCtx()
     {
         for (auto &s : free_slots) release_slot(s.get());
         if (d_refres) { (void)hipSetDevice(device); (void)hipFree(d_refres); }
+        (void)hipSetDevice(device);
+        for (hipEvent_t e : pq_ev) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {pq_t0, pq_t1, pq_init}) if (e) (void)hipEventDestroy(e);
+        if (pq_h) (void)hipStreamDestroy(pq_h);
+        if (pq_d) (void)hipStreamDestroy(pq_d);
+        if (pq_hout) (void)hipHostFree(pq_hout);
     }
     static void release_slot(Slot *s)
     {
         (void)hipSetDevice(s->device);
         (void)hipFree(s->d_pairs); (void)hipFree(s->d_ref); (void)hipFree(s->d_qer);
         (void)hipFree(s->d_keys); (void)hipFree(s->d_keys2); (void)hipFree(s->d_vals); (void)hipFree(s->d_order);
-        (void)hipFree(s->d_tmp); (void)hipFree(s->d_meta); (void)hipFree(s->d_scratch);
+        (void)hipFree(s->d_tmp); (void)hipFree(s->d_meta); (void)hipFree(s->d_scratch); (void)hipFree(s->d_pq);
         (void)hipFree(s->d_stage);
         if (s->h_stage) (void)hipHostFree(s->h_stage);
         (void)hipFree(s->d_mjobs); (void)hipFree(s->d_mrows); (void)hipFree(s->d_mmeta);
@@ -480,6 +495,7 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.mid_batch = 32768;
     kp.group_kernel = 1;
     kp.busy_min = 0;                 // measured slower at every setting: off
+    kp.persist = getenv("BSW_PERSIST") ? (int8_t)std::min(2, std::max(0, atoi(getenv("BSW_PERSIST")))) : 0;
     kp.lds_pad = getenv("BSW_PC_LDS_PAD") ? std::max(0, atoi(getenv("BSW_PC_LDS_PAD"))) : 0;   // experiment knob
 }
 
@@ -554,6 +570,21 @@ static void ensure_cu_streams(Slot &s)
     }
     s.hstream = h;
     s.dstream = d;
+}
+
+// persistent DP grid: two waves per SIMD on every CU (the kernel's occupancy), so every wave of the
+// grid is resident at once and none waits to be dispatched behind the others
+static int32_t pq_grid(int device)
+{
+    static std::atomic<int32_t> cu[16] = {};
+    if (device < 0 || device >= 16) return 2048;
+    int32_t v = cu[device].load();
+    if (v == 0) {
+        hipDeviceProp_t pr;
+        v = hipGetDeviceProperties(&pr, device) == hipSuccess && pr.multiProcessorCount > 0 ? pr.multiProcessorCount : 256;
+        cu[device].store(v);
+    }
+    return 8 * v;
 }
 
 static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
@@ -709,7 +740,22 @@ static int run_dp(const KParams &kp, Slot &s)
         }
         for (int c = 0; c < kNumLaneClasses; ++c) {
             const int32_t np = counts[kPkClass0 + c];
-            if (np > 0) {
+            if (np > 0 && kp.persist >= 2 && kLaneQmax[c] == 160 && kp.kern8 == 1) {
+                // the persistent tile-queue form (BSW_OPT_PERSIST 2): every tile runnable at once
+                hipStream_t ps = next_stream();
+                BSW_TRY(grow(s.d_pq, s.cap_pq, (size_t)4));
+                BSW_TRY(hipMemsetAsync(s.d_pq, 0, 4 * sizeof(int32_t), ps));
+                PqArgs a{};
+                a.kp = kp; a.w = w; a.pairs = d_pairs; a.order = s.d_order; a.ref = d_ref; a.qer = d_qer;
+                a.err = d_err; a.head = s.d_pq; a.ready = nullptr; a.abort = nullptr;
+                a.nchunks = 1; a.ntiles = (np + 63) / 64;
+                a.chunks[0] = PqChunk{0, off, np, 0, 0, 0, 0};
+                BSW_TRY(launch_pq_kernel(a, std::min(a.ntiles, pq_grid(s.device)), ps));
+                s.stats.n_launches++;
+                s.stats.n_packed += np;
+                if (cell_bits == 8) s.stats.n_u8 += np;
+                else s.stats.n_i16 += np;
+            } else if (np > 0) {
                 BSW_TRY(launch_pc_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
                                          d_err, next_stream()));
                 s.stats.n_launches++;
@@ -1456,6 +1502,321 @@ static int host_shard_fast(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, con
     return rc;
 }
 
+// ---------------------------------------------------------------- host pipeline, persistent DP
+// One chunk published to the running persistent DP kernel: *ready = the chunk's last tile + 1.  The
+// chunk's inputs were written by the kernels before this one on the same stream (their end-of-kernel
+// release); the store is a relaxed agent-scope atomic (write-through), the pollers read it with
+// relaxed agent-scope loads and take an agent acquire before the chunk's inputs (bsw_pc.hip).
+__global__ void pq_publish_kernel(int32_t *ready, int32_t v)
+{
+    __hip_atomic_store(ready, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the persistent pipeline's streams: CU-masked, the helper stream on the first pq_nres CUs of the
+// mask numbering, the DP stream on the rest (BSW_PQ_RESERVE, default 8)
+static bool ensure_pq_streams(DeviceCtx &dc)
+{
+    if (dc.pq_h) return true;
+    if (dc.pq_failed) return false;
+    dc.pq_failed = true;
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, dc.device) != hipSuccess) return false;
+    const int ncu = pr.multiProcessorCount;
+    const char *e = getenv("BSW_PQ_RESERVE");
+    const int nr = e ? std::max(1, atoi(e)) : 8;
+    if (ncu < 4 * nr || ncu > 1024) return false;
+    uint32_t hm[32] = {}, dm[32] = {};
+    const int nw = (ncu + 31) / 32;
+    for (int c = 0; c < ncu; ++c) dm[c / 32] |= 1u << (c % 32);
+    // the first nr CUs of the mask numbering: a spread set (one CU per 32-bit mask word) left the
+    // helper's 256-thread kernels waiting for the DP grid to end (tools/pq_stream_probe.hip, 2 s
+    // per kernel) while CUs 0-7 run them at once beside a full grid
+    for (int c = 0; c < nr; ++c) {
+        hm[c / 32] |= 1u << (c % 32);
+        dm[c / 32] &= ~(1u << (c % 32));
+    }
+    hipStream_t h = nullptr, d = nullptr;
+    if (hipExtStreamCreateWithCUMask(&h, (uint32_t)nw, hm) != hipSuccess) return false;
+    if (hipExtStreamCreateWithCUMask(&d, (uint32_t)nw, dm) != hipSuccess) {
+        (void)hipStreamDestroy(h);
+        return false;
+    }
+    bool ok = true;
+    for (hipEvent_t &ev : dc.pq_ev) ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&dc.pq_init, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreate(&dc.pq_t0) == hipSuccess && hipEventCreate(&dc.pq_t1) == hipSuccess;
+    if (!ok) {
+        (void)hipStreamDestroy(h);
+        (void)hipStreamDestroy(d);
+        return false;
+    }
+    dc.pq_h = h;
+    dc.pq_d = d;
+    dc.pq_nres = nr;
+    dc.pq_ncu = ncu;
+    dc.pq_failed = false;
+    return true;
+}
+
+// plan_kernel's schedule key (keymode 2) for a staged nibble chunk: PairIn records whose idr / idq
+// are nibble indices into ref4 / qer4; every pair is in a packed-column class (host_shard_pq's
+// precondition).  vals = the chunk-local index.  Seed identities as seed_matches, from nibbles.
+__device__ __forceinline__ uint32_t nib_at(const uint8_t *__restrict__ b4, int64_t k)
+{
+    return (b4[k >> 1] >> (4 * (k & 1))) & 15u;
+}
+__global__ void plan_nib_kernel(const PairIn *__restrict__ recs, int32_t m, const uint8_t *__restrict__ ref4,
+                                const uint8_t *__restrict__ qer4, uint32_t *__restrict__ keys, int32_t *__restrict__ vals)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const PairIn p = recs[i];
+    const int qlen = max(p.len2, 0), tlen = max(p.len1, 0);
+    const int c = kPkClass0 + (qlen + 1 <= 32 ? 0 : qlen + 1 <= 64 ? 1 : qlen + 1 <= 96 ? 2 : qlen + 1 <= 128 ? 3 : 4);
+    int mt = 31;
+    if (qlen >= 40 && tlen >= 46) {
+        uint8_t qb[30], rb[42];
+#pragma unroll
+        for (int j = 0; j < 30; ++j) qb[j] = (uint8_t)nib_at(qer4, (int64_t)p.idq + 10 + j);
+#pragma unroll
+        for (int j = 0; j < 42; ++j) rb[j] = (uint8_t)nib_at(ref4, (int64_t)p.idr + 4 + j);
+        int best = 0;
+#pragma unroll
+        for (int sft = 0; sft <= 12; ++sft) {
+            int n = 0;
+#pragma unroll
+            for (int j = 0; j < 30; ++j) n += qb[j] == rb[j + sft];
+            best = max(best, n);
+        }
+        mt = best;
+    }
+    const int rel = mt > 18;
+    keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) | ((uint32_t)(1 - rel) << 19) |
+              ((uint32_t)(63 - min(tlen >> 5, 63)) << 13) | ((uint32_t)(31 - min(mt, 31)) << 8) |
+              (uint32_t)(255 - min(max(p.h0, 0), 255));
+    vals[i] = i;
+}
+
+// One chunk of the persistent pipeline staged for in-place reading: [PairIn x m | target nibbles |
+// query nibbles], idr / idq rewritten as nibble indices from the chunk's byte extents.
+struct PqStaged {
+    size_t ref_off = 0, qer_off = 0, bytes = 0;
+};
+static size_t pq_stage_bytes(int32_t m, size_t rb, size_t qb, PqStaged &c)
+{
+    c.ref_off = align256((size_t)m * sizeof(PairIn));
+    c.qer_off = align256(c.ref_off + (rb + 1) / 2 + 8);
+    c.bytes = align256(c.qer_off + (qb + 1) / 2 + 8);
+    return c.bytes;
+}
+static void pq_stage(uint8_t *h, const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t m, int64_t r_lo,
+                     size_t rb, int64_t q_lo, size_t qb, const PqStaged &c)
+{
+    PairIn *rec = (PairIn *)h;
+    const int nk = (int)std::max<int64_t>(1, m >> 14), nr = (int)std::max<size_t>(1, rb >> 22),
+              nq = (int)std::max<size_t>(1, qb >> 22);
+    auto even = [](size_t total, int k, int parts) {
+        return k == parts ? total : (total * (size_t)k / (size_t)parts) & ~(size_t)31;
+    };
+    HostPool::get().parallel_for(nk + nr + nq, [&](int t) {
+        if (t < nk) {
+            const int32_t a0 = (int32_t)((int64_t)m * t / nk), a1 = (int32_t)((int64_t)m * (t + 1) / nk);
+            for (int32_t i = a0; i < a1; ++i) {
+                const SeqPair &p = pairs[i];
+                rec[i] = PairIn{p.len1 > 0 ? (int32_t)(p.idr - r_lo) : 0, p.len2 > 0 ? (int32_t)(p.idq - q_lo) : 0,
+                                p.len1, p.len2, p.h0};
+            }
+        } else if (t < nk + nr) {
+            const size_t a0 = even(rb, t - nk, nr), a1 = even(rb, t - nk + 1, nr);
+            pack_nibbles(h + c.ref_off + a0 / 2, ref + r_lo + a0, a1 - a0);
+        } else {
+            const size_t a0 = even(qb, t - nk - nr, nq), a1 = even(qb, t - nk - nr + 1, nq);
+            pack_nibbles(h + c.qer_off + a0 / 2, qer + q_lo + a0, a1 - a0);
+        }
+    });
+    memset(h + c.ref_off + (rb + 1) / 2, 0, 8);
+    memset(h + c.qer_off + (qb + 1) / 2, 0, 8);
+}
+
+// A host-buffer call as ONE persistent DP launch (BSW_OPT_PERSIST >= 1).  The
+// pq_kernel grid starts first, on the DP CUs, and takes 64-pair tiles as chunks are published.  Per
+// chunk: the host stages PairIn records + nibble-packed extents into one of three pinned buffers;
+// a copy stream moves them into the chunk's own region of the call's device buffer (chunks stay
+// resident until the call ends: the DP reads them in place, nothing is unpacked); the helper stream
+// (a few reserved CUs) computes the chunk's schedule keys from the nibbles, sorts them, and
+// publishes the chunk.  No chunk waits for another's DP to drain, and the call has one DP tail
+// instead of one per chunk.  At the end: one D2H of the 24 output bytes per pair, scattered into the
+// caller's records.  Preconditions (host_shard): every pair fits pc_kernel<160>, the chunks'
+// byte extents are bulk.  Returns 1 (nothing done) when the streams are unavailable.
+static int host_shard_pq(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref, const uint8_t *qer,
+                         int32_t n, int32_t w, int cell_bits, const std::vector<std::pair<int32_t, int32_t>> &chs,
+                         const std::vector<BlkStat> &bs, bsw_stats_t *st)
+{
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t_start = now();
+    std::lock_guard<std::mutex> g(dc.pq_mu);
+    BSW_TRY(hipSetDevice(dc.device));
+    if (!ensure_pq_streams(dc)) return 1;
+    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;
+    constexpr int kSlots = 3;
+    std::unique_ptr<Slot> slots[kSlots];
+    int rc = BSW_OK;
+    for (int k = 0; k < kSlots; ++k) {
+        slots[k] = dc.acquire(rc);
+        if (rc) {
+            for (int j = 0; j < k; ++j) dc.give_back(std::move(slots[j]));
+            return rc;
+        }
+    }
+    hipStream_t H = dc.pq_h, D = dc.pq_d;
+    Slot &cs = *slots[0];                       // the call's device buffers; its stream copies
+    hipStream_t C = cs.stream;
+    const int nch = (int)chs.size();
+    bool launched = false;
+    double stage_ms = 0;
+    struct ChunkGeo { int32_t a, m; int64_t r_lo, q_lo; size_t rb, qb, off; PqStaged ps; };
+    std::vector<ChunkGeo> geo((size_t)nch);
+    rc = [&]() -> int {
+        int32_t mmax = 0, ntiles = 0;
+        size_t dev_bytes = 0, host_max[kSlots] = {};
+        for (int c = 0; c < nch; ++c) {
+            ChunkGeo &q = geo[(size_t)c];
+            q.a = chs[c].first * kStageBlk;
+            q.m = std::min(n, chs[c].second * kStageBlk) - q.a;
+            int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+            for (int32_t b = chs[c].first; b < chs[c].second; ++b) {
+                r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
+                q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi);
+            }
+            if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+            if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+            q.r_lo = r_lo; q.q_lo = q_lo; q.rb = (size_t)(r_hi - r_lo); q.qb = (size_t)(q_hi - q_lo);
+            const size_t cb = pq_stage_bytes(q.m, q.rb, q.qb, q.ps);
+            q.off = dev_bytes;
+            dev_bytes += cb;
+            host_max[c % kSlots] = std::max(host_max[c % kSlots], cb);
+            mmax = std::max(mmax, q.m);
+            ntiles += (q.m + 63) / 64;
+        }
+        // every buffer at its final size before the grid starts: a hipFree / hipHostFree inside the
+        // loop would wait for the device -- i.e. for the running grid, which waits for this thread
+        BSW_TRY(grow(cs.d_stage, cs.cap_dstage, dev_bytes));
+        BSW_TRY(grow_sort(cs, std::max(n, mmax)));
+        BSW_TRY(grow(cs.d_pq, cs.cap_pq, (size_t)4));
+        BSW_TRY(grow(cs.d_scratch, cs.cap_scratch, (size_t)n * 3 + 1));     // 24 B per pair of outputs
+        size_t tmp_bytes = 0;
+        BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, cs.d_keys, cs.d_keys2, cs.d_vals, cs.d_order,
+                                                   mmax, 0, kKeyBits, H));
+        BSW_TRY(grow(cs.d_tmp, cs.cap_tmp, tmp_bytes));
+        for (int k = 0; k < kSlots; ++k) {
+            Slot &s = *slots[k];
+            if (host_max[k] > s.cap_stage) {
+                if (s.h_stage) (void)hipHostFree(s.h_stage);
+                s.h_stage = nullptr; s.cap_stage = 0;
+                BSW_TRY(hipHostMalloc(&s.h_stage, host_max[k], 0));
+                s.cap_stage = host_max[k];
+            }
+        }
+        if (dc.pq_hout_cap < (size_t)n * 24) {
+            if (dc.pq_hout) (void)hipHostFree(dc.pq_hout);
+            dc.pq_hout = nullptr; dc.pq_hout_cap = 0;
+            const size_t cap = (size_t)n * 24 + (size_t)n * 6;
+            BSW_TRY(hipHostMalloc(&dc.pq_hout, cap, 0));
+            dc.pq_hout_cap = cap;
+        }
+        PqArgs a{};
+        a.kp = kp; a.w = w; a.order = cs.d_order;
+        a.nbase = cs.d_stage; a.out24 = (int32_t *)cs.d_scratch;
+        a.err = cs.d_meta + kMetaErr; a.head = cs.d_pq; a.ready = cs.d_pq + 1; a.abort = cs.d_pq + 2;
+        a.nchunks = nch; a.ntiles = ntiles;
+        for (int c = 0, t = 0; c < nch; ++c) {
+            const ChunkGeo &q = geo[(size_t)c];
+            a.chunks[c] = PqChunk{t, q.a, q.m, q.a, (int64_t)q.off, (int64_t)(q.off + q.ps.ref_off),
+                                  (int64_t)(q.off + q.ps.qer_off)};
+            t += (q.m + 63) / 64;
+        }
+        // the queue words are zeroed on the helper stream and the DP stream waits for that: the
+        // helper stream never waits on the DP stream (an event recorded there could complete only
+        // with the grid, which waits for the helper stream's chunks)
+        BSW_TRY(hipMemsetAsync(cs.d_meta, 0, kMetaWords * sizeof(int32_t), H));
+        BSW_TRY(hipMemsetAsync(cs.d_pq, 0, 4 * sizeof(int32_t), H));
+        BSW_TRY(hipEventRecord(dc.pq_init, H));
+        BSW_TRY(hipStreamWaitEvent(D, dc.pq_init, 0));
+        BSW_TRY(hipEventRecord(dc.pq_t0, D));
+        BSW_TRY(launch_pq_kernel(a, std::min(ntiles, 8 * (dc.pq_ncu - dc.pq_nres)), D));
+        launched = true;
+        BSW_TRY(hipEventRecord(dc.pq_t1, D));
+        for (int c = 0, tend = 0; c < nch; ++c) {
+            const int k = c % kSlots;
+            Slot &s = *slots[k];
+            const ChunkGeo &q = geo[(size_t)c];
+            tend += (q.m + 63) / 64;
+            if (c >= kSlots) BSW_TRY(hipEventSynchronize(dc.pq_ev[k]));   // slot k's last copy done
+            const auto t0 = now();
+            pq_stage((uint8_t *)s.h_stage, pairs + q.a, ref, qer, q.m, q.r_lo, q.rb, q.q_lo, q.qb, q.ps);
+            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
+            uint8_t *dst = cs.d_stage + q.off;
+            BSW_TRY(hipMemcpyAsync(dst, s.h_stage, q.ps.bytes, hipMemcpyHostToDevice, C));
+            BSW_TRY(hipEventRecord(dc.pq_ev[k], C));
+            BSW_TRY(hipStreamWaitEvent(H, dc.pq_ev[k], 0));
+            hipLaunchKernelGGL(plan_nib_kernel, dim3((unsigned)((q.m + 255) / 256)), dim3(256), 0, H, (const PairIn *)dst,
+                               q.m, dst + q.ps.ref_off, dst + q.ps.qer_off, cs.d_keys, cs.d_vals);
+            BSW_TRY(hipGetLastError());
+            size_t tb = cs.cap_tmp;
+            BSW_TRY(hipcub::DeviceRadixSort::SortPairs(cs.d_tmp, tb, cs.d_keys, cs.d_keys2, cs.d_vals,
+                                                       cs.d_order + q.a, q.m, 0, kKeyBits, H));
+            hipLaunchKernelGGL(pq_publish_kernel, dim3(1), dim3(1), 0, H, cs.d_pq + 1, tend);
+            BSW_TRY(hipGetLastError());
+            if (dbg)
+                fprintf(stderr, "pq chunk %d: %d pairs, staged %.3f .. %.3f ms\n", c, (int)q.m,
+                        std::chrono::duration<double, std::milli>(t0 - t_start).count(),
+                        std::chrono::duration<double, std::milli>(now() - t_start).count());
+        }
+        BSW_TRY(hipMemcpyAsync(dc.pq_hout, cs.d_scratch, (size_t)n * 24, hipMemcpyDeviceToHost, D));
+        BSW_TRY(hipMemcpyAsync(cs.h_meta + kMetaErr, cs.d_meta + kMetaErr, sizeof(int32_t), hipMemcpyDeviceToHost, D));
+        BSW_TRY(hipStreamSynchronize(D));
+        if (dbg)
+            fprintf(stderr, "pq drained at %.3f ms\n", std::chrono::duration<double, std::milli>(now() - t_start).count());
+        const int32_t err = cs.h_meta[kMetaErr];
+        if (err & 8) return BSW_E_HIP;                         // aborted / poll bound (no caller record written)
+        if (err) return BSW_E_RANGE;
+        const int32_t *o = (const int32_t *)dc.pq_hout;
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(HostPool::workers() + 1, n >> 15));
+        HostPool::get().parallel_for(nt, [&](int t) {
+            for (int32_t i = (int32_t)((int64_t)n * t / nt); i < (int32_t)((int64_t)n * (t + 1) / nt); ++i) {
+                const int32_t *q = o + 6 * (int64_t)i;
+                SeqPair &p = pairs[i];
+                p.score = q[0]; p.tle = q[1]; p.gtle = q[2]; p.qle = q[3]; p.gscore = q[4]; p.max_off = q[5];
+            }
+        });
+        return BSW_OK;
+    }();
+    if (rc != BSW_OK && dbg)
+        fprintf(stderr, "host_shard_pq: n %d, %d chunks: rc %d (%s), grid launched %d\n", (int)n, nch, rc,
+                bsw_strerror(rc), (int)launched);
+    if (rc != BSW_OK && launched) {
+        // end the running grid (its waves poll *abort), then drain every stream
+        int32_t one = 1;
+        if (hipMemcpyAsync(cs.d_pq + 2, &one, sizeof(one), hipMemcpyHostToDevice, H) == hipSuccess)
+            (void)hipStreamSynchronize(H);
+        (void)hipStreamSynchronize(D);
+        (void)hipStreamSynchronize(H);
+        (void)hipStreamSynchronize(C);
+    }
+    if (rc == BSW_OK && st) {
+        bsw_stats_t agg{};
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, dc.pq_t0, dc.pq_t1) == hipSuccess) agg.kernel_ms = ms;
+        agg.n_packed = n; agg.n_launches = 1;
+        (cell_bits == 8 ? agg.n_u8 : agg.n_i16) += n;
+        agg.stage_ms = (float)stage_ms;
+        agg.host_ms = (float)std::chrono::duration<double, std::milli>(now() - t_start).count();
+        *st = agg;
+    }
+    for (int k = 0; k < kSlots; ++k) dc.give_back(std::move(slots[k]), rc);
+    return rc;
+}
+
 // One device's share of a host-buffer call: a pipeline of chunks over the device's slots (four by default).
 // Per chunk: stage into the slot's pinned buffer (records + nibble-packed sequences, host
 // pool) -> one H2D -> unpack -> plan / sort -> DP kernels -> D2H of the records.  The calling
@@ -1483,6 +1844,30 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
     std::vector<BlkStat> bs;
     if (!prepass(pairs, n, bs)) return BSW_E_RANGE;
     if (chunk <= 0) chunk = n;
+    // the persistent DP pipeline (BSW_OPT_PERSIST >= 1) when every pair fits pc_kernel<160>, the call is
+    // past the small-batch kernels' sizes and its chunks' byte extents are bulk and ascending
+    if (kp0.persist >= 1 && kp0.pk_ok && kp0.kern8 == 1 && !kp0.misroute && kp0.maxsc == 1 && two_bit &&
+        n > kp0.small_batch && n > kp0.mid_batch) {
+        bool ok = true;
+        for (const BlkStat &b : bs) ok = ok && b.fast;
+        const auto chs = fast_chunks(bs, n, chunk);
+        ok = ok && !chs.empty() && (int)chs.size() <= kPqMaxChunks;
+        for (size_t c = 0; ok && c < chs.size(); ++c) {
+            int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
+            for (int32_t b = chs[c].first; b < chs[c].second; ++b) {
+                r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi); r_sum += bs[b].r_sum;
+                q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi); q_sum += bs[b].q_sum;
+            }
+            // bulk extents (the staged bytes ~ the chunk's own), nibble offsets inside int32
+            if (r_lo != INT64_MAX) ok = ok && (r_hi - r_lo) <= r_sum + r_sum / 4 + 4096 && (r_hi - r_lo) < ((int64_t)1 << 30);
+            if (q_lo != INT64_MAX) ok = ok && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096 && (q_hi - q_lo) < ((int64_t)1 << 30);
+        }
+        if (getenv("BSW_DEBUG_HP")) fprintf(stderr, "persistent pipeline: eligible %d (%d chunks)\n", (int)ok, (int)chs.size());
+        if (ok) {
+            const int r = host_shard_pq(kp0, dc, pairs, ref, qer, n, w, cell_bits, chs, bs, st);
+            if (r != 1) return r;
+        }
+    }
     // the fast path (no device helper kernels) when every pair fits the packed-column kernel and the
     // call is past the small-batch kernels' sizes (those are latency-bound: the row-group kernel)
     // opt-in (BSW_HP_FAST=1, read per call): same box, interleaved, the general pipeline ran 1M-pair
@@ -3102,6 +3487,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     if (!ctx) return BSW_E_INVAL;
     const bool b01 = value == 0 || value == 1;
     switch (option) {
+    case BSW_OPT_PERSIST: if (value < 0 || value > 2) return BSW_E_INVAL; ctx->kp.persist = (int8_t)value; return BSW_OK;
     case BSW_OPT_BUSY_MIN: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.busy_min = (int32_t)value; return BSW_OK;
     case BSW_OPT_KERNEL8: if (value < 0 || value > 2) return BSW_E_INVAL; ctx->kp.kern8 = (int8_t)value; return BSW_OK;
     case BSW_OPT_FORK: if (!b01) return BSW_E_INVAL; ctx->kp.fork = (int8_t)value; return BSW_OK;

@@ -586,29 +586,27 @@ __device__ __forceinline__ int pc_lastpos(std::integer_sequence<int, G...>, cons
 // chunk -- records as PairIn in schedule order, sequences as nibbles (idr / idq nibble indices),
 // outputs as 6 x int32 into out24 -- so the chunk needs no unpack, plan, sort or gather kernel.
 // The target stream then carries 8 codes per dword: 9 dwords per lane per 64-row chunk.
-template <int QMAX, int WPB, bool BY, bool NIB = false>
-__global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams kp, const int32_t w,
-                                                    SeqPair *__restrict__ pairs,
-                                                    const int32_t *__restrict__ order,
-                                                    const int32_t n,
-                                                    const uint8_t *__restrict__ ref,
-                                                    const uint8_t *__restrict__ qer,
-                                                    int32_t *__restrict__ err,
-                                                    const PairIn *__restrict__ recs = nullptr,
-                                                    int32_t *__restrict__ out24 = nullptr)
+template <int QMAX, bool NIB> constexpr int pc_cdw() { return NIB ? kPcChunkDwN : kPcChunkDw; }
+
+// One wave's 64 pairs (lane slot gid runs pair idx_base + order[gid]; slots >= n idle): the whole
+// DP of pc_kernel, shared by the one-launch-per-64-pairs form (pc_kernel) and the persistent
+// tile-queue form (pq_kernel).  s_tgt / s_prof: the caller's LDS (s_prof filled and synced).
+template <int QMAX, int WPB, bool BY, bool NIB>
+__device__ __forceinline__ void pc_body(const KParams &kp, const int32_t w, SeqPair *__restrict__ pairs,
+                                        const int32_t *__restrict__ order, const int32_t n,
+                                        const uint8_t *__restrict__ ref, const uint8_t *__restrict__ qer,
+                                        int32_t *__restrict__ err, const PairIn *__restrict__ recs,
+                                        int32_t *__restrict__ out24, const int gid, const int32_t idx_base,
+                                        uint32_t (&s_tgt)[WPB][2][pc_cdw<QMAX, NIB>()][64],
+                                        const uint2 (&s_prof)[8])
 {
     constexpr int NG = QMAX / 4;        // groups = query words (4 codes each)
-    constexpr int CDW = NIB ? kPcChunkDwN : kPcChunkDw;   // target dwords per lane per 64-row chunk
+    constexpr int CDW = pc_cdw<QMAX, NIB>();   // target dwords per lane per 64-row chunk
 #ifdef BSW_PC_STATS
     const unsigned long long t_wave0 = wall_clock64();
 #endif
-    __shared__ uint32_t s_tgt[WPB][2][CDW][64];   // 8.7 KB per wave (4.6 KB for nibbles)
-    __shared__ uint2 s_prof[8];                           // per-row score profiles, by target code
-    if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
-    __syncthreads();
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = gid < n;
-    const int idx = valid ? (order ? order[gid] : gid) : 0;
+    const int idx = valid ? idx_base + (order ? order[gid] : gid) : 0;
     SeqPair *sp = pairs + idx;
     int idr = 0, idq = 0, tlen = 0, qlen = 0, h0 = 0;
     if (valid) {
@@ -891,6 +889,103 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
     }
 }
 
+template <int QMAX, int WPB, bool BY, bool NIB = false>
+__global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams kp, const int32_t w,
+                                                    SeqPair *__restrict__ pairs,
+                                                    const int32_t *__restrict__ order,
+                                                    const int32_t n,
+                                                    const uint8_t *__restrict__ ref,
+                                                    const uint8_t *__restrict__ qer,
+                                                    int32_t *__restrict__ err,
+                                                    const PairIn *__restrict__ recs = nullptr,
+                                                    int32_t *__restrict__ out24 = nullptr)
+{
+    __shared__ uint32_t s_tgt[WPB][2][pc_cdw<QMAX, NIB>()][64];   // 8.7 KB per wave (4.6 KB for nibbles)
+    __shared__ uint2 s_prof[8];                           // per-row score profiles, by target code
+    if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
+    __syncthreads();
+    pc_body<QMAX, WPB, BY, NIB>(kp, w, pairs, order, n, ref, qer, err, recs, out24,
+                                blockIdx.x * blockDim.x + threadIdx.x, 0, s_tgt, s_prof);
+}
+
+// Persistent tile-queue form: a grid of at most ~2 waves per SIMD, each wave
+// taking 64-pair tiles from ONE device-scope counter until the queue is empty -- no per-wave
+// dispatch, and a wave that finishes early takes the next tile instead of idling through the
+// launch's tail.  Tiles belong to chunks (PqChunk: the tile range, the chunk's slots in `order`,
+// the base added to its order values).  Chunks may be published while the kernel runs (the host
+// pipeline: chunk c's inputs land, are planned and sorted on other CUs, then a one-thread kernel
+// raises *ready to the chunk's last tile): a wave whose tile is not yet published polls *ready
+// (relaxed agent-scope loads, s_sleep) and then takes an agent-scope acquire before reading the
+// chunk's inputs.  *abort (host) or a poll past kPqSpinTicks ends every wave (err |= 8): no wave
+// ever waits without bound.
+[[maybe_unused]] constexpr unsigned long long kPqSpinTicks = 400000000ull;   // 4 s of s_memrealtime (100 MHz)
+
+typedef const PqArgs __attribute__((address_space(4))) *PqArgsK;   // the kernarg segment's copy
+
+template <int QMAX, bool NIB>
+__global__ __launch_bounds__(64, 2) void pq_kernel(const PqArgs args)
+{
+#ifdef __HIP_DEVICE_COMPILE__            // (the kernarg-segment reads have no host form)
+    __shared__ uint32_t s_tgt[1][2][pc_cdw<QMAX, NIB>()][64];
+    __shared__ uint2 s_prof[8];
+    if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(args.kp.prof[threadIdx.x][0], args.kp.prof[threadIdx.x][1]);
+    __syncthreads();
+    int known = -1;                         // tiles [0, known) known published (-1: not read yet)
+    int c = 0;                              // chunk cursor (tiles are taken in increasing order)
+    for (;;) {
+        // the arguments are re-read from the kernarg segment per tile (scalar loads, once per ~1 ms
+        // of DP) instead of held in SGPRs across the tile's DP: the row loop needs every SGPR it has
+        // (held, they spilled 34 SGPRs)
+        PqArgsK a = (PqArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(a));
+        int t = 0;
+        if (threadIdx.x == 0) t = __hip_atomic_fetch_add(a->head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t >= a->ntiles) break;
+        if (known < 0) known = a->ready ? 0 : a->ntiles;
+        if (t >= known) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            int v = 0, ab = 0;
+            for (;;) {
+                v = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(a->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                ab = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(a->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (v > t || ab) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kPqSpinTicks) { ab = 2; break; }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (ab) {
+                if (threadIdx.x == 0) atomicOr(a->err, 8);
+                break;
+            }
+            known = v;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // the chunk's inputs, fresh
+        }
+        while (c + 1 < a->nchunks && t >= a->chunks[c + 1].tile0) ++c;
+        const int tile0 = a->chunks[c].tile0, slot0 = a->chunks[c].slot0;
+        const int m = a->chunks[c].m, idx_base = a->chunks[c].idx_base;
+        const KParams kp = a->kp;
+        const int gid = slot0 + (t - tile0) * 64 + (int)threadIdx.x;
+        if constexpr (NIB) {
+            // the chunk as staged (records, nibbles) inside the call's device buffer; outputs at the
+            // chunk's pairs of the call's 24-B output array
+            const uint8_t *nb = a->nbase;
+            pc_body<QMAX, 1, false, true>(kp, a->w, nullptr, a->order, slot0 + m, nb + a->chunks[c].ref_off,
+                                          nb + a->chunks[c].qer_off, a->err,
+                                          (const PairIn *)(nb + a->chunks[c].rec_off),
+                                          a->out24 + 6 * (int64_t)idx_base, gid, 0, s_tgt, s_prof);
+        } else {
+            pc_body<QMAX, 1, false, false>(kp, a->w, a->pairs, a->order, slot0 + m, a->ref, a->qer, a->err, nullptr,
+                                           nullptr, gid, idx_base, s_tgt, s_prof);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): the tile's last target DMA into s_tgt
+    }
+#else
+    (void)args;
+#endif
+}
+
 #ifdef BSW_PC_STATS
 // [rows, groups entered, fast, masked-R, masked-L, lastpos scans, waves, uniform-end rows] summed over waves
 extern "C" int bsw_pc_stats(unsigned long long *out, int reset)
@@ -935,6 +1030,17 @@ hipError_t launch_pc_nib_kernel(const KParams &kp, int32_t w, const PairIn *recs
     const unsigned grid = (unsigned)((n + 63) / 64);
     hipLaunchKernelGGL((pc_kernel<160, 1, false, true>), dim3(grid), dim3(64), (unsigned)max(kp.lds_pad, 0), s, kp, w,
                        (SeqPair *)nullptr, order, n, ref4, qer4, err, recs, out24);
+    return hipGetLastError();
+}
+
+hipError_t launch_pq_kernel(const PqArgs &args, int32_t grid, hipStream_t s)
+{
+    if (grid <= 0 || args.nchunks <= 0 || args.nchunks > kPqMaxChunks || !args.head || (args.ready && !args.abort))
+        return hipErrorInvalidValue;
+    if (args.nbase)
+        hipLaunchKernelGGL((pq_kernel<160, true>), dim3((unsigned)grid), dim3(64), 0, s, args);
+    else
+        hipLaunchKernelGGL((pq_kernel<160, false>), dim3((unsigned)grid), dim3(64), 0, s, args);
     return hipGetLastError();
 }
 

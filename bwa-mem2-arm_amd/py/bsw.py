@@ -205,7 +205,7 @@ class Engine:
 
     _OPTS = {"kernel8": OPT_KERNEL8, "fork": OPT_FORK, "sortkey": OPT_SORTKEY, "glob_band": OPT_GLOB_BAND,
              "ext_chunk": OPT_EXT_CHUNK, "host_chunk": OPT_HOST_CHUNK, "long": OPT_LONG, "host_pack": OPT_HOST_PACK,
-             "small_batch": OPT_SMALL_BATCH, "split_min": OPT_SPLIT_MIN, "coalesce": OPT_COALESCE, "coalesce_leaders": OPT_COALESCE_LEADERS, "group_kernel": OPT_GROUP_KERNEL, "mid_batch": OPT_MID_BATCH, "busy_min": 15, "coalesce_linger": 16,
+             "small_batch": OPT_SMALL_BATCH, "split_min": OPT_SPLIT_MIN, "coalesce": OPT_COALESCE, "coalesce_leaders": OPT_COALESCE_LEADERS, "group_kernel": OPT_GROUP_KERNEL, "mid_batch": OPT_MID_BATCH, "busy_min": 15, "coalesce_linger": 16, "persist": 17,
              "test_misroute": OPT_TEST_MISROUTE, "test_fail_alloc": OPT_TEST_FAIL_ALLOC}
 
     def set_option(self, name, value: int):

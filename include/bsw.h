@@ -227,6 +227,13 @@ enum {
                                  so batches fill up.  Measured at 150: 8 callers +16-25% at 1K-4K
                                  pairs per call, 4 / 16 callers mixed, hence off by
                                  default.  A lone caller never waits.  Outputs are identical     */
+    BSW_OPT_PERSIST = 17,     /* packed-column pairs of the 160-column class (C2's) on the
+                                 persistent tile-queue kernel: one grid of ~2 waves per SIMD
+                                 taking 64-pair tiles from a device counter instead of one wave
+                                 per 64 pairs.  0 = off, 1 = host-buffer pipeline calls (chunks
+                                 are published to the running kernel as they land), 2 = also
+                                 device calls.  Default: see bsw_host.cpp.
+                                 Outputs are identical either way                               */
     BSW_OPT_TEST_MISROUTE = 100, /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
     BSW_OPT_TEST_FAIL_ALLOC = 101 /* tests only: the next `value` (0..1000000) device buffer

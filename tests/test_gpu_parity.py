@@ -906,3 +906,91 @@ def test_coalesced_small_calls(c2_full):
         assert not errs, errs[0]
         assert bad_seen == [1]
         e.close()
+
+
+@pytest.mark.parametrize("persist", [2])
+def test_persistent_tile_queue_device_api(c2_full, persist):
+    """BSW_OPT_PERSIST 2: the 160-column packed-column class runs on the persistent tile-queue
+    kernel (bsw_pc.hip pq_kernel: a grid of 2 waves per SIMD taking 64-pair tiles from a device
+    counter).  The full C2 batch (15,625 tiles, more than the grid) and ragged small batches
+    (partial last tiles, fewer tiles than the grid, one pair) equal the oracle; only the six
+    output fields change."""
+    pairs, ref, qer, want = c2_full
+    e = bsw.Engine(small_batch=0, mid_batch=0)
+    e.set_option("persist", persist)
+    dr = hiprt.DeviceBuffer.from_array(ref)
+    dq = hiprt.DeviceBuffer.from_array(qer)
+    for n in (1, 63, 64, 65, 1000, 131_071, len(pairs)):
+        src = pairs[:n].copy()
+        dp = hiprt.DeviceBuffer.from_array(src)
+        e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, n, 100)
+        got = dp.download(np.empty_like(src))
+        _assert_same(want[:n], got, f"persistent n={n}")
+        for f in ("idr", "idq", "len1", "len2", "h0"):
+            assert np.array_equal(got[f], src[f])
+        st = e.last_stats()
+        assert st.n_packed == n and st.n_launches >= 1
+    e.close()
+
+
+def test_persistent_tile_queue_mixed_classes(eng):
+    """Mixed shapes under BSW_OPT_PERSIST 2: only the 160-column packed class takes the persistent
+    kernel; the other classes (short queries, int16 / wide fallbacks) run as before, all == oracle."""
+    pairs, ref, qer = bswgen.random_pairs(20_000, seed=77, tlen=(0, 330), qlen=(0, 200))
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
+    e = bsw.Engine(small_batch=0, mid_batch=0)
+    e.set_option("persist", 2)
+    got = pairs.copy()
+    e.get_scores(got, ref, qer, 100)
+    _assert_same(want, got, "persistent mixed")
+    e.close()
+
+
+@pytest.mark.parametrize("chunk,nrich", [(65536, False), (262144, False), (262144, True)])
+def test_persistent_host_pipeline(c2_full, chunk, nrich):
+    """BSW_OPT_PERSIST 1: a contiguous host-buffer call runs as ONE persistent DP launch fed chunk by
+    chunk (bsw_host.cpp host_shard_pq: chunks staged, copied, planned and sorted on a few reserved
+    CUs and published to the running grid).  Extra N bases, empty sequences, the 8-bit regime's
+    edge h0 values and (nrich) chunks past the 2-bit staging's 1/32 exception bound (nibble
+    fallback) -- outputs equal the oracle, inputs untouched, one launch per call."""
+    pairs, ref, qer, _ = c2_full
+    n = 300_000
+    p = pairs[:n].copy()
+    r, q = ref.copy(), qer.copy()
+    q[13::997] = 4
+    r[5::1201] = 4
+    if nrich:
+        q[: int(p["idq"][150_000])][::19] = 4        # > 1/32 non-ACGT in the first half's queries
+    p["len2"][::5001] = 0
+    p["len1"][3::7001] = 0
+    qs = p["len2"] > 0
+    sel = qs & (np.arange(n) % 13 == 0)
+    p["h0"][sel] = 255 - np.minimum(p["len2"], p["len1"])[sel]
+    want = p.copy()
+    oracle.get_scores(_oparams(), want, r, q, 100, nthreads=16)
+    e = bsw.Engine(host_chunk=chunk)
+    e.set_option("persist", 1)
+    for rep in range(2):                               # a second call reuses the grown buffers
+        got = p.copy()
+        e.get_scores(got, r, q, 100)
+        _assert_same(want, got, f"persistent host chunk {chunk} nrich {nrich} call {rep}")
+        for f in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid"):
+            assert np.array_equal(got[f], p[f])
+        st = e.last_stats()
+        assert st.n_packed == n and st.n_launches == 1 and st.n_group == 0
+    e.close()
+
+
+def test_persistent_host_pipeline_falls_back(c2_full):
+    """Calls the persistent pipeline does not take (permuted records: byte extents not ascending;
+    a pair past the 8-bit regime) run on the chunked pipeline, outputs == oracle."""
+    pairs, ref, qer, want = c2_full
+    e = bsw.Engine()
+    e.set_option("persist", 1)
+    perm = np.random.default_rng(9).permutation(200_000)
+    got = pairs[:200_000][perm].copy()
+    e.get_scores(got, ref, qer, 100)
+    _assert_same(want[:200_000][perm], got, "persistent fallback permuted")
+    assert e.last_stats().n_launches > 1
+    e.close()

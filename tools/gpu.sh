@@ -105,8 +105,10 @@ for step in "$@"; do
     unset)
         unset "${arg?}"; echo "unset $arg" ;;
     py)
-        log=$O/$(basename "$arg" .py)_$n.log
-        timeout -k 10 600 python -u "$arg" > "$log" 2>&1 || fail "$step" $? "$log"
+        # py:<file>[,arg,...] (commas for spaces)
+        pa=($(sp "$arg"))
+        log=$O/$(basename "${pa[0]}" .py)_$n.log
+        timeout -k 10 600 python -u "${pa[@]}" > "$log" 2>&1 || fail "$step" $? "$log"
         tail -5 "$log" ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
