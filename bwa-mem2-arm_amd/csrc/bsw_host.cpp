@@ -330,6 +330,7 @@ struct DeviceCtx {
     int pq_nres = 0, pq_ncu = 0;
     bool pq_failed = false;             // stream creation failed once: the general pipeline
     hipEvent_t pq_ev[8] = {}, pq_t0 = nullptr, pq_t1 = nullptr, pq_init = nullptr;
+    hipEvent_t pq_dbg[2][64] = {};      // BSW_DEBUG_HP: per-chunk copy / publish timestamps
     void *pq_hout = nullptr; size_t pq_hout_cap = 0;   // pinned: the call's 24-B outputs
 
     ~DeviceCtx()
@@ -339,6 +340,7 @@ struct DeviceCtx {
         (void)hipSetDevice(device);
         for (hipEvent_t e : pq_ev) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : {pq_t0, pq_t1, pq_init}) if (e) (void)hipEventDestroy(e);
+        for (auto &r : pq_dbg) for (hipEvent_t e : r) if (e) (void)hipEventDestroy(e);
         if (pq_h) (void)hipStreamDestroy(pq_h);
         if (pq_d) (void)hipStreamDestroy(pq_d);
         if (pq_hout) (void)hipHostFree(pq_hout);
@@ -1513,7 +1515,7 @@ __global__ void pq_publish_kernel(int32_t *ready, int32_t v)
 }
 
 // the persistent pipeline's streams: CU-masked, the helper stream on the first pq_nres CUs of the
-// mask numbering, the DP stream on the rest (BSW_PQ_RESERVE, default 8)
+// mask numbering, the DP stream on the rest (BSW_PQ_RESERVE, default 16)
 static bool ensure_pq_streams(DeviceCtx &dc)
 {
     if (dc.pq_h) return true;
@@ -1523,7 +1525,7 @@ static bool ensure_pq_streams(DeviceCtx &dc)
     if (hipGetDeviceProperties(&pr, dc.device) != hipSuccess) return false;
     const int ncu = pr.multiProcessorCount;
     const char *e = getenv("BSW_PQ_RESERVE");
-    const int nr = e ? std::max(1, atoi(e)) : 8;
+    const int nr = e ? std::max(1, atoi(e)) : 16;
     if (ncu < 4 * nr || ncu > 1024) return false;
     uint32_t hm[32] = {}, dm[32] = {};
     const int nw = (ncu + 31) / 32;
@@ -1561,9 +1563,19 @@ static bool ensure_pq_streams(DeviceCtx &dc)
 // plan_kernel's schedule key (keymode 2) for a staged nibble chunk: PairIn records whose idr / idq
 // are nibble indices into ref4 / qer4; every pair is in a packed-column class (host_shard_pq's
 // precondition).  vals = the chunk-local index.  Seed identities as seed_matches, from nibbles.
-__device__ __forceinline__ uint32_t nib_at(const uint8_t *__restrict__ b4, int64_t k)
+// n (<= 8 * (W - 1)) codes from nibble index k of b4 as W aligned dwords realigned to the code
+// (dword loads: the staged extents carry 8 bytes of padding; 72 byte loads per pair made this
+// kernel load-issue-bound on the helper stream's few CUs)
+template <int W>
+__device__ __forceinline__ void nib_words(const uint8_t *__restrict__ b4, int64_t k, uint32_t (&a)[W - 1])
 {
-    return (b4[k >> 1] >> (4 * (k & 1))) & 15u;
+    const uint32_t *wp = (const uint32_t *)b4 + (k >> 3);
+    uint32_t w[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) w[i] = wp[i];
+    const uint32_t sh = 4u * (uint32_t)(k & 7);
+#pragma unroll
+    for (int i = 0; i < W - 1; ++i) a[i] = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
 }
 __global__ void plan_nib_kernel(const PairIn *__restrict__ recs, int32_t m, const uint8_t *__restrict__ ref4,
                                 const uint8_t *__restrict__ qer4, uint32_t *__restrict__ keys, int32_t *__restrict__ vals)
@@ -1574,12 +1586,15 @@ __global__ void plan_nib_kernel(const PairIn *__restrict__ recs, int32_t m, cons
     const int qlen = max(p.len2, 0), tlen = max(p.len1, 0);
     const int c = kPkClass0 + (qlen + 1 <= 32 ? 0 : qlen + 1 <= 64 ? 1 : qlen + 1 <= 96 ? 2 : qlen + 1 <= 128 ? 3 : 4);
     int mt = 31;
-    if (qlen >= 40 && tlen >= 46) {
+    if (qlen >= 40 && tlen >= 46) {          // seed_matches: query[10, 40) vs target[4 + s, 34 + s), s <= 12
+        uint32_t qa[4], ra[6];
+        nib_words<5>(qer4, (int64_t)p.idq + 10, qa);
+        nib_words<7>(ref4, (int64_t)p.idr + 4, ra);
         uint8_t qb[30], rb[42];
 #pragma unroll
-        for (int j = 0; j < 30; ++j) qb[j] = (uint8_t)nib_at(qer4, (int64_t)p.idq + 10 + j);
+        for (int j = 0; j < 30; ++j) qb[j] = (uint8_t)((qa[j >> 3] >> (4 * (j & 7))) & 15u);
 #pragma unroll
-        for (int j = 0; j < 42; ++j) rb[j] = (uint8_t)nib_at(ref4, (int64_t)p.idr + 4 + j);
+        for (int j = 0; j < 42; ++j) rb[j] = (uint8_t)((ra[j >> 3] >> (4 * (j & 7))) & 15u);
         int best = 0;
 #pragma unroll
         for (int sft = 0; sft <= 12; ++sft) {
@@ -1757,6 +1772,11 @@ static int host_shard_pq(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const
             stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
             uint8_t *dst = cs.d_stage + q.off;
             BSW_TRY(hipMemcpyAsync(dst, s.h_stage, q.ps.bytes, hipMemcpyHostToDevice, C));
+            if (dbg) {
+                if (!dc.pq_dbg[0][c]) BSW_TRY(hipEventCreate(&dc.pq_dbg[0][c]));
+                if (!dc.pq_dbg[1][c]) BSW_TRY(hipEventCreate(&dc.pq_dbg[1][c]));
+                BSW_TRY(hipEventRecord(dc.pq_dbg[0][c], C));
+            }
             BSW_TRY(hipEventRecord(dc.pq_ev[k], C));
             BSW_TRY(hipStreamWaitEvent(H, dc.pq_ev[k], 0));
             hipLaunchKernelGGL(plan_nib_kernel, dim3((unsigned)((q.m + 255) / 256)), dim3(256), 0, H, (const PairIn *)dst,
@@ -1767,6 +1787,7 @@ static int host_shard_pq(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const
                                                        cs.d_order + q.a, q.m, 0, kKeyBits, H));
             hipLaunchKernelGGL(pq_publish_kernel, dim3(1), dim3(1), 0, H, cs.d_pq + 1, tend);
             BSW_TRY(hipGetLastError());
+            if (dbg) BSW_TRY(hipEventRecord(dc.pq_dbg[1][c], H));
             if (dbg)
                 fprintf(stderr, "pq chunk %d: %d pairs, staged %.3f .. %.3f ms\n", c, (int)q.m,
                         std::chrono::duration<double, std::milli>(t0 - t_start).count(),
@@ -1775,8 +1796,18 @@ static int host_shard_pq(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const
         BSW_TRY(hipMemcpyAsync(dc.pq_hout, cs.d_scratch, (size_t)n * 24, hipMemcpyDeviceToHost, D));
         BSW_TRY(hipMemcpyAsync(cs.h_meta + kMetaErr, cs.d_meta + kMetaErr, sizeof(int32_t), hipMemcpyDeviceToHost, D));
         BSW_TRY(hipStreamSynchronize(D));
-        if (dbg)
+        if (dbg) {
             fprintf(stderr, "pq drained at %.3f ms\n", std::chrono::duration<double, std::milli>(now() - t_start).count());
+            for (int c = 0; c < nch; ++c) {      // device timeline from the grid's start event
+                float cp = 0.f, pb = 0.f;
+                (void)hipEventElapsedTime(&cp, dc.pq_t0, dc.pq_dbg[0][c]);
+                (void)hipEventElapsedTime(&pb, dc.pq_t0, dc.pq_dbg[1][c]);
+                fprintf(stderr, "pq chunk %d: copied at %.3f, published at %.3f ms after the grid start\n", c, cp, pb);
+            }
+            float kt = 0.f;
+            (void)hipEventElapsedTime(&kt, dc.pq_t0, dc.pq_t1);
+            fprintf(stderr, "pq grid span %.3f ms\n", kt);
+        }
         const int32_t err = cs.h_meta[kMetaErr];
         if (err & 8) return BSW_E_HIP;                         // aborted / poll bound (no caller record written)
         if (err) return BSW_E_RANGE;
@@ -1796,6 +1827,209 @@ static int host_shard_pq(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const
                 bsw_strerror(rc), (int)launched);
     if (rc != BSW_OK && launched) {
         // end the running grid (its waves poll *abort), then drain every stream
+        int32_t one = 1;
+        if (hipMemcpyAsync(cs.d_pq + 2, &one, sizeof(one), hipMemcpyHostToDevice, H) == hipSuccess)
+            (void)hipStreamSynchronize(H);
+        (void)hipStreamSynchronize(D);
+        (void)hipStreamSynchronize(H);
+        (void)hipStreamSynchronize(C);
+    }
+    if (rc == BSW_OK && st) {
+        bsw_stats_t agg{};
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, dc.pq_t0, dc.pq_t1) == hipSuccess) agg.kernel_ms = ms;
+        agg.n_packed = n; agg.n_launches = 1;
+        (cell_bits == 8 ? agg.n_u8 : agg.n_i16) += n;
+        agg.stage_ms = (float)stage_ms;
+        agg.host_ms = (float)std::chrono::duration<double, std::milli>(now() - t_start).count();
+        *st = agg;
+    }
+    for (int k = 0; k < kSlots; ++k) dc.give_back(std::move(slots[k]), rc);
+    return rc;
+}
+
+// The 2-bit form of the persistent pipeline (BSW_PQ_2BIT=1, experiment): chunks cross PCIe as 2-bit
+// codes + exception words + 20-B records (stage_chunk; ~45% fewer bytes than nibbles) and the
+// helper CUs expand them (stage_in_kernel) into call-wide byte buffers at the chunk's caller offsets;
+// the DP grid reads SeqPair records and bytes.  Needs ascending chunk extents (one span each for
+// targets and queries: r0..r1, q0..q1).  Otherwise as host_shard_pq.
+static int host_shard_pq2(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref, const uint8_t *qer,
+                          int32_t n, int32_t w, int cell_bits, const std::vector<std::pair<int32_t, int32_t>> &chs,
+                          const std::vector<BlkStat> &bs, int64_t r0, int64_t r1, int64_t q0, int64_t q1,
+                          bsw_stats_t *st)
+{
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t_start = now();
+    std::lock_guard<std::mutex> g(dc.pq_mu);
+    BSW_TRY(hipSetDevice(dc.device));
+    if (!ensure_pq_streams(dc)) return 1;
+    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;
+    constexpr int kSlots = 3;
+    std::unique_ptr<Slot> slots[kSlots];
+    int rc = BSW_OK;
+    for (int k = 0; k < kSlots; ++k) {
+        slots[k] = dc.acquire(rc);
+        if (rc) {
+            for (int j = 0; j < k; ++j) dc.give_back(std::move(slots[j]));
+            return rc;
+        }
+    }
+    hipStream_t H = dc.pq_h, D = dc.pq_d;
+    Slot &cs = *slots[0];
+    hipStream_t C = cs.stream;
+    const int nch = (int)chs.size();
+    bool launched = false;
+    double stage_ms = 0;
+    rc = [&]() -> int {
+        int32_t mmax = 0, ntiles = 0;
+        for (const auto &c : chs) {
+            const int32_t m = std::min(n, c.second * kStageBlk) - c.first * kStageBlk;
+            mmax = std::max(mmax, m);
+            ntiles += (m + 63) / 64;
+        }
+        BSW_TRY(grow(cs.d_pairs, cs.cap_pairs, (size_t)n));
+        BSW_TRY(grow(cs.d_ref, cs.cap_ref, (size_t)(r1 - r0) + 16));
+        BSW_TRY(grow(cs.d_qer, cs.cap_qer, (size_t)(q1 - q0) + 16));
+        BSW_TRY(grow_sort(cs, n));
+        BSW_TRY(grow(cs.d_pq, cs.cap_pq, (size_t)4));
+        BSW_TRY(grow(cs.d_scratch, cs.cap_scratch, (size_t)n * 3 + 1));
+        size_t tmp_bytes = 0;
+        BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, cs.d_keys, cs.d_keys2, cs.d_vals, cs.d_order,
+                                                   mmax, 0, kKeyBits, H));
+        BSW_TRY(grow(cs.d_tmp, cs.cap_tmp, tmp_bytes));
+        // every staging buffer at its final size before the grid starts (no hipFree mid-call)
+        for (int c = 0; c < nch; ++c) {
+            Slot &s = *slots[c % kSlots];
+            int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+            for (int32_t b = chs[c].first; b < chs[c].second; ++b) {
+                r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
+                q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi);
+            }
+            const size_t rb = r_lo == INT64_MAX ? 0 : (size_t)(r_hi - r_lo), qb = q_lo == INT64_MAX ? 0 : (size_t)(q_hi - q_lo);
+            const size_t m = (size_t)(std::min(n, chs[c].second * kStageBlk) - chs[c].first * kStageBlk);
+            const size_t b2 = std::max(align256(align256(align256(m * sizeof(PairIn)) + (rb + 3) / 4 + 4) + (qb + 3) / 4 + 4) +
+                                           ((rb + qb) / 32 + 1024) * 4, m * 24);
+            const size_t b4 = align256(align256(m * sizeof(SeqPair)) + (rb + 1) / 2 + 4) + (qb + 1) / 2 + 4;
+            const size_t need = std::max(b2, b4) + 4096;
+            if (need > s.cap_stage) {
+                if (s.h_stage) (void)hipHostFree(s.h_stage);
+                s.h_stage = nullptr; s.cap_stage = 0;
+                BSW_TRY(hipHostMalloc(&s.h_stage, need, 0));
+                s.cap_stage = need;
+            }
+            BSW_TRY(grow(s.d_stage, s.cap_dstage, need));
+        }
+        if (dc.pq_hout_cap < (size_t)n * 24) {
+            if (dc.pq_hout) (void)hipHostFree(dc.pq_hout);
+            dc.pq_hout = nullptr; dc.pq_hout_cap = 0;
+            const size_t cap = (size_t)n * 24 + (size_t)n * 6;
+            BSW_TRY(hipHostMalloc(&dc.pq_hout, cap, 0));
+            dc.pq_hout_cap = cap;
+        }
+        PqArgs a{};
+        a.kp = kp; a.w = w; a.pairs = cs.d_pairs; a.order = cs.d_order;
+        a.ref = cs.d_ref - r0; a.qer = cs.d_qer - q0;
+        a.err = cs.d_meta + kMetaErr; a.head = cs.d_pq; a.ready = cs.d_pq + 1; a.abort = cs.d_pq + 2;
+        a.nchunks = nch; a.ntiles = ntiles;
+        for (int c = 0, t = 0; c < nch; ++c) {
+            const int32_t a0 = chs[c].first * kStageBlk, m = std::min(n, chs[c].second * kStageBlk) - a0;
+            a.chunks[c] = PqChunk{t, a0, m, a0, 0, 0, 0};
+            t += (m + 63) / 64;
+        }
+        BSW_TRY(hipMemsetAsync(cs.d_meta, 0, kMetaWords * sizeof(int32_t), H));
+        BSW_TRY(hipMemsetAsync(cs.d_pq, 0, 4 * sizeof(int32_t), H));
+        BSW_TRY(hipEventRecord(dc.pq_init, H));
+        BSW_TRY(hipStreamWaitEvent(D, dc.pq_init, 0));
+        BSW_TRY(hipEventRecord(dc.pq_t0, D));
+        BSW_TRY(launch_pq_kernel(a, std::min(ntiles, 8 * (dc.pq_ncu - dc.pq_nres)), D));
+        launched = true;
+        BSW_TRY(hipEventRecord(dc.pq_t1, D));
+        for (int c = 0, tend = 0; c < nch; ++c) {
+            const int k = c % kSlots;
+            Slot &s = *slots[k];
+            const int32_t b = chs[c].first, nb = chs[c].second - b;
+            const int32_t a0 = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a0;
+            tend += (m + 63) / 64;
+            if (c >= kSlots) BSW_TRY(hipEventSynchronize(dc.pq_ev[k]));   // slot k's last chunk expanded
+            const auto t0 = now();
+            StagedChunk sc;
+            if (int r = stage_chunk(s, pairs + a0, ref, qer, m, bs.data() + b, nb, true, sc)) return r;
+            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
+            if (!sc.packed) return BSW_E_HIP;                 // (cannot happen: host_shard checked the extents)
+            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, sc.bytes, hipMemcpyHostToDevice, C));
+            BSW_TRY(hipEventRecord(dc.pq_init, C));
+            BSW_TRY(hipStreamWaitEvent(H, dc.pq_init, 0));
+            uint8_t *dr = cs.d_ref + (sc.r_base - r0), *dq = cs.d_qer + (sc.q_base - q0);
+            if (sc.mode == kStage2bit) {
+                const int64_t tr = ((int64_t)sc.rb + 15) / 16, tq = ((int64_t)sc.qb + 15) / 16;
+                const int64_t nthr = tr + tq + m;
+                hipLaunchKernelGGL(stage_in_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, H,
+                                   s.d_stage + sc.ref_off, (int64_t)sc.rb, s.d_stage + sc.qer_off, (int64_t)sc.qb,
+                                   (const uint32_t *)(s.d_stage + sc.exc_off), sc.n_exr, sc.n_exr + sc.n_exq,
+                                   (const PairIn *)(s.d_stage + sc.pair_off), m, dr, dq, cs.d_pairs + a0,
+                                   (int32_t *)nullptr);
+            } else {                                           // nibbles + whole records
+                const int64_t tr = ((int64_t)sc.rb + 7) / 8, tq = ((int64_t)sc.qb + 7) / 8;
+                if (tr > 0)
+                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, H,
+                                       s.d_stage + sc.ref_off, dr, (int64_t)sc.rb);
+                if (tq > 0)
+                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, H,
+                                       s.d_stage + sc.qer_off, dq, (int64_t)sc.qb);
+                BSW_TRY(hipMemcpyAsync(cs.d_pairs + a0, s.d_stage + sc.pair_off, (size_t)m * sizeof(SeqPair),
+                                       hipMemcpyDeviceToDevice, H));
+            }
+            BSW_TRY(hipGetLastError());
+            BSW_TRY(hipEventRecord(dc.pq_ev[k], H));
+            hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, H, cs.d_pairs + a0, m, kp,
+                               w, 1, 0, a.ref, a.qer, cs.d_keys, cs.d_vals, cs.d_meta, cs.d_meta + kMetaMaxq,
+                               (int)kp.keymode, 0);
+            BSW_TRY(hipGetLastError());
+            size_t tb = cs.cap_tmp;
+            BSW_TRY(hipcub::DeviceRadixSort::SortPairs(cs.d_tmp, tb, cs.d_keys, cs.d_keys2, cs.d_vals,
+                                                       cs.d_order + a0, m, 0, kKeyBits, H));
+            hipLaunchKernelGGL(pq_publish_kernel, dim3(1), dim3(1), 0, H, cs.d_pq + 1, tend);
+            BSW_TRY(hipGetLastError());
+            if (dbg) {
+                if (!dc.pq_dbg[1][c]) BSW_TRY(hipEventCreate(&dc.pq_dbg[1][c]));
+                BSW_TRY(hipEventRecord(dc.pq_dbg[1][c], H));
+            }
+        }
+        int32_t *d_out = (int32_t *)cs.d_scratch;
+        hipLaunchKernelGGL(gather_outputs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, D, cs.d_pairs, d_out,
+                           n);
+        BSW_TRY(hipGetLastError());
+        BSW_TRY(hipMemcpyAsync(dc.pq_hout, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, D));
+        BSW_TRY(hipMemcpyAsync(cs.h_meta + kMetaErr, cs.d_meta + kMetaErr, sizeof(int32_t), hipMemcpyDeviceToHost, D));
+        BSW_TRY(hipStreamSynchronize(D));
+        if (dbg) {
+            for (int c = 0; c < nch; ++c) {
+                float pb = 0.f;
+                (void)hipEventElapsedTime(&pb, dc.pq_t0, dc.pq_dbg[1][c]);
+                fprintf(stderr, "pq2 chunk %d: published at %.3f ms after the grid start\n", c, pb);
+            }
+            float kt = 0.f;
+            (void)hipEventElapsedTime(&kt, dc.pq_t0, dc.pq_t1);
+            fprintf(stderr, "pq2 grid span %.3f ms\n", kt);
+        }
+        const int32_t err = cs.h_meta[kMetaErr];
+        if (err & 8) return BSW_E_HIP;
+        if (err) return BSW_E_RANGE;
+        const int32_t *o = (const int32_t *)dc.pq_hout;
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(HostPool::workers() + 1, n >> 15));
+        HostPool::get().parallel_for(nt, [&](int t) {
+            for (int32_t i = (int32_t)((int64_t)n * t / nt); i < (int32_t)((int64_t)n * (t + 1) / nt); ++i) {
+                const int32_t *q = o + 6 * (int64_t)i;
+                SeqPair &p = pairs[i];
+                p.score = q[0]; p.tle = q[1]; p.gtle = q[2]; p.qle = q[3]; p.gscore = q[4]; p.max_off = q[5];
+            }
+        });
+        return BSW_OK;
+    }();
+    if (rc != BSW_OK && dbg)
+        fprintf(stderr, "host_shard_pq2: n %d, %d chunks: rc %d (%s), grid launched %d\n", (int)n, nch, rc,
+                bsw_strerror(rc), (int)launched);
+    if (rc != BSW_OK && launched) {
         int32_t one = 1;
         if (hipMemcpyAsync(cs.d_pq + 2, &one, sizeof(one), hipMemcpyHostToDevice, H) == hipSuccess)
             (void)hipStreamSynchronize(H);
@@ -1850,7 +2084,26 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
         n > kp0.small_batch && n > kp0.mid_batch) {
         bool ok = true;
         for (const BlkStat &b : bs) ok = ok && b.fast;
-        const auto chs = fast_chunks(bs, n, chunk);
+        // chunks: a first one that fills the grid's waves (~2K tiles), then `chunk`-sized ones (no
+        // ramp: there are no per-chunk tails to hide); BSW_PQ_FIRST / BSW_PQ_CHUNK (blocks) override
+        std::vector<std::pair<int32_t, int32_t>> chs;
+        {
+            const int32_t nblk = (int32_t)bs.size();
+            const char *e1 = getenv("BSW_PQ_FIRST"), *e2 = getenv("BSW_PQ_CHUNK");
+            const int32_t first = e1 ? std::max(1, atoi(e1)) : 31;
+            const int32_t step = e2 ? std::max(1, atoi(e2)) : std::max<int32_t>(1, chunk / kStageBlk);
+            for (int32_t b = 0, nb = first; b < nblk; b += nb, nb = step) {
+                int64_t bytes = 0;
+                int32_t k = 0;
+                for (; k < nb && b + k < nblk; ++k) {
+                    const int64_t x = bs[b + k].r_sum + bs[b + k].q_sum;
+                    if (k > 0 && bytes + x > ((int64_t)1 << 29)) break;
+                    bytes += x;
+                }
+                chs.emplace_back(b, b + k);
+                nb = k;
+            }
+        }
         ok = ok && !chs.empty() && (int)chs.size() <= kPqMaxChunks;
         for (size_t c = 0; ok && c < chs.size(); ++c) {
             int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
@@ -1863,6 +2116,25 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
             if (q_lo != INT64_MAX) ok = ok && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096 && (q_hi - q_lo) < ((int64_t)1 << 30);
         }
         if (getenv("BSW_DEBUG_HP")) fprintf(stderr, "persistent pipeline: eligible %d (%d chunks)\n", (int)ok, (int)chs.size());
+        if (ok && getenv("BSW_PQ_2BIT")) {        // (experiment) the 2-bit form: ascending extents, one span
+            int64_t r0 = INT64_MAX, r1 = 0, q0 = INT64_MAX, q1 = 0, pr = INT64_MIN, pqx = INT64_MIN;
+            bool asc = true;
+            for (const auto &ch : chs) {
+                int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
+                for (int32_t b = ch.first; b < ch.second; ++b) {
+                    r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
+                    q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi);
+                }
+                if (r_lo != INT64_MAX) { asc = asc && r_lo >= pr; pr = r_hi; r0 = std::min(r0, r_lo); r1 = std::max(r1, r_hi); }
+                if (q_lo != INT64_MAX) { asc = asc && q_lo >= pqx; pqx = q_hi; q0 = std::min(q0, q_lo); q1 = std::max(q1, q_hi); }
+            }
+            if (r0 == INT64_MAX) r0 = r1 = 0;
+            if (q0 == INT64_MAX) q0 = q1 = 0;
+            if (asc) {
+                const int r = host_shard_pq2(kp0, dc, pairs, ref, qer, n, w, cell_bits, chs, bs, r0, r1, q0, q1, st);
+                if (r != 1) return r;
+            }
+        }
         if (ok) {
             const int r = host_shard_pq(kp0, dc, pairs, ref, qer, n, w, cell_bits, chs, bs, st);
             if (r != 1) return r;
