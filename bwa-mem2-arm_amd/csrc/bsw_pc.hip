@@ -586,27 +586,29 @@ __device__ __forceinline__ int pc_lastpos(std::integer_sequence<int, G...>, cons
 // chunk -- records as PairIn in schedule order, sequences as nibbles (idr / idq nibble indices),
 // outputs as 6 x int32 into out24 -- so the chunk needs no unpack, plan, sort or gather kernel.
 // The target stream then carries 8 codes per dword: 9 dwords per lane per 64-row chunk.
-template <int QMAX, bool NIB> constexpr int pc_cdw() { return NIB ? kPcChunkDwN : kPcChunkDw; }
-
-// One wave's 64 pairs (lane slot gid runs pair idx_base + order[gid]; slots >= n idle): the whole
-// DP of pc_kernel, shared by the one-launch-per-64-pairs form (pc_kernel) and the persistent
-// tile-queue form (pq_kernel).  s_tgt / s_prof: the caller's LDS (s_prof filled and synced).
-template <int QMAX, int WPB, bool BY, bool NIB>
-__device__ __forceinline__ void pc_body(const KParams &kp, const int32_t w, SeqPair *__restrict__ pairs,
-                                        const int32_t *__restrict__ order, const int32_t n,
-                                        const uint8_t *__restrict__ ref, const uint8_t *__restrict__ qer,
-                                        int32_t *__restrict__ err, const PairIn *__restrict__ recs,
-                                        int32_t *__restrict__ out24, const int gid, const int32_t idx_base,
-                                        uint32_t (&s_tgt)[WPB][2][pc_cdw<QMAX, NIB>()][64],
-                                        const uint2 (&s_prof)[8])
+template <int QMAX, int WPB, bool BY, bool NIB = false>
+__global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams kp, const int32_t w,
+                                                    SeqPair *__restrict__ pairs,
+                                                    const int32_t *__restrict__ order,
+                                                    const int32_t n,
+                                                    const uint8_t *__restrict__ ref,
+                                                    const uint8_t *__restrict__ qer,
+                                                    int32_t *__restrict__ err,
+                                                    const PairIn *__restrict__ recs = nullptr,
+                                                    int32_t *__restrict__ out24 = nullptr)
 {
     constexpr int NG = QMAX / 4;        // groups = query words (4 codes each)
-    constexpr int CDW = pc_cdw<QMAX, NIB>();   // target dwords per lane per 64-row chunk
+    constexpr int CDW = NIB ? kPcChunkDwN : kPcChunkDw;   // target dwords per lane per 64-row chunk
 #ifdef BSW_PC_STATS
     const unsigned long long t_wave0 = wall_clock64();
 #endif
+    __shared__ uint32_t s_tgt[WPB][2][CDW][64];   // 8.7 KB per wave (4.6 KB for nibbles)
+    __shared__ uint2 s_prof[8];                           // per-row score profiles, by target code
+    if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
+    __syncthreads();
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = gid < n;
-    const int idx = valid ? idx_base + (order ? order[gid] : gid) : 0;
+    const int idx = valid ? (order ? order[gid] : gid) : 0;
     SeqPair *sp = pairs + idx;
     int idr = 0, idq = 0, tlen = 0, qlen = 0, h0 = 0;
     if (valid) {
@@ -889,24 +891,7 @@ __device__ __forceinline__ void pc_body(const KParams &kp, const int32_t w, SeqP
     }
 }
 
-template <int QMAX, int WPB, bool BY, bool NIB = false>
-__global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams kp, const int32_t w,
-                                                    SeqPair *__restrict__ pairs,
-                                                    const int32_t *__restrict__ order,
-                                                    const int32_t n,
-                                                    const uint8_t *__restrict__ ref,
-                                                    const uint8_t *__restrict__ qer,
-                                                    int32_t *__restrict__ err,
-                                                    const PairIn *__restrict__ recs = nullptr,
-                                                    int32_t *__restrict__ out24 = nullptr)
-{
-    __shared__ uint32_t s_tgt[WPB][2][pc_cdw<QMAX, NIB>()][64];   // 8.7 KB per wave (4.6 KB for nibbles)
-    __shared__ uint2 s_prof[8];                           // per-row score profiles, by target code
-    if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
-    __syncthreads();
-    pc_body<QMAX, WPB, BY, NIB>(kp, w, pairs, order, n, ref, qer, err, recs, out24,
-                                blockIdx.x * blockDim.x + threadIdx.x, 0, s_tgt, s_prof);
-}
+template <int QMAX, bool NIB> constexpr int pc_cdw() { return NIB ? kPcChunkDwN : kPcChunkDw; }
 
 // Persistent tile-queue form: a grid of at most ~2 waves per SIMD, each wave
 // taking 64-pair tiles from ONE device-scope counter until the queue is empty -- no per-wave
@@ -967,17 +952,23 @@ __global__ __launch_bounds__(64, 2) void pq_kernel(const PqArgs args)
         const int m = a->chunks[c].m, idx_base = a->chunks[c].idx_base;
         const KParams kp = a->kp;
         const int gid = slot0 + (t - tile0) * 64 + (int)threadIdx.x;
-        if constexpr (NIB) {
-            // the chunk as staged (records, nibbles) inside the call's device buffer; outputs at the
-            // chunk's pairs of the call's 24-B output array
-            const uint8_t *nb = a->nbase;
-            pc_body<QMAX, 1, false, true>(kp, a->w, nullptr, a->order, slot0 + m, nb + a->chunks[c].ref_off,
-                                          nb + a->chunks[c].qer_off, a->err,
-                                          (const PairIn *)(nb + a->chunks[c].rec_off),
-                                          a->out24 + 6 * (int64_t)idx_base, gid, 0, s_tgt, s_prof);
-        } else {
-            pc_body<QMAX, 1, false, false>(kp, a->w, a->pairs, a->order, slot0 + m, a->ref, a->qer, a->err, nullptr,
-                                           nullptr, gid, idx_base, s_tgt, s_prof);
+        [[maybe_unused]] constexpr int WPB = 1;
+        constexpr bool BY = false;
+        const int32_t w = a->w, n = slot0 + m;
+        const int32_t *order = a->order;
+        int32_t *err = a->err;
+        // NIB: the chunk as staged (records, nibbles) inside the call's device buffer; outputs at the
+        // chunk's pairs of the call's 24-B output array
+        const uint8_t *nb = NIB ? a->nbase : nullptr;
+        SeqPair *pairs = NIB ? nullptr : a->pairs;
+        const uint8_t *ref = NIB ? nb + a->chunks[c].ref_off : a->ref;
+        const uint8_t *qer = NIB ? nb + a->chunks[c].qer_off : a->qer;
+        const PairIn *recs = NIB ? (const PairIn *)(nb + a->chunks[c].rec_off) : nullptr;
+        int32_t *out24 = NIB ? a->out24 + 6 * (int64_t)idx_base : nullptr;
+        const int32_t idx_off = NIB ? 0 : idx_base;
+        {
+            const int32_t idx_base = idx_off;
+#include "bsw_pc_body.inc"
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): the tile's last target DMA into s_tgt
     }
