@@ -84,15 +84,22 @@ constexpr int kQpShr2 = 0x40;                      // quad_perm [0, 0, 0, 1]
 constexpr int kQpXor1 = 0xB1;                      // quad_perm [1, 0, 3, 2]
 constexpr int kQpXor2 = 0x4E;                      // quad_perm [2, 3, 0, 1]
 
+// GS = 32: two DPP rows per group -- the scans end with row_bcast:15 (row 2k's last lane into
+// row 2k + 1), the one-lane shift is wave_shr:1 (then lane 0 of each group cleared), the all-reduce
+// ends with v_permlane16_swap (rows 2k <-> 2k + 1)
+#define GQ_BC15(x) __builtin_amdgcn_update_dpp(0, (x), 0x142, 0xa, 0xf, false)
+#define GQ_WSHR1(x) __builtin_amdgcn_update_dpp(0, (x), 0x138, 0xf, 0xf, true)
+
 // inclusive max scan over the group's lanes of non-negative x
 template <int GS>
 __device__ __forceinline__ int grp_scan_max0(int x)
 {
-    if constexpr (GS == 16) {
+    if constexpr (GS == 16 || GS == 32) {
         x = max(x, GQ_SHR0(x, 1));
         x = max(x, GQ_SHR0(x, 2));
         x = max(x, GQ_SHR0(x, 4));
         x = max(x, GQ_SHR0(x, 8));
+        if constexpr (GS == 32) x = max(x, GQ_BC15(x));
     } else {
         x = max(x, GQ_QP(x, kQpShr1));
         x = max(x, GQ_QP(x, kQpShr2));
@@ -104,7 +111,10 @@ template <int GS>
 __device__ __forceinline__ int grp_shr1_0(int x, int gl)
 {
     if constexpr (GS == 16) return GQ_SHR0(x, 1);
-    else {
+    else if constexpr (GS == 32) {
+        const int y = GQ_WSHR1(x);
+        return gl == 0 ? 0 : y;
+    } else {
         const int y = GQ_QP(x, kQpShr1);
         return gl == 0 ? 0 : y;
     }
@@ -113,11 +123,15 @@ __device__ __forceinline__ int grp_shr1_0(int x, int gl)
 template <int GS>
 __device__ __forceinline__ uint32_t grp_max_u32(uint32_t x)
 {
-    if constexpr (GS == 16) {
+    if constexpr (GS == 16 || GS == 32) {
         x = max(x, (uint32_t)GQ_ROR((int)x, 8));
         x = max(x, (uint32_t)GQ_ROR((int)x, 4));
         x = max(x, (uint32_t)GQ_ROR((int)x, 2));
         x = max(x, (uint32_t)GQ_ROR((int)x, 1));
+        if constexpr (GS == 32) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+            x = max((uint32_t)sw[0], (uint32_t)sw[1]);
+        }
     } else {
         x = max(x, (uint32_t)GQ_QP((int)x, kQpXor1));
         x = max(x, (uint32_t)GQ_QP((int)x, kQpXor2));
@@ -135,7 +149,7 @@ __device__ __forceinline__ int gq_init_h(int j, int h0, int qlen, int oe_ins, in
 // Targets are staged in LDS (a global-load prefetch would be waited for at the loop's register
 // copy in the same row), so a target longer than gq_tmax(GS) takes the planned path: 1 KB per
 // pair for 16-lane groups (4 per wave), 512 B for quads (16 per wave: 8 KB of LDS per wave).
-__host__ __device__ constexpr int gq_tmax(int gs) { return gs == 16 ? 1024 : 512; }
+__host__ __device__ constexpr int gq_tmax(int gs) { return gs >= 16 ? 1024 : 512; }
 
 // Same int16 bounds as the wave kernel (bsw_host.cpp wv_class); the whole query is resident,
 // so the band cap only limits [beg, end).
@@ -157,6 +171,7 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
                                                 int32_t *__restrict__ out24)
 {
     static_assert((GS == 16 && (C == 4 || C == 6 || C == 8 || C == 10)) ||
+                  (GS == 32 && (C == 2 || C == 4 || C == 6)) ||
                   (GS == 4 && (C == 16 || C == 24 || C == 32 || C == 40)), "group size / columns per lane");
     constexpr int R = C / 2;                       // packed registers per plane
     constexpr int G = (C + 3) / 4;                 // query words per lane (4 codes each)
@@ -386,7 +401,7 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
             else row(std::false_type{}, std::false_type{}, K8c);
         }
     };
-    if constexpr (GS == 16) {         // (the quad form keeps one path: its registers are the limit)
+    if constexpr (GS >= 16) {         // (the quad form keeps one path: its registers are the limit)
         if (k8) rows(std::true_type{});
         else rows(std::false_type{});
     } else {
@@ -411,6 +426,12 @@ __global__ __launch_bounds__(64) void gq_kernel(const KParams kp, const int32_t 
 
 int gq_cols_for(int max_qlen, int gs)
 {
+    if (gs == 32) {                      // latency form: two DPP rows per pair, 2 pairs per wave
+        if (max_qlen <= 64) return 2;
+        if (max_qlen <= 128) return 4;
+        if (max_qlen <= 160) return 6;
+        return -1;
+    }
     if (gs == 16) {
         if (max_qlen <= 64) return 4;
         if (max_qlen <= 96) return 6;
@@ -445,6 +466,9 @@ hipError_t launch_gq_kernel(int gs, int cols, const KParams &kp, int32_t w, SeqP
     case 1606: GQ_L(6, 16); break;
     case 1608: GQ_L(8, 16); break;
     case 1610: GQ_L(10, 16); break;
+    case 3202: GQ_L(2, 32); break;
+    case 3204: GQ_L(4, 32); break;
+    case 3206: GQ_L(6, 32); break;
     case 416: GQ_L(16, 4); break;
     case 424: GQ_L(24, 4); break;
     case 432: GQ_L(32, 4); break;

@@ -601,12 +601,18 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     // small batches (kt_for-sized calls): the row-group kernel (bsw_gq.hip) straight on the
     // call's stream -- no plan, no sort, no class-count readback
     // medium batches: the quad form (4 lanes per pair, targets <= 512 bytes)
-    const int gs = n <= kp.small_batch ? 16 : 4;
-    const bool gq_size = !pc.tput && (n <= kp.small_batch || n <= kp.mid_batch);
-    const bool gq_fit = pc.gq_maxq == -2 || (pc.gq_maxq >= 0 && (gs == 16 || pc.gq_maxt <= 512));
+    // the 32-lane latency form (two DPP rows per pair: ~21% fewer instructions per row) for batches
+    // of at most 2048 pairs -- 1K calls 0.277 -> 0.25 ms, 8 callers without coalescing +8%; at 4K+
+    // pairs per batch the 16-lane form's fewer instructions per cell win (percall_bench, same box,
+    // profiles/r05/gq32_percall.txt).  BSW_GQ32_MAX (pairs, read per call) overrides
+    const char *g32 = getenv("BSW_GQ32_MAX");
+    const int32_t gq32_max = g32 ? atoi(g32) : 2048;
+    const int gs = n <= gq32_max ? 32 : n <= kp.small_batch ? 16 : 4;
+    const bool gq_size = !pc.tput && (n <= kp.small_batch || n <= kp.mid_batch || n <= gq32_max);
+    const bool gq_fit = pc.gq_maxq == -2 || (pc.gq_maxq >= 0 && (gs >= 16 || pc.gq_maxt <= 512));
     if (kp.group_kernel && gq_size && gq_fit && kp.long_route == 1 && kp.maxsc == 1 && !kp.misroute) {
         const bool checked = pc.gq_maxq >= 0;
-        const int cols = checked ? gq_cols_for(pc.gq_maxq, gs) : (gs == 16 ? 10 : 40);
+        const int cols = checked ? gq_cols_for(pc.gq_maxq, gs) : (gs == 32 ? 6 : gs == 16 ? 10 : 40);
         int32_t *d_err = s.d_meta + kMetaErr;
         // the DP stream when the call has one (host pipeline: the helper stream holds few CUs)
         hipStream_t fs = pc.stream;

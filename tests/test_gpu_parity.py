@@ -994,3 +994,59 @@ def test_persistent_host_pipeline_falls_back(c2_full):
     _assert_same(want[:200_000][perm], got, "persistent fallback permuted")
     assert e.last_stats().n_launches > 1
     e.close()
+
+
+@pytest.mark.parametrize("w", [0, 1, 7, 100, 200])
+def test_group_kernel_32lane(w, monkeypatch):
+    """The row-group kernel's 32-lane latency form (bsw_gq.hip GS = 32: two DPP rows per pair, scans
+    closed by row_bcast:15, the column shift by wave_shr:1, reductions by v_permlane16_swap), routed
+    by BSW_GQ32_MAX (read per call): random shapes (queries 0..160 -> 2 / 4 / 6 columns per lane,
+    targets 0..400, h0 0..200), the 255/256 key boundary, host and device entry points == oracle."""
+    monkeypatch.setenv("BSW_GQ32_MAX", "1000000")
+    e = bsw.Engine()
+    for qhi in (60, 120, 160):
+        pairs, ref, qer = bswgen.random_pairs(3000, seed=7100 + w + qhi, tlen=(0, 400), qlen=(0, qhi), h0=(0, 200))
+        want = pairs.copy()
+        oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+        got = pairs.copy()
+        e.get_scores(got, ref, qer, w)
+        _assert_same(want, got, f"gq32 host w={w} qlen<={qhi}")
+        assert e.last_stats().n_group == len(pairs)
+        dp, dr, dq = (hiprt.DeviceBuffer.from_array(a) for a in (pairs.copy(), ref, qer))
+        e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, len(pairs), w, 16)
+        _assert_same(want, dp.download(np.empty_like(pairs)), f"gq32 device w={w} qlen<={qhi}")
+        assert e.last_stats().n_group == len(pairs)
+    rng = np.random.default_rng(3255 + w)
+    items = []
+    for k in range(64):
+        qlen = int(rng.choice([40, 100, 150, 159, 160]))
+        q = rng.integers(0, 4, qlen).astype(np.uint8)
+        t = np.concatenate([q, rng.integers(0, 4, int(rng.integers(0, 140))).astype(np.uint8)])
+        h0 = 255 - qlen + ((k // 2) % 2)          # waves of two pairs: at 255 / at 256
+        items.append((t, q, h0))
+    pairs, ref, qer = bswgen.assemble(items)
+    want = pairs.copy()
+    oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
+    got = pairs.copy()
+    e.get_scores(got, ref, qer, w)
+    _assert_same(want, got, f"gq32 255/256 w={w}")
+    e.close()
+
+
+def test_group_kernel_32lane_golden(golden, monkeypatch):
+    """Every golden batch through the 32-lane form where the scoring qualifies (BSW_GQ32_MAX)."""
+    monkeypatch.setenv("BSW_GQ32_MAX", "1000000")
+    engines, ran = {}, 0
+    for name, pairs, ref, qer, w, sc in golden:
+        key = tuple(sorted(sc.items()))
+        if key not in engines:
+            engines[key] = bsw.Engine(_gparams(sc))
+        got = pairs.copy()
+        for f in bsw.OUT_FIELDS:
+            got[f] = -9
+        engines[key].get_scores(got, ref, qer, w)
+        _assert_same(pairs, got, f"gq32 golden {name}")
+        ran += engines[key].last_stats().n_group
+    assert ran > 0
+    for e in engines.values():
+        e.close()
