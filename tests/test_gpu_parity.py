@@ -476,10 +476,12 @@ def test_group_kernel_random(w):
 
 
 @pytest.mark.parametrize("quad", [False, True])
-def test_group_kernel_golden(golden, quad):
+def test_group_kernel_golden(golden, quad, monkeypatch):
     """Every golden batch on the default engine (small batches: the row-group kernel where the
     scoring qualifies, the planned path otherwise) and on the device entry point; quad: every
-    batch on the 4-lanes-per-pair form (BSW_OPT_SMALL_BATCH 0)."""
+    batch on the 4-lanes-per-pair form (BSW_OPT_SMALL_BATCH 0).  The 16-lane form here
+    (BSW_GQ32_MAX 0: batches of <= 2048 pairs would take the 32-lane form, tested on its own)."""
+    monkeypatch.setenv("BSW_GQ32_MAX", "0")
     engines, ran = {}, 0
     for name, pairs, ref, qer, w, sc in golden:
         key = tuple(sorted(sc.items()))
@@ -503,13 +505,14 @@ def test_group_kernel_golden(golden, quad):
 
 
 @pytest.mark.parametrize("w", [5, 100])
-def test_group_kernel_score_255_boundary(w):
+def test_group_kernel_score_255_boundary(w, monkeypatch):
     """The row-group kernel's 8-bit row-max key (bsw_gq.hip, K8: H << 8 | j in 16 bits) holds only
     when every live pair of the wave has h0 + min(qlen, tlen) <= 255.  Identical query / target
     pairs with h0 = 255 - qlen drive H to exactly 255 on the diagonal; waves of four pairs (16
     lanes each) mix them with pairs at h0 + qlen = 256 (the wave then runs the 16-bit key) and
     with near-identical ones, in every position of the wave.  Host and device entry points, both
-    routed to the 16-lane form, equal the oracle."""
+    routed to the 16-lane form (BSW_GQ32_MAX 0), equal the oracle."""
+    monkeypatch.setenv("BSW_GQ32_MAX", "0")
     rng = np.random.default_rng(255 + w)
     items = []
     for k in range(64):
