@@ -559,8 +559,10 @@ static void ensure_cu_streams(Slot &s)
     uint32_t hm[32] = {}, dm[32] = {};
     const int nw = (ncu + 31) / 32;
     for (int c = 0; c < ncu; ++c) dm[c / 32] |= 1u << (c % 32);
-    for (int r = 0; r < nr; ++r) {
-        const int c = r * (ncu / nr);
+    // the first nr CUs of the mask numbering (a set spread one CU per 32-bit mask word left 256-thread
+    // helper kernels waiting for a full DP grid: tools/pq_stream_probe.hip -- the round-4 A/B of this
+    // split, hostpath_ab_r4j.txt, ran with that spread set)
+    for (int c = 0; c < nr; ++c) {
         hm[c / 32] |= 1u << (c % 32);
         dm[c / 32] &= ~(1u << (c % 32));
     }
@@ -606,9 +608,10 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     // pairs per batch the 16-lane form's fewer instructions per cell win (percall_bench, same box,
     // profiles/r05/gq32_percall.txt).  BSW_GQ32_MAX (pairs, read per call) overrides
     const char *g32 = getenv("BSW_GQ32_MAX");
-    const int32_t gq32_max = g32 ? atoi(g32) : 2048;
+    // (within the small-batch range: BSW_OPT_SMALL_BATCH 0 keeps every batch off the 16/32-lane forms)
+    const int32_t gq32_max = std::min<int32_t>(g32 ? atoi(g32) : 2048, kp.small_batch);
     const int gs = n <= gq32_max ? 32 : n <= kp.small_batch ? 16 : 4;
-    const bool gq_size = !pc.tput && (n <= kp.small_batch || n <= kp.mid_batch || n <= gq32_max);
+    const bool gq_size = !pc.tput && (n <= kp.small_batch || n <= kp.mid_batch);
     const bool gq_fit = pc.gq_maxq == -2 || (pc.gq_maxq >= 0 && (gs >= 16 || pc.gq_maxt <= 512));
     if (kp.group_kernel && gq_size && gq_fit && kp.long_route == 1 && kp.maxsc == 1 && !kp.misroute) {
         const bool checked = pc.gq_maxq >= 0;
