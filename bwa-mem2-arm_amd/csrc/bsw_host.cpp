@@ -261,6 +261,7 @@ struct Slot {
     hipEvent_t evh = nullptr;           // inputs ready on the call's stream (pstream waits)
     hipEvent_t evd = nullptr;           // host pipeline: a chunk's DP done (its outputs' readback waits)
     PlanCall plan;                      // arguments of the last run_plan (run_dp's input)
+    bool ownq = false;                  // `stream` has a hardware queue of its own (DeviceCtx::acquire)
     int fast = 0;                       // last run_plan launched the row-group kernel: 2 = host-
                                         //   checked batch, 1 = kernel-checked (flag read back)
 };
@@ -318,6 +319,7 @@ struct DeviceCtx {
     int agg_leaders = 0;
     int agg_leaders_max = 4;            // BSW_OPT_COALESCE_LEADERS
     int agg_linger_us = 0;              // BSW_OPT_COALESCE_LINGER (off: a trade-off by caller count)
+    std::atomic<int> ownq_n{0};         // slots whose stream got a hardware queue of its own (acquire)
     std::mutex mu;
     std::vector<std::unique_ptr<Slot>> free_slots;
     uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
@@ -345,8 +347,9 @@ struct DeviceCtx {
         if (pq_d) (void)hipStreamDestroy(pq_d);
         if (pq_hout) (void)hipHostFree(pq_hout);
     }
-    static void release_slot(Slot *s)
+    void release_slot(Slot *s)
     {
+        if (s->ownq) ownq_n.fetch_sub(1);
         (void)hipSetDevice(s->device);
         (void)hipFree(s->d_pairs); (void)hipFree(s->d_ref); (void)hipFree(s->d_qer);
         (void)hipFree(s->d_keys); (void)hipFree(s->d_keys2); (void)hipFree(s->d_vals); (void)hipFree(s->d_order);
@@ -395,7 +398,29 @@ struct DeviceCtx {
         s->device = device;
         rc = hip_rc(hipSetDevice(device));
         if (rc) return nullptr;
-        if ((rc = hip_rc(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)))) return nullptr;
+        // The slot's stream through a CU mask of EVERY CU: a masked stream gets a hardware queue of its
+        // own, so concurrent kt_for-sized calls do not share the runtime's four queues
+        // (GPU_MAX_HW_QUEUES) and serialise their kernels behind each other.  Measured (percall_bench,
+        // 8 C++ callers, same box x2, profiles/r05/slot_ownq_percall.txt): 1K pairs per call without
+        // coalescing 9.4-9.5 -> 10.7-11.0 M/s, 4K 30.4-30.8 -> 34.7-34.9, 10K 40.5-40.9 -> 42.1-42.5;
+        // 1M-pair host calls unchanged.  The first 16 slots of a device (BSW_SLOT_OWNQ=0: none)
+        static const bool ownq = !getenv("BSW_SLOT_OWNQ") || atoi(getenv("BSW_SLOT_OWNQ")) != 0;
+        bool made = false;
+        if (ownq && ownq_n.fetch_add(1) < 16) {
+            hipDeviceProp_t pr;
+            if (hipGetDeviceProperties(&pr, device) == hipSuccess && pr.multiProcessorCount > 0 &&
+                pr.multiProcessorCount <= 1024) {
+                uint32_t m[32] = {};
+                const int ncu = pr.multiProcessorCount;
+                for (int c = 0; c < ncu; ++c) m[c / 32] |= 1u << (c % 32);
+                made = hipExtStreamCreateWithCUMask(&s->stream, (uint32_t)((ncu + 31) / 32), m) == hipSuccess;
+            }
+            s->ownq = made;
+            if (!made) ownq_n.fetch_sub(1);
+        } else if (ownq) {
+            ownq_n.fetch_sub(1);
+        }
+        if (!made && (rc = hip_rc(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)))) return nullptr;
         if ((rc = hip_rc(hipEventCreate(&s->ev0)))) return nullptr;
         if ((rc = hip_rc(hipEventCreate(&s->ev1)))) return nullptr;
         if ((rc = hip_rc(hipMalloc((void **)&s->d_meta, kMetaWords * sizeof(int32_t))))) return nullptr;
