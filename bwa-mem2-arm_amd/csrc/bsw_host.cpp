@@ -855,11 +855,16 @@ static int run_device(const KParams &kp, Slot &s, SeqPair *d_pairs, const uint8_
 
 // Wait for run_device's work (through the guard readback), record the DP kernel time; a
 // tripped range guard is BSW_E_RANGE (the affected pairs' outputs were not written).
-static int finish_stats(Slot &s)
+static int finish_stats(Slot &s, bool spin = false)
 {
     if (s.timed) {
         float ms = 0.f;
         s.timed = false;
+        if (spin) {         // a short batch: poll instead of the runtime's blocking wait (wake-up latency)
+            hipError_t q;
+            while ((q = hipStreamQuery(s.run_stream)) == hipErrorNotReady) _mm_pause();
+            BSW_TRY(q);
+        }
         BSW_TRY(hipStreamSynchronize(s.run_stream));
         BSW_TRY(hipEventElapsedTime(&ms, s.ev0, s.ev1));
         s.stats.kernel_ms = ms;
@@ -2663,7 +2668,8 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
             BSW_TRY(hipGetLastError());
         }
         BSW_TRY(hipMemcpyAsync(s.h_stage, s.d_stage, (size_t)N * 24, hipMemcpyDeviceToHost, s.stream));
-        if ((r = finish_stats(s))) return r;
+        static const bool spin = getenv("BSW_SMALL_SPIN") && atoi(getenv("BSW_SMALL_SPIN")) != 0;
+        if ((r = finish_stats(s, spin))) return r;
         const auto tg4 = std::chrono::steady_clock::now();
         if (getenv("BSW_DEBUG_AGG")) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -2671,14 +2677,20 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
                     (int)segs.size(), N, ms(tg0, tg1), ms(tg1, tg2), ms(tg2, tg3), ms(tg3, tg4), s.stats.kernel_ms);
         }
         const int32_t *out = (const int32_t *)s.h_stage;
-        HostPool::get().parallel_for((int)segs.size(), [&](int g) {
+        auto scatter = [&](int g) {
             SeqPair *p = segs[g].r->pairs;
             const int32_t *q = out + 6 * (int64_t)segs[g].p_off;
             for (int32_t i = 0; i < segs[g].r->n; ++i, q += 6) {
                 p[i].score = q[0]; p[i].tle = q[1]; p[i].gtle = q[2];
                 p[i].qle = q[3]; p[i].gscore = q[4]; p[i].max_off = q[5];
             }
-        });
+        };
+        // a few thousand records: on this thread (waking the host pool costs more than the copy)
+        static const bool pool_scatter = getenv("BSW_SMALL_POOL") && atoi(getenv("BSW_SMALL_POOL")) != 0;
+        if (!pool_scatter && N <= 16384)
+            for (int g = 0; g < (int)segs.size(); ++g) scatter(g);
+        else
+            HostPool::get().parallel_for((int)segs.size(), scatter);
         st = s.stats;
         st.stage_ms = (float)std::chrono::duration<double, std::milli>(tg1 - tg0).count();
         return BSW_OK;
