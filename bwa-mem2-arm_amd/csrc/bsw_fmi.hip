@@ -310,10 +310,20 @@ __device__ __forceinline__ EntT<uint64_t> ent_get(const EntP *p)
                           (uint64_t)v.z, (uint64_t)((v.w >> 16 & 0x7fffu) | (v.w >> 31) << 31)};
 }
 
+// The interval vectors' first kSmemLds entries live in LDS, [vector][slot][lane] as 16-B words (one
+// ds_read/write_b128 per entry, conflict-free), the rest in the HBM scratch: by the PMC of a 3 Gb
+// launch the sweeps' write-then-re-read of the vectors was most of the walk's ~55 KB fetched per read
+// (DESIGN.md §8).  8 KB of LDS per one-wave workgroup at 4 slots (16-B entries only; 0 = off).
+#ifndef BSW_SMEM_LDS
+#define BSW_SMEM_LDS 4
+#endif
+constexpr int kSmemLds = BSW_SMEM_LDS;
+
 template <class U, class S = EntT<U>>
 struct Lane {
     const uint8_t *q;
     int len;
+    uint4 *lds;              // this lane's LDS slots: [v][j] at lds[(v * kSmemLds + j) * 64] (or nullptr)
     S *sa, *sb;              // scratch vectors, element j at [j * stride]
     size_t stride;
     int scap;                // scratch entries per vector
@@ -335,6 +345,33 @@ __device__ __forceinline__ void push_out(Lane<U, S> &L, IvT<U> v, uint32_t start
     ++L.nout;
 }
 
+// vector v (0: sa, 1: sb), entry j
+template <class U, class S>
+__device__ __forceinline__ void vput(Lane<U, S> &L, int v, int j, const EntT<U> &e)
+{
+    if constexpr (kSmemLds > 0 && sizeof(S) == 16) {
+        if (j < kSmemLds) {
+            S t;
+            ent_put(&t, e);
+            L.lds[(v * kSmemLds + j) * 64] = *reinterpret_cast<const uint4 *>(&t);
+            return;
+        }
+    }
+    ent_put((v ? L.sb : L.sa) + (size_t)j * L.stride, e);
+}
+template <class U, class S>
+__device__ __forceinline__ EntT<U> vget(const Lane<U, S> &L, int v, int j)
+{
+    if constexpr (kSmemLds > 0 && sizeof(S) == 16) {
+        if (j < kSmemLds) {
+            S t;
+            *reinterpret_cast<uint4 *>(&t) = L.lds[(v * kSmemLds + j) * 64];
+            return ent_get(&t);
+        }
+    }
+    return ent_get((v ? L.sb : L.sa) + (size_t)j * L.stride);
+}
+
 // bwt_smem1a with max_intv = 0 (bwt_smem1): SMEMs overlapping x with occurrence >= min_intv;
 // those of length >= keep_len go to the output.  Returns the next x.
 //
@@ -354,8 +391,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
     const int qx = q[x];
     if (qx > 3) return x + 1;
     if (min_intv < 1) min_intv = 1;
-    S *curr = L.sa, *prev = L.sb;
-    const size_t st = L.stride;
+    int curr = 0, prev = 1;                               // vector ids (vput / vget)
     IvT<U> ik = set_intv(f, qx);
     U ikend = (U)(x + 1);
     int nc = 0, i;
@@ -380,7 +416,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
             ik.k = p;
             ikend = (U)((uint32_t)e | kTextFlag);
             if (e < len) {
-                if (nc < L.scap) ent_put(curr + (size_t)nc * st, EntT<U>{ik.k, ik.l, ik.s, ikend});
+                if (nc < L.scap) vput(L, curr, nc, EntT<U>{ik.k, ik.l, ik.s, ikend});
                 else L.overflow = 1;
                 ++nc;
             }
@@ -399,27 +435,27 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
             const IvT<U> ok = i + 1 - x <= f.kt ? ktab_get(f, i + 1 - x, code) : forward_ext(f, ik, qi);
 #endif
             if (ok.s != ik.s) {
-                if (nc < L.scap) ent_put(curr + (size_t)nc * st, EntT<U>{ik.k, ik.l, ik.s, ikend});
+                if (nc < L.scap) vput(L, curr, nc, EntT<U>{ik.k, ik.l, ik.s, ikend});
                 else L.overflow = 1;
                 ++nc;
                 if (ok.s < min_intv) break;
             }
             ik = ok; ikend = (U)(i + 1);
         } else {
-            if (nc < L.scap) ent_put(curr + (size_t)nc * st, EntT<U>{ik.k, ik.l, ik.s, ikend});
+            if (nc < L.scap) vput(L, curr, nc, EntT<U>{ik.k, ik.l, ik.s, ikend});
             else L.overflow = 1;
             ++nc;
             break;
         }
     }
     if (i == len) {
-        if (nc < L.scap) ent_put(curr + (size_t)nc * st, EntT<U>{ik.k, ik.l, ik.s, ikend});
+        if (nc < L.scap) vput(L, curr, nc, EntT<U>{ik.k, ik.l, ik.s, ikend});
         else L.overflow = 1;
         ++nc;
     }
     nc = min(nc, L.scap);
     // upstream reverses curr (longest matches first); here prev is read back to front once
-    const int ret = (int)((uint32_t)ent_get(curr + (size_t)(nc - 1) * st).e & ~kTextFlag);
+    const int ret = (int)((uint32_t)vget(L, curr, nc - 1).e & ~kTextFlag);
     if (prune && ret - x < keep_len) {
         // b_min: extend q[x] to the left while it keeps >= min_intv occurrences; stop as soon as
         // the bound reaches keep_len (then the sweep must run)
@@ -438,7 +474,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
         }
         if (ret - b < keep_len) return ret;
     }
-    { S *t = curr; curr = prev; prev = t; }
+    { const int t = curr; curr = prev; prev = t; }
     int np = nc;
     bool rev = true;
     int nmem = 0;
@@ -471,7 +507,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
 #pragma unroll
           for (int u = 0; u < kBackUnroll; ++u) {
               const int j = min(j0 + u, np - 1);
-              pvs[u] = ent_get(prev + (size_t)(rev ? np - 1 - j : j) * st);
+              pvs[u] = vget(L, prev, rev ? np - 1 - j : j);
           }
 #pragma unroll
           for (int u = 0; u < kBackUnroll; ++u) oks[u] = ext_of(pvs[u]);
@@ -498,7 +534,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
                 const bool to_text = f.text && ok.s == 1;
                 const U k2 = tm ? ok.k : (to_text ? f.sa[ok.k] : ok.k);
                 if (nc < L.scap)
-                    ent_put(curr + (size_t)nc * st, EntT<U>{k2, ok.l, ok.s, (U)(pe | ((tm || to_text) ? kTextFlag : 0u))});
+                    vput(L, curr, nc, EntT<U>{k2, ok.l, ok.s, (U)(pe | ((tm || to_text) ? kTextFlag : 0u))});
                 else L.overflow = 1;
                 ++nc;
                 last_cs = ok.s;
@@ -508,7 +544,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
         if (nc == 0) break;
         np = min(nc, L.scap);
         rev = false;
-        { S *t = curr; curr = prev; prev = t; }
+        { const int t = curr; curr = prev; prev = t; }
     }
     return ret;
 }
@@ -582,10 +618,12 @@ template <class U, class S>
 __device__ int smem_read(const FmiDevT<U> &f, const MemOpt &opt, const uint8_t *__restrict__ reads,
                          const int64_t *__restrict__ read_off, const int32_t *__restrict__ read_len, int32_t n0,
                          int32_t n, int t, S *__restrict__ scratch, int32_t scap,
-                         bsw_bwtintv_t *__restrict__ mems, int32_t cap, int32_t *__restrict__ n_mems)
+                         bsw_bwtintv_t *__restrict__ mems, int32_t cap, int32_t *__restrict__ n_mems,
+                         uint4 *lds)
 {
     const int r = n0 + t;                                    // read index
     Lane<U, S> L;
+    L.lds = lds;
     L.q = reads + read_off[r];
     L.len = read_len[r];
     // [slot][read]: a wave's lanes at the same slot touch one contiguous run (a [read][slot] layout,
@@ -661,9 +699,12 @@ __global__ BSW_SMEM_LB void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
                                                   bsw_bwtintv_t *__restrict__ mems, int32_t cap,
                                                   int32_t *__restrict__ n_mems, int32_t *__restrict__ err)
 {
+    static_assert(kSmemBlock == 64 || kSmemLds == 0, "LDS vector slots assume one wave per workgroup");
+    __shared__ uint4 s_vec[kSmemLds > 0 ? 2 * kSmemLds * 64 : 1];
     const int t = blockIdx.x * blockDim.x + threadIdx.x;    // lane within this chunk
     if (t >= n) return;
-    const int e = smem_read(f, opt, reads, read_off, read_len, n0, n, t, scratch, scap, mems, cap, n_mems);
+    const int e = smem_read(f, opt, reads, read_off, read_len, n0, n, t, scratch, scap, mems, cap, n_mems,
+                            kSmemLds > 0 ? s_vec + (threadIdx.x & 63) : nullptr);
     if (e) atomicOr(err, e);
 }
 
