@@ -317,6 +317,9 @@ __device__ __forceinline__ EntT<uint64_t> ent_get(const EntP *p)
 #ifndef BSW_SMEM_LDS
 #define BSW_SMEM_LDS 4
 #endif
+#ifndef BSW_SMEM_VIRT
+#define BSW_SMEM_VIRT 1          // 0: every interval-vector entry stored (smem1's virtual entries off)
+#endif
 constexpr int kSmemLds = BSW_SMEM_LDS;
 
 template <class U, class S = EntT<U>>
@@ -396,6 +399,26 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
     U ikend = (U)(x + 1);
     int nc = 0, i;
     const bool text = f.text && min_intv <= 1;
+    // Virtual entries: an entry whose string the next sweep step extends from the k-mer table
+    // (extension length b = pe - i <= kt at the reading step i) needs none of its (k, l, s) -- the
+    // table entry of q[i, pe) comes from the read's 2-bit window -- and is never output (its length
+    // b - 1 < keep_len), so it is kept as bit b of a per-vector mask instead of a 16-B entry.  The
+    // vectors are ordered by descending pe in sweep order, so the stored entries are exactly the
+    // leading ones (b > vmax) and the mask holds the tail.  0 = off (no table, or keep_len < kt).
+    const int vmax = (BSW_SMEM_VIRT && keep_len >= f.kt) ? f.kt : 0;
+    uint32_t vmask = 0;                                    // forward entries, bit b: pe = x - 1 + b
+    int nf = 0;                                           // forward entries stored
+    auto fpush = [&](U e) {
+        const int b = (int)((uint32_t)e & ~kTextFlag) - (x - 1);
+        if (b <= vmax) {
+            vmask |= 1u << b;
+        } else {
+            if (nf < L.scap) vput(L, curr, nf, EntT<U>{ik.k, ik.l, ik.s, e});
+            else L.overflow = 1;
+            ++nf;
+        }
+        ++nc;
+    };
 #if BSW_SMEM_KPF
     KPre<U> pre;
     pre.init(f, q, x, len);
@@ -415,11 +438,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
             const int e = i + match_run(f.text, (uint64_t)p + (uint64_t)(i - x), q + i, len - i);
             ik.k = p;
             ikend = (U)((uint32_t)e | kTextFlag);
-            if (e < len) {
-                if (nc < L.scap) vput(L, curr, nc, EntT<U>{ik.k, ik.l, ik.s, ikend});
-                else L.overflow = 1;
-                ++nc;
-            }
+            if (e < len) fpush(ikend);
             i = e;
             break;
         }
@@ -435,27 +454,21 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
             const IvT<U> ok = i + 1 - x <= f.kt ? ktab_get(f, i + 1 - x, code) : forward_ext(f, ik, qi);
 #endif
             if (ok.s != ik.s) {
-                if (nc < L.scap) vput(L, curr, nc, EntT<U>{ik.k, ik.l, ik.s, ikend});
-                else L.overflow = 1;
-                ++nc;
+                fpush(ikend);
                 if (ok.s < min_intv) break;
             }
             ik = ok; ikend = (U)(i + 1);
         } else {
-            if (nc < L.scap) vput(L, curr, nc, EntT<U>{ik.k, ik.l, ik.s, ikend});
-            else L.overflow = 1;
-            ++nc;
+            fpush(ikend);
             break;
         }
     }
-    if (i == len) {
-        if (nc < L.scap) vput(L, curr, nc, EntT<U>{ik.k, ik.l, ik.s, ikend});
-        else L.overflow = 1;
-        ++nc;
-    }
-    nc = min(nc, L.scap);
-    // upstream reverses curr (longest matches first); here prev is read back to front once
-    const int ret = (int)((uint32_t)vget(L, curr, nc - 1).e & ~kTextFlag);
+    if (i == len) fpush(ikend);
+    nf = min(nf, L.scap);
+    // upstream reverses curr (longest matches first); here prev is read back to front once.  The
+    // longest match is the last stored entry, or the mask's highest bit when none is stored
+    const int ret = nf > 0 ? (int)((uint32_t)vget(L, curr, nf - 1).e & ~kTextFlag)
+                           : x - 1 + (31 - __builtin_clz(vmask));
     if (prune && ret - x < keep_len) {
         // b_min: extend q[x] to the left while it keeps >= min_intv occurrences; stop as soon as
         // the bound reaches keep_len (then the sweep must run)
@@ -475,7 +488,8 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
         if (ret - b < keep_len) return ret;
     }
     { const int t = curr; curr = prev; prev = t; }
-    int np = nc;
+    int np = nf;                                          // prev: stored entries, then the mask
+    uint32_t pmask = vmask;                               // bit b: pe = i + b at the reading step i
     bool rev = true;
     int nmem = 0;
     uint32_t last_start = 0;
@@ -483,6 +497,8 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
         const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
         win = win >> 2 | (uint64_t)(c & 3) << 62;      // q[i, i + 32)
         nc = 0;
+        int ncf = 0;                                      // curr entries stored
+        uint32_t cmask = 0;                               // curr entries virtual (bit pe - i + 1)
         U last_cs = 0;
         // the entries' extensions are independent loads: compute kBackUnroll of them before
         // their (sequential, order-dependent) bookkeeping, so a lane has that many block loads in
@@ -501,6 +517,38 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
             }
             return ok;
         };
+        // bwt_smem1a's per-entry bookkeeping, in vector order (stored entries, then virtual ones)
+        auto book = [&](const EntT<U> &pv, const IvT<U> &ok) {
+            const bool tm = ((uint32_t)pv.e & kTextFlag) != 0;   // text mode: pv.k = text position
+            const uint32_t pe = (uint32_t)pv.e & ~kTextFlag;
+            if (c < 0 || ok.s < min_intv) {
+                if (nc == 0) {
+                    if (nmem == 0 || (uint32_t)(i + 1) < last_start) {
+                        last_start = (uint32_t)(i + 1);
+                        ++nmem;
+                        if ((int)(pe - last_start) >= keep_len)   // (never a virtual entry)
+                            push_out(L, tm ? text_intv(f, pv.k, (int)(pe - last_start)) : IvT<U>{pv.k, pv.l, pv.s},
+                                     last_start, pe);
+                    }
+                }
+            } else if (nc == 0 || ok.s != last_cs) {
+                const int b = (int)pe - i + 1;                 // its extension length at step i - 1
+                if (b <= vmax) {
+                    cmask |= 1u << b;
+                } else {
+                    // an interval down to one occurrence continues in text mode (one SA load now,
+                    // then cached text reads instead of occurrence blocks)
+                    const bool to_text = f.text && ok.s == 1;
+                    const U k2 = tm ? ok.k : (to_text ? f.sa[ok.k] : ok.k);
+                    if (ncf < L.scap)
+                        vput(L, curr, ncf, EntT<U>{k2, ok.l, ok.s, (U)(pe | ((tm || to_text) ? kTextFlag : 0u))});
+                    else L.overflow = 1;
+                    ++ncf;
+                }
+                ++nc;
+                last_cs = ok.s;
+            }
+        };
         for (int j0 = 0; j0 < np; j0 += kBackUnroll) {
           EntT<U> pvs[kBackUnroll];
           IvT<U> oks[kBackUnroll];
@@ -514,35 +562,29 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
 #pragma unroll
           for (int u = 0; u < kBackUnroll; ++u) {
             if (j0 + u >= np) break;
-            const EntT<U> pv = pvs[u];
-            const IvT<U> ok = oks[u];
-            const bool tm = ((uint32_t)pv.e & kTextFlag) != 0;   // text mode: pv.k = text position
-            const uint32_t pe = (uint32_t)pv.e & ~kTextFlag;
-            if (c < 0 || ok.s < min_intv) {
-                if (nc == 0) {
-                    if (nmem == 0 || (uint32_t)(i + 1) < last_start) {
-                        last_start = (uint32_t)(i + 1);
-                        ++nmem;
-                        if ((int)(pe - last_start) >= keep_len)
-                            push_out(L, tm ? text_intv(f, pv.k, (int)(pe - last_start)) : IvT<U>{pv.k, pv.l, pv.s},
-                                     last_start, pe);
-                    }
-                }
-            } else if (nc == 0 || ok.s != last_cs) {
-                // an interval down to one occurrence continues in text mode (one SA load now,
-                // then cached text reads instead of occurrence blocks)
-                const bool to_text = f.text && ok.s == 1;
-                const U k2 = tm ? ok.k : (to_text ? f.sa[ok.k] : ok.k);
-                if (nc < L.scap)
-                    vput(L, curr, nc, EntT<U>{k2, ok.l, ok.s, (U)(pe | ((tm || to_text) ? kTextFlag : 0u))});
-                else L.overflow = 1;
-                ++nc;
-                last_cs = ok.s;
-            }
+            book(pvs[u], oks[u]);
+          }
+        }
+        for (uint32_t mm = pmask; mm != 0;) {             // the virtual entries, longest first
+          int bs[kBackUnroll];
+          IvT<U> oks[kBackUnroll];
+#pragma unroll
+          for (int u = 0; u < kBackUnroll; ++u) {
+              bs[u] = mm ? 31 - __builtin_clz(mm) : 0;
+              mm &= ~(1u << bs[u]);
+          }
+#pragma unroll
+          for (int u = 0; u < kBackUnroll; ++u)
+              oks[u] = (c >= 0 && bs[u] > 0) ? ktab_get(f, bs[u], win >> (64 - 2 * bs[u])) : IvT<U>{0, 0, 0};
+#pragma unroll
+          for (int u = 0; u < kBackUnroll; ++u) {
+            if (bs[u] == 0) break;
+            book(EntT<U>{0, 0, 0, (U)(i + bs[u])}, oks[u]);
           }
         }
         if (nc == 0) break;
-        np = min(nc, L.scap);
+        np = min(ncf, L.scap);
+        pmask = cmask;
         rev = false;
         { const int t = curr; curr = prev; prev = t; }
     }
