@@ -54,6 +54,10 @@ struct FmiDevT {                     // kernel view of the resident index (U = r
     // significant); 16 B per entry (ktab_get)
     const uint4 *ktab;
     int kt;
+    // the same levels' counts s alone, 4 B per entry (null: off) -- the sweeps' virtual entries
+    // need only s, and a level's 4-B form is 4x denser in the caches (levels <= 12 of a 3 Gb
+    // genome: 89 MB)
+    const uint32_t *stab;
 };
 
 // text-mode interval entries keep the occurrence's text position in k; their end carries this
@@ -64,6 +68,10 @@ constexpr uint32_t kTextFlag = 0x80000000u;
 #define BSW_SMEM_BACK_UNROLL 2
 #endif
 constexpr int kBackUnroll = BSW_SMEM_BACK_UNROLL;   // backward sweep: entries extended together
+#ifndef BSW_SMEM_VIRT_UNROLL
+#define BSW_SMEM_VIRT_UNROLL BSW_SMEM_BACK_UNROLL
+#endif
+constexpr int kVirtUnroll = BSW_SMEM_VIRT_UNROLL;   // the same for the virtual entries' table loads
 
 struct MemOpt {
     int32_t min_seed_len, split_width, max_mem_intv, split_len;
@@ -480,7 +488,9 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
             if (c > 3) break;
             const int m = x + 2 - b;                     // length of q[b - 1, x]
             if (m <= f.kt) bcode |= (uint64_t)c << (2 * (m - 1));   // (kt <= 15: the shift stays < 64)
-            const IvT<U> ok = m <= f.kt ? ktab_get(f, m, bcode) : backward_ext(f, bk, c);
+            // (only s matters below kt: bk is extended by blocks only once m > kt)
+            const IvT<U> ok = (m < f.kt && f.stab) ? IvT<U>{0, 0, (U)f.stab[ktab_off(m) + bcode]}
+                              : m <= f.kt ? ktab_get(f, m, bcode) : backward_ext(f, bk, c);
             if (ok.s < min_intv) break;
             bk = ok;
             --b;
@@ -566,18 +576,23 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
           }
         }
         for (uint32_t mm = pmask; mm != 0;) {             // the virtual entries, longest first
-          int bs[kBackUnroll];
-          IvT<U> oks[kBackUnroll];
+          int bs[kVirtUnroll];
+          IvT<U> oks[kVirtUnroll];
 #pragma unroll
-          for (int u = 0; u < kBackUnroll; ++u) {
+          for (int u = 0; u < kVirtUnroll; ++u) {
               bs[u] = mm ? 31 - __builtin_clz(mm) : 0;
               mm &= ~(1u << bs[u]);
           }
 #pragma unroll
-          for (int u = 0; u < kBackUnroll; ++u)
-              oks[u] = (c >= 0 && bs[u] > 0) ? ktab_get(f, bs[u], win >> (64 - 2 * bs[u])) : IvT<U>{0, 0, 0};
+          for (int u = 0; u < kVirtUnroll; ++u)
+              // below vmax the extension stays virtual (only its s matters): the counts-only table
+              oks[u] = (c >= 0 && bs[u] > 0)
+                           ? ((bs[u] < vmax && f.stab)
+                                  ? IvT<U>{0, 0, (U)f.stab[ktab_off(bs[u]) + (win >> (64 - 2 * bs[u]))]}
+                                  : ktab_get(f, bs[u], win >> (64 - 2 * bs[u])))
+                           : IvT<U>{0, 0, 0};
 #pragma unroll
-          for (int u = 0; u < kBackUnroll; ++u) {
+          for (int u = 0; u < kVirtUnroll; ++u) {
             if (bs[u] == 0) break;
             book(EntT<U>{0, 0, 0, (U)(i + bs[u])}, oks[u]);
           }
@@ -776,6 +791,13 @@ __global__ void ktab_kernel(const FmiDevT<U> f, int j, uint4 *__restrict__ tab)
     }
 }
 
+// the k-mer table's counts alone (s < 2^32: the host checks the single-base counts), grid-stride
+__global__ void stab_kernel(const uint4 *__restrict__ tab, uint64_t ents, uint32_t *__restrict__ stab)
+{
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ents; c += (uint64_t)gridDim.x * blockDim.x)
+        stab[c] = tab[c].z;
+}
+
 template <class S>
 __global__ void sa_kernel(const S *__restrict__ sa, uint64_t nrows, const uint64_t *__restrict__ k, int64_t n,
                           int64_t *__restrict__ pos)
@@ -877,6 +899,7 @@ struct bsw_fmi {
     uint8_t *d_text = nullptr;                // text mode: T + 64 bytes of 0xFF padding
     void *d_isa = nullptr;                    // text mode: SA^-1 (uint32_t or uint64_t)
     uint4 *d_ktab = nullptr;                  // k-mer interval table (levels 1 .. kt)
+    uint32_t *d_stab = nullptr;               // its counts s alone (FmiDevT::stab)
     int kt = 0;
     std::vector<uint32_t> sa;                 // host-built index: host copies (tests, bwt_sa)
     std::vector<FmiBlock> h_blk;              // host-only index (device < 0): the occurrence blocks
@@ -1070,6 +1093,25 @@ int build_ktab(bsw_fmi_t *f, FmiDevT<U> &dv)
     dv.kt = kt;
     f->kt = kt;
     f->dev_bytes += (int64_t)(ents * sizeof(uint4));
+    // the counts-only copy (BSW_FMI_STAB=0: off) when every count fits 32 bits: the largest is a
+    // single base's (~1.8e9 at 3 Gb)
+    int64_t smax = 0;
+    for (int c = 0; c < 4; ++c) smax = std::max(smax, f->count[c + 1] - f->count[c]);
+    const char *se = getenv("BSW_FMI_STAB");
+    if ((se == nullptr || atoi(se) != 0) && smax < ((int64_t)1 << 32)) {
+        if (hipMalloc(&f->d_stab, ents * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            f->d_stab = nullptr;                       // optional: the walks use the full entries
+            return BSW_OK;
+        }
+        const unsigned grid = (unsigned)std::min<uint64_t>(1u << 16, (ents + 255) / 256);
+        hipLaunchKernelGGL(stab_kernel, dim3(grid), dim3(256), 0, f->stream, f->d_ktab, (uint64_t)ents, f->d_stab);
+        rc = hip_rc(hipGetLastError());
+        if (!rc) rc = hip_rc(hipStreamSynchronize(f->stream));
+        if (rc) return rc;
+        dv.stab = f->d_stab;
+        f->dev_bytes += (int64_t)(ents * sizeof(uint32_t));
+    }
     return BSW_OK;
 }
 
@@ -1222,6 +1264,7 @@ void bsw_fmi_destroy(bsw_fmi_t *f)
     if (f->d_text) (void)hipFree(f->d_text);
     if (f->d_isa) (void)hipFree(f->d_isa);
     if (f->d_ktab) (void)hipFree(f->d_ktab);
+    if (f->d_stab) (void)hipFree(f->d_stab);
     if (f->d_err) (void)hipFree(f->d_err);
     if (f->d_scratch) (void)hipFree(f->d_scratch);
     if (f->ev0) (void)hipEventDestroy(f->ev0);
