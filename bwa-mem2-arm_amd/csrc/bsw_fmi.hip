@@ -329,12 +329,22 @@ __device__ __forceinline__ EntT<uint64_t> ent_get(const EntP *p)
 #define BSW_SMEM_VIRT 1          // 0: every interval-vector entry stored (smem1's virtual entries off)
 #endif
 constexpr int kSmemLds = BSW_SMEM_LDS;
+// the narrow (32-bit) index's walk: no LDS slots and 5 waves per SIMD (16 Mb, with virtual entries:
+// 74.4 vs 71.1 M reads/s without the slots, 73.2 at 5 waves, profiles/r05/smem_virtual_entries_ab.txt)
+#ifndef BSW_SMEM_LDS_NARROW
+#define BSW_SMEM_LDS_NARROW 0
+#endif
+#ifndef BSW_SMEM_WAVES_NARROW
+#define BSW_SMEM_WAVES_NARROW 5
+#endif
+template <class U, class S>
+constexpr int lds_slots() { return sizeof(S) != 16 ? 0 : sizeof(U) == 8 ? kSmemLds : BSW_SMEM_LDS_NARROW; }
 
 template <class U, class S = EntT<U>>
 struct Lane {
     const uint8_t *q;
     int len;
-    uint4 *lds;              // this lane's LDS slots: [v][j] at lds[(v * kSmemLds + j) * 64] (or nullptr)
+    uint4 *lds;              // this lane's LDS slots: [v][j] at lds[(v * K + j) * 64], K = lds_slots (or nullptr)
     S *sa, *sb;              // scratch vectors, element j at [j * stride]
     size_t stride;
     int scap;                // scratch entries per vector
@@ -360,11 +370,12 @@ __device__ __forceinline__ void push_out(Lane<U, S> &L, IvT<U> v, uint32_t start
 template <class U, class S>
 __device__ __forceinline__ void vput(Lane<U, S> &L, int v, int j, const EntT<U> &e)
 {
-    if constexpr (kSmemLds > 0 && sizeof(S) == 16) {
-        if (j < kSmemLds) {
+    constexpr int K = lds_slots<U, S>();
+    if constexpr (K > 0) {
+        if (j < K) {
             S t;
             ent_put(&t, e);
-            L.lds[(v * kSmemLds + j) * 64] = *reinterpret_cast<const uint4 *>(&t);
+            L.lds[(v * K + j) * 64] = *reinterpret_cast<const uint4 *>(&t);
             return;
         }
     }
@@ -373,10 +384,11 @@ __device__ __forceinline__ void vput(Lane<U, S> &L, int v, int j, const EntT<U> 
 template <class U, class S>
 __device__ __forceinline__ EntT<U> vget(const Lane<U, S> &L, int v, int j)
 {
-    if constexpr (kSmemLds > 0 && sizeof(S) == 16) {
-        if (j < kSmemLds) {
+    constexpr int K = lds_slots<U, S>();
+    if constexpr (K > 0) {
+        if (j < K) {
             S t;
-            *reinterpret_cast<uint4 *>(&t) = L.lds[(v * kSmemLds + j) * 64];
+            *reinterpret_cast<uint4 *>(&t) = L.lds[(v * K + j) * 64];
             return ent_get(&t);
         }
     }
@@ -746,7 +758,7 @@ template <class U, class S>
 #if BSW_SMEM_WAVES > 0
 #define BSW_SMEM_LB __launch_bounds__(kSmemBlock, BSW_SMEM_WAVES)
 #else
-#define BSW_SMEM_LB __launch_bounds__(kSmemBlock)
+#define BSW_SMEM_LB __launch_bounds__(kSmemBlock, sizeof(U) == 4 ? BSW_SMEM_WAVES_NARROW : 1)
 #endif
 __global__ BSW_SMEM_LB void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
                                                   const uint8_t *__restrict__ reads,
@@ -756,12 +768,13 @@ __global__ BSW_SMEM_LB void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
                                                   bsw_bwtintv_t *__restrict__ mems, int32_t cap,
                                                   int32_t *__restrict__ n_mems, int32_t *__restrict__ err)
 {
-    static_assert(kSmemBlock == 64 || kSmemLds == 0, "LDS vector slots assume one wave per workgroup");
-    __shared__ uint4 s_vec[kSmemLds > 0 ? 2 * kSmemLds * 64 : 1];
+    constexpr int K = lds_slots<U, S>();
+    static_assert(kSmemBlock == 64 || K == 0, "LDS vector slots assume one wave per workgroup");
+    __shared__ uint4 s_vec[K > 0 ? 2 * K * 64 : 1];
     const int t = blockIdx.x * blockDim.x + threadIdx.x;    // lane within this chunk
     if (t >= n) return;
     const int e = smem_read(f, opt, reads, read_off, read_len, n0, n, t, scratch, scap, mems, cap, n_mems,
-                            kSmemLds > 0 ? s_vec + (threadIdx.x & 63) : nullptr);
+                            K > 0 ? s_vec + (threadIdx.x & 63) : nullptr);
     if (e) atomicOr(err, e);
 }
 
