@@ -238,13 +238,23 @@ struct KPre {
     uint32_t nm;                 // bit t: q[x + t] is N, or x + t >= len
     int P;                       // lengths 1 .. P are table-served: N-free, <= kt
     int m;                       // the length the next take() returns
+    bool so;                     // lengths < P load the count alone (FmiDevT::stab)
+    bool part;                   // the last take() returned a count alone (k, l unset)
     uint4 e0, e1;                // entries of lengths m, m + 1
     __device__ __forceinline__ int base(int t) const { return (nm >> t & 1) ? 4 : (int)(pw >> (30 - 2 * t) & 3); }
     __device__ __forceinline__ uint4 load(const FmiDevT<U> &f, int len) const
     {
+        if (len < P && so) return uint4{0, 0, f.stab[ktab_off(len) + (pw >> (32 - 2 * len))], 0};
         return len <= P ? f.ktab[ktab_off(len) + (pw >> (32 - 2 * len))] : uint4{0, 0, 0, 0};
     }
-    __device__ __forceinline__ void init(const FmiDevT<U> &f, const uint8_t *q, int x, int len)
+    // the full interval of q[x, x + len) (len <= P), for a walk that needs k of a count-only entry
+    __device__ __forceinline__ IvT<U> full(const FmiDevT<U> &f, int len) const
+    {
+        return ktab_get(f, len, (uint64_t)(pw >> (32 - 2 * len)));
+    }
+    // sonly: the caller needs k, l of a table-served walk entry only at length P (its last, which
+    // forward_ext continues from and which the sweeps store) or through full()
+    __device__ __forceinline__ void init(const FmiDevT<U> &f, const uint8_t *q, int x, int len, bool sonly = false)
     {
         const int nb = min(16, len - x);                         // >= 1
         const uintptr_t a = (uintptr_t)(q + x);
@@ -268,6 +278,8 @@ struct KPre {
             }
         }
         P = min(f.kt, (int)__builtin_ctz(nm | 0x10000u));
+        so = sonly && f.stab != nullptr;
+        part = false;
         m = 2;
         e0 = load(f, 2);
         e1 = load(f, 3);
@@ -276,6 +288,7 @@ struct KPre {
     __device__ __forceinline__ IvT<U> take(const FmiDevT<U> &f)
     {
         const uint4 e = e0;
+        part = m < P && so;
         e0 = e1;
         e1 = load(f, m + 2);
         ++m;
@@ -416,6 +429,7 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
     if (min_intv < 1) min_intv = 1;
     int curr = 0, prev = 1;                               // vector ids (vput / vget)
     IvT<U> ik = set_intv(f, qx);
+    bool ik_part = false;                                 // ik holds its count alone (KPre::part)
     U ikend = (U)(x + 1);
     int nc = 0, i;
     const bool text = f.text && min_intv <= 1;
@@ -440,8 +454,10 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
         ++nc;
     };
 #if BSW_SMEM_KPF
+    // with virtual entries every forward push shorter than kt is virtual (s alone matters), so the
+    // table loads below P fetch counts only; k, l come from the full table at P or on demand
     KPre<U> pre;
-    pre.init(f, q, x, len);
+    pre.init(f, q, x, len, vmax > 0);
     uint64_t win = (uint64_t)pre.pw << 32;              // q[x, x + 16), q[x] in bits 63:62 (the sweep)
 #else
     // q[x, i) as a base-4 code (table lookups while i + 1 - x <= kt) and as a 2-bit window with
@@ -454,6 +470,9 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
             // text after it, and the first step that does not (mismatch, read N, text end) pushes
             // ik and stops -- so compare read and text directly, then push ik as a text-mode
             // entry (its k, l are only needed if it is output)
+#if BSW_SMEM_KPF
+            if (ik_part) ik = pre.full(f, i - x);           // a count-only table entry: its k
+#endif
             const U p = f.sa[ik.k];
             const int e = i + match_run(f.text, (uint64_t)p + (uint64_t)(i - x), q + i, len - i);
             ik.k = p;
@@ -465,19 +484,22 @@ __device__ int smem1(const FmiDevT<U> &f, Lane<U, S> &L, int x, U min_intv, int 
 #if BSW_SMEM_KPF
         const int qi = i - x < 16 ? pre.base(i - x) : q[i];
         if (qi < 4) {
-            const IvT<U> ok = i + 1 - x <= pre.P ? pre.take(f) : forward_ext(f, ik, qi);
+            const bool tk = i + 1 - x <= pre.P;
+            const IvT<U> ok = tk ? pre.take(f) : forward_ext(f, ik, qi);
+            const bool ok_part = tk && pre.part;
 #else
         const int qi = q[i];
         if (qi < 4) {
             code = code << 2 | (uint64_t)qi;
             if (i - x < 32) win |= (uint64_t)qi << (62 - 2 * (i - x));
             const IvT<U> ok = i + 1 - x <= f.kt ? ktab_get(f, i + 1 - x, code) : forward_ext(f, ik, qi);
+            const bool ok_part = false;
 #endif
             if (ok.s != ik.s) {
                 fpush(ikend);
                 if (ok.s < min_intv) break;
             }
-            ik = ok; ikend = (U)(i + 1);
+            ik = ok; ik_part = ok_part; ikend = (U)(i + 1);
         } else {
             fpush(ikend);
             break;
@@ -626,9 +648,11 @@ __device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U, S> &L, int x, int min
     const int qx = q[x];
     if (qx > 3) return x + 1;
     IvT<U> ik = set_intv(f, qx);
+    bool ik_part = false;                                 // ik holds its count alone (KPre::part)
 #if BSW_SMEM_KPF
+    // outputs are >= min_len > kt bases long: below P the walk needs counts only
     KPre<U> pre;
-    pre.init(f, q, x, L.len);
+    pre.init(f, q, x, L.len, min_len > f.kt);
 #else
     uint64_t code = (uint64_t)qx;                        // q[x, i) as a base-4 code
 #endif
@@ -643,6 +667,9 @@ __device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U, S> &L, int x, int min
             while (t < lim && q[t] < 4) ++t;                 // first N in [i, is]
             if (t < lim) return t + 1;
             if (is >= L.len) return L.len;
+#if BSW_SMEM_KPF
+            if (ik_part) ik = pre.full(f, i - x);           // a count-only table entry: its k
+#endif
             const U p = f.sa[ik.k];
             if (match_run(f.text, (uint64_t)p + (uint64_t)(i - x), q + i, is + 1 - i) == is + 1 - i)
                 push_out(L, text_intv(f, p, is + 1 - x), (uint32_t)x, (uint32_t)(is + 1));
@@ -651,18 +678,22 @@ __device__ int seed_strategy1(const FmiDevT<U> &f, Lane<U, S> &L, int x, int min
 #if BSW_SMEM_KPF
         const int qi = i - x < 16 ? pre.base(i - x) : q[i];
         if (qi < 4) {
-            const IvT<U> ok = i + 1 - x <= pre.P ? pre.take(f) : forward_ext(f, ik, qi);
+            const bool tk = i + 1 - x <= pre.P;
+            const IvT<U> ok = tk ? pre.take(f) : forward_ext(f, ik, qi);
+            const bool ok_part = tk && pre.part;
 #else
         const int qi = q[i];
         if (qi < 4) {
             code = code << 2 | (uint64_t)qi;
             const IvT<U> ok = i + 1 - x <= f.kt ? ktab_get(f, i + 1 - x, code) : forward_ext(f, ik, qi);
+            const bool ok_part = false;
 #endif
             if (ok.s < max_intv && i - x >= min_len) {
                 if (ok.s > 0) push_out(L, ok, (uint32_t)x, (uint32_t)(i + 1));
                 return i + 1;
             }
             ik = ok;
+            ik_part = ok_part;
         } else {
             return i + 1;
         }
