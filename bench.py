@@ -590,6 +590,10 @@ def rccl_group(world):
     to = datetime.timedelta(seconds=120)
     if world > 1:
         return dist.new_group(backend="nccl", timeout=to)
+    if not dist.is_initialized() and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") and os.environ.get("MASTER_PORT"):
+        # one rank under torchrun: its tcp:// store would be a client of the agent's store, so take
+        # torchrun's rendezvous (env://) instead of a private port
+        dist.init_process_group("nccl", rank=0, world_size=1, timeout=to)
     if not dist.is_initialized():
         import socket
         s = socket.socket()
