@@ -64,12 +64,16 @@ struct FmiDevT {                     // kernel view of the resident index (U = r
 // flag (k, l are resolved through SA^-1 only when the interval is output)
 constexpr uint32_t kTextFlag = 0x80000000u;
 
+// backward sweep: stored entries extended together.  1 since the virtual entries: the stored part of a
+// vector is mostly one or two long entries, and a batch pads with duplicate extensions of its last entry
+// (random block loads for nothing): C4 at 3 Gb 221.5 -> 208.0 ms per step at 1, 264.7 at 3
+// (profiles/r05/smem_virtual_entries_ab.txt)
 #ifndef BSW_SMEM_BACK_UNROLL
-#define BSW_SMEM_BACK_UNROLL 2
+#define BSW_SMEM_BACK_UNROLL 1
 #endif
-constexpr int kBackUnroll = BSW_SMEM_BACK_UNROLL;   // backward sweep: entries extended together
+constexpr int kBackUnroll = BSW_SMEM_BACK_UNROLL;
 #ifndef BSW_SMEM_VIRT_UNROLL
-#define BSW_SMEM_VIRT_UNROLL BSW_SMEM_BACK_UNROLL
+#define BSW_SMEM_VIRT_UNROLL 2
 #endif
 constexpr int kVirtUnroll = BSW_SMEM_VIRT_UNROLL;   // the same for the virtual entries' table loads
 
