@@ -354,6 +354,11 @@ constexpr int kSmemLds = BSW_SMEM_LDS;
 #ifndef BSW_SMEM_WAVES_NARROW
 #define BSW_SMEM_WAVES_NARROW 5
 #endif
+// the wide (64-bit) walk at 5 waves too since its stored extensions go one at a time (96 VGPRs, 4
+// spilled; LDS 5 x 4 x 8 KB = the CU's 160 KB): C4 207.4 / 207.9 -> 204.2 / 204.9 ms per step
+#ifndef BSW_SMEM_WAVES_WIDE
+#define BSW_SMEM_WAVES_WIDE 5
+#endif
 template <class U, class S>
 constexpr int lds_slots() { return sizeof(S) != 16 ? 0 : sizeof(U) == 8 ? kSmemLds : BSW_SMEM_LDS_NARROW; }
 
@@ -793,7 +798,7 @@ template <class U, class S>
 #if BSW_SMEM_WAVES > 0
 #define BSW_SMEM_LB __launch_bounds__(kSmemBlock, BSW_SMEM_WAVES)
 #else
-#define BSW_SMEM_LB __launch_bounds__(kSmemBlock, sizeof(U) == 4 ? BSW_SMEM_WAVES_NARROW : 1)
+#define BSW_SMEM_LB __launch_bounds__(kSmemBlock, sizeof(U) == 4 ? BSW_SMEM_WAVES_NARROW : BSW_SMEM_WAVES_WIDE)
 #endif
 __global__ BSW_SMEM_LB void smem_kernel(const FmiDevT<U> f, const MemOpt opt,
                                                   const uint8_t *__restrict__ reads,
