@@ -17,7 +17,7 @@ SHIMTEST := $(LIBDIR)/bsw_shim_example
 ORACLE   := oracle/liboracle.so
 
 HIP_SRCS := $(CSRC)/bsw_kernels.hip $(CSRC)/bsw_pc.hip $(CSRC)/bsw_wv.hip $(CSRC)/bsw_gq.hip $(CSRC)/bsw_mate.hip $(CSRC)/bsw_global.hip $(CSRC)/bsw_ext_dev.hip $(CSRC)/bsw_fmi.hip $(CSRC)/bsw_fmi_build.hip $(CSRC)/bsw_memchain.hip $(CSRC)/bsw_chain.hip $(CSRC)/bsw_host.cpp $(CSRC)/bsw_ext.cpp $(CSRC)/bsw_pack.cpp $(CSRC)/bsw_devcache.cpp
-HIP_HDRS := $(CSRC)/bsw_pc_body.inc $(CSRC)/bsw_devcache.h $(CSRC)/bsw_pool.h $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h $(CSRC)/bsw_fmi_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h include/bsw_fmi.h
+HIP_HDRS := $(CSRC)/bsw_devcache.h $(CSRC)/bsw_pool.h $(CSRC)/bsw_kernels.h $(CSRC)/bsw_mate_k.h include/bsw_mate.h $(CSRC)/bsw_global_k.h include/bsw_global.h $(CSRC)/bsw_ext_k.h $(CSRC)/bsw_wave.h $(CSRC)/bsw_internal.h $(CSRC)/bsw_fmi_internal.h include/bsw.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_batch.h include/bsw_fmi.h
 
 all: product synth oracle percall
 

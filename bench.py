@@ -37,6 +37,7 @@ import statistics
 import sys
 import time
 
+T_START = time.perf_counter()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "bwa-mem2-arm_amd", "py"))
 
@@ -369,13 +370,17 @@ def main():
     ap.add_argument("--rccl-chunks", type=int, default=4,
                     help="RCCL C2 leg: pieces per rank (chunk k + 1 scatters while chunk k is scored)")
     ap.add_argument("--rccl-pairs", type=int, default=6_000_000,
-                    help="default C2 line at N > 1: pairs of the strong-scaling RCCL leg reported beside the weak "
-                         "value (one batch on GPU 0, RCCL scatter -> score -> RCCL gather); 0 = off")
+                    help="default C2 line at N > 1: pairs of the strong-scaling RCCL leg whose throughput is the "
+                         "line's value (one batch on GPU 0, RCCL scatter -> score -> RCCL gather; the per-rank "
+                         "resident rate is weak_value); 0 = off (the weak rate is the value)")
     ap.add_argument("--c5-reads", type=int, default=10_000_000,
                     help="default C2 line at N > 1: PE reads of the C5 sub-object (BASELINE configs[4]: the read "
                          "set resident on GPU 0, RCCL read scatter, the whole GPU front end on every rank, records "
                          "gathered); 0 = off")
     ap.add_argument("--c5-ref-mb", type=int, default=3000, help="C5 sub-object: reference size (Mb)")
+    ap.add_argument("--budget-s", type=float, default=600.0,
+                    help="N > 1: wall-clock budget of the whole run (the driver's timeout is not published); "
+                         "the C5 sub-object runs only when twice its projected time fits what is left")
     ap.add_argument("--transport", default="host", choices=("host", "rccl"),
                     help="strong: host (default) -- every rank holds its range in host memory and the call "
                          "stages it over its own PCIe link; rccl -- the whole batch resident on GPU 0, scattered "
@@ -454,12 +459,15 @@ def main():
 
     res = np.empty_like(pairs)
     d_pairs.download(res)
-    # N > 1: the strong-scaling RCCL leg beside the weak value (every rank takes part)
-    # N > 1: the strong-scaling RCCL legs beside the weak value (every rank takes part): the C2 batch
-    # scatter and C5 (BASELINE configs[4]: the PE read set over the whole front end).  Each leg's
-    # ranks agree over gloo before and after their RCCL phases, so a failing rank makes the leg
-    # report an error on every rank instead of leaving the others blocked in a collective
+    # N > 1: the HEADLINE is the RCCL batch scatter (BASELINE configs[4]): one batch resident on
+    # GPU 0, scattered over the ranks by RCCL, scored, outputs gathered back -- timed over exactly
+    # --steps steps after --warmup; the weak rate above (every rank its own resident 1M pairs, no
+    # data movement) is reported beside it as weak_value.  C5 on the whole front end follows when
+    # the run's wall-clock budget and every rank's free device memory allow it.  Each leg's ranks
+    # agree over gloo before and after their RCCL phases, so a failing rank makes the leg report
+    # an error on every rank instead of leaving the others blocked in a collective
     rccl = c5 = None
+    budget = {}
     if world > 1:
         share = f"{world} ranks share {args.distinct_gpus} GPU(s) (--rehearse): RCCL needs one GPU per rank"
         def leg(fn, *a, **k):
@@ -468,11 +476,17 @@ def main():
             except Exception as e:  # noqa: BLE001  (symmetric failures: every rank lands here)
                 return {"error": repr(e)[:400]}
         if args.rccl_pairs > 0:
-            rccl = {"skipped": share} if args.distinct_gpus < world else \
-                leg(rccl_c2_leg, args, rank, local, world, args.rccl_pairs, steps=10, warmup=2, eng=eng)
+            # ranks sharing a GPU (--rehearse) cannot form an RCCL communicator: the same leg then runs
+            # with a gloo group over host-staged buffers (every key of the real line, labelled)
+            rccl = leg(rccl_c2_leg, args, rank, local, world, args.rccl_pairs, steps=args.steps, warmup=args.warmup,
+                       eng=eng, transport="nccl" if args.distinct_gpus >= world else "gloo")
         if args.c5_reads > 0:
-            c5 = {"skipped": share} if args.distinct_gpus < world else \
-                leg(rccl_c5_leg, args, rank, local, world, args.c5_reads, args.c5_ref_mb, steps=5, warmup=1)
+            if args.distinct_gpus < world:
+                c5 = {"skipped": share}
+            else:
+                why, budget = c5_guard(args, rank, world)
+                c5 = {"skipped": why, "budget": budget} if why else \
+                    leg(rccl_c5_leg, args, rank, local, world, args.c5_reads, args.c5_ref_mb, steps=5, warmup=1)
     if rank != 0:
         return
     total_pairs = args.pairs * world * args.steps
@@ -535,8 +549,8 @@ def main():
         e0.close()
     if args.distinct_gpus < world:
         out["rehearsal"] = f"{world} ranks on {args.distinct_gpus} GPU(s): not a scaling measurement"
-    if rccl is not None:
-        out["rccl_strong"] = rccl
+    if world > 1:
+        out = multi_gpu_line(out, rccl, args, world)
     if c5 is not None:
         out["c5"] = dict(c5, workload=f"C5 (BASELINE configs[4]): {args.c5_reads} PE 150 bp reads vs a "
                                       f"{args.c5_ref_mb} Mb random reference, RCCL read scatter over {world} GPUs")
@@ -578,18 +592,105 @@ def main():
     print(json.dumps(out), flush=True)
 
 
-def rccl_group(world):
+def multi_gpu_line(out: dict, rccl, args, world: int) -> dict:
+    """The N > 1 line: value = the RCCL batch-scatter leg's throughput (strong scaling: one batch of
+    --rccl-pairs C2 pairs from GPU 0 over every rank, scatter + score + gather timed), with the
+    per-rank resident rate kept as weak_value / weak.  When the RCCL leg did not produce a value
+    (ranks sharing GPUs, --rccl-pairs 0, or a failure, reported in rccl_strong) the weak rate stays
+    the value and `headline` says why."""
+    weak = {k: out[k] for k in ("value", "ms_per_step", "steps", "warmup", "kernel_only_value")}
+    weak["scaling"] = "weak"
+    weak["workload"] = out["config"]["workload"]
+    if rccl is None or "value" not in rccl:
+        out["weak_value"] = out["value"]
+        out["headline"] = ("weak: every rank's own resident batch (the RCCL batch-scatter leg did not run: "
+                           f"{(rccl or {}).get('skipped') or (rccl or {}).get('error') or '--rccl-pairs 0'})")
+        if rccl is not None:
+            out["rccl_strong"] = rccl
+        return out
+    leg = dict(rccl)
+    out["weak_value"] = weak.pop("value")
+    out["weak"] = weak
+    out["value"] = leg.pop("value")
+    out["ms_per_step"] = leg.pop("ms_per_step")
+    out["steps"], out["warmup"] = leg.pop("steps"), leg.pop("warmup")
+    out["scaling"] = leg.pop("scaling")
+    out["headline"] = "rccl_strong: one batch on GPU 0, RCCL scatter -> score -> RCCL gather (weak rate in weak_value)"
+    out["config"] = dict(out["config"], workload=(
+        f"C5 batch scatter (BASELINE configs[4]): one batch of {leg['total_pairs']} C2 pairs (150 bp query / 300 bp "
+        f"ref, w={args.w}) resident on GPU 0 in the 2-bit wire form, split over {world} ranks by static band cells, "
+        f"RCCL scatter -> bsw_get_scores_packed_device -> RCCL gather of the outputs, all inside the timed region"),
+        total_pairs=leg["total_pairs"], parallelism=f"split{world} (bsw_split_by_cells; RCCL scatter + gather)")
+    out["config"].pop("pairs_per_gpu", None)
+    out["kernel_only_value"] = None                # a per-rank kernel rate: in weak
+    out["rccl_strong"] = leg
+    return out
+
+
+# Wall-clock guard of the N > 1 line's secondary legs.  The driver runs `bench.py --gpus N` under a
+# timeout it does not publish; --budget-s (default 600 s) is the assumed limit for the whole run,
+# counted from the process start (T_START).  A leg starts only if the time left covers twice its
+# projection.
+
+
+def c5_projection_s(args, world: int) -> float:
+    """Projected wall time of rccl_c5_leg (steps 5, warmup 1), from the round-6 one-rank 3 Gb run
+    (profiles/r06/c5_one_rank_3gb.json): every rank generates the reference (~6 s per Gb) and builds
+    its index on its GPU (~1 s per Gb incl. the two-strand text upload); rank 0 generates the reads
+    (~1 s per M reads); sizing + warm-up + 5 steps over 1/world of the reads each (~25 ms per M reads
+    per step on one GPU), then the one-GPU rerun of the whole set (3 x) and the record check."""
+    gb = args.c5_ref_mb / 1000.0
+    mr = args.c5_reads / 1e6
+    return 7.0 * gb + 1.0 * mr + (7 * 0.025 * mr) / world + 4 * 0.025 * mr + 0.3 * mr + 10.0
+
+
+def c5_device_bytes(args, rank: int) -> int:
+    """Device bytes rccl_c5_leg needs on a rank: the wide FM-index (~47.5 B per reference base,
+    profiles/r05: 142.6 GB at 3 Gb) + the two-strand text for extension (2 B per base) + the read
+    shard and front-end buffers; rank 0 also holds the whole read set, the gathered records and a
+    one-GPU front end over every read (~1.3 KB per read at 64 interval slots)"""
+    bases = args.c5_ref_mb * 1_000_000
+    reads = args.c5_reads
+    per_read = 1300
+    return int(49.5 * bases + per_read * reads * (2 if rank == 0 else 1) + (8 << 30))
+
+
+def c5_guard(args, rank: int, world: int):
+    """(reason to skip, budget dict) -- collective: every rank checks its free device memory, rank 0
+    the time budget; the ranks agree over gloo, so all skip or all run"""
+    free, total = hiprt.mem_get_info()
+    need = c5_device_bytes(args, rank)
+    left = args.budget_s - (time.perf_counter() - T_START)
+    proj = c5_projection_s(args, world)
+    mem_ok = free >= need
+    time_ok = left >= 2 * proj
+    ok = agree(mem_ok and time_ok, world)
+    info = {"budget_s": args.budget_s, "elapsed_s": round(time.perf_counter() - T_START, 1),
+            "projected_s": round(proj, 1), "rank0_free_device_bytes": free, "rank0_need_device_bytes": need,
+            "device_total_bytes": total}
+    if ok:
+        return None, info
+    why = []
+    if not time_ok:
+        why.append(f"projected {proj:.0f} s (x2 margin) past the {left:.0f} s left of --budget-s {args.budget_s}")
+    if not mem_ok:
+        why.append(f"rank {rank}: {free / 2**30:.1f} GiB free device memory < {need / 2**30:.1f} GiB needed")
+    return ("; ".join(why) or "another rank lacks the device memory or time for C5"), info
+
+
+def rccl_group(world, backend="nccl"):
     """The data-path process group over RCCL (torch.distributed backend "nccl" on ROCm).  World > 1:
-    a new nccl group beside the gloo control-plane group dist_init made.  World 1: a one-rank nccl
-    group of its own (RCCL still runs the scatter / gather: a one-rank communicator), so the RCCL
-    path is exercised on a one-GPU box too."""
+    a new nccl group beside the gloo control-plane group dist_init made (backend "gloo": the
+    rehearsal's stand-in when ranks share GPUs).  World 1: a one-rank nccl group of its own (RCCL
+    still runs the scatter / gather: a one-rank communicator), so the RCCL path is exercised on a
+    one-GPU box too."""
     import datetime
     import torch.distributed as dist
     # a collective that never completes (a rank that failed before it) ends the job at this
     # timeout; 120 s bounds what a broken leg costs the driver's scaling run
     to = datetime.timedelta(seconds=120)
     if world > 1:
-        return dist.new_group(backend="nccl", timeout=to)
+        return dist.new_group(backend=backend, timeout=to)
     if not dist.is_initialized() and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") and os.environ.get("MASTER_PORT"):
         # one rank under torchrun: its tcp:// store would be a client of the agent's store, so take
         # torchrun's rendezvous (env://) instead of a private port
@@ -604,7 +705,7 @@ def rccl_group(world):
     return dist.group.WORLD
 
 
-def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump=""):
+def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump="", transport="nccl"):
     """Strong scaling over RCCL (BASELINE configs[4]'s batch scatter): ONE batch of
     `total` C2 pairs generated on rank 0 and resident on GPU 0 in the engine's 2-bit wire form
     (shards.BatchScatter: contiguous ranges of equal static band cells, each cut into
@@ -617,13 +718,16 @@ def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump="
     time of the same job, and the check that the gathered outputs are identical to it).
     A rank whose scoring fails keeps taking part in every collective and the ranks agree on the
     outcome over gloo afterwards (one rank must not leave the others blocked in RCCL).
-    Returns the leg's dict on rank 0, None elsewhere."""
+    transport "gloo" (the --rehearse run, ranks sharing GPUs): the same steps with a gloo group over
+    host buffers, each piece copied to the GPU to be scored and its outputs copied back -- labelled,
+    never a scaling measurement.  Returns the leg's dict on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
     import shards
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    g = rccl_group(world)
+    g = rccl_group(world, "nccl" if transport == "nccl" else "gloo")
+    wire_dev = dev if transport == "nccl" else torch.device("cpu")
     meta_g = dist.group.WORLD if world > 1 else None
     cfg = bsw.synth_cfg(h0_hi=args.h0_hi)
     t0 = time.perf_counter()
@@ -636,7 +740,7 @@ def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump="
             err = e
     if not agree(err is None, world):
         return {"error": f"batch generation failed: {err!r}"[:400]} if rank == 0 else None
-    bs = shards.BatchScatter(rank, world, g, dev, pairs, ref, qer, w=args.w, meta_group=meta_g,
+    bs = shards.BatchScatter(rank, world, g, wire_dev, pairs, ref, qer, w=args.w, meta_group=meta_g,
                              chunks=args.rccl_chunks)
     setup_s = time.perf_counter() - t0
     own = eng is None
@@ -644,8 +748,15 @@ def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump="
         eng = bsw.Engine(device=local)
 
     def score(c, recv, row, out):
-        eng.get_scores_packed_device(recv.data_ptr(), bsw.Packed.from_row(row), args.w, args.cell_bits,
-                                     out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        if transport == "nccl":
+            eng.get_scores_packed_device(recv.data_ptr(), bsw.Packed.from_row(row), args.w, args.cell_bits,
+                                         out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+            return
+        r_d = recv.to(dev)                                   # rehearsal: host-staged piece
+        o_d = torch.empty(out.shape, dtype=out.dtype, device=dev)
+        eng.get_scores_packed_device(r_d.data_ptr(), bsw.Packed.from_row(row), args.w, args.cell_bits,
+                                     o_d.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        out.copy_(o_d.cpu())
 
     for _ in range(warmup):
         bs.step(score)
@@ -693,6 +804,8 @@ def rccl_c2_leg(args, rank, local, world, total, steps, warmup, eng=None, dump="
         "total_pairs": total, "pairs_rank0": bs.n_me, "chunks": bs.chunks,
         "wire_bytes_per_pair": round(bs.wire_bytes / total, 1), "shard_buffer_bytes": bs.S,
         "rccl_world_size": rws, "backend": dist.get_backend(g),
+        **({} if transport == "nccl" else
+           {"rehearsal": "gloo over host-staged buffers: ranks share GPUs, not a scaling measurement"}),
         "phase_ms_max_over_ranks": {k: round(v, 3) for k, v in phase.items()},
         "single_gpu_ms": round(one_ms, 3), "single_gpu_value": round(total / (one_ms * 1e-3) / 1e6, 3),
         "strong_speedup_vs_single_gpu": round(one_ms / ms, 3),

@@ -944,6 +944,7 @@ struct bsw_fmi {
     int64_t n = 0;                            // |T|
     bool wide = false;                        // 64-bit rows / counts / suffix array
     bool gpu_built = false;
+    bool plain_ent = false;                   // BSW_FMI_PLAIN_ENT: 32-B interval-vector entries always
     FmiDevT<uint32_t> dv32{};
     FmiDevT<uint64_t> dv64{};
     void *d_blk = nullptr;                    // FmiBlock (narrow) or FmiBlockW (wide)
@@ -994,8 +995,7 @@ int launch_collect(bsw_fmi_t *f, const FmiDevT<U> &dv, const MemOpt &mo, const u
     if constexpr (sizeof(U) == 8) {
         uint64_t smax = 0;
         for (int c = 0; c < 4; ++c) smax = std::max<uint64_t>(smax, (uint64_t)(f->count[c + 1] - f->count[c]));
-        packed = smax < (1ull << 32) && (uint64_t)f->n + 2 < (1ull << 40) && max_len < 32767 &&
-                 getenv("BSW_SMEM_WIDE_ENT") == nullptr;
+        packed = smax < (1ull << 32) && (uint64_t)f->n + 2 < (1ull << 40) && max_len < 32767 && !f->plain_ent;
     }
     const size_t esz = packed ? sizeof(EntP) : sizeof(EntT<U>);
     // chunk so the two scratch vectors stay within 16 GB (of 288 GB: one launch for up to ~3M
@@ -1203,7 +1203,7 @@ void bsw_mem_opt_default(bsw_mem_opt_t *opt)
 
 int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, bsw_fmi_t **out)
 {
-    if (!out || (!ref && ref_len > 0) || ref_len < 0 || (flags & ~7)) return BSW_E_INVAL;
+    if (!out || (!ref && ref_len > 0) || ref_len < 0 || (flags & ~15)) return BSW_E_INVAL;
     const bool text = !(flags & BSW_FMI_NO_TEXT);
     *out = nullptr;
     for (int64_t i = 0; i < ref_len; ++i)
@@ -1220,6 +1220,7 @@ int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, b
         const int rc = bsw::fmi_build_gpu(ref, ref_len, device, wide, &g);
         if (rc) return rc;
         bsw_fmi_t *f = new bsw_fmi_t;
+        f->plain_ent = (flags & BSW_FMI_PLAIN_ENT) != 0;
         f->device = device;
         f->n = g.n;
         f->wide = wide;
@@ -1248,6 +1249,7 @@ int bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, b
         t[n - 1 - i] = (uint8_t)(3 - ref[i]);
     }
     bsw_fmi_t *f = new bsw_fmi_t;
+    f->plain_ent = (flags & BSW_FMI_PLAIN_ENT) != 0;
     f->device = device;
     f->n = n;
     build_sa(t.data(), n, f->sa);

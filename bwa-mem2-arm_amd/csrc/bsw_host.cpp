@@ -151,19 +151,7 @@ __global__ void plan_kernel(const SeqPair *__restrict__ pairs, int32_t n, const 
             keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
                       ((uint32_t)(1 - rel) << 19) | ((uint32_t)(2047 - min(tlen, 2047)) << 8) |
                       (uint32_t)(255 - min(max(p.h0, 0), 255));
-        else if (keymode >= 3) {
-            // compact 16-bit keys (experiment, BSW_KEYMODE): class | qlen desc inside the class's
-            // 32-column bucket | related | identities desc | h0 desc, coarsened to fit 16 bits
-            const int ub = (c < kWideClass) ? 32 * ((c % kNumLaneClasses) + 1) : 255;
-            const int qd = max(0, ub - qlen);
-            const uint32_t hd = (uint32_t)(255 - min(max(p.h0, 0), 255));
-            const uint32_t k16 = keymode == 3
-                ? ((uint32_t)c << 12) | ((uint32_t)min(15, qd >> 1) << 8) | ((uint32_t)(1 - rel) << 7) |
-                      ((uint32_t)(31 - min(mt, 31)) << 2) | (hd >> 6)
-                : ((uint32_t)c << 12) | ((uint32_t)min(31, qd) << 7) | ((uint32_t)(1 - rel) << 6) |
-                      ((uint32_t)(31 - min(mt, 31)) << 1) | (hd >> 7);
-            keys[i] = k16 << 16;
-        } else
+        else
             keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) |
                       ((uint32_t)(1 - rel) << 19) | ((uint32_t)(63 - min(tlen >> 5, 63)) << 13) |
                       ((uint32_t)(31 - min(mt, 31)) << 8) | (uint32_t)(255 - min(max(p.h0, 0), 255));
@@ -202,8 +190,6 @@ struct PlanCall {
     int gq_maxq = -2, gq_maxt = 0;
     int32_t *d_out24 = nullptr;         // row-group kernel, host-checked batch: outputs as 6 x int32
                                         //   per pair here instead of into d_pairs
-    bool tput = false;                  // throughput routing: no latency kernels (row-group, small-
-                                        //   batch wave routing) -- a coalesced batch on a busy device
 };
 
 struct Slot {
@@ -220,7 +206,6 @@ struct Slot {
     int32_t *d_meta = nullptr;          // counts[kMetaCounts], maxq_wide, err
     int32_t *h_meta = nullptr;          // pinned mirror
     int2 *d_scratch = nullptr; size_t cap_scratch = 0;
-    int32_t *d_pq = nullptr; size_t cap_pq = 0;   // persistent DP kernel: head, ready, abort words
     // host-buffer pipeline: pinned staging of one chunk and its device copy
     void *h_stage = nullptr; size_t cap_stage = 0;
     uint8_t *d_stage = nullptr; size_t cap_dstage = 0;
@@ -253,11 +238,6 @@ struct Slot {
     bsw_stats_t stats{};
     hipEvent_t evm = nullptr;           // class-count readback of the last run_plan
     hipStream_t pstream = nullptr;      // high-priority stream of run_plan
-    // host pipeline (host_shard): a stream confined to a few reserved CUs for everything of a
-    // chunk but its DP (copies, unpack / plan / sort kernels, outputs' gather and readback) and one
-    // over the other CUs for the DP -- so the next chunk's preparation never waits for wave slots
-    // behind the current chunk's DP workgroups (null: not created / masking unavailable)
-    hipStream_t hstream = nullptr, dstream = nullptr;
     hipEvent_t evh = nullptr;           // inputs ready on the call's stream (pstream waits)
     hipEvent_t evd = nullptr;           // host pipeline: a chunk's DP done (its outputs' readback waits)
     PlanCall plan;                      // arguments of the last run_plan (run_dp's input)
@@ -325,27 +305,11 @@ struct DeviceCtx {
     uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
     int64_t refres_len = -1;
     std::shared_mutex refmu;            // extension calls hold it shared while they use d_refres
-    // persistent host pipeline (host_shard_pq): one call at a time per device, on a CU-masked pair
-    // of streams -- the DP grid on all but pq_nres CUs, the chunks' helper kernels on those
-    std::mutex pq_mu;
-    hipStream_t pq_h = nullptr, pq_d = nullptr;
-    int pq_nres = 0, pq_ncu = 0;
-    bool pq_failed = false;             // stream creation failed once: the general pipeline
-    hipEvent_t pq_ev[8] = {}, pq_t0 = nullptr, pq_t1 = nullptr, pq_init = nullptr;
-    hipEvent_t pq_dbg[2][64] = {};      // BSW_DEBUG_HP: per-chunk copy / publish timestamps
-    void *pq_hout = nullptr; size_t pq_hout_cap = 0;   // pinned: the call's 24-B outputs
 
     ~DeviceCtx()
     {
         for (auto &s : free_slots) release_slot(s.get());
         if (d_refres) { (void)hipSetDevice(device); (void)hipFree(d_refres); }
-        (void)hipSetDevice(device);
-        for (hipEvent_t e : pq_ev) if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : {pq_t0, pq_t1, pq_init}) if (e) (void)hipEventDestroy(e);
-        for (auto &r : pq_dbg) for (hipEvent_t e : r) if (e) (void)hipEventDestroy(e);
-        if (pq_h) (void)hipStreamDestroy(pq_h);
-        if (pq_d) (void)hipStreamDestroy(pq_d);
-        if (pq_hout) (void)hipHostFree(pq_hout);
     }
     void release_slot(Slot *s)
     {
@@ -353,7 +317,7 @@ struct DeviceCtx {
         (void)hipSetDevice(s->device);
         (void)hipFree(s->d_pairs); (void)hipFree(s->d_ref); (void)hipFree(s->d_qer);
         (void)hipFree(s->d_keys); (void)hipFree(s->d_keys2); (void)hipFree(s->d_vals); (void)hipFree(s->d_order);
-        (void)hipFree(s->d_tmp); (void)hipFree(s->d_meta); (void)hipFree(s->d_scratch); (void)hipFree(s->d_pq);
+        (void)hipFree(s->d_tmp); (void)hipFree(s->d_meta); (void)hipFree(s->d_scratch);
         (void)hipFree(s->d_stage);
         if (s->h_stage) (void)hipHostFree(s->h_stage);
         (void)hipFree(s->d_mjobs); (void)hipFree(s->d_mrows); (void)hipFree(s->d_mmeta);
@@ -373,8 +337,6 @@ struct DeviceCtx {
         if (s->evh) (void)hipEventDestroy(s->evh);
         if (s->evd) (void)hipEventDestroy(s->evd);
         if (s->pstream) (void)hipStreamDestroy(s->pstream);
-        if (s->hstream) (void)hipStreamDestroy(s->hstream);
-        if (s->dstream) (void)hipStreamDestroy(s->dstream);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         if (s->stream) (void)hipStreamDestroy(s->stream);
         for (int k = 0; k < Slot::kSide; ++k) {
@@ -403,10 +365,14 @@ struct DeviceCtx {
         // (GPU_MAX_HW_QUEUES) and serialise their kernels behind each other.  Measured (percall_bench,
         // 8 C++ callers, same box x2, profiles/r05/slot_ownq_percall.txt): 1K pairs per call without
         // coalescing 9.4-9.5 -> 10.7-11.0 M/s, 4K 30.4-30.8 -> 34.7-34.9, 10K 40.5-40.9 -> 42.1-42.5;
-        // 1M-pair host calls unchanged.  The first 16 slots of a device (BSW_SLOT_OWNQ=0: none)
-        static const bool ownq = !getenv("BSW_SLOT_OWNQ") || atoi(getenv("BSW_SLOT_OWNQ")) != 0;
+        // 1M-pair host calls unchanged.  The first 16 slots of a device.
+        // A CU-masked stream is a BLOCKING stream (hipExtStreamCreateWithCUMask takes no flags): it
+        // orders against the legacy null stream.  The library itself issues nothing on the null
+        // stream (its copies run on non-blocking streams of its own: bsw_set_reference, the FM-index
+        // build); a caller's own null-stream work waits for, and is waited on by, these slots'
+        // kernels ("Streams")
         bool made = false;
-        if (ownq && ownq_n.fetch_add(1) < 16) {
+        if (ownq_n.fetch_add(1) < 16) {
             hipDeviceProp_t pr;
             if (hipGetDeviceProperties(&pr, device) == hipSuccess && pr.multiProcessorCount > 0 &&
                 pr.multiProcessorCount <= 1024) {
@@ -417,7 +383,7 @@ struct DeviceCtx {
             }
             s->ownq = made;
             if (!made) ownq_n.fetch_sub(1);
-        } else if (ownq) {
+        } else {
             ownq_n.fetch_sub(1);
         }
         if (!made && (rc = hip_rc(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)))) return nullptr;
@@ -446,7 +412,7 @@ struct DeviceCtx {
     {
         if (rc) {
             (void)hipSetDevice(s->device);
-            for (hipStream_t st : {s->stream, s->pstream, s->hstream, s->dstream, s->run_stream, s->side[0], s->side[1],
+            for (hipStream_t st : {s->stream, s->pstream, s->run_stream, s->side[0], s->side[1],
                                    s->side[2]})
                 if (st) (void)hipStreamSynchronize(st);
         }
@@ -514,16 +480,17 @@ static void make_kparams(const bsw_params_t &p, KParams &kp)
     kp.pk_ok = ok ? 1 : 0;
     // routing / scheduling defaults; bsw_set_option changes them per context
     kp.kern8 = 1;
-    kp.keymode = getenv("BSW_KEYMODE") ? (int8_t)atoi(getenv("BSW_KEYMODE")) : 2;   // (env: experiments)
+    kp.keymode = 2;
     kp.misroute = 0;
     kp.fork = 1;
     kp.long_route = 1;
     kp.small_batch = 32768;          // 16-lane row-group form up to 32K pairs
     kp.mid_batch = 32768;
     kp.group_kernel = 1;
-    kp.busy_min = 0;                 // measured slower at every setting: off
-    kp.persist = getenv("BSW_PERSIST") ? (int8_t)std::min(2, std::max(0, atoi(getenv("BSW_PERSIST")))) : 0;
-    kp.lds_pad = getenv("BSW_PC_LDS_PAD") ? std::max(0, atoi(getenv("BSW_PC_LDS_PAD"))) : 0;   // experiment knob
+    // the row-group kernel's 32-lane latency form for batches of at most 2048 pairs: 1K calls 0.277
+    // -> 0.25 ms, 8 callers without coalescing +8%; from 4K pairs the 16-lane form's fewer
+    // instructions per cell win (percall_bench, same box, profiles/r05/gq32_percall.txt)
+    kp.gq32_max = 2048;
 }
 
 // keys / keys2 / vals / order (radix-sort buffers) grow together
@@ -560,62 +527,6 @@ static int ensure_pstream(Slot &s)
     return BSW_OK;
 }
 
-// The host pipeline's CU split (experiment knob, off by default): BSW_HP_RESERVE_CUS = n > 0 CUs,
-// spread evenly over the device (one per XCD for 8 on a 256-CU MI355X), serve the helper stream and
-// the rest the DP stream.  Measured (profiles/r04/hostpath_ab_r4j.txt): no better than the
-// high-priority helper stream for 1M-pair calls (70.8 / 73.4 vs 75.7 M/s on one box), and the
-// per-slot masked queues cost concurrent small calls a third of their rate (8 x 1K without
-// coalescing 6.4-7.4 vs 9-10 M/s): every masked stream is a hardware queue of its own.
-static int reserve_cus()
-{
-    static const int v = [] {
-        const char *e = getenv("BSW_HP_RESERVE_CUS");
-        return e ? std::max(0, atoi(e)) : 0;
-    }();
-    return v;
-}
-static void ensure_cu_streams(Slot &s)
-{
-    if (s.hstream || reserve_cus() == 0) return;
-    hipDeviceProp_t pr;
-    if (hipGetDeviceProperties(&pr, s.device) != hipSuccess) return;
-    const int ncu = pr.multiProcessorCount, nr = reserve_cus();
-    if (ncu < 2 * nr || ncu > 1024) return;
-    uint32_t hm[32] = {}, dm[32] = {};
-    const int nw = (ncu + 31) / 32;
-    for (int c = 0; c < ncu; ++c) dm[c / 32] |= 1u << (c % 32);
-    // the first nr CUs of the mask numbering (a set spread one CU per 32-bit mask word left 256-thread
-    // helper kernels waiting for a full DP grid: tools/pq_stream_probe.hip -- the round-4 A/B of this
-    // split, hostpath_ab_r4j.txt, ran with that spread set)
-    for (int c = 0; c < nr; ++c) {
-        hm[c / 32] |= 1u << (c % 32);
-        dm[c / 32] &= ~(1u << (c % 32));
-    }
-    hipStream_t h = nullptr, d = nullptr;
-    if (hipExtStreamCreateWithCUMask(&h, (uint32_t)nw, hm) != hipSuccess) return;
-    if (hipExtStreamCreateWithCUMask(&d, (uint32_t)nw, dm) != hipSuccess) {
-        (void)hipStreamDestroy(h);
-        return;
-    }
-    s.hstream = h;
-    s.dstream = d;
-}
-
-// persistent DP grid: two waves per SIMD on every CU (the kernel's occupancy), so every wave of the
-// grid is resident at once and none waits to be dispatched behind the others
-static int32_t pq_grid(int device)
-{
-    static std::atomic<int32_t> cu[16] = {};
-    if (device < 0 || device >= 16) return 2048;
-    int32_t v = cu[device].load();
-    if (v == 0) {
-        hipDeviceProp_t pr;
-        v = hipGetDeviceProperties(&pr, device) == hipSuccess && pr.multiProcessorCount > 0 ? pr.multiProcessorCount : 256;
-        cu[device].store(v);
-    }
-    return 8 * v;
-}
-
 static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
 {
     s.stats = bsw_stats_t{};
@@ -627,16 +538,13 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     const int32_t n = pc.n;
     // small batches (kt_for-sized calls): the row-group kernel (bsw_gq.hip) straight on the
     // call's stream -- no plan, no sort, no class-count readback
-    // medium batches: the quad form (4 lanes per pair, targets <= 512 bytes)
-    // the 32-lane latency form (two DPP rows per pair: ~21% fewer instructions per row) for batches
-    // of at most 2048 pairs -- 1K calls 0.277 -> 0.25 ms, 8 callers without coalescing +8%; at 4K+
-    // pairs per batch the 16-lane form's fewer instructions per cell win (percall_bench, same box,
-    // profiles/r05/gq32_percall.txt).  BSW_GQ32_MAX (pairs, read per call) overrides
-    const char *g32 = getenv("BSW_GQ32_MAX");
-    // (within the small-batch range: BSW_OPT_SMALL_BATCH 0 keeps every batch off the 16/32-lane forms)
-    const int32_t gq32_max = std::min<int32_t>(g32 ? atoi(g32) : 2048, kp.small_batch);
+    // medium batches: the quad form (4 lanes per pair, targets <= 512 bytes); at most
+    // kp.gq32_max pairs: the 32-lane latency form (two DPP rows per pair, ~21% fewer instructions
+    // per row; BSW_OPT_GQ32_MAX) -- within the small-batch range (BSW_OPT_SMALL_BATCH 0 keeps every
+    // batch off the 16/32-lane forms)
+    const int32_t gq32_max = std::min<int32_t>(kp.gq32_max, kp.small_batch);
     const int gs = n <= gq32_max ? 32 : n <= kp.small_batch ? 16 : 4;
-    const bool gq_size = !pc.tput && (n <= kp.small_batch || n <= kp.mid_batch);
+    const bool gq_size = n <= kp.small_batch || n <= kp.mid_batch;
     const bool gq_fit = pc.gq_maxq == -2 || (pc.gq_maxq >= 0 && (gs >= 16 || pc.gq_maxt <= 512));
     if (kp.group_kernel && gq_size && gq_fit && kp.long_route == 1 && kp.maxsc == 1 && !kp.misroute) {
         const bool checked = pc.gq_maxq >= 0;
@@ -691,7 +599,7 @@ static int run_plan(const KParams &kp, Slot &s, const PlanCall &pc)
     // lane-per-pair wave lives ~1.2 ms whatever the batch size, so they are latency-bound; the
     // wave-per-alignment kernel spreads each pair over 64 lanes -- 0.35 vs 1.39 ms per call at
     // 1K C2 pairs, 1.05 vs 1.58 at 10K, slower past ~20K
-    const int32_t long_route = (kp.long_route == 1 && n <= kp.small_batch && !pc.tput) ? 2 : kp.long_route;
+    const int32_t long_route = (kp.long_route == 1 && n <= kp.small_batch) ? 2 : kp.long_route;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                        pc.d_pairs, n, kp, pc.w, pc_route, long_route, pc.d_ref, pc.d_qer, s.d_keys,
                        s.d_vals, d_counts, d_maxq, (int)kp.keymode, (int)kp.misroute);
@@ -776,22 +684,7 @@ static int run_dp(const KParams &kp, Slot &s)
         }
         for (int c = 0; c < kNumLaneClasses; ++c) {
             const int32_t np = counts[kPkClass0 + c];
-            if (np > 0 && kp.persist >= 2 && kLaneQmax[c] == 160 && kp.kern8 == 1) {
-                // the persistent tile-queue form (BSW_OPT_PERSIST 2): every tile runnable at once
-                hipStream_t ps = next_stream();
-                BSW_TRY(grow(s.d_pq, s.cap_pq, (size_t)4));
-                BSW_TRY(hipMemsetAsync(s.d_pq, 0, 4 * sizeof(int32_t), ps));
-                PqArgs a{};
-                a.kp = kp; a.w = w; a.pairs = d_pairs; a.order = s.d_order; a.ref = d_ref; a.qer = d_qer;
-                a.err = d_err; a.head = s.d_pq; a.ready = nullptr; a.abort = nullptr;
-                a.nchunks = 1; a.ntiles = (np + 63) / 64;
-                a.chunks[0] = PqChunk{0, off, np, 0, 0, 0, 0};
-                BSW_TRY(launch_pq_kernel(a, std::min(a.ntiles, pq_grid(s.device)), ps));
-                s.stats.n_launches++;
-                s.stats.n_packed += np;
-                if (cell_bits == 8) s.stats.n_u8 += np;
-                else s.stats.n_i16 += np;
-            } else if (np > 0) {
+            if (np > 0) {
                 BSW_TRY(launch_pc_kernel(kLaneQmax[c], kp, w, d_pairs, s.d_order + off, np, d_ref, d_qer,
                                          d_err, next_stream()));
                 s.stats.n_launches++;
@@ -935,16 +828,6 @@ __global__ void unpack2_kernel(const uint8_t *__restrict__ in, uint8_t *__restri
     }
 }
 
-// exception words of a 2-bit chunk: the first n_r patch ref, the rest qer
-__global__ void patch_codes_kernel(const uint32_t *__restrict__ exc, int32_t n_r, int32_t n_all,
-                                   uint8_t *__restrict__ ref, uint8_t *__restrict__ qer)
-{
-    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_all) return;
-    const uint32_t e = exc[t];
-    (t < n_r ? ref : qer)[e >> 4] = (uint8_t)(e & 15u);
-}
-
 // (PairIn: the kernels' input fields of a SeqPair, bsw_kernels.h)
 
 __global__ void expand_pairs_kernel(const PairIn *__restrict__ in, SeqPair *__restrict__ out, int32_t n)
@@ -960,8 +843,8 @@ __global__ void expand_pairs_kernel(const PairIn *__restrict__ in, SeqPair *__re
 
 // The whole staged input of a coalesced batch in one launch (what unpack2 x2 + patch_codes +
 // expand_pairs + two pad memsets did in six): index space = ref 16-code units, qer units, pairs.
-// Exception words (pos << 4 | code) are ascending per buffer, so a unit finds its own by a
-// binary search and patches them after unpacking (no second pass, no race).
+// Exception words (pos << 2 | code bits 2-3, bsw_pack.cpp) are ascending per buffer, so a unit finds
+// its own by a binary search and patches them after unpacking (no second pass, no race).
 __device__ __forceinline__ void unpack_unit(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int64_t n,
                                             int64_t t, const uint32_t *__restrict__ exc, int32_t ne)
 {
@@ -981,11 +864,11 @@ __device__ __forceinline__ void unpack_unit(const uint8_t *__restrict__ in, uint
         int32_t lo = 0, hi = ne;                       // first exception at or past o
         while (lo < hi) {
             const int32_t mid = (lo + hi) >> 1;
-            if ((int64_t)(exc[mid] >> 4) < o) lo = mid + 1; else hi = mid;
+            if ((int64_t)(exc[mid] >> 2) < o) lo = mid + 1; else hi = mid;
         }
-        for (; lo < ne && (int64_t)(exc[lo] >> 4) < o + 16; ++lo) {
-            const int k = (int)((exc[lo] >> 4) - o);
-            w[k >> 2] = (w[k >> 2] & ~(0xffu << (8 * (k & 3)))) | ((exc[lo] & 15u) << (8 * (k & 3)));
+        for (; lo < ne && (int64_t)(exc[lo] >> 2) < o + 16; ++lo) {
+            const int k = (int)((exc[lo] >> 2) - o);
+            w[k >> 2] |= (exc[lo] & 3u) << (8 * (k & 3) + 2);     // code bits 2-3 over the plane's 0-1
         }
     }
     if (o + 16 <= n) {
@@ -1037,20 +920,18 @@ constexpr int32_t kStageBlk = 4096;           // pairs per block (a chunk is who
 struct BlkStat {
     int64_t r_lo, r_hi, q_lo, q_hi, r_sum, q_sum;
     bool bad;
-    bool fast;                  // every pair fits the packed-column kernel (host_shard_fast)
 };
 
 // blocks [b0, b1) of bs (sized for every block of the n pairs); false if any pair there is invalid
 static bool prepass_range(const SeqPair *pairs, int32_t n, std::vector<BlkStat> &bs, int32_t b0, int32_t b1)
 {
     auto blk = [&](int32_t b) {
-        BlkStat t{INT64_MAX, 0, INT64_MAX, 0, 0, 0, false, true};
+        BlkStat t{INT64_MAX, 0, INT64_MAX, 0, 0, 0, false};
         const int32_t e = std::min(n, (b + 1) * kStageBlk);
         for (int32_t i = b * kStageBlk; i < e; ++i) {
             const SeqPair &p = pairs[i];
             t.bad |= p.len1 < 0 || p.len2 < 0 || p.len1 > BSW_MAX_LEN || p.len2 > BSW_MAX_LEN || p.idr < 0 ||
                      p.idq < 0;
-            t.fast &= p.len2 < 160 && p.h0 >= 0 && p.h0 + std::min(std::max(p.len1, 0), std::max(p.len2, 0)) <= 255;
             if (p.len1 > 0) { t.r_lo = std::min<int64_t>(t.r_lo, p.idr); t.r_hi = std::max<int64_t>(t.r_hi, (int64_t)p.idr + p.len1); t.r_sum += p.len1; }
             if (p.len2 > 0) { t.q_lo = std::min<int64_t>(t.q_lo, p.idq); t.q_hi = std::max<int64_t>(t.q_hi, (int64_t)p.idq + p.len2); t.q_sum += p.len2; }
         }
@@ -1173,7 +1054,7 @@ static int stage_chunk(Slot &s, const SeqPair *pairs, const uint8_t *ref, const 
     c.qb = (size_t)(bulk ? q_hi - q_lo : q_sum);
     c.packed = bulk;
     c.n = n;
-    if (bulk && two_bit && c.rb < ((size_t)1 << 28) && c.qb < ((size_t)1 << 28)) {
+    if (bulk && two_bit && c.rb < ((size_t)1 << 30) && c.qb < ((size_t)1 << 30)) {
         const int r = stage_2bit(s, pairs, ref + r_lo, qer + q_lo, n, c);
         if (r != 1) {                       // 1: too many exception bytes -> nibbles below
             c.r_base = r_lo; c.q_base = q_lo;
@@ -1262,834 +1143,6 @@ static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, int mode)
     }
 }
 
-// ---------------------------------------------------------------- host pipeline, fast path
-// A host-buffer call whose every pair fits the packed-column kernel (bwa-style scoring, qlen <
-// 160, h0 + min(len1, len2) <= 255) and whose chunks' byte extents are contiguous (the upstream
-// layout) runs with NO device helper kernel: per chunk the host computes each pair's schedule key
-// (plan_kernel's key of that class, from the same bytes: fast_keys), sorts the chunk by it (a
-// parallel stable LSD radix over the key bytes that vary), stages the records in that order as
-// 20-B PairIn with nibble offsets and the byte extents as nibbles; the device runs one H2D, one
-// pc_kernel<160, nibbles> reading the staged chunk in place and writing 24 B of outputs per pair,
-// and one D2H.  Why: in the general pipeline every chunk's unpack / plan / sort / gather kernels
-// wait ~0.3-1.6 ms for wave slots behind the previous chunk's DP waves (kernel + copy trace,
-// profiles/r05/hostpath_trace_timeline.txt), so consecutive chunks' DP kernels could not overlap
-// (9.6 ms of chunk DP for 6.85 ms of work).  Outputs are identical (pairs are independent; the
-// order only schedules).  Off by default (measured slower); BSW_HP_FAST=1 turns it on.
-struct FastChunk {
-    int32_t a = 0, m = 0;                    // pairs [a, a + m) of the call
-    size_t perm_off = 0, ref_off = 0, qer_off = 0, err_off = 0, out_off = 0, h2d = 0, dev = 0;
-    int64_t r_lo = 0, q_lo = 0;
-    std::chrono::steady_clock::time_point t0;   // (BSW_DEBUG_HP timeline)
-};
-
-// The schedule order of a chunk, on ONE thread (it runs beside the pool staging the next chunk):
-// perm[k] = the pair in slot k, by ascending key, stable.  Only the key bits that vary in the
-// chunk count (compacted by pext): one counting pass when they fit 16 bits (C2: related +
-// identities + h0 = 14 bits), else an LSD radix of 8-bit digits over (key << 32 | pair) words.
-static void sort_order(const uint32_t *keys, int32_t m, int32_t *perm, std::vector<uint64_t> &kv,
-                       std::vector<uint64_t> &tmp)
-{
-    if (m <= 1) {
-        if (m == 1) perm[0] = 0;
-        return;
-    }
-    uint32_t vor = 0, vand = ~0u;
-    for (int32_t i = 0; i < m; ++i) { vor |= keys[i]; vand &= keys[i]; }
-    const uint32_t vary = vor ^ vand;
-    const int bits = __builtin_popcount(vary);
-    kv.resize((size_t)m);
-    compact_keys(keys, 0, m, vary, kv.data());
-    if (bits <= 16) {
-        std::vector<int32_t> cnt((size_t)1 << bits, 0);
-        for (int32_t i = 0; i < m; ++i) ++cnt[kv[i] >> 32];
-        int32_t run = 0;
-        for (auto &c : cnt) {
-            const int32_t x = c;
-            c = run;
-            run += x;
-        }
-        for (int32_t i = 0; i < m; ++i) perm[cnt[kv[i] >> 32]++] = (int32_t)(uint32_t)kv[i];
-        return;
-    }
-    tmp.resize((size_t)m);
-    uint64_t *src = kv.data(), *dst = tmp.data();
-    int32_t hist[256];
-    for (int d = 0; 8 * d < bits; ++d) {
-        const int sh = 32 + 8 * d;
-        std::fill(hist, hist + 256, 0);
-        for (int32_t i = 0; i < m; ++i) ++hist[(src[i] >> sh) & 0xffu];
-        int32_t run = 0;
-        for (int x = 0; x < 256; ++x) {
-            const int32_t c = hist[x];
-            hist[x] = run;
-            run += c;
-        }
-        for (int32_t i = 0; i < m; ++i) dst[hist[(src[i] >> sh) & 0xffu]++] = src[i];
-        std::swap(src, dst);
-    }
-    for (int32_t i = 0; i < m; ++i) perm[i] = (int32_t)(uint32_t)src[i];
-}
-
-// Stage one chunk (records in the caller's order as PairIn with nibble offsets, schedule keys,
-// both byte extents as nibbles) with the host pool.  `side` runs on the calling thread while the
-// pool works (the previous chunk's sort and launch).
-static int stage_fast(Slot &s, const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t m,
-                      const BlkStat *bs, int32_t nblk, FastChunk &c, std::vector<uint32_t> &keys,
-                      const std::function<void()> &side)
-{
-    c.t0 = std::chrono::steady_clock::now();
-    int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
-    for (int32_t b = 0; b < nblk; ++b) {
-        r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
-        q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi);
-    }
-    if (r_lo == INT64_MAX) r_lo = r_hi = 0;
-    if (q_lo == INT64_MAX) q_lo = q_hi = 0;
-    const size_t rb = (size_t)(r_hi - r_lo), qb = (size_t)(q_hi - q_lo);
-    c.m = m;
-    c.r_lo = r_lo; c.q_lo = q_lo;
-    c.perm_off = align256((size_t)m * sizeof(PairIn));
-    c.ref_off = align256(c.perm_off + (size_t)m * 4);
-    c.qer_off = align256(c.ref_off + (rb + 1) / 2 + 8);
-    // the range-guard word travels inside the H2D (zeroed by the host) and the D2H (beside the
-    // outputs): a memset or a 4-byte readback is a blit kernel that waits for wave slots behind
-    // the previous chunk's DP waves, and holds its stream meanwhile (trace)
-    c.err_off = align256(c.qer_off + (qb + 1) / 2 + 8);
-    c.h2d = c.err_off + 256;
-    c.out_off = c.err_off + 256;
-    c.dev = c.out_off + (size_t)m * 24;
-    const size_t hb = std::max(c.h2d, (size_t)256 + (size_t)m * 24);
-    if (hb > s.cap_stage) {
-        const size_t cap = std::max(hb + hb / 4, s.cap_stage * 3 / 2);
-        if (s.h_stage) (void)hipHostFree(s.h_stage);
-        s.h_stage = nullptr; s.cap_stage = 0;
-        BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));
-        s.cap_stage = cap;
-    }
-    keys.resize((size_t)m);
-    uint8_t *h = (uint8_t *)s.h_stage;
-    PairIn *rec = (PairIn *)h;
-    // task 0 (the calling thread): `side`; then records + keys (pieces of 8K pairs) and both nibble
-    // packs (pieces of ~4 MB) as one pool job list
-    const int nk = (int)std::max<int64_t>(1, m >> 13), nr = (int)std::max<size_t>(1, rb >> 22),
-              nq = (int)std::max<size_t>(1, qb >> 22);
-    auto even = [](size_t total, int k, int parts) {
-        return k == parts ? total : (total * (size_t)k / (size_t)parts) & ~(size_t)31;
-    };
-    HostPool::get().parallel_for(1 + nk + nr + nq, [&](int t) {
-        if (t == 0) {
-            side();
-            return;
-        }
-        --t;
-        if (t < nk) {
-            const int32_t a0 = (int32_t)((int64_t)m * t / nk), a1 = (int32_t)((int64_t)m * (t + 1) / nk);
-            fast_keys(pairs + a0, a1 - a0, ref, qer, keys.data() + a0);
-            for (int32_t i = a0; i < a1; ++i) {
-                const SeqPair &p = pairs[i];
-                rec[i] = PairIn{p.len1 > 0 ? (int32_t)(p.idr - r_lo) : 0, p.len2 > 0 ? (int32_t)(p.idq - q_lo) : 0,
-                                p.len1, p.len2, p.h0};
-            }
-        } else if (t < nk + nr) {
-            const size_t a0 = even(rb, t - nk, nr), a1 = even(rb, t - nk + 1, nr);
-            pack_nibbles(h + c.ref_off + a0 / 2, ref + r_lo + a0, a1 - a0);
-        } else {
-            const size_t a0 = even(qb, t - nk - nr, nq), a1 = even(qb, t - nk - nr + 1, nq);
-            pack_nibbles(h + c.qer_off + a0 / 2, qer + q_lo + a0, a1 - a0);
-        }
-    });
-    memset(h + c.ref_off + (rb + 1) / 2, 0, 8);
-    memset(h + c.qer_off + (qb + 1) / 2, 0, 8);
-    memset(h + c.err_off, 0, 256);
-    if (getenv("BSW_DEBUG_HP"))
-        fprintf(stderr, "fast stage %d pairs: %.3f ms\n", (int)m,
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c.t0).count());
-    return BSW_OK;
-}
-
-// the fast path's chunks as block ranges [first, second): the general pipeline's schedule (a first
-// chunk of 16 blocks or 1/32 of the call, doubling up to `chunk` pairs, at most 512 MB of bytes)
-static std::vector<std::pair<int32_t, int32_t>> fast_chunks(const std::vector<BlkStat> &bs, int32_t n, int32_t chunk)
-{
-    (void)n;
-    std::vector<std::pair<int32_t, int32_t>> out;
-    const int32_t nblk = (int32_t)bs.size();
-    const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
-    int32_t cur = std::min(cap_blk, nblk <= 32 ? nblk : std::max<int32_t>(16, nblk / 32));
-    const int32_t first = cur;
-    for (int32_t b = 0, nb = 0; b < nblk; b += nb, cur = std::min(cap_blk, cur * 2)) {
-        // ramp down again toward the end: the last chunk's H2D + kernel (one wave lifetime at
-        // least) are the call's tail once the host has staged everything (chunks' kernels overlap)
-        cur = std::min(cur, std::max(first, (nblk - b) / 2));
-        int64_t bytes = 0;
-        for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
-            const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
-            if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
-            bytes += x;
-        }
-        out.emplace_back(b, b + nb);
-    }
-    return out;
-}
-
-static int host_shard_fast(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref, const uint8_t *qer,
-                           int32_t n, int32_t w, int cell_bits, int32_t chunk, const std::vector<BlkStat> &bs,
-                           bsw_stats_t *st)
-{
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    const auto t_start = now();
-    constexpr int kSlots = 4;
-    std::unique_ptr<Slot> slots[kSlots];
-    FastChunk fc[kSlots];
-    bool pend[kSlots] = {};
-    std::vector<uint32_t> keys[kSlots];
-    std::vector<uint64_t> kv[kSlots], tmp[kSlots];
-    // (a slot is reused only after finish(): its chunk was launched one step after staging, so a
-    // staged-but-unlaunched chunk never sits in the slot being restaged -- kSlots >= 2)
-    bsw_stats_t agg{};
-    double stage_ms = 0;
-    int rc = BSW_OK;
-    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;
-    auto finish = [&](int k) -> int {
-        if (!pend[k]) return BSW_OK;
-        pend[k] = false;
-        Slot &s = *slots[k];
-        const auto tw = now();
-        // the readbacks are queued only now: copies of all streams pass one copy engine in order,
-        // so a D2H queued right behind its kernel held every later chunk's H2D until that kernel
-        // ended (kernel + copy trace: chunks fully serialised)
-        BSW_TRY(hipMemcpyAsync(s.h_stage, s.d_stage + fc[k].err_off, 256 + (size_t)fc[k].m * 24,
-                               hipMemcpyDeviceToHost, s.stream));
-        BSW_TRY(hipStreamSynchronize(s.stream));
-        float ms = 0.f;
-        BSW_TRY(hipEventElapsedTime(&ms, s.ev0, s.ev1));
-        agg.kernel_ms += ms;
-        if (dbg)
-            fprintf(stderr, "fast finish slot %d: waited %.3f ms at %.3f, kernel %.3f ms\n", k,
-                    std::chrono::duration<double, std::milli>(now() - tw).count(),
-                    std::chrono::duration<double, std::milli>(tw - t_start).count(), ms);
-        if (((const int32_t *)s.h_stage)[0] != 0) return BSW_E_RANGE;
-        const int32_t *o = (const int32_t *)((const uint8_t *)s.h_stage + 256);   // outputs, caller's order
-        const int32_t m = fc[k].m, a = fc[k].a;
-        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(HostPool::workers() + 1, m >> 15));
-        HostPool::get().parallel_for(nt, [&](int t) {
-            for (int32_t j = (int32_t)((int64_t)m * t / nt); j < (int32_t)((int64_t)m * (t + 1) / nt); ++j) {
-                const int32_t *q = o + 6 * (int64_t)j;
-                SeqPair &p = pairs[a + j];
-                p.score = q[0]; p.tle = q[1]; p.gtle = q[2]; p.qle = q[3]; p.gscore = q[4]; p.max_off = q[5];
-            }
-        });
-        agg.n_packed += m; agg.n_launches += 1;
-        (cell_bits == 8 ? agg.n_u8 : agg.n_i16) += m;     // as run_dp counts the packed classes
-        return BSW_OK;
-    };
-    // chunk c's sort and launch run on the calling thread while the pool stages chunk c + 1
-    // (stage_fast's side task): the sort is off the staging path, at one chunk of latency
-    int prev = -1;                                   // slot holding a staged chunk not yet launched
-    int side_rc = BSW_OK;
-    auto launch = [&](int k) {
-        if (k < 0 || side_rc) return;
-        side_rc = [&]() -> int {
-            Slot &s = *slots[k];
-            const FastChunk &c = fc[k];
-            uint8_t *h = (uint8_t *)s.h_stage;
-            sort_order(keys[k].data(), c.m, (int32_t *)(h + c.perm_off), kv[k], tmp[k]);
-            BSW_TRY(grow(s.d_stage, s.cap_dstage, c.dev));
-            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.h2d, hipMemcpyHostToDevice, s.stream));
-            BSW_TRY(hipEventRecord(s.ev0, s.stream));
-            BSW_TRY(launch_pc_nib_kernel(kp, w, (const PairIn *)s.d_stage, (const int32_t *)(s.d_stage + c.perm_off),
-                                         c.m, s.d_stage + c.ref_off, s.d_stage + c.qer_off,
-                                         (int32_t *)(s.d_stage + c.out_off), (int32_t *)(s.d_stage + c.err_off),
-                                         s.stream));
-            BSW_TRY(hipEventRecord(s.ev1, s.stream));
-            pend[k] = true;
-            return BSW_OK;
-        }();
-    };
-    rc = [&]() -> int {
-        BSW_TRY(hipSetDevice(dc.device));
-        int k = 0;
-        for (const auto &ch : fast_chunks(bs, n, chunk)) {
-            const int32_t b = ch.first, nb = ch.second - ch.first;
-            const int32_t a = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a;
-            if (int r = finish(k)) return r;
-            if (!slots[k]) {
-                int r = BSW_OK;
-                slots[k] = dc.acquire(r);
-                if (r) return r;
-            }
-            const int p = prev;
-            const auto t0 = now();
-            if (int r = stage_fast(*slots[k], pairs + a, ref, qer, m, bs.data() + b, nb, fc[k], keys[k],
-                                   [&] { launch(p); }))
-                return r;
-            if (side_rc) return side_rc;
-            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
-            fc[k].a = a;
-            prev = k;
-            k = (k + 1) % kSlots;
-        }
-        launch(prev);
-        if (side_rc) return side_rc;
-        for (int j = 0; j < kSlots; ++j)
-            if (int r = finish(j)) return r;
-        return BSW_OK;
-    }();
-    for (int j = 0; j < kSlots; ++j)
-        if (slots[j]) dc.give_back(std::move(slots[j]), rc);
-    agg.stage_ms = (float)stage_ms;
-    agg.host_ms = (float)std::chrono::duration<double, std::milli>(now() - t_start).count();
-    if (rc == BSW_OK && st) *st = agg;
-    return rc;
-}
-
-// ---------------------------------------------------------------- host pipeline, persistent DP
-// One chunk published to the running persistent DP kernel: *ready = the chunk's last tile + 1.  The
-// chunk's inputs were written by the kernels before this one on the same stream (their end-of-kernel
-// release); the store is a relaxed agent-scope atomic (write-through), the pollers read it with
-// relaxed agent-scope loads and take an agent acquire before the chunk's inputs (bsw_pc.hip).
-__global__ void pq_publish_kernel(int32_t *ready, int32_t v)
-{
-    __hip_atomic_store(ready, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// the persistent pipeline's streams: CU-masked, the helper stream on the first pq_nres CUs of the
-// mask numbering, the DP stream on the rest (BSW_PQ_RESERVE, default 16)
-static bool ensure_pq_streams(DeviceCtx &dc)
-{
-    if (dc.pq_h) return true;
-    if (dc.pq_failed) return false;
-    dc.pq_failed = true;
-    hipDeviceProp_t pr;
-    if (hipGetDeviceProperties(&pr, dc.device) != hipSuccess) return false;
-    const int ncu = pr.multiProcessorCount;
-    const char *e = getenv("BSW_PQ_RESERVE");
-    const int nr = e ? std::max(1, atoi(e)) : 16;
-    if (ncu < 4 * nr || ncu > 1024) return false;
-    uint32_t hm[32] = {}, dm[32] = {};
-    const int nw = (ncu + 31) / 32;
-    for (int c = 0; c < ncu; ++c) dm[c / 32] |= 1u << (c % 32);
-    // the first nr CUs of the mask numbering: a spread set (one CU per 32-bit mask word) left the
-    // helper's 256-thread kernels waiting for the DP grid to end (tools/pq_stream_probe.hip, 2 s
-    // per kernel) while CUs 0-7 run them at once beside a full grid
-    for (int c = 0; c < nr; ++c) {
-        hm[c / 32] |= 1u << (c % 32);
-        dm[c / 32] &= ~(1u << (c % 32));
-    }
-    hipStream_t h = nullptr, d = nullptr;
-    if (hipExtStreamCreateWithCUMask(&h, (uint32_t)nw, hm) != hipSuccess) return false;
-    if (hipExtStreamCreateWithCUMask(&d, (uint32_t)nw, dm) != hipSuccess) {
-        (void)hipStreamDestroy(h);
-        return false;
-    }
-    bool ok = true;
-    for (hipEvent_t &ev : dc.pq_ev) ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&dc.pq_init, hipEventDisableTiming) == hipSuccess;
-    ok = ok && hipEventCreate(&dc.pq_t0) == hipSuccess && hipEventCreate(&dc.pq_t1) == hipSuccess;
-    if (!ok) {
-        (void)hipStreamDestroy(h);
-        (void)hipStreamDestroy(d);
-        return false;
-    }
-    dc.pq_h = h;
-    dc.pq_d = d;
-    dc.pq_nres = nr;
-    dc.pq_ncu = ncu;
-    dc.pq_failed = false;
-    return true;
-}
-
-// plan_kernel's schedule key (keymode 2) for a staged nibble chunk: PairIn records whose idr / idq
-// are nibble indices into ref4 / qer4; every pair is in a packed-column class (host_shard_pq's
-// precondition).  vals = the chunk-local index.  Seed identities as seed_matches, from nibbles.
-// n (<= 8 * (W - 1)) codes from nibble index k of b4 as W aligned dwords realigned to the code
-// (dword loads: the staged extents carry 8 bytes of padding; 72 byte loads per pair made this
-// kernel load-issue-bound on the helper stream's few CUs)
-template <int W>
-__device__ __forceinline__ void nib_words(const uint8_t *__restrict__ b4, int64_t k, uint32_t (&a)[W - 1])
-{
-    const uint32_t *wp = (const uint32_t *)b4 + (k >> 3);
-    uint32_t w[W];
-#pragma unroll
-    for (int i = 0; i < W; ++i) w[i] = wp[i];
-    const uint32_t sh = 4u * (uint32_t)(k & 7);
-#pragma unroll
-    for (int i = 0; i < W - 1; ++i) a[i] = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
-}
-__global__ void plan_nib_kernel(const PairIn *__restrict__ recs, int32_t m, const uint8_t *__restrict__ ref4,
-                                const uint8_t *__restrict__ qer4, uint32_t *__restrict__ keys, int32_t *__restrict__ vals)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const PairIn p = recs[i];
-    const int qlen = max(p.len2, 0), tlen = max(p.len1, 0);
-    const int c = kPkClass0 + (qlen + 1 <= 32 ? 0 : qlen + 1 <= 64 ? 1 : qlen + 1 <= 96 ? 2 : qlen + 1 <= 128 ? 3 : 4);
-    int mt = 31;
-    if (qlen >= 40 && tlen >= 46) {          // seed_matches: query[10, 40) vs target[4 + s, 34 + s), s <= 12
-        uint32_t qa[4], ra[6];
-        nib_words<5>(qer4, (int64_t)p.idq + 10, qa);
-        nib_words<7>(ref4, (int64_t)p.idr + 4, ra);
-        uint8_t qb[30], rb[42];
-#pragma unroll
-        for (int j = 0; j < 30; ++j) qb[j] = (uint8_t)((qa[j >> 3] >> (4 * (j & 7))) & 15u);
-#pragma unroll
-        for (int j = 0; j < 42; ++j) rb[j] = (uint8_t)((ra[j >> 3] >> (4 * (j & 7))) & 15u);
-        int best = 0;
-#pragma unroll
-        for (int sft = 0; sft <= 12; ++sft) {
-            int n = 0;
-#pragma unroll
-            for (int j = 0; j < 30; ++j) n += qb[j] == rb[j + sft];
-            best = max(best, n);
-        }
-        mt = best;
-    }
-    const int rel = mt > 18;
-    keys[i] = ((uint32_t)c << 28) | ((uint32_t)(255 - min(qlen, 255)) << 20) | ((uint32_t)(1 - rel) << 19) |
-              ((uint32_t)(63 - min(tlen >> 5, 63)) << 13) | ((uint32_t)(31 - min(mt, 31)) << 8) |
-              (uint32_t)(255 - min(max(p.h0, 0), 255));
-    vals[i] = i;
-}
-
-// One chunk of the persistent pipeline staged for in-place reading: [PairIn x m | target nibbles |
-// query nibbles], idr / idq rewritten as nibble indices from the chunk's byte extents.
-struct PqStaged {
-    size_t ref_off = 0, qer_off = 0, bytes = 0;
-};
-static size_t pq_stage_bytes(int32_t m, size_t rb, size_t qb, PqStaged &c)
-{
-    c.ref_off = align256((size_t)m * sizeof(PairIn));
-    c.qer_off = align256(c.ref_off + (rb + 1) / 2 + 8);
-    c.bytes = align256(c.qer_off + (qb + 1) / 2 + 8);
-    return c.bytes;
-}
-static void pq_stage(uint8_t *h, const SeqPair *pairs, const uint8_t *ref, const uint8_t *qer, int32_t m, int64_t r_lo,
-                     size_t rb, int64_t q_lo, size_t qb, const PqStaged &c)
-{
-    PairIn *rec = (PairIn *)h;
-    const int nk = (int)std::max<int64_t>(1, m >> 14), nr = (int)std::max<size_t>(1, rb >> 22),
-              nq = (int)std::max<size_t>(1, qb >> 22);
-    auto even = [](size_t total, int k, int parts) {
-        return k == parts ? total : (total * (size_t)k / (size_t)parts) & ~(size_t)31;
-    };
-    HostPool::get().parallel_for(nk + nr + nq, [&](int t) {
-        if (t < nk) {
-            const int32_t a0 = (int32_t)((int64_t)m * t / nk), a1 = (int32_t)((int64_t)m * (t + 1) / nk);
-            for (int32_t i = a0; i < a1; ++i) {
-                const SeqPair &p = pairs[i];
-                rec[i] = PairIn{p.len1 > 0 ? (int32_t)(p.idr - r_lo) : 0, p.len2 > 0 ? (int32_t)(p.idq - q_lo) : 0,
-                                p.len1, p.len2, p.h0};
-            }
-        } else if (t < nk + nr) {
-            const size_t a0 = even(rb, t - nk, nr), a1 = even(rb, t - nk + 1, nr);
-            pack_nibbles(h + c.ref_off + a0 / 2, ref + r_lo + a0, a1 - a0);
-        } else {
-            const size_t a0 = even(qb, t - nk - nr, nq), a1 = even(qb, t - nk - nr + 1, nq);
-            pack_nibbles(h + c.qer_off + a0 / 2, qer + q_lo + a0, a1 - a0);
-        }
-    });
-    memset(h + c.ref_off + (rb + 1) / 2, 0, 8);
-    memset(h + c.qer_off + (qb + 1) / 2, 0, 8);
-}
-
-// A host-buffer call as ONE persistent DP launch (BSW_OPT_PERSIST >= 1).  The
-// pq_kernel grid starts first, on the DP CUs, and takes 64-pair tiles as chunks are published.  Per
-// chunk: the host stages PairIn records + nibble-packed extents into one of three pinned buffers;
-// a copy stream moves them into the chunk's own region of the call's device buffer (chunks stay
-// resident until the call ends: the DP reads them in place, nothing is unpacked); the helper stream
-// (a few reserved CUs) computes the chunk's schedule keys from the nibbles, sorts them, and
-// publishes the chunk.  No chunk waits for another's DP to drain, and the call has one DP tail
-// instead of one per chunk.  At the end: one D2H of the 24 output bytes per pair, scattered into the
-// caller's records.  Preconditions (host_shard): every pair fits pc_kernel<160>, the chunks'
-// byte extents are bulk.  Returns 1 (nothing done) when the streams are unavailable.
-static int host_shard_pq(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref, const uint8_t *qer,
-                         int32_t n, int32_t w, int cell_bits, const std::vector<std::pair<int32_t, int32_t>> &chs,
-                         const std::vector<BlkStat> &bs, bsw_stats_t *st)
-{
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    const auto t_start = now();
-    std::lock_guard<std::mutex> g(dc.pq_mu);
-    BSW_TRY(hipSetDevice(dc.device));
-    if (!ensure_pq_streams(dc)) return 1;
-    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;
-    constexpr int kSlots = 3;
-    std::unique_ptr<Slot> slots[kSlots];
-    int rc = BSW_OK;
-    for (int k = 0; k < kSlots; ++k) {
-        slots[k] = dc.acquire(rc);
-        if (rc) {
-            for (int j = 0; j < k; ++j) dc.give_back(std::move(slots[j]));
-            return rc;
-        }
-    }
-    hipStream_t H = dc.pq_h, D = dc.pq_d;
-    Slot &cs = *slots[0];                       // the call's device buffers; its stream copies
-    hipStream_t C = cs.stream;
-    const int nch = (int)chs.size();
-    bool launched = false;
-    double stage_ms = 0;
-    struct ChunkGeo { int32_t a, m; int64_t r_lo, q_lo; size_t rb, qb, off; PqStaged ps; };
-    std::vector<ChunkGeo> geo((size_t)nch);
-    rc = [&]() -> int {
-        int32_t mmax = 0, ntiles = 0;
-        size_t dev_bytes = 0, host_max[kSlots] = {};
-        for (int c = 0; c < nch; ++c) {
-            ChunkGeo &q = geo[(size_t)c];
-            q.a = chs[c].first * kStageBlk;
-            q.m = std::min(n, chs[c].second * kStageBlk) - q.a;
-            int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
-            for (int32_t b = chs[c].first; b < chs[c].second; ++b) {
-                r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
-                q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi);
-            }
-            if (r_lo == INT64_MAX) r_lo = r_hi = 0;
-            if (q_lo == INT64_MAX) q_lo = q_hi = 0;
-            q.r_lo = r_lo; q.q_lo = q_lo; q.rb = (size_t)(r_hi - r_lo); q.qb = (size_t)(q_hi - q_lo);
-            const size_t cb = pq_stage_bytes(q.m, q.rb, q.qb, q.ps);
-            q.off = dev_bytes;
-            dev_bytes += cb;
-            host_max[c % kSlots] = std::max(host_max[c % kSlots], cb);
-            mmax = std::max(mmax, q.m);
-            ntiles += (q.m + 63) / 64;
-        }
-        // every buffer at its final size before the grid starts: a hipFree / hipHostFree inside the
-        // loop would wait for the device -- i.e. for the running grid, which waits for this thread
-        BSW_TRY(grow(cs.d_stage, cs.cap_dstage, dev_bytes));
-        BSW_TRY(grow_sort(cs, std::max(n, mmax)));
-        BSW_TRY(grow(cs.d_pq, cs.cap_pq, (size_t)4));
-        BSW_TRY(grow(cs.d_scratch, cs.cap_scratch, (size_t)n * 3 + 1));     // 24 B per pair of outputs
-        size_t tmp_bytes = 0;
-        BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, cs.d_keys, cs.d_keys2, cs.d_vals, cs.d_order,
-                                                   mmax, 0, kKeyBits, H));
-        BSW_TRY(grow(cs.d_tmp, cs.cap_tmp, tmp_bytes));
-        for (int k = 0; k < kSlots; ++k) {
-            Slot &s = *slots[k];
-            if (host_max[k] > s.cap_stage) {
-                if (s.h_stage) (void)hipHostFree(s.h_stage);
-                s.h_stage = nullptr; s.cap_stage = 0;
-                BSW_TRY(hipHostMalloc(&s.h_stage, host_max[k], 0));
-                s.cap_stage = host_max[k];
-            }
-        }
-        if (dc.pq_hout_cap < (size_t)n * 24) {
-            if (dc.pq_hout) (void)hipHostFree(dc.pq_hout);
-            dc.pq_hout = nullptr; dc.pq_hout_cap = 0;
-            const size_t cap = (size_t)n * 24 + (size_t)n * 6;
-            BSW_TRY(hipHostMalloc(&dc.pq_hout, cap, 0));
-            dc.pq_hout_cap = cap;
-        }
-        PqArgs a{};
-        a.kp = kp; a.w = w; a.order = cs.d_order;
-        a.nbase = cs.d_stage; a.out24 = (int32_t *)cs.d_scratch;
-        a.err = cs.d_meta + kMetaErr; a.head = cs.d_pq; a.ready = cs.d_pq + 1; a.abort = cs.d_pq + 2;
-        a.nchunks = nch; a.ntiles = ntiles;
-        for (int c = 0, t = 0; c < nch; ++c) {
-            const ChunkGeo &q = geo[(size_t)c];
-            a.chunks[c] = PqChunk{t, q.a, q.m, q.a, (int64_t)q.off, (int64_t)(q.off + q.ps.ref_off),
-                                  (int64_t)(q.off + q.ps.qer_off)};
-            t += (q.m + 63) / 64;
-        }
-        // the queue words are zeroed on the helper stream and the DP stream waits for that: the
-        // helper stream never waits on the DP stream (an event recorded there could complete only
-        // with the grid, which waits for the helper stream's chunks)
-        BSW_TRY(hipMemsetAsync(cs.d_meta, 0, kMetaWords * sizeof(int32_t), H));
-        BSW_TRY(hipMemsetAsync(cs.d_pq, 0, 4 * sizeof(int32_t), H));
-        BSW_TRY(hipEventRecord(dc.pq_init, H));
-        BSW_TRY(hipStreamWaitEvent(D, dc.pq_init, 0));
-        BSW_TRY(hipEventRecord(dc.pq_t0, D));
-        BSW_TRY(launch_pq_kernel(a, std::min(ntiles, 8 * (dc.pq_ncu - dc.pq_nres)), D));
-        launched = true;
-        BSW_TRY(hipEventRecord(dc.pq_t1, D));
-        for (int c = 0, tend = 0; c < nch; ++c) {
-            const int k = c % kSlots;
-            Slot &s = *slots[k];
-            const ChunkGeo &q = geo[(size_t)c];
-            tend += (q.m + 63) / 64;
-            if (c >= kSlots) BSW_TRY(hipEventSynchronize(dc.pq_ev[k]));   // slot k's last copy done
-            const auto t0 = now();
-            pq_stage((uint8_t *)s.h_stage, pairs + q.a, ref, qer, q.m, q.r_lo, q.rb, q.q_lo, q.qb, q.ps);
-            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
-            uint8_t *dst = cs.d_stage + q.off;
-            BSW_TRY(hipMemcpyAsync(dst, s.h_stage, q.ps.bytes, hipMemcpyHostToDevice, C));
-            if (dbg) {
-                if (!dc.pq_dbg[0][c]) BSW_TRY(hipEventCreate(&dc.pq_dbg[0][c]));
-                if (!dc.pq_dbg[1][c]) BSW_TRY(hipEventCreate(&dc.pq_dbg[1][c]));
-                BSW_TRY(hipEventRecord(dc.pq_dbg[0][c], C));
-            }
-            BSW_TRY(hipEventRecord(dc.pq_ev[k], C));
-            BSW_TRY(hipStreamWaitEvent(H, dc.pq_ev[k], 0));
-            hipLaunchKernelGGL(plan_nib_kernel, dim3((unsigned)((q.m + 255) / 256)), dim3(256), 0, H, (const PairIn *)dst,
-                               q.m, dst + q.ps.ref_off, dst + q.ps.qer_off, cs.d_keys, cs.d_vals);
-            BSW_TRY(hipGetLastError());
-            size_t tb = cs.cap_tmp;
-            BSW_TRY(hipcub::DeviceRadixSort::SortPairs(cs.d_tmp, tb, cs.d_keys, cs.d_keys2, cs.d_vals,
-                                                       cs.d_order + q.a, q.m, 0, kKeyBits, H));
-            hipLaunchKernelGGL(pq_publish_kernel, dim3(1), dim3(1), 0, H, cs.d_pq + 1, tend);
-            BSW_TRY(hipGetLastError());
-            if (dbg) BSW_TRY(hipEventRecord(dc.pq_dbg[1][c], H));
-            if (dbg)
-                fprintf(stderr, "pq chunk %d: %d pairs, staged %.3f .. %.3f ms\n", c, (int)q.m,
-                        std::chrono::duration<double, std::milli>(t0 - t_start).count(),
-                        std::chrono::duration<double, std::milli>(now() - t_start).count());
-        }
-        BSW_TRY(hipMemcpyAsync(dc.pq_hout, cs.d_scratch, (size_t)n * 24, hipMemcpyDeviceToHost, D));
-        BSW_TRY(hipMemcpyAsync(cs.h_meta + kMetaErr, cs.d_meta + kMetaErr, sizeof(int32_t), hipMemcpyDeviceToHost, D));
-        BSW_TRY(hipStreamSynchronize(D));
-        if (dbg) {
-            fprintf(stderr, "pq drained at %.3f ms\n", std::chrono::duration<double, std::milli>(now() - t_start).count());
-            for (int c = 0; c < nch; ++c) {      // device timeline from the grid's start event
-                float cp = 0.f, pb = 0.f;
-                (void)hipEventElapsedTime(&cp, dc.pq_t0, dc.pq_dbg[0][c]);
-                (void)hipEventElapsedTime(&pb, dc.pq_t0, dc.pq_dbg[1][c]);
-                fprintf(stderr, "pq chunk %d: copied at %.3f, published at %.3f ms after the grid start\n", c, cp, pb);
-            }
-            float kt = 0.f;
-            (void)hipEventElapsedTime(&kt, dc.pq_t0, dc.pq_t1);
-            fprintf(stderr, "pq grid span %.3f ms\n", kt);
-        }
-        const int32_t err = cs.h_meta[kMetaErr];
-        if (err & 8) return BSW_E_HIP;                         // aborted / poll bound (no caller record written)
-        if (err) return BSW_E_RANGE;
-        const int32_t *o = (const int32_t *)dc.pq_hout;
-        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(HostPool::workers() + 1, n >> 15));
-        HostPool::get().parallel_for(nt, [&](int t) {
-            for (int32_t i = (int32_t)((int64_t)n * t / nt); i < (int32_t)((int64_t)n * (t + 1) / nt); ++i) {
-                const int32_t *q = o + 6 * (int64_t)i;
-                SeqPair &p = pairs[i];
-                p.score = q[0]; p.tle = q[1]; p.gtle = q[2]; p.qle = q[3]; p.gscore = q[4]; p.max_off = q[5];
-            }
-        });
-        return BSW_OK;
-    }();
-    if (rc != BSW_OK && dbg)
-        fprintf(stderr, "host_shard_pq: n %d, %d chunks: rc %d (%s), grid launched %d\n", (int)n, nch, rc,
-                bsw_strerror(rc), (int)launched);
-    if (rc != BSW_OK && launched) {
-        // end the running grid (its waves poll *abort), then drain every stream
-        int32_t one = 1;
-        if (hipMemcpyAsync(cs.d_pq + 2, &one, sizeof(one), hipMemcpyHostToDevice, H) == hipSuccess)
-            (void)hipStreamSynchronize(H);
-        (void)hipStreamSynchronize(D);
-        (void)hipStreamSynchronize(H);
-        (void)hipStreamSynchronize(C);
-    }
-    if (rc == BSW_OK && st) {
-        bsw_stats_t agg{};
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, dc.pq_t0, dc.pq_t1) == hipSuccess) agg.kernel_ms = ms;
-        agg.n_packed = n; agg.n_launches = 1;
-        (cell_bits == 8 ? agg.n_u8 : agg.n_i16) += n;
-        agg.stage_ms = (float)stage_ms;
-        agg.host_ms = (float)std::chrono::duration<double, std::milli>(now() - t_start).count();
-        *st = agg;
-    }
-    for (int k = 0; k < kSlots; ++k) dc.give_back(std::move(slots[k]), rc);
-    return rc;
-}
-
-// The 2-bit form of the persistent pipeline (BSW_PQ_2BIT=1, experiment): chunks cross PCIe as 2-bit
-// codes + exception words + 20-B records (stage_chunk; ~45% fewer bytes than nibbles) and the
-// helper CUs expand them (stage_in_kernel) into call-wide byte buffers at the chunk's caller offsets;
-// the DP grid reads SeqPair records and bytes.  Needs ascending chunk extents (one span each for
-// targets and queries: r0..r1, q0..q1).  Otherwise as host_shard_pq.
-static int host_shard_pq2(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref, const uint8_t *qer,
-                          int32_t n, int32_t w, int cell_bits, const std::vector<std::pair<int32_t, int32_t>> &chs,
-                          const std::vector<BlkStat> &bs, int64_t r0, int64_t r1, int64_t q0, int64_t q1,
-                          bsw_stats_t *st)
-{
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    const auto t_start = now();
-    std::lock_guard<std::mutex> g(dc.pq_mu);
-    BSW_TRY(hipSetDevice(dc.device));
-    if (!ensure_pq_streams(dc)) return 1;
-    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;
-    constexpr int kSlots = 3;
-    std::unique_ptr<Slot> slots[kSlots];
-    int rc = BSW_OK;
-    for (int k = 0; k < kSlots; ++k) {
-        slots[k] = dc.acquire(rc);
-        if (rc) {
-            for (int j = 0; j < k; ++j) dc.give_back(std::move(slots[j]));
-            return rc;
-        }
-    }
-    hipStream_t H = dc.pq_h, D = dc.pq_d;
-    Slot &cs = *slots[0];
-    hipStream_t C = cs.stream;
-    const int nch = (int)chs.size();
-    bool launched = false;
-    double stage_ms = 0;
-    rc = [&]() -> int {
-        int32_t mmax = 0, ntiles = 0;
-        for (const auto &c : chs) {
-            const int32_t m = std::min(n, c.second * kStageBlk) - c.first * kStageBlk;
-            mmax = std::max(mmax, m);
-            ntiles += (m + 63) / 64;
-        }
-        BSW_TRY(grow(cs.d_pairs, cs.cap_pairs, (size_t)n));
-        BSW_TRY(grow(cs.d_ref, cs.cap_ref, (size_t)(r1 - r0) + 16));
-        BSW_TRY(grow(cs.d_qer, cs.cap_qer, (size_t)(q1 - q0) + 16));
-        BSW_TRY(grow_sort(cs, n));
-        BSW_TRY(grow(cs.d_pq, cs.cap_pq, (size_t)4));
-        BSW_TRY(grow(cs.d_scratch, cs.cap_scratch, (size_t)n * 3 + 1));
-        size_t tmp_bytes = 0;
-        BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, cs.d_keys, cs.d_keys2, cs.d_vals, cs.d_order,
-                                                   mmax, 0, kKeyBits, H));
-        BSW_TRY(grow(cs.d_tmp, cs.cap_tmp, tmp_bytes));
-        // every staging buffer at its final size before the grid starts (no hipFree mid-call)
-        for (int c = 0; c < nch; ++c) {
-            Slot &s = *slots[c % kSlots];
-            int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
-            for (int32_t b = chs[c].first; b < chs[c].second; ++b) {
-                r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
-                q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi);
-            }
-            const size_t rb = r_lo == INT64_MAX ? 0 : (size_t)(r_hi - r_lo), qb = q_lo == INT64_MAX ? 0 : (size_t)(q_hi - q_lo);
-            const size_t m = (size_t)(std::min(n, chs[c].second * kStageBlk) - chs[c].first * kStageBlk);
-            const size_t b2 = std::max(align256(align256(align256(m * sizeof(PairIn)) + (rb + 3) / 4 + 4) + (qb + 3) / 4 + 4) +
-                                           ((rb + qb) / 32 + 1024) * 4, m * 24);
-            const size_t b4 = align256(align256(m * sizeof(SeqPair)) + (rb + 1) / 2 + 4) + (qb + 1) / 2 + 4;
-            const size_t need = std::max(b2, b4) + 4096;
-            if (need > s.cap_stage) {
-                if (s.h_stage) (void)hipHostFree(s.h_stage);
-                s.h_stage = nullptr; s.cap_stage = 0;
-                BSW_TRY(hipHostMalloc(&s.h_stage, need, 0));
-                s.cap_stage = need;
-            }
-            BSW_TRY(grow(s.d_stage, s.cap_dstage, need));
-        }
-        if (dc.pq_hout_cap < (size_t)n * 24) {
-            if (dc.pq_hout) (void)hipHostFree(dc.pq_hout);
-            dc.pq_hout = nullptr; dc.pq_hout_cap = 0;
-            const size_t cap = (size_t)n * 24 + (size_t)n * 6;
-            BSW_TRY(hipHostMalloc(&dc.pq_hout, cap, 0));
-            dc.pq_hout_cap = cap;
-        }
-        PqArgs a{};
-        a.kp = kp; a.w = w; a.pairs = cs.d_pairs; a.order = cs.d_order;
-        a.ref = cs.d_ref - r0; a.qer = cs.d_qer - q0;
-        a.err = cs.d_meta + kMetaErr; a.head = cs.d_pq; a.ready = cs.d_pq + 1; a.abort = cs.d_pq + 2;
-        a.nchunks = nch; a.ntiles = ntiles;
-        for (int c = 0, t = 0; c < nch; ++c) {
-            const int32_t a0 = chs[c].first * kStageBlk, m = std::min(n, chs[c].second * kStageBlk) - a0;
-            a.chunks[c] = PqChunk{t, a0, m, a0, 0, 0, 0};
-            t += (m + 63) / 64;
-        }
-        BSW_TRY(hipMemsetAsync(cs.d_meta, 0, kMetaWords * sizeof(int32_t), H));
-        BSW_TRY(hipMemsetAsync(cs.d_pq, 0, 4 * sizeof(int32_t), H));
-        BSW_TRY(hipEventRecord(dc.pq_init, H));
-        BSW_TRY(hipStreamWaitEvent(D, dc.pq_init, 0));
-        BSW_TRY(hipEventRecord(dc.pq_t0, D));
-        BSW_TRY(launch_pq_kernel(a, std::min(ntiles, 8 * (dc.pq_ncu - dc.pq_nres)), D));
-        launched = true;
-        BSW_TRY(hipEventRecord(dc.pq_t1, D));
-        for (int c = 0, tend = 0; c < nch; ++c) {
-            const int k = c % kSlots;
-            Slot &s = *slots[k];
-            const int32_t b = chs[c].first, nb = chs[c].second - b;
-            const int32_t a0 = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a0;
-            tend += (m + 63) / 64;
-            if (c >= kSlots) BSW_TRY(hipEventSynchronize(dc.pq_ev[k]));   // slot k's last chunk expanded
-            const auto t0 = now();
-            StagedChunk sc;
-            if (int r = stage_chunk(s, pairs + a0, ref, qer, m, bs.data() + b, nb, true, sc)) return r;
-            stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
-            if (!sc.packed) return BSW_E_HIP;                 // (cannot happen: host_shard checked the extents)
-            BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, sc.bytes, hipMemcpyHostToDevice, C));
-            BSW_TRY(hipEventRecord(dc.pq_init, C));
-            BSW_TRY(hipStreamWaitEvent(H, dc.pq_init, 0));
-            uint8_t *dr = cs.d_ref + (sc.r_base - r0), *dq = cs.d_qer + (sc.q_base - q0);
-            if (sc.mode == kStage2bit) {
-                const int64_t tr = ((int64_t)sc.rb + 15) / 16, tq = ((int64_t)sc.qb + 15) / 16;
-                const int64_t nthr = tr + tq + m;
-                hipLaunchKernelGGL(stage_in_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, H,
-                                   s.d_stage + sc.ref_off, (int64_t)sc.rb, s.d_stage + sc.qer_off, (int64_t)sc.qb,
-                                   (const uint32_t *)(s.d_stage + sc.exc_off), sc.n_exr, sc.n_exr + sc.n_exq,
-                                   (const PairIn *)(s.d_stage + sc.pair_off), m, dr, dq, cs.d_pairs + a0,
-                                   (int32_t *)nullptr);
-            } else {                                           // nibbles + whole records
-                const int64_t tr = ((int64_t)sc.rb + 7) / 8, tq = ((int64_t)sc.qb + 7) / 8;
-                if (tr > 0)
-                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, H,
-                                       s.d_stage + sc.ref_off, dr, (int64_t)sc.rb);
-                if (tq > 0)
-                    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, H,
-                                       s.d_stage + sc.qer_off, dq, (int64_t)sc.qb);
-                BSW_TRY(hipMemcpyAsync(cs.d_pairs + a0, s.d_stage + sc.pair_off, (size_t)m * sizeof(SeqPair),
-                                       hipMemcpyDeviceToDevice, H));
-            }
-            BSW_TRY(hipGetLastError());
-            BSW_TRY(hipEventRecord(dc.pq_ev[k], H));
-            hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, H, cs.d_pairs + a0, m, kp,
-                               w, 1, 0, a.ref, a.qer, cs.d_keys, cs.d_vals, cs.d_meta, cs.d_meta + kMetaMaxq,
-                               (int)kp.keymode, 0);
-            BSW_TRY(hipGetLastError());
-            size_t tb = cs.cap_tmp;
-            BSW_TRY(hipcub::DeviceRadixSort::SortPairs(cs.d_tmp, tb, cs.d_keys, cs.d_keys2, cs.d_vals,
-                                                       cs.d_order + a0, m, 0, kKeyBits, H));
-            hipLaunchKernelGGL(pq_publish_kernel, dim3(1), dim3(1), 0, H, cs.d_pq + 1, tend);
-            BSW_TRY(hipGetLastError());
-            if (dbg) {
-                if (!dc.pq_dbg[1][c]) BSW_TRY(hipEventCreate(&dc.pq_dbg[1][c]));
-                BSW_TRY(hipEventRecord(dc.pq_dbg[1][c], H));
-            }
-        }
-        int32_t *d_out = (int32_t *)cs.d_scratch;
-        hipLaunchKernelGGL(gather_outputs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, D, cs.d_pairs, d_out,
-                           n);
-        BSW_TRY(hipGetLastError());
-        BSW_TRY(hipMemcpyAsync(dc.pq_hout, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, D));
-        BSW_TRY(hipMemcpyAsync(cs.h_meta + kMetaErr, cs.d_meta + kMetaErr, sizeof(int32_t), hipMemcpyDeviceToHost, D));
-        BSW_TRY(hipStreamSynchronize(D));
-        if (dbg) {
-            for (int c = 0; c < nch; ++c) {
-                float pb = 0.f;
-                (void)hipEventElapsedTime(&pb, dc.pq_t0, dc.pq_dbg[1][c]);
-                fprintf(stderr, "pq2 chunk %d: published at %.3f ms after the grid start\n", c, pb);
-            }
-            float kt = 0.f;
-            (void)hipEventElapsedTime(&kt, dc.pq_t0, dc.pq_t1);
-            fprintf(stderr, "pq2 grid span %.3f ms\n", kt);
-        }
-        const int32_t err = cs.h_meta[kMetaErr];
-        if (err & 8) return BSW_E_HIP;
-        if (err) return BSW_E_RANGE;
-        const int32_t *o = (const int32_t *)dc.pq_hout;
-        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(HostPool::workers() + 1, n >> 15));
-        HostPool::get().parallel_for(nt, [&](int t) {
-            for (int32_t i = (int32_t)((int64_t)n * t / nt); i < (int32_t)((int64_t)n * (t + 1) / nt); ++i) {
-                const int32_t *q = o + 6 * (int64_t)i;
-                SeqPair &p = pairs[i];
-                p.score = q[0]; p.tle = q[1]; p.gtle = q[2]; p.qle = q[3]; p.gscore = q[4]; p.max_off = q[5];
-            }
-        });
-        return BSW_OK;
-    }();
-    if (rc != BSW_OK && dbg)
-        fprintf(stderr, "host_shard_pq2: n %d, %d chunks: rc %d (%s), grid launched %d\n", (int)n, nch, rc,
-                bsw_strerror(rc), (int)launched);
-    if (rc != BSW_OK && launched) {
-        int32_t one = 1;
-        if (hipMemcpyAsync(cs.d_pq + 2, &one, sizeof(one), hipMemcpyHostToDevice, H) == hipSuccess)
-            (void)hipStreamSynchronize(H);
-        (void)hipStreamSynchronize(D);
-        (void)hipStreamSynchronize(H);
-        (void)hipStreamSynchronize(C);
-    }
-    if (rc == BSW_OK && st) {
-        bsw_stats_t agg{};
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, dc.pq_t0, dc.pq_t1) == hipSuccess) agg.kernel_ms = ms;
-        agg.n_packed = n; agg.n_launches = 1;
-        (cell_bits == 8 ? agg.n_u8 : agg.n_i16) += n;
-        agg.stage_ms = (float)stage_ms;
-        agg.host_ms = (float)std::chrono::duration<double, std::milli>(now() - t_start).count();
-        *st = agg;
-    }
-    for (int k = 0; k < kSlots; ++k) dc.give_back(std::move(slots[k]), rc);
-    return rc;
-}
-
 // One device's share of a host-buffer call: a pipeline of chunks over the device's slots (four by default).
 // Per chunk: stage into the slot's pinned buffer (records + nibble-packed sequences, host
 // pool) -> one H2D -> unpack -> plan / sort -> DP kernels -> D2H of the records.  The calling
@@ -2099,17 +1152,11 @@ static int host_shard_pq2(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
 // chunk k's kernels only after chunk k + 1 was staged: ~1.4 ms of idle GPU per chunk in the
 // rocprofv3 timeline).  Chunks ramp from ~n/32 pairs up to `chunk` so the first kernels start
 // early.  Outputs are identical to one unchunked call (pairs are independent).
-static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref,
+static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const uint8_t *ref,
                       const uint8_t *qer, int32_t n, int32_t w, int cell_bits, int32_t chunk, bool two_bit,
                       bsw_stats_t *st)
 {
     if (n == 0) return BSW_OK;
-    // the chunks' DP kernels run with LDS padding that caps their waves per CU, so the next chunk's
-    // helper kernels (unpack, plan, sort, gather, copies) find free wave slots instead of queuing
-    // ~1 ms behind DP waves (kernel + copy trace): BSW_HP_LDS_PAD bytes (experiment)
-    static const int hp_pad = getenv("BSW_HP_LDS_PAD") ? std::max(0, atoi(getenv("BSW_HP_LDS_PAD"))) : -1;
-    KParams kp = kp0;
-    if (hp_pad >= 0) kp.lds_pad = hp_pad;
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto t_start = now();
     // the whole prepass (validation + per-block byte extents) before chunk 0: validating only chunk
@@ -2117,123 +1164,30 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
     std::vector<BlkStat> bs;
     if (!prepass(pairs, n, bs)) return BSW_E_RANGE;
     if (chunk <= 0) chunk = n;
-    // the persistent DP pipeline (BSW_OPT_PERSIST >= 1) when every pair fits pc_kernel<160>, the call is
-    // past the small-batch kernels' sizes and its chunks' byte extents are bulk and ascending
-    if (kp0.persist >= 1 && kp0.pk_ok && kp0.kern8 == 1 && !kp0.misroute && kp0.maxsc == 1 && two_bit &&
-        n > kp0.small_batch && n > kp0.mid_batch) {
-        bool ok = true;
-        for (const BlkStat &b : bs) ok = ok && b.fast;
-        // chunks: a first one that fills the grid's waves (~2K tiles), then `chunk`-sized ones (no
-        // ramp: there are no per-chunk tails to hide); BSW_PQ_FIRST / BSW_PQ_CHUNK (blocks) override
-        std::vector<std::pair<int32_t, int32_t>> chs;
-        {
-            const int32_t nblk = (int32_t)bs.size();
-            const char *e1 = getenv("BSW_PQ_FIRST"), *e2 = getenv("BSW_PQ_CHUNK");
-            const int32_t first = e1 ? std::max(1, atoi(e1)) : 31;
-            const int32_t step = e2 ? std::max(1, atoi(e2)) : std::max<int32_t>(1, chunk / kStageBlk);
-            for (int32_t b = 0, nb = first; b < nblk; b += nb, nb = step) {
-                int64_t bytes = 0;
-                int32_t k = 0;
-                for (; k < nb && b + k < nblk; ++k) {
-                    const int64_t x = bs[b + k].r_sum + bs[b + k].q_sum;
-                    if (k > 0 && bytes + x > ((int64_t)1 << 29)) break;
-                    bytes += x;
-                }
-                chs.emplace_back(b, b + k);
-                nb = k;
-            }
-        }
-        ok = ok && !chs.empty() && (int)chs.size() <= kPqMaxChunks;
-        for (size_t c = 0; ok && c < chs.size(); ++c) {
-            int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
-            for (int32_t b = chs[c].first; b < chs[c].second; ++b) {
-                r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi); r_sum += bs[b].r_sum;
-                q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi); q_sum += bs[b].q_sum;
-            }
-            // bulk extents (the staged bytes ~ the chunk's own), nibble offsets inside int32
-            if (r_lo != INT64_MAX) ok = ok && (r_hi - r_lo) <= r_sum + r_sum / 4 + 4096 && (r_hi - r_lo) < ((int64_t)1 << 30);
-            if (q_lo != INT64_MAX) ok = ok && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096 && (q_hi - q_lo) < ((int64_t)1 << 30);
-        }
-        if (getenv("BSW_DEBUG_HP")) fprintf(stderr, "persistent pipeline: eligible %d (%d chunks)\n", (int)ok, (int)chs.size());
-        if (ok && getenv("BSW_PQ_2BIT")) {        // (experiment) the 2-bit form: ascending extents, one span
-            int64_t r0 = INT64_MAX, r1 = 0, q0 = INT64_MAX, q1 = 0, pr = INT64_MIN, pqx = INT64_MIN;
-            bool asc = true;
-            for (const auto &ch : chs) {
-                int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0;
-                for (int32_t b = ch.first; b < ch.second; ++b) {
-                    r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi);
-                    q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi);
-                }
-                if (r_lo != INT64_MAX) { asc = asc && r_lo >= pr; pr = r_hi; r0 = std::min(r0, r_lo); r1 = std::max(r1, r_hi); }
-                if (q_lo != INT64_MAX) { asc = asc && q_lo >= pqx; pqx = q_hi; q0 = std::min(q0, q_lo); q1 = std::max(q1, q_hi); }
-            }
-            if (r0 == INT64_MAX) r0 = r1 = 0;
-            if (q0 == INT64_MAX) q0 = q1 = 0;
-            if (asc) {
-                const int r = host_shard_pq2(kp0, dc, pairs, ref, qer, n, w, cell_bits, chs, bs, r0, r1, q0, q1, st);
-                if (r != 1) return r;
-            }
-        }
-        if (ok) {
-            const int r = host_shard_pq(kp0, dc, pairs, ref, qer, n, w, cell_bits, chs, bs, st);
-            if (r != 1) return r;
-        }
-    }
-    // the fast path (no device helper kernels) when every pair fits the packed-column kernel and the
-    // call is past the small-batch kernels' sizes (those are latency-bound: the row-group kernel)
-    // opt-in (BSW_HP_FAST=1, read per call): same box, interleaved, the general pipeline ran 1M-pair
-    // calls in 12.1 ms and this path in 14.9 ms (profiles/r05/hostpath_fast_ab.txt: the host sort +
-    // nibble staging of each chunk is slower than the device plan / sort it replaces)
-    const char *fe = getenv("BSW_HP_FAST");
-    const bool fast_on = fe != nullptr && atoi(fe) != 0;
-    if (fast_on && kp0.pk_ok && kp0.kern8 == 1 && !kp0.misroute && kp0.maxsc == 1 && n > kp0.small_batch &&
-        n > kp0.mid_batch && two_bit) {
-        bool ok = true;
-        for (const BlkStat &b : bs) ok = ok && b.fast;
-        // every chunk's byte extents must be contiguous (the upstream layout; permuted batches take the
-        // general path, which gathers) and addressable as int32 nibble offsets
-        for (const auto &ch : fast_chunks(bs, n, chunk)) {
-            int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
-            for (int32_t b = ch.first; b < ch.second; ++b) {
-                r_lo = std::min(r_lo, bs[b].r_lo); r_hi = std::max(r_hi, bs[b].r_hi); r_sum += bs[b].r_sum;
-                q_lo = std::min(q_lo, bs[b].q_lo); q_hi = std::max(q_hi, bs[b].q_hi); q_sum += bs[b].q_sum;
-            }
-            if (r_lo == INT64_MAX) r_lo = r_hi = 0;
-            if (q_lo == INT64_MAX) q_lo = q_hi = 0;
-            ok = ok && (r_hi - r_lo) <= r_sum + r_sum / 4 + 4096 && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096 &&
-                 (r_hi - r_lo) < ((int64_t)1 << 30) && (q_hi - q_lo) < ((int64_t)1 << 30);
-        }
-        if (ok) return host_shard_fast(kp, dc, pairs, ref, qer, n, w, cell_bits, chunk, bs, st);
-    }
     // slots are taken as chunks start (a one-chunk call takes one); chunk k + nslots stages only
     // once chunk k's outputs are back.  4 since round 4: with the helper stream the fourth slot
     // lets the next chunk stage a DP generation earlier (same box, alternating: 84.7 / 87.7 vs
     // 77.0 / 78.8 M/s per 1M-pair call; 5 slots pay more first-call allocation,
-    // profiles/r04/hostpath_slots_r4w.txt).  BSW_HP_SLOTS (2..6) overrides
-    constexpr int kMaxSlots = 6;
-    static const int nslots = [] {
-        const char *e = getenv("BSW_HP_SLOTS");
-        return e ? std::min(6, std::max(2, atoi(e))) : 4;
-    }();
+    // profiles/r04/hostpath_slots_r4w.txt)
+    constexpr int nslots = 4;
     int rc = BSW_OK;
-    std::unique_ptr<Slot> slots[kMaxSlots];
+    std::unique_ptr<Slot> slots[nslots];
     slots[0] = dc.acquire(rc);
     if (rc) return rc;
-    int32_t pend_at[kMaxSlots] = {}, pend_n[kMaxSlots] = {};  // chunk in flight per slot
-    int32_t pend_seq[kMaxSlots] = {-1, -1, -1, -1, -1, -1};
-    int pend_mode[kMaxSlots] = {};
+    int32_t pend_at[nslots] = {}, pend_n[nslots] = {};  // chunk in flight per slot
+    int32_t pend_seq[nslots] = {-1, -1, -1, -1};
+    int pend_mode[nslots] = {};
     bsw_stats_t agg{};
     // Everything but the DP kernels runs on the slot's high-priority stream: the next chunk's
     // copies, unpack / plan / sort kernels and the outputs' readback are dispatched ahead of the
-    // queued DP workgroups instead of behind them (BSW_HP_ONE_STREAM=1: all on the slot's stream)
-    const bool hp_split = getenv("BSW_HP_ONE_STREAM") == nullptr;
+    // queued DP workgroups instead of behind them
     // launcher thread: chunk seq numbers in order; launched[k] = last seq whose DP is enqueued
     struct Launcher {
         std::mutex mu;
         std::condition_variable cv;
         struct Job { int first; int32_t second; int mode; };
         std::deque<Job> q;                        // (slot, seq, staging mode)
-        int32_t launched[kMaxSlots] = {-1, -1, -1, -1, -1, -1};
+        int32_t launched[nslots] = {-1, -1, -1, -1};
         bool stop = false;
         int rc = BSW_OK;
     } L;
@@ -2259,8 +1213,8 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
             // guard readback) is done: on the DP stream they would queue behind the next chunks'
             // DP workgroups (a 1.4 ms copy in the trace)
             hipStream_t os = p.run_stream;
-            hipStream_t hs = p.plan.plan_stream;       // the chunk's helper stream (hp_split)
-            if (!r && hp_split && hs && p.run_stream != hs) {
+            hipStream_t hs = p.plan.plan_stream;       // the chunk's helper stream
+            if (!r && hs && p.run_stream != hs) {
                 if (!p.evd && hipEventCreateWithFlags(&p.evd, hipEventDisableTiming) != hipSuccess) r = BSW_E_HIP;
                 if (!r && (hipEventRecord(p.evd, p.run_stream) != hipSuccess ||
                            hipStreamWaitEvent(hs, p.evd, 0) != hipSuccess))
@@ -2318,11 +1272,8 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
     auto enqueue = [&](int k, int32_t seq, const StagedChunk &c, int32_t m) -> int {
         Slot &s = *slots[k];
         const int r = [&]() -> int {
-            if (hp_split) {
-                if (int e = ensure_pstream(s)) return e;
-                ensure_cu_streams(s);
-            }
-            hipStream_t hs = hp_split ? (s.hstream ? s.hstream : s.pstream) : s.stream;
+            if (int e = ensure_pstream(s)) return e;
+            hipStream_t hs = s.pstream;
             BSW_TRY(grow(s.d_stage, s.cap_dstage, c.bytes));
             BSW_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, c.bytes, hipMemcpyHostToDevice, hs));
             const uint8_t *d_r = s.d_stage + c.ref_off, *d_q = s.d_stage + c.qer_off;
@@ -2368,10 +1319,8 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
             pc.d_ref = d_r - c.r_base;
             pc.d_qer = d_q - c.q_base;
             pc.n = m; pc.w = w; pc.cell_bits = cell_bits; pc.stream = hs;
-            if (hp_split) {
-                pc.dp_stream = s.dstream ? s.dstream : s.stream;
-                pc.plan_stream = hs;
-            }
+            pc.dp_stream = s.stream;
+            pc.plan_stream = hs;
             return run_plan(kp, s, pc);
         }();
         {
@@ -2395,13 +1344,11 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
         bool stop = false;
     } E;
     const int32_t nblk0 = (int32_t)bs.size();
-    // the first chunk: 16 blocks (64K pairs) or 1/32 of the call; BSW_HP_FIRST_BLK (experiment
-    // knob) overrides the 16.  The same size decides whether the call runs as several chunks
-    // (enqueuer thread) and cuts the chunks below
-    static const int32_t kFirst = getenv("BSW_HP_FIRST_BLK") ? std::max(1, atoi(getenv("BSW_HP_FIRST_BLK"))) : 16;
+    // the first chunk: 16 blocks (64K pairs) or 1/32 of the call.  The same size decides whether
+    // the call runs as several chunks (enqueuer thread) and cuts the chunks below
     const int32_t first_blk = std::min(std::max<int32_t>(1, chunk / kStageBlk),
-                                       nblk0 <= 32 ? nblk0 : std::max<int32_t>(kFirst, nblk0 / 32));
-    const bool async = nblk0 > first_blk && getenv("BSW_HP_INLINE_ENQ") == nullptr;
+                                       nblk0 <= 32 ? nblk0 : std::max<int32_t>(16, nblk0 / 32));
+    const bool async = nblk0 > first_blk;
     std::thread enqueuer;
     if (async)
         enqueuer = std::thread([&] {
@@ -2434,10 +1381,6 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
         if (enqueuer.joinable()) enqueuer.join();
     };
     double stage_ms = 0;
-    const bool dbg = getenv("BSW_DEBUG_HP") != nullptr;     // per-chunk host timeline (A/B tooling)
-    auto ms_since = [&](std::chrono::steady_clock::time_point t) {
-        return std::chrono::duration<double, std::milli>(t - t_start).count();
-    };
     rc = [&]() -> int {
         BSW_TRY(hipSetDevice(dc.device));
         int k = 0;
@@ -2459,7 +1402,6 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
             // two generations at two waves per SIMD -- and the call got ~1 ms slower; as its own
             // launch it runs beside the last chunk on another queue.  Measured)
             const int32_t a = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a;
-            const auto tw = now();
             int r = finish(k);                          // slot k's last chunk
             if (r) return r;
             if (!slots[k]) {
@@ -2471,9 +1413,6 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
             const auto t0 = now();
             if ((r = stage_chunk(s, pairs + a, ref, qer, m, bs.data() + b, nb, two_bit, c))) return r;
             stage_ms += std::chrono::duration<double, std::milli>(now() - t0).count();
-            if (dbg)
-                fprintf(stderr, "hp chunk %d: %d pairs  finish-wait %.3f..%.3f  stage %.3f..%.3f ms\n", (int)seq, (int)m,
-                        ms_since(tw), ms_since(t0), ms_since(t0), ms_since(now()));
             pend_at[k] = a; pend_n[k] = m; pend_mode[k] = c.mode; pend_seq[k] = seq;
             if (async) {
                 {
@@ -2489,7 +1428,6 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
             const int r = finish(j);
             if (r) return r;
         }
-        if (dbg) fprintf(stderr, "hp drained at %.3f ms\n", ms_since(now()));
         return BSW_OK;
     }();
     stop_enqueuer();                                    // drains its queue first (every job reaches the launcher)
@@ -2500,8 +1438,7 @@ static int host_shard(const KParams &kp0, DeviceCtx &dc, SeqPair *pairs, const u
         if (!slots[k]) continue;
         if (rc) {                                       // nothing in flight on a returned slot
             (void)hipStreamSynchronize(slots[k]->stream);
-            for (hipStream_t st : {slots[k]->pstream, slots[k]->hstream, slots[k]->dstream})
-                if (st) (void)hipStreamSynchronize(st);
+            if (slots[k]->pstream) (void)hipStreamSynchronize(slots[k]->pstream);
         }
         dc.give_back(std::move(slots[k]));
     }
@@ -2542,7 +1479,7 @@ struct AggSeg {                                 // one call inside a coalesced b
 };
 
 static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg> &segs, int32_t N, int64_t r_tot,
-                            int64_t q_tot, int32_t w, int cell_bits, bool busy, bsw_stats_t &st)
+                            int64_t q_tot, int32_t w, int cell_bits, bsw_stats_t &st)
 {
     int rc = BSW_OK;
     auto slot = dc.acquire(rc);
@@ -2644,20 +1581,11 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
             }
         pc.gq_maxq = gq_max;
         pc.gq_maxt = gq_mt;
-        // another batch is already on this device (concurrent kt_for callers): the GPU is shared,
-        // so a batch of busy_min pairs or more goes to the packed-column lane kernels (~5x the
-        // row-group kernel's work per cell's instructions) instead of the latency kernels
-        if (busy && kp.busy_min > 0 && N >= kp.busy_min) {
-            pc.tput = true;
-            pc.gq_maxq = -1;
-        }
         // host-checked row-group batch: the kernel writes the 24 output bytes per pair straight
         // into the staging buffer (its inputs were expanded out of it above)
         if (pc.gq_maxq >= 0) pc.d_out24 = (int32_t *)s.d_stage;
         int r = run_plan(kp, s, pc);
-        const auto tg2 = std::chrono::steady_clock::now();
         if (!r) r = run_dp(kp, s);
-        const auto tg3 = std::chrono::steady_clock::now();
         if (r) {
             (void)hipStreamSynchronize(s.stream);
             return r;
@@ -2669,16 +1597,8 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
         }
         BSW_TRY(hipMemcpyAsync(s.h_stage, s.d_stage, (size_t)N * 24, hipMemcpyDeviceToHost, s.stream));
         // the leader polls its batch (~0.3 ms) instead of the runtime's blocking wait: 8 callers x 1K
-        // coalesced 11.4 / 12.4 -> 14.1 / 13.5 M/s (same box, alternating; profiles/r05/slot_ownq_percall.txt);
-        // BSW_SMALL_SPIN=0 restores the blocking wait
-        static const bool spin = !getenv("BSW_SMALL_SPIN") || atoi(getenv("BSW_SMALL_SPIN")) != 0;
-        if ((r = finish_stats(s, spin))) return r;
-        const auto tg4 = std::chrono::steady_clock::now();
-        if (getenv("BSW_DEBUG_AGG")) {
-            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-            fprintf(stderr, "agg batch %d calls %d pairs: stage %.3f enqueue %.3f plan-wait %.3f dp+d2h %.3f (kernel %.3f)\n",
-                    (int)segs.size(), N, ms(tg0, tg1), ms(tg1, tg2), ms(tg2, tg3), ms(tg3, tg4), s.stats.kernel_ms);
-        }
+        // coalesced 11.4 / 12.4 -> 14.1 / 13.5 M/s (same box, alternating; profiles/r05/slot_ownq_percall.txt)
+        if ((r = finish_stats(s, true))) return r;
         const int32_t *out = (const int32_t *)s.h_stage;
         auto scatter = [&](int g) {
             SeqPair *p = segs[g].r->pairs;
@@ -2689,8 +1609,7 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
             }
         };
         // a few thousand records: on this thread (waking the host pool costs more than the copy)
-        static const bool pool_scatter = getenv("BSW_SMALL_POOL") && atoi(getenv("BSW_SMALL_POOL")) != 0;
-        if (!pool_scatter && N <= 16384)
+        if (N <= 16384)
             for (int g = 0; g < (int)segs.size(); ++g) scatter(g);
         else
             HostPool::get().parallel_for((int)segs.size(), scatter);
@@ -2705,8 +1624,7 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
 // One coalesced batch: calls that fail validation get BSW_E_RANGE; calls whose buffers are not
 // contiguous (scattered idr / idq) and batches with too many non-ACGT bytes run on their own
 // through host_shard.
-static void run_group(const KParams &kp, DeviceCtx &dc, std::vector<AggReq *> &G, int32_t chunk, bool two_bit,
-                      bool busy)
+static void run_group(const KParams &kp, DeviceCtx &dc, std::vector<AggReq *> &G, int32_t chunk, bool two_bit)
 {
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<AggSeg> segs;
@@ -2732,9 +1650,8 @@ static void run_group(const KParams &kp, DeviceCtx &dc, std::vector<AggReq *> &G
     }
     if (!segs.empty()) {
         bsw_stats_t st{};
-        const int rc = (r_tot < ((int64_t)1 << 28) && q_tot < ((int64_t)1 << 28))
-                           ? run_group_staged(kp, dc, segs, N, r_tot, q_tot, segs[0].r->w, segs[0].r->cell_bits, busy,
-                                              st)
+        const int rc = (r_tot < ((int64_t)1 << 30) && q_tot < ((int64_t)1 << 30))
+                           ? run_group_staged(kp, dc, segs, N, r_tot, q_tot, segs[0].r->w, segs[0].r->cell_bits, st)
                            : 1;
         if (rc == 1) {
             for (auto &g : segs) alone.push_back(g.r);
@@ -2764,7 +1681,6 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
     while (!me.done) {
         if (dc.agg_leaders < dc.agg_leaders_max && !dc.agg_q.empty()) {
             // lead: every queued call with the front call's (w, cell_bits, end_bonus), FIFO
-            const bool busy = dc.agg_leaders > 0;     // another batch in flight on this device
             // linger only when there are more callers than leader slots (batching is then the only
             // way to serve them all) and two or more batches run: with fewer callers the batches
             // must overlap instead -- a lingering leader serialised 2 callers (1K: 4.0 vs 6.8 M/s)
@@ -2808,7 +1724,7 @@ static int coalesced_call(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, cons
             lk.unlock();
             KParams gk = kp;
             gk.end_bonus = feb;
-            run_group(gk, dc, G, chunk, two_bit, busy);
+            run_group(gk, dc, G, chunk, two_bit);
             lk.lock();
             dc.agg_run -= tot;
             --dc.agg_nrun;
@@ -2957,8 +1873,8 @@ static int glob_device(const GlobParams &gp, Slot &s, SeqPair *d_pairs, const ui
     const bool want = d_cigar && stride > 0;
     // column classes keep only a narrow corridor of the traceback matrix (glob_lane_kernel: 3 dwords
     // per row instead of the band's ~10 at bwa-shaped w); jobs whose path leaves it rerun below with
-    // the full band window.  BSW_GLOB_TB_DW (experiment): dwords per row, 0 = full window always
-    static const int tb_env = getenv("BSW_GLOB_TB_DW") ? std::max(0, atoi(getenv("BSW_GLOB_TB_DW"))) : 3;
+    // the full band window
+    constexpr int tb_env = 3;
     if (want) BSW_TRY(grow(s.d_gretry, s.cap_gretry, (size_t)n + 1));
     BSW_TRY(hipEventRecord(s.ev0, st));
     int32_t off = 0;
@@ -3183,8 +2099,8 @@ static int one_device(bsw_ctx_t *ctx, int64_t n)
 
 // Recovery of a host-buffer range whose run on device d0 failed with BSW_E_NOMEM / BSW_E_HIP
 // (bsw.h, bsw_get_scores): 1. again on d0 after its cached slots are freed, 2. on each other
-// device of the context, 3. in halves (down to one 4096-pair staging block), each half the same
-// way.  No coalescing here: the range runs as a call of its own.  Outputs are identical to an
+// device of the context, 3. (BSW_E_NOMEM only) in halves (down to one 4096-pair staging block),
+// each half the same way.  No coalescing here: the range runs as a call of its own.  Outputs are identical to an
 // undisturbed call -- pairs are independent, and a failed run writes no input field (staged
 // records go back as outputs only or as the caller's own bytes).  `how` gets the deepest step
 // used.  Upstream plans to degrade on engine errors instead of aborting the run
@@ -3210,7 +2126,9 @@ static int recover_range(bsw_ctx_t *ctx, const KParams &kp, int d0, SeqPair *pai
         }
         if (!recoverable(rc)) return rc;
     }
-    if (n <= kStageBlk) return rc;
+    // halves only for memory: a smaller range needs smaller buffers, but it cannot fix a HIP error
+    // (a sticky context error repeats on every rerun)
+    if (rc != BSW_E_NOMEM || n <= kStageBlk) return rc;
     const int32_t h = std::max<int32_t>(kStageBlk, (n / 2) & ~(kStageBlk - 1));
     bsw_stats_t a{}, b{};
     if ((rc = recover_range(ctx, kp, d0, pairs, ref, qer, h, w, cell_bits, &a, how))) return rc;
@@ -3406,7 +2324,7 @@ int bsw_get_scores_packed_device(bsw_ctx_t *ctx, const void *d_packed, const bsw
     if (d.n < 0 || w < 0 || (cell_bits != 8 && cell_bits != 16)) return BSW_E_INVAL;
     if (d.n == 0) return BSW_OK;
     if (!d_packed || !d_out || d.ref_bytes < 0 || d.qer_bytes < 0 || d.n_exc_ref < 0 || d.n_exc_qer < 0 ||
-        d.ref_bytes >= ((int64_t)1 << 28) || d.qer_bytes >= ((int64_t)1 << 28) ||
+        d.ref_bytes >= ((int64_t)1 << 30) || d.qer_bytes >= ((int64_t)1 << 30) ||
         ((d.rec_off | d.ref_off | d.qer_off | d.exc_off) & 3) != 0)
         return BSW_E_INVAL;
     bsw::DeviceCtx &dc = *ctx->devs[0];
@@ -3706,7 +2624,16 @@ int bsw_set_reference(bsw_ctx_t *ctx, const uint8_t *ref, int64_t ref_len)
         dc.d_refres = nullptr;
         dc.refres_len = -1;
         BSW_TRY(hipMalloc((void **)&dc.d_refres, (size_t)ref_len + 64));
-        if (ref_len > 0) BSW_TRY(hipMemcpy(dc.d_refres, ref, (size_t)ref_len, hipMemcpyHostToDevice));
+        if (ref_len > 0) {
+            // on a non-blocking stream of its own: a null-stream copy would order against every
+            // blocking (CU-masked) slot stream of the process (DeviceCtx::acquire)
+            hipStream_t cs = nullptr;
+            BSW_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+            hipError_t e = hipMemcpyAsync(dc.d_refres, ref, (size_t)ref_len, hipMemcpyHostToDevice, cs);
+            if (e == hipSuccess) e = hipStreamSynchronize(cs);
+            (void)hipStreamDestroy(cs);
+            BSW_TRY(e);
+        }
         dc.refres_len = ref_len;
     }
     return BSW_OK;
@@ -3808,8 +2735,7 @@ int bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value)
     if (!ctx) return BSW_E_INVAL;
     const bool b01 = value == 0 || value == 1;
     switch (option) {
-    case BSW_OPT_PERSIST: if (value < 0 || value > 2) return BSW_E_INVAL; ctx->kp.persist = (int8_t)value; return BSW_OK;
-    case BSW_OPT_BUSY_MIN: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.busy_min = (int32_t)value; return BSW_OK;
+    case BSW_OPT_GQ32_MAX: if (value < 0 || value > INT32_MAX) return BSW_E_INVAL; ctx->kp.gq32_max = (int32_t)value; return BSW_OK;
     case BSW_OPT_KERNEL8: if (value < 0 || value > 2) return BSW_E_INVAL; ctx->kp.kern8 = (int8_t)value; return BSW_OK;
     case BSW_OPT_FORK: if (!b01) return BSW_E_INVAL; ctx->kp.fork = (int8_t)value; return BSW_OK;
     case BSW_OPT_SORTKEY: if (!b01) return BSW_E_INVAL; ctx->kp.keymode = value ? 2 : 0; return BSW_OK;

@@ -38,15 +38,12 @@ struct KParams {
                                 //   BSW_OPT_GROUP_KERNEL)
     int32_t mid_batch;          // host: calls / chunks of (small_batch, mid_batch] pairs run on
                                 //   the quad row-group kernel (BSW_OPT_MID_BATCH, 0 = off)
-    int32_t busy_min;           // host: coalesced batches of at least this many pairs run on the
-                                //   lane kernels when another batch is in flight (BSW_OPT_BUSY_MIN)
     int32_t small_batch;        // host: calls / chunks of at most this many pairs run every
                                 //   qualifying pair on the wave kernel (latency, not
                                 //   throughput, bounds them; BSW_OPT_SMALL_BATCH, 0 = off)
-    int8_t persist;             // host: BSW_OPT_PERSIST (0 off, 1 host pipeline, 2 + device calls)
-    int32_t lds_pad;            // host: dynamic LDS bytes per packed-column workgroup (0 = none).
-                                //   LDS caps the DP waves per CU, so a host-pipeline chunk's DP
-                                //   leaves wave slots for the next chunk's helper kernels
+    int32_t gq32_max;           // host: batches of at most this many pairs (within small_batch)
+                                //   take the row-group kernel's 32-lane latency form
+                                //   (BSW_OPT_GQ32_MAX, default 2048)
 };
 
 // The kernels' input fields of a SeqPair (staged without the caller bookkeeping and outputs):
@@ -71,49 +68,6 @@ hipError_t launch_lane_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *p
 hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,
                             const int32_t *order, int32_t n, const uint8_t *ref,
                             const uint8_t *qer, int32_t *err, hipStream_t s);
-
-// Persistent tile-queue form of the QMAX-160 packed-column kernel (bsw_pc.hip pq_kernel).  Tiles are
-// 64 consecutive slots of `order`; chunk k owns tiles [chunks[k].tile0, chunks[k + 1].tile0) and
-// slots [slot0, slot0 + m).  PqArgs travels as the kernel's argument (~2.8 KB of kernarg; *head
-// zeroed before the launch).  ready == nullptr: every tile is runnable at launch; else tile t waits
-// until *ready > t (the host publishes chunks in tile order) and *abort != 0 ends the kernel
-// (err |= 8, as a 4-s poll does).  Same pair contract as launch_pc_kernel(160).
-//   nbase == nullptr: slot s runs pair idx_base + order[s] of `pairs` (SeqPair, byte sequences
-//     ref / qer indexed by idr / idq), outputs into the records;
-//   nbase != nullptr (the host pipeline): chunk k is a staged region of nbase -- PairIn records at
-//     rec_off, nibble-packed target / query extents at ref_off / qer_off (idr / idq = nibble
-//     indices) -- slot s runs the chunk's record order[s] and writes its 6 x int32 outputs to
-//     out24[6 (idx_base + order[s]) ..].
-struct PqChunk {
-    int32_t tile0, slot0, m, idx_base;
-    int64_t rec_off, ref_off, qer_off;
-};
-constexpr int kPqMaxChunks = 64;
-struct PqArgs {
-    KParams kp;
-    int32_t w;
-    SeqPair *pairs;
-    const int32_t *order;
-    const uint8_t *ref, *qer;
-    const uint8_t *nbase;
-    int32_t *out24;
-    int32_t *err;
-    int32_t *head;
-    const int32_t *ready;
-    const int32_t *abort;
-    int32_t nchunks, ntiles;
-    PqChunk chunks[kPqMaxChunks];
-};
-hipError_t launch_pq_kernel(const PqArgs &args, int32_t grid, hipStream_t s);
-
-// The same kernel (QMAX 160) over a host-staged chunk read in place (the host
-// pipeline's fast path): lane slot k runs pair order[k] (the host's schedule order), reading its
-// input fields recs[order[k]] -- idr / idq = NIBBLE indices into ref4 / qer4 (two codes per byte,
-// low nibble first; both 4-byte aligned) -- and writing its outputs as 6 x int32 to
-// out24[6 order[k] ..].  Same eligibility as launch_pc_kernel (qlen < 160, h0 + min(len1, len2)
-// <= 255, kp.pk_ok).
-hipError_t launch_pc_nib_kernel(const KParams &kp, int32_t w, const PairIn *recs, const int32_t *order, int32_t n,
-                                const uint8_t *ref4, const uint8_t *qer4, int32_t *out24, int32_t *err, hipStream_t s);
 
 // Wave-per-alignment band kernel (bsw_wv.hip): one SeqPair per wavefront, the row spread over
 // the 64 lanes as a sliding window of 64 * cols absolute columns (cols = 4, 8 or 16).  Needs

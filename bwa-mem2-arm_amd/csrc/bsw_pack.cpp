@@ -44,9 +44,13 @@ void pack_nibbles(uint8_t *dst, const uint8_t *src, size_t nbytes)
 }
 
 // 2-bit packing (round 2): staged byte k = code[4k] | code[4k+1] << 2 | code[4k+2] << 4 |
-// code[4k+3] << 6 (low two bits), plus an exception word (pos << 4 | low nibble) for every
-// byte outside 0..3 (N bases: 0.1% on C2), patched in HBM after the 2-bit unpack -- the same
-// bytes in HBM as the nibble path, at a quarter of the byte-per-base PCIe traffic.
+// code[4k+3] << 6 (low two bits), plus an exception word for every byte outside 0..3 (N bases:
+// 0.1% on C2), patched in HBM after the 2-bit unpack -- the same bytes in HBM as the nibble path,
+// at a quarter of the byte-per-base PCIe traffic.  Exception word (round 6) = pos << 2 | bits 2-3
+// of the code: the low two bits are already in the 2-bit plane, so positions get 30 bits (extents
+// up to 1 GiB; 28 bits with the whole nibble in the word).
+static inline uint32_t exc_word(uint32_t pos, uint8_t code) { return (pos << 2) | ((code & 15u) >> 2); }
+
 static inline __m128i pack2_lanes(__m128i x)      // 4 codes per dword -> one byte (low byte)
 {
     x = _mm_and_si128(x, _mm_set1_epi8(3));
@@ -59,7 +63,7 @@ static void pack_2bit_sse2(uint8_t *dst, const uint8_t *src, size_t nbytes, uint
 {
     auto scan = [&](size_t a, size_t b) {
         for (size_t k = a; k < b; ++k)
-            if (src[k] & 0xfc) exc.push_back(((pos0 + (uint32_t)k) << 4) | (src[k] & 15u));
+            if (src[k] & 0xfc) exc.push_back(exc_word(pos0 + (uint32_t)k, src[k]));
     };
     const __m128i hi = _mm_set1_epi8((char)0xfc), z = _mm_setzero_si128();
     const bool nt = ((uintptr_t)dst & 15) == 0;      // streaming stores (see pack_nibbles)
@@ -97,7 +101,7 @@ __attribute__((target("avx2"))) static inline void exc_avx2(__m256i v, const uin
         _mm256_cmpeq_epi8(_mm256_and_si256(v, _mm256_set1_epi8((char)0xfc)), _mm256_setzero_si256()));
     while (m) {
         const size_t k = at + (size_t)__builtin_ctz(m);
-        exc.push_back(((pos0 + (uint32_t)k) << 4) | (src[k] & 15u));
+        exc.push_back(exc_word(pos0 + (uint32_t)k, src[k]));
         m &= m - 1;
     }
 }
@@ -223,7 +227,7 @@ extern "C" int bsw_pack_batch(const SeqPair *pairs, const uint8_t *ref, const ui
     if (r_lo == INT64_MAX) r_lo = r_hi = 0;
     if (q_lo == INT64_MAX) q_lo = q_hi = 0;
     const int64_t rb = r_hi - r_lo, qb = q_hi - q_lo;
-    if (rb >= ((int64_t)1 << 28) || qb >= ((int64_t)1 << 28)) return BSW_E_RANGE;
+    if (rb >= ((int64_t)1 << 30) || qb >= ((int64_t)1 << 30)) return BSW_E_RANGE;
     if ((rb > 0 && !ref) || (qb > 0 && !qer)) return BSW_E_INVAL;
     auto count_exc = [](const uint8_t *s, int64_t len) {
         int64_t c = 0;

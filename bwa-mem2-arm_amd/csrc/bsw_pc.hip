@@ -41,7 +41,6 @@
 namespace bsw {
 
 constexpr int kPcChunkDw = 17;           // dwords per lane per 64-row target chunk (as lane kernel)
-constexpr int kPcChunkDwN = 9;           // the same for nibble-packed targets (8 codes per dword)
 #ifdef BSW_PC_STATS
 __device__ unsigned long long g_pc_stats[8];
 // per-wave schedule record (tools/pc_times.py): start / end (s_memrealtime, 100 MHz), XCC id and
@@ -582,27 +581,21 @@ __device__ __forceinline__ int pc_lastpos(std::integer_sequence<int, G...>, cons
 
 // WPB waves per workgroup: with 1, a wave's slot (and its LDS) is reused as soon as that wave
 // ends, instead of when the slowest of its block's waves ends.
-// NIB (the host pipeline's fast path, launch_pc_nib_kernel): inputs read in place from a staged
-// chunk -- records as PairIn in schedule order, sequences as nibbles (idr / idq nibble indices),
-// outputs as 6 x int32 into out24 -- so the chunk needs no unpack, plan, sort or gather kernel.
-// The target stream then carries 8 codes per dword: 9 dwords per lane per 64-row chunk.
-template <int QMAX, int WPB, bool BY, bool NIB = false>
+template <int QMAX, int WPB, bool BY>
 __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams kp, const int32_t w,
                                                     SeqPair *__restrict__ pairs,
                                                     const int32_t *__restrict__ order,
                                                     const int32_t n,
                                                     const uint8_t *__restrict__ ref,
                                                     const uint8_t *__restrict__ qer,
-                                                    int32_t *__restrict__ err,
-                                                    const PairIn *__restrict__ recs = nullptr,
-                                                    int32_t *__restrict__ out24 = nullptr)
+                                                    int32_t *__restrict__ err)
 {
     constexpr int NG = QMAX / 4;        // groups = query words (4 codes each)
-    constexpr int CDW = NIB ? kPcChunkDwN : kPcChunkDw;   // target dwords per lane per 64-row chunk
+    constexpr int CDW = kPcChunkDw;     // target dwords per lane per 64-row chunk
 #ifdef BSW_PC_STATS
     const unsigned long long t_wave0 = wall_clock64();
 #endif
-    __shared__ uint32_t s_tgt[WPB][2][CDW][64];   // 8.7 KB per wave (4.6 KB for nibbles)
+    __shared__ uint32_t s_tgt[WPB][2][CDW][64];   // 8.7 KB per wave
     __shared__ uint2 s_prof[8];                           // per-row score profiles, by target code
     if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(kp.prof[threadIdx.x][0], kp.prof[threadIdx.x][1]);
     __syncthreads();
@@ -612,12 +605,7 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
     SeqPair *sp = pairs + idx;
     int idr = 0, idq = 0, tlen = 0, qlen = 0, h0 = 0;
     if (valid) {
-        if constexpr (NIB) {
-            const PairIn r = recs[idx];
-            idr = r.idr; idq = r.idq; tlen = r.len1; qlen = r.len2; h0 = r.h0;
-        } else {
-            idr = sp->idr; idq = sp->idq; tlen = sp->len1; qlen = sp->len2; h0 = sp->h0;
-        }
+        idr = sp->idr; idq = sp->idq; tlen = sp->len1; qlen = sp->len2; h0 = sp->h0;
         if (qlen >= QMAX || qlen < 0 || tlen < 0 || h0 < 0 || h0 + min(qlen, tlen) > 255 || idr < 0 || idq < 0) {
             atomicOr(err, 1);
             valid = false;
@@ -626,28 +614,7 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
     // query codes, 4 per VGPR in byte order {c0, c2, c1, c3}: aligned dword loads (a dword
     // holding a byte of the query never leaves that byte's page), realigned by v_alignbyte
     uint32_t qs[NG];
-    if constexpr (NIB) {
-        // nibbles: the stream realigned by the lane's nibble offset (v_alignbit), then each group's
-        // 16 bits {c0, c1, c2, c3} spread to the bytes {c0, c2, c1, c3}
-        constexpr int NW = NG / 2 + 1;                    // dwords of 8 codes (+1: the offset)
-        uint32_t wv[NW + 1];
-        const uint32_t *wp = (const uint32_t *)qer + ((uint32_t)idq >> 3);
-        const uint32_t shb = 4u * ((uint32_t)idq & 7u);
-        const int nw = (valid && qlen > 0) ? (int)(((idq & 7) + qlen + 7) >> 3) : 0;
-        if (nw > 0) {
-#pragma unroll
-            for (int g = 0; g <= NW; ++g) wv[g] = wp[min(g, nw - 1)];
-        } else {
-#pragma unroll
-            for (int g = 0; g <= NW; ++g) wv[g] = 0;
-        }
-#pragma unroll
-        for (int g = 0; g < NG; g += 2) {
-            const uint32_t a = __builtin_amdgcn_alignbit(wv[g / 2 + 1], wv[g / 2], shb);
-            qs[g] = (a & 0x0F0Fu) | ((a & 0xF0F0u) << 12);
-            if (g + 1 < NG) qs[g + 1] = ((a >> 16) & 0x0F0Fu) | (((a >> 16) & 0xF0F0u) << 12);
-        }
-    } else {
+    {
         uint32_t wv[NG + 1];
         const uintptr_t qa = (uintptr_t)(qer + idq);
         const uint32_t *wp = (const uint32_t *)(qa & ~(uintptr_t)3);
@@ -708,18 +675,17 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
     }
     int best = h0, best_i = -1, best_j = -1, max_ie = -1, gsc = -1, moff = 0, endc = qlen;
     bool alive = valid && tlen > 0;
-    // target bases HBM -> LDS by LDS-DMA, 64-row chunks double-buffered (as the lane kernel);
-    // NIB: nibble stream, tsh = the first code's nibble offset in its dword
-    const uint8_t *tp = NIB ? ref + (((uint32_t)idr >> 3) << 2) : ref + idr;
-    const int tsh = NIB ? (idr & 7) : (int)((uintptr_t)tp & 3);
-    const uint32_t *twp = (const uint32_t *)(NIB ? tp : tp - tsh);
-    const int tlast = NIB ? max((tsh + tlen - 1) >> 3, 0) : max((tsh + tlen - 1) >> 2, 0);
+    // target bases HBM -> LDS by LDS-DMA, 64-row chunks double-buffered (as the lane kernel)
+    const uint8_t *tp = ref + idr;
+    const int tsh = (int)((uintptr_t)tp & 3);
+    const uint32_t *twp = (const uint32_t *)(tp - tsh);
+    const int tlast = max((tsh + tlen - 1) >> 2, 0);
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     auto issue_chunk = [&](int ch) {
         uint32_t *dst = &s_tgt[wv][ch & 1][0][0];
 #pragma unroll
         for (int k = 0; k < CDW; ++k)
-            __builtin_amdgcn_global_load_lds((gptr_t)(twp + min((NIB ? 8 : 16) * ch + k, tlast)),
+            __builtin_amdgcn_global_load_lds((gptr_t)(twp + min(16 * ch + k, tlast)),
                                              (lptr_t)(dst + 64 * k), 4, 0, 0);
     };
     if (alive) { issue_chunk(0); issue_chunk(1); }
@@ -745,12 +711,12 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
         // the row's target base and score profile first: their LDS reads then overlap the band
         // bookkeeping below instead of stalling the first group (lgkmcnt wait)
         // every lane reads (a dead lane's slots are harmless): no exec-masked block on the row's path
-        if ((i & (NIB ? 7 : 3)) == 0) {    // new 4-row block (8 rows for nibbles): bases from LDS
+        if ((i & 3) == 0) {                // new 4-row block: bases from LDS
             if ((i & 63) == 0) {              // chunk boundary: its DMA was issued 64 rows ago
                 __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
                 __builtin_amdgcn_sched_barrier(0);
             }
-            const int k = NIB ? (i >> 3) & 7 : (i >> 2) & 15;
+            const int k = (i >> 2) & 15;
             // the two dwords by inline asm: the compiler would otherwise put a vmcnt(0) before
             // every LDS read (it cannot tell this buffer from the one the in-flight LDS-DMA
             // refill writes) -- this chunk's DMA was waited for at its first row above
@@ -758,15 +724,14 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
             uint2 d;
             asm volatile("ds_read2st64_b32 %0, %1 offset1:1\n\ts_waitcnt lgkmcnt(0)"
                          : "=v"(d) : "v"(la) : "memory");
-            tcur = NIB ? __builtin_amdgcn_alignbit(d.y, d.x, 4u * (uint32_t)tsh)
-                       : __builtin_amdgcn_alignbyte(d.y, d.x, tsh);
+            tcur = __builtin_amdgcn_alignbyte(d.y, d.x, tsh);
             if ((i & 63) == 0) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (i > 0 && act) issue_chunk((i >> 6) + 1);   // refill the buffer just drained
             }
         }
         // per-row score profile of target base t (8 bytes: mat[t][q], q = 0..7)
-        const uint32_t tcode = NIB ? (tcur >> (4 * (i & 7))) & 0xfu : (tcur >> (8 * (i & 3))) & 0xffu;
+        const uint32_t tcode = (tcur >> (8 * (i & 3))) & 0xffu;
         const uint2 pr = s_prof[min(tcode, 7u)];   // one ds_read_b64 (codes > 4 score as N)
         __builtin_amdgcn_sched_barrier(0);
         const int beg = max(0, i - wl);
@@ -877,104 +842,13 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
     }
 #endif
     if (valid) {
-        if constexpr (NIB) {
-            int32_t *o = out24 + 6 * (int64_t)idx;
-            o[0] = best; o[1] = best_i + 1; o[2] = max_ie + 1; o[3] = best_j + 1; o[4] = gsc; o[5] = moff;
-        } else {
-            sp->score = best;
-            sp->tle = best_i + 1;
-            sp->gtle = max_ie + 1;
-            sp->qle = best_j + 1;
-            sp->gscore = gsc;
-            sp->max_off = moff;
-        }
+        sp->score = best;
+        sp->tle = best_i + 1;
+        sp->gtle = max_ie + 1;
+        sp->qle = best_j + 1;
+        sp->gscore = gsc;
+        sp->max_off = moff;
     }
-}
-
-template <int QMAX, bool NIB> constexpr int pc_cdw() { return NIB ? kPcChunkDwN : kPcChunkDw; }
-
-// Persistent tile-queue form: a grid of at most ~2 waves per SIMD, each wave
-// taking 64-pair tiles from ONE device-scope counter until the queue is empty -- no per-wave
-// dispatch, and a wave that finishes early takes the next tile instead of idling through the
-// launch's tail.  Tiles belong to chunks (PqChunk: the tile range, the chunk's slots in `order`,
-// the base added to its order values).  Chunks may be published while the kernel runs (the host
-// pipeline: chunk c's inputs land, are planned and sorted on other CUs, then a one-thread kernel
-// raises *ready to the chunk's last tile): a wave whose tile is not yet published polls *ready
-// (relaxed agent-scope loads, s_sleep) and then takes an agent-scope acquire before reading the
-// chunk's inputs.  *abort (host) or a poll past kPqSpinTicks ends every wave (err |= 8): no wave
-// ever waits without bound.
-[[maybe_unused]] constexpr unsigned long long kPqSpinTicks = 400000000ull;   // 4 s of s_memrealtime (100 MHz)
-
-typedef const PqArgs __attribute__((address_space(4))) *PqArgsK;   // the kernarg segment's copy
-
-template <int QMAX, bool NIB>
-__global__ __launch_bounds__(64, 2) void pq_kernel(const PqArgs args)
-{
-#ifdef __HIP_DEVICE_COMPILE__            // (the kernarg-segment reads have no host form)
-    __shared__ uint32_t s_tgt[1][2][pc_cdw<QMAX, NIB>()][64];
-    __shared__ uint2 s_prof[8];
-    if (threadIdx.x < 8) s_prof[threadIdx.x] = make_uint2(args.kp.prof[threadIdx.x][0], args.kp.prof[threadIdx.x][1]);
-    __syncthreads();
-    int known = -1;                         // tiles [0, known) known published (-1: not read yet)
-    int c = 0;                              // chunk cursor (tiles are taken in increasing order)
-    for (;;) {
-        // the arguments are re-read from the kernarg segment per tile (scalar loads, once per ~1 ms
-        // of DP) instead of held in SGPRs across the tile's DP: the row loop needs every SGPR it has
-        // (held, they spilled 34 SGPRs)
-        PqArgsK a = (PqArgsK)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(a));
-        int t = 0;
-        if (threadIdx.x == 0) t = __hip_atomic_fetch_add(a->head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = __builtin_amdgcn_readfirstlane(t);
-        if (t >= a->ntiles) break;
-        if (known < 0) known = a->ready ? 0 : a->ntiles;
-        if (t >= known) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            int v = 0, ab = 0;
-            for (;;) {
-                v = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(a->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                ab = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(a->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                if (v > t || ab) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kPqSpinTicks) { ab = 2; break; }
-                __builtin_amdgcn_s_sleep(8);
-            }
-            if (ab) {
-                if (threadIdx.x == 0) atomicOr(a->err, 8);
-                break;
-            }
-            known = v;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // the chunk's inputs, fresh
-        }
-        while (c + 1 < a->nchunks && t >= a->chunks[c + 1].tile0) ++c;
-        const int tile0 = a->chunks[c].tile0, slot0 = a->chunks[c].slot0;
-        const int m = a->chunks[c].m, idx_base = a->chunks[c].idx_base;
-        const KParams kp = a->kp;
-        const int gid = slot0 + (t - tile0) * 64 + (int)threadIdx.x;
-        [[maybe_unused]] constexpr int WPB = 1;
-        constexpr bool BY = false;
-        const int32_t w = a->w, n = slot0 + m;
-        const int32_t *order = a->order;
-        int32_t *err = a->err;
-        // NIB: the chunk as staged (records, nibbles) inside the call's device buffer; outputs at the
-        // chunk's pairs of the call's 24-B output array
-        const uint8_t *nb = NIB ? a->nbase : nullptr;
-        SeqPair *pairs = NIB ? nullptr : a->pairs;
-        const uint8_t *ref = NIB ? nb + a->chunks[c].ref_off : a->ref;
-        const uint8_t *qer = NIB ? nb + a->chunks[c].qer_off : a->qer;
-        const PairIn *recs = NIB ? (const PairIn *)(nb + a->chunks[c].rec_off) : nullptr;
-        int32_t *out24 = NIB ? a->out24 + 6 * (int64_t)idx_base : nullptr;
-        const int32_t idx_off = NIB ? 0 : idx_base;
-        {
-            const int32_t idx_base = idx_off;
-#include "bsw_pc_body.inc"
-        }
-        __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): the tile's last target DMA into s_tgt
-    }
-#else
-    (void)args;
-#endif
 }
 
 #ifdef BSW_PC_STATS
@@ -1002,37 +876,13 @@ static void launch_pc_q(const KParams &kp, int32_t w, SeqPair *pairs, const int3
                         const uint8_t *ref, const uint8_t *qer, int32_t *err, hipStream_t s)
 {
     const unsigned grid = (unsigned)((n + 63) / 64);
-    // one wave per workgroup: a finished wave's slot and LDS are reused at once;
-    // kp.lds_pad: dynamic LDS per workgroup, which caps the waves per CU (host pipeline, §5)
-    const unsigned pad = (unsigned)max(kp.lds_pad, 0);
+    // one wave per workgroup: a finished wave's slot and LDS are reused at once
     if (kp.kern8 == 2)                 // byte planes (BSW_OPT_KERNEL8 = 2)
-        hipLaunchKernelGGL((pc_kernel<QMAX, 1, true>), dim3(grid), dim3(64), pad, s, kp, w, pairs, order, n,
+        hipLaunchKernelGGL((pc_kernel<QMAX, 1, true>), dim3(grid), dim3(64), 0, s, kp, w, pairs, order, n,
                            ref, qer, err);
     else
-        hipLaunchKernelGGL((pc_kernel<QMAX, 1, false>), dim3(grid), dim3(64), pad, s, kp, w, pairs, order,
+        hipLaunchKernelGGL((pc_kernel<QMAX, 1, false>), dim3(grid), dim3(64), 0, s, kp, w, pairs, order,
                            n, ref, qer, err);
-}
-
-hipError_t launch_pc_nib_kernel(const KParams &kp, int32_t w, const PairIn *recs, const int32_t *order, int32_t n,
-                                const uint8_t *ref4, const uint8_t *qer4, int32_t *out24, int32_t *err, hipStream_t s)
-{
-    if (n <= 0) return hipSuccess;
-    if (((uintptr_t)ref4 | (uintptr_t)qer4) & 3) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)((n + 63) / 64);
-    hipLaunchKernelGGL((pc_kernel<160, 1, false, true>), dim3(grid), dim3(64), (unsigned)max(kp.lds_pad, 0), s, kp, w,
-                       (SeqPair *)nullptr, order, n, ref4, qer4, err, recs, out24);
-    return hipGetLastError();
-}
-
-hipError_t launch_pq_kernel(const PqArgs &args, int32_t grid, hipStream_t s)
-{
-    if (grid <= 0 || args.nchunks <= 0 || args.nchunks > kPqMaxChunks || !args.head || (args.ready && !args.abort))
-        return hipErrorInvalidValue;
-    if (args.nbase)
-        hipLaunchKernelGGL((pq_kernel<160, true>), dim3((unsigned)grid), dim3(64), 0, s, args);
-    else
-        hipLaunchKernelGGL((pq_kernel<160, false>), dim3((unsigned)grid), dim3(64), 0, s, args);
-    return hipGetLastError();
 }
 
 hipError_t launch_pc_kernel(int qmax, const KParams &kp, int32_t w, SeqPair *pairs,

@@ -47,6 +47,8 @@ OPT_COALESCE = 11
 OPT_COALESCE_LEADERS = 12
 OPT_GROUP_KERNEL = 13
 OPT_MID_BATCH = 14
+OPT_COALESCE_LINGER = 16
+OPT_GQ32_MAX = 18
 OPT_TEST_MISROUTE = 100
 OPT_TEST_FAIL_ALLOC = 101
 
@@ -205,7 +207,8 @@ class Engine:
 
     _OPTS = {"kernel8": OPT_KERNEL8, "fork": OPT_FORK, "sortkey": OPT_SORTKEY, "glob_band": OPT_GLOB_BAND,
              "ext_chunk": OPT_EXT_CHUNK, "host_chunk": OPT_HOST_CHUNK, "long": OPT_LONG, "host_pack": OPT_HOST_PACK,
-             "small_batch": OPT_SMALL_BATCH, "split_min": OPT_SPLIT_MIN, "coalesce": OPT_COALESCE, "coalesce_leaders": OPT_COALESCE_LEADERS, "group_kernel": OPT_GROUP_KERNEL, "mid_batch": OPT_MID_BATCH, "busy_min": 15, "coalesce_linger": 16, "persist": 17,
+             "small_batch": OPT_SMALL_BATCH, "split_min": OPT_SPLIT_MIN, "coalesce": OPT_COALESCE, "coalesce_leaders": OPT_COALESCE_LEADERS, "group_kernel": OPT_GROUP_KERNEL, "mid_batch": OPT_MID_BATCH,
+             "coalesce_linger": OPT_COALESCE_LINGER, "gq32_max": OPT_GQ32_MAX,
              "test_misroute": OPT_TEST_MISROUTE, "test_fail_alloc": OPT_TEST_FAIL_ALLOC}
 
     def set_option(self, name, value: int):
@@ -712,7 +715,7 @@ def mem_opt(**kw) -> MemOpt:
     return o
 
 
-FMI_GPU_BUILD, FMI_WIDE, FMI_NO_TEXT = 1, 2, 4
+FMI_GPU_BUILD, FMI_WIDE, FMI_NO_TEXT, FMI_PLAIN_ENT = 1, 2, 4, 8
 
 
 class Fmi:

@@ -37,6 +37,7 @@ def rt():
         _rt.hipGetDeviceCount.argtypes = [ctypes.POINTER(ctypes.c_int)]
         _rt.hipGetErrorString.restype = ctypes.c_char_p
         _rt.hipGetErrorString.argtypes = [ctypes.c_int]
+        _rt.hipMemGetInfo.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
     return _rt
 
 
@@ -53,6 +54,13 @@ def device_count() -> int:
 
 def set_device(d: int):
     check(rt().hipSetDevice(d))
+
+
+def mem_get_info() -> tuple:
+    """(free, total) bytes of the current device (hipMemGetInfo)"""
+    f, t = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    check(rt().hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)))
+    return int(f.value), int(t.value)
 
 
 def synchronize():

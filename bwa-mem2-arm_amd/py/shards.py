@@ -278,13 +278,31 @@ def unpack_packed(buf: np.ndarray, desc_row):
     def codes(off, nb, exc):
         b = buf[off:off + (nb + 3) // 4]
         out = np.stack([(b >> (2 * k)) & 3 for k in range(4)], axis=1).reshape(-1)[:nb].astype(np.uint8)
-        out[(exc >> 4).astype(np.int64)] = (exc & 15).astype(np.uint8)
+        pos = (exc >> 2).astype(np.int64)
+        out[pos] = (out[pos] & 3) | ((exc & 3) << 2).astype(np.uint8)
         return out
 
     exc = buf[d.exc_off:d.exc_off + 4 * (d.n_exc_ref + d.n_exc_qer)].view(np.uint32)
     ref = codes(d.ref_off, d.ref_bytes, exc[:d.n_exc_ref])
     qer = codes(d.qer_off, d.qer_bytes, exc[d.n_exc_ref:])
     return pairs, ref, qer
+
+
+WIRE_EXTENT_MAX = 1 << 30          # bsw_pack_batch: extents below 2^30 bytes (30-bit exception positions)
+
+
+def pieces_fit(pairs: np.ndarray, cut, chunks: int) -> bool:
+    """every rank's `chunks` pieces (chunk_cut) have ref and qer extents below WIRE_EXTENT_MAX"""
+    for r in range(len(cut) - 1):
+        lo, hi = int(cut[r]), int(cut[r + 1])
+        cc = chunk_cut(hi - lo, chunks)
+        for c in range(chunks):
+            p = pairs[lo + int(cc[c]):lo + int(cc[c + 1])]
+            for idx, ln in (("idr", "len1"), ("idq", "len2")):
+                m = p[ln] > 0
+                if m.any() and int((p[idx][m].astype(np.int64) + p[ln][m]).max() - p[idx][m].min()) >= WIRE_EXTENT_MAX:
+                    return False
+    return True
 
 
 def chunk_cut(n: int, chunks: int) -> np.ndarray:
@@ -342,25 +360,35 @@ class BatchScatter:
         self.src = None
         self.pairs = self.cut = None
         # chunk count: at least `chunks`, and enough that every piece's byte extents stay inside
-        # the wire form's 2^28-byte bound (with a 2x margin): decided on rank 0, broadcast
+        # the wire form's 2^30-byte bound -- checked on the pieces as they will be cut (by pair
+        # count: a skewed or permuted range can hold a long extent in one piece) -- then packed, all
+        # on rank 0 before anything is broadcast; a failure there broadcasts -1 so every rank
+        # raises together instead of leaving the others blocked in the broadcast below
         ch = torch.tensor([max(1, chunks)], dtype=torch.int64)
+        bufs = desc = size = None
+        err = None
         if rank == 0:
-            self.pairs = pairs
-            self.cut = bsw.split_by_cells(pairs, w, world)
-            for r in range(world):
-                p = pairs[int(self.cut[r]):int(self.cut[r + 1])]
-                for idx, ln in (("idr", "len1"), ("idq", "len2")):
-                    m = p[ln] > 0
-                    if m.any():
-                        ext = int((p[idx][m].astype(np.int64) + p[ln][m]).max() - p[idx][m].min())
-                        ch[0] = max(int(ch[0]), -(-ext // (1 << 27)))
+            try:
+                self.pairs = pairs
+                self.cut = bsw.split_by_cells(pairs, w, world)
+                c = int(ch[0])
+                while not pieces_fit(pairs, self.cut, c):
+                    if c >= len(pairs):
+                        raise ValueError("a single pair's extent passes the wire form's 2^30-byte bound")
+                    c = min(2 * c, len(pairs))
+                ch[0] = c
+                bufs, desc, size = pack_chunks(pairs, ref, qer, self.cut, c)
+            except Exception as e:  # noqa: BLE001  (re-raised below, on every rank)
+                err = e
+                ch[0] = -1
         if world > 1:
             dist.broadcast(ch, src=0, group=meta_group)
+        if int(ch.item()) < 0:
+            raise RuntimeError(f"BatchScatter: rank 0 could not pack the batch: {err!r}")
         chunks = self.chunks = int(ch.item())
         nf = len(bsw.Packed.FIELDS)
         meta_t = torch.zeros((world, chunks, nf + 1), dtype=torch.int64)
         if rank == 0:
-            bufs, desc, size = pack_chunks(pairs, ref, qer, self.cut, chunks)
             meta_t[:, :, :nf] = torch.from_numpy(desc)
             meta_t[:, :, nf] = torch.from_numpy(np.broadcast_to(size, (world, chunks)).copy())
             self.src = []

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BSW_ABI_VERSION 7
+#define BSW_ABI_VERSION 8
 
 enum {
     BSW_OK = 0,
@@ -85,8 +85,9 @@ void bsw_destroy(bsw_ctx_t *ctx);
  * (h0 + max(mat) * min(len1, len2) <= 255), int16 for the rest (overflow fallback).
  * Recovery (ABI version 7): when a device run fails with BSW_E_NOMEM or BSW_E_HIP the call is
  * run again before any error is returned -- once on the same device after its cached slots
- * (streams + buffers) are freed, then on each other device of the context, then in halves
- * (recursively, down to 4096 pairs), each half the same way.  Outputs are identical (pairs are
+ * (streams + buffers) are freed, then on each other device of the context, then -- for
+ * BSW_E_NOMEM only (ABI 8: halving cannot cure a HIP error) -- in halves (recursively, down to
+ * 4096 pairs), each half the same way.  Outputs are identical (pairs are
  * independent; a failed run writes no input field).  bsw_last_stats().recovery says which step
  * completed the call.  Upstream's plan for engine errors is to degrade, not abort
  * (PHASE2_IMPLEMENTATION_SUMMARY.md:210-225); there is still no CPU path. */
@@ -105,10 +106,11 @@ int  bsw_get_scores_device(bsw_ctx_t *ctx, SeqPair *d_pairs, const uint8_t *d_re
  * transport format, ~133 bytes per C2 pair instead of 56 + 450 -- what a batch scatter moves
  * between GPUs (bench.py's RCCL legs).  One buffer, offsets 256-aligned:
  *   [rec: n x 20 B {idr, idq, len1, len2, h0} | ref: 2-bit codes of the batch's ref extent + 4 pad
- *    | qer: the same for its qer extent | exc: one uint32 pos << 4 | code per byte outside 0..3
- *    (ref ones first, then qer ones, ascending)]
- * idr / idq are rebased to the extents (empty sequences: 0).  Extents must stay below 2^28 bytes
- * (exception positions are 28 bits): larger batches are packed in pieces. */
+ *    | qer: the same for its qer extent | exc: one uint32 pos << 2 | (code & 15) >> 2 per byte
+ *    outside 0..3 -- the code's low two bits are in the 2-bit plane (ref ones first, then qer
+ *    ones, ascending; ABI 8, 28-bit positions with the whole nibble before)]
+ * idr / idq are rebased to the extents (empty sequences: 0).  Extents must stay below 2^30 bytes
+ * (exception positions are 30 bits): larger batches are packed in pieces. */
 typedef struct bsw_packed_t {
     int32_t n;                            /* pairs                                        */
     int32_t n_exc_ref, n_exc_qer;         /* exception words of each extent               */
@@ -119,7 +121,7 @@ typedef struct bsw_packed_t {
 /* Host-only.  Fills *desc for pairs[0, n) over seqBufRef / seqBufQer; with dst == NULL only sizes
  * it (desc->total_bytes), else writes the packed batch into dst (cap bytes, >= total_bytes).
  * BSW_E_RANGE: a bad pair (negative or > BSW_MAX_LEN length, negative offset) or an extent past
- * 2^28 bytes. */
+ * 2^30 bytes. */
 int  bsw_pack_batch(const SeqPair *pairs, const uint8_t *seqBufRef, const uint8_t *seqBufQer, int32_t n,
                     void *dst, int64_t cap, bsw_packed_t *desc);
 /* Device-resident scoring of a packed batch on the context's first device: d_packed is the
@@ -214,12 +216,6 @@ enum {
                                  BSW_OPT_GROUP_KERNEL is on -- an empty range at the defaults (the
                                  16-lane form measured faster up to 32K pairs; lower
                                  BSW_OPT_SMALL_BATCH to use it).  Outputs are identical either way */
-    BSW_OPT_BUSY_MIN = 15,    /* coalesced batches (BSW_OPT_COALESCE) of at least this many pairs
-                                 that start while another batch is in flight on their device run
-                                 on the planned packed-column lane kernels instead of the row-
-                                 group kernel (default 0 = never: measured slower at 10K-pair
-                                 calls x 8 callers; an experiment knob).  Outputs
-                                 are identical either way                                       */
     BSW_OPT_COALESCE_LINGER = 16, /* microseconds (0..100000, default 0): with more concurrent
                                  callers than BSW_OPT_COALESCE_LEADERS and two or more batches
                                  running, a new leader waits up to this long for 4096 queued pairs
@@ -227,19 +223,21 @@ enum {
                                  so batches fill up.  Measured at 150: 8 callers +16-25% at 1K-4K
                                  pairs per call, 4 / 16 callers mixed, hence off by
                                  default.  A lone caller never waits.  Outputs are identical     */
-    BSW_OPT_PERSIST = 17,     /* packed-column pairs of the 160-column class (C2's) on the
-                                 persistent tile-queue kernel: one grid of ~2 waves per SIMD
-                                 taking 64-pair tiles from a device counter instead of one wave
-                                 per 64 pairs.  0 = off, 1 = host-buffer pipeline calls (chunks
-                                 are published to the running kernel as they land), 2 = also
-                                 device calls.  Default: see bsw_host.cpp.
-                                 Outputs are identical either way                               */
+    /* 15 and 17 (a busy-device routing knob and the persistent tile-queue kernel, ABI 7) were
+       removed in ABI 8 after measuring slower than the defaults: BSW_E_INVAL */
+    BSW_OPT_GQ32_MAX = 18,    /* batches of at most this many pairs (within BSW_OPT_SMALL_BATCH) run on
+                                 the row-group kernel's 32-lane latency form (two DPP rows per pair);
+                                 larger small batches on its 16-lane form.  Default 2048 (the
+                                 crossover measured with 8 callers); 0 = off.
+                                 Outputs are identical either way (ABI version 8)                */
     BSW_OPT_TEST_MISROUTE = 100, /* tests only: 1 = every pair to the QMAX=32 lane class, so
                                  any longer query trips the kernels' range guard (BSW_E_RANGE) */
     BSW_OPT_TEST_FAIL_ALLOC = 101 /* tests only: the next `value` (0..1000000) device buffer
-                                 allocations of the engine's host-buffer path fail with
-                                 hipErrorOutOfMemory (process-wide count), so the recovery of
-                                 bsw_get_scores can be exercised                               */
+                                 growths of the engine fail with hipErrorOutOfMemory, so the
+                                 recovery of bsw_get_scores can be exercised.  The count is
+                                 PROCESS-WIDE and consumed by every path's buffer growth (host-
+                                 buffer and device calls, global / CIGAR, extension) of every
+                                 context: set it only while one call runs                      */
 };
 int  bsw_set_option(bsw_ctx_t *ctx, int option, int64_t value);
 

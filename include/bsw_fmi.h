@@ -91,7 +91,10 @@ int  bsw_fmi_build(const uint8_t *ref, int64_t ref_len, int device, bsw_fmi_t **
  * the inverse suffix array (4 / 8 B per row) in HBM: once an interval is down to one occurrence
  * the SMEM walk extends it by comparing read and text directly instead of one dependent
  * occurrence-block load per base (outputs identical). */
-enum { BSW_FMI_GPU_BUILD = 1, BSW_FMI_WIDE = 2, BSW_FMI_NO_TEXT = 4 };
+/* BSW_FMI_PLAIN_ENT (tests, ABI 8): the wide index's SMEM walk keeps its interval vectors in plain
+ * 32-B entries even when every value fits the packed 16-B form (the fallback of indexes past 2^40
+ * rows or with a single base's count past 2^32), so that path is exercised at small sizes. */
+enum { BSW_FMI_GPU_BUILD = 1, BSW_FMI_WIDE = 2, BSW_FMI_NO_TEXT = 4, BSW_FMI_PLAIN_ENT = 8 };
 int  bsw_fmi_build2(const uint8_t *ref, int64_t ref_len, int device, int flags, bsw_fmi_t **out);
 void bsw_fmi_destroy(bsw_fmi_t *fmi);
 int  bsw_fmi_get_info(const bsw_fmi_t *fmi, bsw_fmi_info_t *out);

@@ -73,7 +73,7 @@ def test_params_default_and_abi_version():
     assert (p.o_del, p.e_del, p.o_ins, p.e_ins, p.zdrop, p.end_bonus) == (6, 1, 6, 1, 100, 5)
     mat = np.frombuffer(bytes(p.mat), np.int8).reshape(5, 5)
     assert mat[0, 0] == 1 and mat[0, 1] == -4 and mat[4, 4] == -1 and mat[2, 4] == -1
-    assert lib.bsw_abi_version() == 7
+    assert lib.bsw_abi_version() == 8
     ref = bsw.default_params()
     assert bytes(ref.mat) == bytes(p.mat)
 

@@ -188,9 +188,9 @@ def test_packed_wire_form_errors():
     with pytest.raises(bsw.BswError):
         bsw.pack_batch(bad, ref, qer)
     big = pairs[:2].copy()
-    big["idr"][1] = (1 << 28)                           # extent past 2^28 bytes
+    big["idr"][1] = (1 << 30)                           # extent past 2^30 bytes
     with pytest.raises(bsw.BswError):
-        bsw.pack_batch(big, np.zeros((1 << 28) + 400, np.uint8), qer)
+        bsw.pack_batch(big, np.zeros((1 << 30) + 400, np.uint8), qer)
 
 
 def _read_scatter_worker(rank, world, port, nreads, q):
@@ -280,3 +280,55 @@ def test_read_shard_pack_roundtrip():
             assert np.array_equal(ln, lens[lo:hi])
             for i in range(hi - lo):
                 assert np.array_equal(rd[of[i]:of[i] + ln[i]], reads[off[lo + i]:off[lo + i] + lens[lo + i]])
+
+
+def _weak_line(world=2):
+    return {"metric": "m", "value": 280.0, "unit": "u", "n_gpus": world, "steps": 20, "warmup": 5,
+            "ms_per_step": 7.1, "scaling": "weak", "kernel_only_value": 290.0,
+            "config": {"workload": "C2: 1000000 SeqPairs/GPU resident", "pairs_per_gpu": 1_000_000,
+                       "parallelism": f"shard{world}"}}
+
+
+def test_multi_gpu_line_headline_is_rccl_leg():
+    """bench.py's N > 1 line: the RCCL batch-scatter leg's throughput is the value (strong scaling),
+    the per-rank resident rate moves to weak_value / weak, the leg's details stay in rccl_strong"""
+    import argparse
+    import bench
+    args = argparse.Namespace(w=100)
+    leg = {"value": 850.0, "unit": "u", "scaling": "strong", "ms_per_step": 7.06, "steps": 20, "warmup": 5,
+           "total_pairs": 6_000_000, "rccl_world_size": 8, "backend": "nccl",
+           "outputs_identical_to_single_gpu": True}
+    out = bench.multi_gpu_line(_weak_line(8), dict(leg), args, 8)
+    assert out["value"] == 850.0 and out["scaling"] == "strong" and out["ms_per_step"] == 7.06
+    assert (out["steps"], out["warmup"]) == (20, 5)
+    assert out["weak_value"] == 280.0 and out["weak"]["scaling"] == "weak" and out["weak"]["ms_per_step"] == 7.1
+    assert out["rccl_strong"]["rccl_world_size"] == 8 and "value" not in out["rccl_strong"]
+    assert "RCCL scatter" in out["config"]["workload"] and out["config"]["total_pairs"] == 6_000_000
+    assert "pairs_per_gpu" not in out["config"] and out["headline"].startswith("rccl_strong")
+    # no RCCL value (skipped / failed): the weak rate stays the value, with the reason
+    for bad in ({"skipped": "2 ranks share 1 GPU(s)"}, {"error": "RuntimeError('x')"}, None):
+        o = bench.multi_gpu_line(_weak_line(2), bad, args, 2)
+        assert o["value"] == 280.0 and o["scaling"] == "weak" and o["weak_value"] == 280.0
+        assert o["headline"].startswith("weak")
+        assert (bad is None) or o["rccl_strong"] == bad
+
+
+def test_c5_guard_budget_and_memory(monkeypatch):
+    """The C5 sub-object's guard: skipped with a stated reason when twice its projected time passes
+    what is left of --budget-s or a rank's free device memory is below the index + buffers"""
+    import argparse
+    import bench
+    import hiprt
+    args = argparse.Namespace(c5_ref_mb=3000, c5_reads=10_000_000, budget_s=10_000.0)
+    need = bench.c5_device_bytes(args, 0)
+    assert 140e9 < need < 200e9                          # ~49.5 B per base of a 3 Gb index + buffers
+    monkeypatch.setattr(hiprt, "mem_get_info", lambda: (280 << 30, 288 << 30))
+    why, info = bench.c5_guard(args, 0, 1)
+    assert why is None and info["projected_s"] > 0
+    monkeypatch.setattr(hiprt, "mem_get_info", lambda: (100 << 30, 288 << 30))
+    why, _ = bench.c5_guard(args, 0, 1)
+    assert why and "device memory" in why
+    monkeypatch.setattr(hiprt, "mem_get_info", lambda: (280 << 30, 288 << 30))
+    args.budget_s = 1.0
+    why, info = bench.c5_guard(args, 0, 1)
+    assert why and "budget" in why and info["budget_s"] == 1.0

@@ -290,15 +290,13 @@ def test_gpu_kmer_table_depths_equal_oracle(levels, flags, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("wide_ent", [None, "1"], ids=["packed16", "plain32"])
-def test_gpu_wide_entry_forms_equal_oracle(wide_ent, monkeypatch):
+def test_gpu_wide_entry_forms_equal_oracle(wide_ent):
     """The wide index's interval vectors in packed 16-B entries (default: 40-bit k / l, 32-bit s,
-    15-bit ends + the text flag) and in plain 32-B entries (BSW_SMEM_WIDE_ENT=1): == the oracle."""
-    if wide_ent:
-        monkeypatch.setenv("BSW_SMEM_WIDE_ENT", wide_ent)
+    15-bit ends + the text flag) and in plain 32-B entries (BSW_FMI_PLAIN_ENT): == the oracle."""
     ref = _long_runs_ref(80_000, 17)
     reads, off, lens = sample_reads(ref, 2000, 151, 19, p_n=0.01)
     o = oracle.FmiRef(ref)
-    f = bsw.Fmi(ref, flags=bsw.FMI_GPU_BUILD | bsw.FMI_WIDE)
+    f = bsw.Fmi(ref, flags=bsw.FMI_GPU_BUILD | bsw.FMI_WIDE | (bsw.FMI_PLAIN_ENT if wide_ent else 0))
     for opt in (dict(), dict(min_seed_len=11, split_width=50)):
         o_out, o_cnt = o.collect_intv(reads, off, lens, cap=512, opt=oracle.mem_opt(**opt), nthreads=8)
         g_out, g_cnt = f.collect_intv(reads, off, lens, cap=512, opt=bsw.mem_opt(**opt))

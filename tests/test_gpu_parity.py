@@ -274,39 +274,6 @@ def test_concurrent_callers(eng):
         _assert_same(wants[k], gots[k], f"thread {k}")
 
 
-def test_busy_device_routing_concurrent():
-    """BSW_OPT_BUSY_MIN (experiment knob): coalesced batches that start while another is in
-    flight take the planned lane kernels instead of the row-group kernel.  8 concurrent callers
-    with the knob at 1 (every busy batch rerouted): outputs equal the oracle."""
-    e = bsw.Engine(busy_min=1)
-    batches = [bsw.synth_batch(3000, pair_base=50_000 * k) for k in range(8)]
-    wants = []
-    for pairs, ref, qer in batches:
-        w_ = pairs.copy()
-        oracle.get_scores(_oparams(), w_, ref, qer, 100, nthreads=2)
-        wants.append(w_)
-    gots = [b[0].copy() for b in batches]
-    errs = []
-
-    def run(k):
-        try:
-            for _ in range(5):
-                gots[k][:] = batches[k][0]
-                e.get_scores(gots[k], batches[k][1], batches[k][2], 100)
-        except Exception as ex:  # noqa: BLE001
-            errs.append(ex)
-
-    th = [threading.Thread(target=run, args=(k,)) for k in range(8)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    assert not errs
-    for k in range(8):
-        _assert_same(wants[k], gots[k], f"busy routing caller {k}")
-    e.close()
-
-
 @pytest.mark.parametrize("chunk", [1, 8192, 1 << 20])
 def test_host_pipeline_chunks(chunk):
     """Host-buffer pipeline (bsw_get_scores): the batch is staged / copied / computed chunk by
@@ -328,13 +295,11 @@ def test_host_pipeline_chunks(chunk):
 
 
 @pytest.mark.parametrize("chunk", [4096, 65536, 262144])
-def test_host_fast_path_equal_oracle(chunk, c2_full, monkeypatch):
-    """The host pipeline's fast path (bsw_host.cpp host_shard_fast: the host computes the schedule
-    keys, sorts each chunk, stages records + nibbles; one pc_kernel<160, nibbles> per chunk reads
-    them in place, no device helper kernels): contiguous C2 batches with extra N bases, empty
-    sequences and the 8-bit regime's edge h0 values, in 1 to ~75 chunks; outputs equal the oracle
-    and only the six output fields change.  The path is opt-in (BSW_HP_FAST=1, read per call)."""
-    monkeypatch.setenv("BSW_HP_FAST", "1")
+def test_host_pipeline_chunks_equal_oracle(chunk, c2_full):
+    """The host pipeline (bsw_host.cpp host_shard: 2-bit staging, H2D, device unpack / plan / sort,
+    DP, 24-B outputs back) over contiguous C2 batches with extra N bases, empty sequences and the
+    8-bit regime's edge h0 values, in 1 to ~75 chunks (chunks of <= 32K pairs take the row-group
+    kernel); outputs equal the oracle and only the six output fields change."""
     pairs, ref, qer, _ = c2_full
     n = 300_000
     p = pairs[:n].copy()
@@ -354,7 +319,7 @@ def test_host_fast_path_equal_oracle(chunk, c2_full, monkeypatch):
     for f in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid"):
         assert np.array_equal(got[f], p[f])
     st = e.last_stats()
-    assert st.n_packed == n and st.n_group == 0 and st.n_launches >= 1
+    assert st.n_packed + st.n_group == n and st.n_launches >= 1
     e.close()
 
 
@@ -480,13 +445,12 @@ def test_group_kernel_golden(golden, quad, monkeypatch):
     """Every golden batch on the default engine (small batches: the row-group kernel where the
     scoring qualifies, the planned path otherwise) and on the device entry point; quad: every
     batch on the 4-lanes-per-pair form (BSW_OPT_SMALL_BATCH 0).  The 16-lane form here
-    (BSW_GQ32_MAX 0: batches of <= 2048 pairs would take the 32-lane form, tested on its own)."""
-    monkeypatch.setenv("BSW_GQ32_MAX", "0")
+    (BSW_OPT_GQ32_MAX 0: batches of <= 2048 pairs would take the 32-lane form, tested on its own)."""
     engines, ran = {}, 0
     for name, pairs, ref, qer, w, sc in golden:
         key = tuple(sorted(sc.items()))
         if key not in engines:
-            engines[key] = bsw.Engine(_gparams(sc), **({"small_batch": 0} if quad else {}))
+            engines[key] = bsw.Engine(_gparams(sc), gq32_max=0, **({"small_batch": 0} if quad else {}))
         got = pairs.copy()
         for f in bsw.OUT_FIELDS:
             got[f] = -9
@@ -511,8 +475,7 @@ def test_group_kernel_score_255_boundary(w, monkeypatch):
     pairs with h0 = 255 - qlen drive H to exactly 255 on the diagonal; waves of four pairs (16
     lanes each) mix them with pairs at h0 + qlen = 256 (the wave then runs the 16-bit key) and
     with near-identical ones, in every position of the wave.  Host and device entry points, both
-    routed to the 16-lane form (BSW_GQ32_MAX 0), equal the oracle."""
-    monkeypatch.setenv("BSW_GQ32_MAX", "0")
+    routed to the 16-lane form (BSW_OPT_GQ32_MAX 0), equal the oracle."""
     rng = np.random.default_rng(255 + w)
     items = []
     for k in range(64):
@@ -530,7 +493,7 @@ def test_group_kernel_score_255_boundary(w, monkeypatch):
     want = pairs.copy()
     oracle.get_scores(_oparams(), want, ref, qer, w, nthreads=8)
     assert (want["score"] == 255).sum() >= 8 and (want["score"] == 256).sum() >= 8
-    e = bsw.Engine()
+    e = bsw.Engine(gq32_max=0)
     for cell_bits in (16, 8):
         got = pairs.copy()
         e.get_scores(got, ref, qer, w, cell_bits)
@@ -803,10 +766,12 @@ def test_options_api(eng):
     assert lib.bsw_set_option(None, bsw.OPT_FORK, 1) == -22
     assert lib.bsw_set_option(eng._ctx, bsw.OPT_SORTKEY, 1) == 0
     assert lib.bsw_set_option(eng._ctx, bsw.OPT_KERNEL8, 3) == -22          # 0, 1, 2 only
-    assert lib.bsw_set_option(eng._ctx, 15, -1) == -22                      # BSW_OPT_BUSY_MIN
+    assert lib.bsw_set_option(eng._ctx, 15, 0) == -22                       # removed in ABI 8
+    assert lib.bsw_set_option(eng._ctx, 17, 0) == -22                       # removed in ABI 8
     assert lib.bsw_set_option(eng._ctx, 16, 100001) == -22                  # BSW_OPT_COALESCE_LINGER
     assert lib.bsw_set_option(eng._ctx, 16, 30) == 0
-    assert lib.bsw_set_option(eng._ctx, 15, 0) == 0
+    assert lib.bsw_set_option(eng._ctx, bsw.OPT_GQ32_MAX, -1) == -22
+    assert lib.bsw_set_option(eng._ctx, bsw.OPT_GQ32_MAX, 2048) == 0
 
 
 @pytest.mark.parametrize("gaps", [(100, 16400, 6, 1), (6, 1, 30000, 2700), (16000, 16000, 16000, 16000)])
@@ -911,102 +876,13 @@ def test_coalesced_small_calls(c2_full):
         e.close()
 
 
-@pytest.mark.parametrize("persist", [2])
-def test_persistent_tile_queue_device_api(c2_full, persist):
-    """BSW_OPT_PERSIST 2: the 160-column packed-column class runs on the persistent tile-queue
-    kernel (bsw_pc.hip pq_kernel: a grid of 2 waves per SIMD taking 64-pair tiles from a device
-    counter).  The full C2 batch (15,625 tiles, more than the grid) and ragged small batches
-    (partial last tiles, fewer tiles than the grid, one pair) equal the oracle; only the six
-    output fields change."""
-    pairs, ref, qer, want = c2_full
-    e = bsw.Engine(small_batch=0, mid_batch=0)
-    e.set_option("persist", persist)
-    dr = hiprt.DeviceBuffer.from_array(ref)
-    dq = hiprt.DeviceBuffer.from_array(qer)
-    for n in (1, 63, 64, 65, 1000, 131_071, len(pairs)):
-        src = pairs[:n].copy()
-        dp = hiprt.DeviceBuffer.from_array(src)
-        e.get_scores_device(dp.ptr, dr.ptr, dq.ptr, n, 100)
-        got = dp.download(np.empty_like(src))
-        _assert_same(want[:n], got, f"persistent n={n}")
-        for f in ("idr", "idq", "len1", "len2", "h0"):
-            assert np.array_equal(got[f], src[f])
-        st = e.last_stats()
-        assert st.n_packed == n and st.n_launches >= 1
-    e.close()
-
-
-def test_persistent_tile_queue_mixed_classes(eng):
-    """Mixed shapes under BSW_OPT_PERSIST 2: only the 160-column packed class takes the persistent
-    kernel; the other classes (short queries, int16 / wide fallbacks) run as before, all == oracle."""
-    pairs, ref, qer = bswgen.random_pairs(20_000, seed=77, tlen=(0, 330), qlen=(0, 200))
-    want = pairs.copy()
-    oracle.get_scores(_oparams(), want, ref, qer, 100, nthreads=8)
-    e = bsw.Engine(small_batch=0, mid_batch=0)
-    e.set_option("persist", 2)
-    got = pairs.copy()
-    e.get_scores(got, ref, qer, 100)
-    _assert_same(want, got, "persistent mixed")
-    e.close()
-
-
-@pytest.mark.parametrize("chunk,nrich", [(65536, False), (262144, False), (262144, True)])
-def test_persistent_host_pipeline(c2_full, chunk, nrich):
-    """BSW_OPT_PERSIST 1: a contiguous host-buffer call runs as ONE persistent DP launch fed chunk by
-    chunk (bsw_host.cpp host_shard_pq: chunks staged, copied, planned and sorted on a few reserved
-    CUs and published to the running grid).  Extra N bases, empty sequences, the 8-bit regime's
-    edge h0 values and (nrich) chunks past the 2-bit staging's 1/32 exception bound (nibble
-    fallback) -- outputs equal the oracle, inputs untouched, one launch per call."""
-    pairs, ref, qer, _ = c2_full
-    n = 300_000
-    p = pairs[:n].copy()
-    r, q = ref.copy(), qer.copy()
-    q[13::997] = 4
-    r[5::1201] = 4
-    if nrich:
-        q[: int(p["idq"][150_000])][::19] = 4        # > 1/32 non-ACGT in the first half's queries
-    p["len2"][::5001] = 0
-    p["len1"][3::7001] = 0
-    qs = p["len2"] > 0
-    sel = qs & (np.arange(n) % 13 == 0)
-    p["h0"][sel] = 255 - np.minimum(p["len2"], p["len1"])[sel]
-    want = p.copy()
-    oracle.get_scores(_oparams(), want, r, q, 100, nthreads=16)
-    e = bsw.Engine(host_chunk=chunk)
-    e.set_option("persist", 1)
-    for rep in range(2):                               # a second call reuses the grown buffers
-        got = p.copy()
-        e.get_scores(got, r, q, 100)
-        _assert_same(want, got, f"persistent host chunk {chunk} nrich {nrich} call {rep}")
-        for f in ("idr", "idq", "id", "len1", "len2", "h0", "seqid", "regid"):
-            assert np.array_equal(got[f], p[f])
-        st = e.last_stats()
-        assert st.n_packed == n and st.n_launches == 1 and st.n_group == 0
-    e.close()
-
-
-def test_persistent_host_pipeline_falls_back(c2_full):
-    """Calls the persistent pipeline does not take (permuted records: byte extents not ascending;
-    a pair past the 8-bit regime) run on the chunked pipeline, outputs == oracle."""
-    pairs, ref, qer, want = c2_full
-    e = bsw.Engine()
-    e.set_option("persist", 1)
-    perm = np.random.default_rng(9).permutation(200_000)
-    got = pairs[:200_000][perm].copy()
-    e.get_scores(got, ref, qer, 100)
-    _assert_same(want[:200_000][perm], got, "persistent fallback permuted")
-    assert e.last_stats().n_launches > 1
-    e.close()
-
-
 @pytest.mark.parametrize("w", [0, 1, 7, 100, 200])
-def test_group_kernel_32lane(w, monkeypatch):
+def test_group_kernel_32lane(w):
     """The row-group kernel's 32-lane latency form (bsw_gq.hip GS = 32: two DPP rows per pair, scans
     closed by row_bcast:15, the column shift by wave_shr:1, reductions by v_permlane16_swap), routed
-    by BSW_GQ32_MAX (read per call): random shapes (queries 0..160 -> 2 / 4 / 6 columns per lane,
+    by BSW_OPT_GQ32_MAX: random shapes (queries 0..160 -> 2 / 4 / 6 columns per lane,
     targets 0..400, h0 0..200), the 255/256 key boundary, host and device entry points == oracle."""
-    monkeypatch.setenv("BSW_GQ32_MAX", "1000000")
-    e = bsw.Engine()
+    e = bsw.Engine(gq32_max=1_000_000)
     for qhi in (60, 120, 160):
         pairs, ref, qer = bswgen.random_pairs(3000, seed=7100 + w + qhi, tlen=(0, 400), qlen=(0, qhi), h0=(0, 200))
         want = pairs.copy()
@@ -1036,14 +912,13 @@ def test_group_kernel_32lane(w, monkeypatch):
     e.close()
 
 
-def test_group_kernel_32lane_golden(golden, monkeypatch):
-    """Every golden batch through the 32-lane form where the scoring qualifies (BSW_GQ32_MAX)."""
-    monkeypatch.setenv("BSW_GQ32_MAX", "1000000")
+def test_group_kernel_32lane_golden(golden):
+    """Every golden batch through the 32-lane form where the scoring qualifies (BSW_OPT_GQ32_MAX)."""
     engines, ran = {}, 0
     for name, pairs, ref, qer, w, sc in golden:
         key = tuple(sorted(sc.items()))
         if key not in engines:
-            engines[key] = bsw.Engine(_gparams(sc))
+            engines[key] = bsw.Engine(_gparams(sc), gq32_max=1_000_000)
         got = pairs.copy()
         for f in bsw.OUT_FIELDS:
             got[f] = -9

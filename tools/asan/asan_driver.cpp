@@ -122,9 +122,9 @@ static void test_pack()
         std::vector<uint8_t> back(n);
         for (size_t k = 0; k < n; ++k) back[k] = (two[k >> 2] >> (2 * (k & 3))) & 3;
         for (uint32_t e : exc) {
-            const uint32_t pos = (e >> 4) - pos0;
+            const uint32_t pos = (e >> 2) - pos0;
             CHECK(pos < n, "exception position %u out of range %zu", pos, n);
-            if (pos < n) back[pos] = e & 15;
+            if (pos < n) back[pos] = (uint8_t)(back[pos] | (e & 3) << 2);
         }
         CHECK(n == 0 || memcmp(back.data(), s, n) == 0, "2-bit round trip, n %zu lead %zu", n, lead);
         for (size_t k = 0; k < n; ++k) {
@@ -148,7 +148,7 @@ static void test_pack()
     size_t bad = 0;
     std::vector<uint8_t> back(n);
     for (size_t k = 0; k < n; ++k) back[k] = (two[k >> 2] >> (2 * (k & 3))) & 3;
-    for (uint32_t e : all) back[e >> 4] = e & 15;
+    for (uint32_t e : all) back[e >> 2] = (uint8_t)(back[e >> 2] | (e & 3) << 2);
     for (size_t k = 0; k < n; ++k) bad += back[k] != src[k];
     CHECK(bad == 0 && all.size() == n / 32, "9 MB pieces: %zu wrong codes, %zu exceptions", bad, all.size());
 }

@@ -102,7 +102,7 @@ int main(int argc, char **argv)
     if (const char *l = getenv("PERCALL_LEADERS")) bsw_set_option(ctx, BSW_OPT_COALESCE_LEADERS, atoi(l));
     if (const char *g = getenv("PERCALL_GROUP")) bsw_set_option(ctx, BSW_OPT_GROUP_KERNEL, atoi(g));
     if (const char *b = getenv("PERCALL_SMALL")) bsw_set_option(ctx, BSW_OPT_SMALL_BATCH, atoi(b));
-    if (const char *b = getenv("PERCALL_BUSY_MIN")) bsw_set_option(ctx, BSW_OPT_BUSY_MIN, atoi(b));
+    if (const char *b = getenv("PERCALL_GQ32_MAX")) bsw_set_option(ctx, BSW_OPT_GQ32_MAX, atoi(b));
     if (const char *b = getenv("PERCALL_LINGER")) bsw_set_option(ctx, BSW_OPT_COALESCE_LINGER, atoi(b));
     std::vector<SeqPair> want = pairs;
     if (bsw_get_scores(ctx, want.data(), ref.data(), qer.data(), N, 100, 16) != BSW_OK) return 3;
