@@ -8,20 +8,24 @@ default scoring (-A1 -B4 -O6 -E1 -d100 -L5); generator bwa-mem2-arm_amd/csrc/bsw
 
 One step = one bsw_get_scores_device() call over the whole resident batch (plan + sort +
 DP kernel + results written back into the SeqPair records in HBM).  Inputs are resident in
-HBM before timing starts.  N GPUs: one process per GPU (torchrun), each with its own
-1M-pair shard (weak scaling, pairs are independent -> no data-path collective); the
-control plane (barriers, max-over-ranks timing) is torch.distributed/gloo.  At N > 1 the
-same line also carries `rccl_strong`: ONE fixed batch (--rccl-pairs, 6M: SeqPair's int32 idr
-addresses at most ~7M C2 windows of 300 bytes) resident on GPU 0 in the 2-bit wire form,
-scattered to the ranks' GPUs over an nccl (= RCCL) group, scored in place, outputs gathered
-back to GPU 0, all timed -- with rccl_world_size and the check that the gathered outputs are
-identical to the same batch scored on GPU 0 alone (BASELINE configs[4]'s batch scatter).
+HBM before timing starts.
+
+N GPUs (one process per GPU, torchrun; control plane = torch.distributed/gloo): the line's value
+is the RCCL batch scatter of BASELINE configs[4] -- ONE batch of --rccl-pairs C2 pairs (6M:
+SeqPair's int32 idr addresses ~7M windows of 300 bytes) resident on GPU 0 in the 2-bit wire form,
+scattered to the ranks' GPUs over an nccl (= RCCL) group, scored in place, outputs gathered back
+to GPU 0, all timed over exactly --steps steps (strong scaling; rccl_world_size and the check that
+the gathered outputs equal the same batch scored on GPU 0 alone are in rccl_strong).  Every rank
+scoring its own resident 1M pairs with no data movement is reported beside it as weak_value.
+C5 on the whole front end (the PE read set scattered, seeding -> chaining -> extension on every
+rank, records gathered) follows in `c5` when --budget-s and every rank's free HBM allow it.
 
 Reported beside the metric:
   roofline     -- dominant kernel (pc_kernel<160> on C2), integer-VALU bound: algorithmic ops
                   = 14 int ops x 25,100 static band cells per pair per
                   launch / HIP-event-timed launch duration, vs the gfx950 packed-int16 VALU
-                  peak; traffic = HBM bytes per launch from rocprofv3 PMC (profiles/).
+                  peak; traffic = HBM bytes per launch from the rocprofv3 PMC passes of THIS
+                  workload (profiles/pmc_latest.json keyed by roofline.pmc_key), else null.
   cpu_baseline -- oracle/bsw_sse41.c (restated upstream SSE4.1 getScores16 design, "port")
                   on a bounded sample of the same batch; best of {affinity set, cgroup quota,
                   16} threads (model, core count and quota recorded), rank 0, N = 1 only.
@@ -92,16 +96,48 @@ def barrier(world: int):
         dist.barrier()
 
 
-def traffic_per_launch(kernel_name: str):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
-    (profiles/pmc_latest.json, written by tools/profile.sh); None if absent."""
-    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+def workload_key(args) -> str:
+    """The PMC lookup key of this run's workload: profiles/pmc_latest.json holds per workload key the
+    kernels of the rocprofv3 PMC passes (tools/profile.sh) that ran exactly this workload
+    (tools/pmc_summary.py reads the key from the profiled run's own JSON line, roofline.pmc_key)"""
+    w = args.workload
+    if w == "c2":
+        return (f"c2:n{args.pairs}:q{args.qlen}:t{args.tlen}:w{args.w}:cb{args.cell_bits}:k8{args.kernel8}:"
+                f"h{args.h0_hi}")
+    if w in ("mate", "global"):
+        return f"{w}:n{args.jobs}:ref{args.ref_mb}"
+    if w == "smem":
+        return f"smem:n{args.reads}:ref{args.smem_ref_mb}{':blocks' if args.fmi_blocks_only else ''}"
+    if w == "c1":
+        return "c1"
+    return f"{w}:n{args.reads}:ref{args.ref_mb}:w{args.w}{':blocks' if args.fmi_blocks_only else ''}"
+
+
+def traffic_for(args, kernel: str, prefix: bool = False) -> dict:
+    """HBM traffic of `kernel` (prefix: the longest-running kernel whose short name starts with it) per
+    launch, from the PMC passes of THIS workload (workload_key) in profiles/pmc_latest.json:
+    {"traffic": bytes, "traffic_kernel", "traffic_source", "counter_GBps": bytes / the traced
+    average launch time}; traffic None when no pass of this workload measured the kernel -- a line
+    never carries another workload's bytes"""
+    key = workload_key(args)
+    none = {"traffic": None, "traffic_source": f"no PMC pass of workload {key} in profiles/pmc_latest.json"}
     try:
-        with open(p) as fh:
+        with open(os.path.join(ROOT, "profiles", "pmc_latest.json")) as fh:
             d = json.load(fh)
-        return d.get(kernel_name, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        return None
+        return none
+    ent = d.get(key)
+    if not isinstance(ent, dict):
+        return none
+    ks = ent.get("kernels", {})
+    c = [(v.get("total_ns", 0), k, v) for k, v in ks.items()
+         if (k.startswith(kernel) if prefix else k == kernel) and v.get("hbm_bytes_per_launch") is not None]
+    if not c:
+        return none
+    _, k, v = max(c, key=lambda x: x[0])
+    b = v["hbm_bytes_per_launch"]
+    return {"traffic": b, "traffic_kernel": k, "traffic_source": ent.get("source"),
+            "counter_GBps": round(b / v["avg_ns"], 1) if v.get("avg_ns") else None}
 
 
 def host_cpu_info() -> dict:
@@ -175,24 +211,6 @@ def _timed(fn, reps):
         fn()
         ts.append(time.perf_counter() - t)
     return statistics.median(ts)
-
-
-def traffic_dominant(prefix: str):
-    """(kernel, HBM bytes per launch) of the longest-running kernel whose short name starts with
-    `prefix` in profiles/pmc_latest.json (rocprofv3 PMC passes of tools/profile.sh), else
-    (None, None)."""
-    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    try:
-        with open(p) as fh:
-            d = json.load(fh)
-    except (OSError, ValueError):
-        return None, None
-    c = [(v.get("total_ns", 0), k, v.get("hbm_bytes_per_launch")) for k, v in d.items()
-         if k.startswith(prefix) and v.get("hbm_bytes_per_launch") is not None]
-    if not c:
-        return None, None
-    _, k, b = max(c)
-    return k, b
 
 
 def cpu_baseline(pairs, ref, qer, w, gpu_pairs, cores):
@@ -508,7 +526,7 @@ def main():
     roof = {
         "bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
         "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
-        "traffic": traffic_per_launch(kname),
+        **traffic_for(args, kname), "pmc_key": workload_key(args),
         "kernel": kname, "launch_ms": round(kms_mean, 4),
         "cells_per_s": round(args.pairs * cells / (kms_mean * 1e-3) / 1e12, 4),
         "cells_unit": f"T band cells/s ({cells:,} static cells/pair)",
@@ -1588,16 +1606,12 @@ def main_mem(args, rank, local, world, c1: bool):
         # (the GPU's k-mer table and text mode skip part of these loads: achieved may pass traffic)
         alg_per_read = n_blocks * 64.0 / S + float(np.mean(lens))
         smem_s = fmi.last_kernel_ms() * 1e-3
-        pmc = traffic_per_launch("smem_kernel")
         ach = alg_per_read * n / smem_s / 1e9
-        out_j["roofline"] = {
-            "bound": "hbm", "kernel": "smem_kernel", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
-            "frac": round(ach / 8000.0, 4),
-            "traffic": pmc, "traffic_note": "HBM bytes per launch of smem_kernel from the committed PMC pass "
-                                            "(profiles/pmc_latest.json; FETCH_SIZE raw: 64-B random requests)",
+        out_j["roofline"] = smem_roofline(args, ach, {
+            "kernel": "smem_kernel",
             "algorithmic": f"{alg_per_read:.0f} B per read ({n_blocks / S:.1f} occurrence-block loads x 64 B "
                            f"+ the read) x {n} reads per step", "launch_ms_per_step": round(smem_s * 1e3, 3),
-            "backward_extensions_per_read": round(n_bext / S, 1)}
+            "backward_extensions_per_read": round(n_bext / S, 1)})
     if not c1:
         # the reference's own published bwa-mem2 rate (another machine and another dataset, SAM output
         # included): beside the oracle leg, never as the baseline of a ratio
@@ -1661,8 +1675,7 @@ def main_mate(args, rank, local, world):
                    "n_fwd": st.n_fwd, "n_rev": st.n_rev},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
                      "unit": "TOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
-                     "traffic": traffic_dominant("mate_kernel")[1],
-                     "traffic_kernel": traffic_dominant("mate_kernel")[0],
+                     **traffic_for(args, "mate_kernel", prefix=True), "pmc_key": workload_key(args),
                      "kernel": "mate forward pass", "launch_ms": round(fwd_ms, 4),
                      "cells_per_s": round(st.cells_fwd / (fwd_ms * 1e-3) / 1e12, 4),
                      "algorithmic": f"{OPS_PER_CELL} int ops x {st.cells_fwd} forward cells per launch"},
@@ -1747,8 +1760,7 @@ def main_global(args, rank, local, world):
         "roofline": {"bound": "valu", "achieved": round(st.cells * OPS_PER_CELL / (kms * 1e-3) / 1e12, 3),
                      "peak": round(VALU_PEAK_TOPS, 1), "unit": "TOP/s",
                      "frac": round(st.cells * OPS_PER_CELL / (kms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
-                     "traffic": traffic_dominant("glob_lane_kernel")[1],
-                     "traffic_kernel": traffic_dominant("glob_lane_kernel")[0],
+                     **traffic_for(args, "glob_lane_kernel", prefix=True), "pmc_key": workload_key(args),
                      "kernel": "glob_lane_kernel<160> (DP + traceback)", "launch_ms": round(kms, 4),
                      "cells_per_s": round(st.cells / (kms * 1e-3) / 1e12, 4),
                      "traceback_matrix_GBps": round(st.z_bytes / (kms * 1e-3) / 1e9, 1),
@@ -1778,6 +1790,26 @@ def main_global(args, rank, local, world):
 
 
 HBM_PEAK_GBS = 8000.0              # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def smem_roofline(args, logical_gbps: float, extra: dict) -> dict:
+    """The SMEM kernel's HBM roofline.  With a PMC pass of this workload: achieved / frac from the
+    COUNTED HBM bytes per launch over the traced launch time (what the memory system moved); the
+    logical rate -- every occurrence-block load the reference algorithm issues counted as 64 B of
+    HBM traffic, although the L2 serves ~30% of them and the GPU's k-mer table / text mode skip
+    others -- beside it as logical_GBps.  Without one: the logical rate, labelled as such."""
+    t = traffic_for(args, "smem_kernel")
+    r = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", **t, "pmc_key": workload_key(args),
+         "logical_GBps": round(logical_gbps, 1), "logical_frac": round(logical_gbps / HBM_PEAK_GBS, 4)}
+    if t.get("counter_GBps"):
+        r.update(achieved=t["counter_GBps"], frac=round(t["counter_GBps"] / HBM_PEAK_GBS, 4),
+                 basis="PMC-counted HBM bytes per launch / traced launch time (this workload's pass)")
+    else:
+        r.update(achieved=round(logical_gbps, 1), frac=round(logical_gbps / HBM_PEAK_GBS, 4),
+                 basis="logical occurrence-block loads x 64 B (no PMC pass of this workload)")
+    r.update(extra)
+    r["note"] = "serial chains of dependent loads: latency-bound, reported against the HBM roof"
+    return r
 
 
 def seeding_reference(n: int, seed: int = 7):
@@ -1881,14 +1913,12 @@ def main_smem(args, rank, local, world):
                    "reads_per_gpu": args.reads, "parallelism": f"shard{world} (independent reads)",
                    "index_device_bytes": fmi.info().device_bytes, "index_build_s": round(build_s, 2),
                    "mems_per_read": round(float(cnt.mean()), 2)},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_dominant("smem_kernel")[1],
-                     "kernel": "smem_kernel", "launch_ms": round(kernel_ms, 4),
-                     "algorithmic": f"{bytes_per_read:.0f} B per read = 64-B occurrence blocks touched by "
-                                    f"{n_ext / S:.1f} backward extensions per read (oracle count on {S} reads"
-                                    f"{'' if small else ' vs a 16 Mb reference of the same generator'}) x "
-                                    f"{args.reads} reads per launch",
-                     "note": "serial chains of dependent loads: latency-bound, reported against the HBM roof"},
+        "roofline": smem_roofline(args, achieved, {
+            "kernel": "smem_kernel", "launch_ms": round(kernel_ms, 4),
+            "algorithmic": f"{bytes_per_read:.0f} B per read = 64-B occurrence blocks touched by "
+                           f"{n_ext / S:.1f} backward extensions per read (oracle count on {S} reads"
+                           f"{'' if small else ' vs a 16 Mb reference of the same generator'}) x "
+                           f"{args.reads} reads per launch"}),
     }
     gpu_out = d_mems.download(np.zeros((args.reads, cap), dtype=bsw.BWTINTV_DTYPE))
     agree = bool(np.array_equal(o_cnt, cnt[:S]) and all(np.array_equal(o_out[i, :o_cnt[i]], gpu_out[i, :o_cnt[i]])

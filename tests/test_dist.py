@@ -174,9 +174,10 @@ def test_packed_wire_form_roundtrip():
         if hi - lo > 1000:
             assert d.n_exc_ref > 0 and d.n_exc_qer > 0
             assert d.total_bytes < (hi - lo) * 160        # vs 56 + 450 bytes per pair unpacked
+            # scored on codes 0..4 (the ABI's alphabet; the oracle's 5x5 matrix has no row 7)
             w1, w2 = sub.copy(), p.copy()
-            oracle.get_scores(oracle.make_params(), w1, ref, qer, 100)
-            oracle.get_scores(oracle.make_params(), w2, r, qq, 100)
+            oracle.get_scores(oracle.make_params(), w1, np.minimum(ref, 4), qer, 100)
+            oracle.get_scores(oracle.make_params(), w2, np.minimum(r, 4), qq, 100)
             for f in bsw.OUT_FIELDS:
                 assert np.array_equal(w1[f], w2[f])
 

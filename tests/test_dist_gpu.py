@@ -161,3 +161,29 @@ def test_rccl_read_scatter_c4mem_one_rank_equal_oracle(tmp_path):
     assert np.array_equal(got["ext"], wext)
     for fld in bsw.ALNREG_DTYPE.names:
         assert np.array_equal(got["out"][fld], want[fld]), fld
+
+
+@pytest.mark.gpu
+def test_two_rank_rehearsal_line_has_headline_keys():
+    """bench.py --gpus 2 under torchrun with both ranks on GPU 0 (--rehearse): the N > 1 line the
+    driver's scaling run prints, with the batch-scatter leg over gloo (ranks sharing a GPU cannot
+    form an RCCL communicator) -- value = that leg's strong-scaling throughput, the per-rank
+    resident rate in weak_value, the gathered outputs identical to the batch scored on one GPU."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--rehearse", "--steps", "3", "--warmup", "1", "--pairs", "100000",
+           "--rccl-pairs", "300000", "--c5-reads", "0", "--no-cpu"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["headline"].startswith("rccl_strong")
+    leg = line["rccl_strong"]
+    assert leg["backend"] == "gloo" and "rehearsal" in leg and leg["rccl_world_size"] == 2
+    assert leg["outputs_identical_to_single_gpu"] is True and leg["total_pairs"] == 300_000
+    assert line["value"] > 0 and line["weak_value"] > 0 and line["weak"]["scaling"] == "weak"
+    assert (line["steps"], line["warmup"]) == (3, 1) and "rehearsal" in line

@@ -1,7 +1,10 @@
 // asan_driver.cpp -- host-only driver for `make asan` (AddressSanitizer + UBSan over the host C / C++
 // of the product and the oracle; no GPU).  Exercises, with result checks:
 //   bsw_pack.cpp     pack_nibbles / pack_2bit on odd lengths, odd offsets, N runs, and a 9 MB
-//                    buffer cut into 64-code-aligned pieces as stage_2bit cuts it
+//                    buffer cut into 64-code-aligned pieces as stage_2bit cuts it; bsw_pack_batch
+//                    (the 2-bit wire form) on random batches packed into exact-size heap buffers,
+//                    decoded and compared, permuted / empty / N-rich batches, extents one below and
+//                    at the 2^30-byte bound, cap < total_bytes and bad records rejected
 //   bsw_batch.c      .bswb write / read round trip, truncated and corrupted files rejected
 //   bsw_synth.c      every generator
 //   bsw_ext.cpp      bsw_extend_seeds (chunked) and bsw_chain2aln through an oracle-backed engine
@@ -151,6 +154,121 @@ static void test_pack()
     for (uint32_t e : all) back[e >> 2] = (uint8_t)(back[e >> 2] | (e & 3) << 2);
     for (size_t k = 0; k < n; ++k) bad += back[k] != src[k];
     CHECK(bad == 0 && all.size() == n / 32, "9 MB pieces: %zu wrong codes, %zu exceptions", bad, all.size());
+}
+
+// the wire form's inverse (bsw.h bsw_packed_t): records, 2-bit planes, exception words
+static bool unpack_wire(const uint8_t *b, const bsw_packed_t &d, std::vector<int32_t> &rec, std::vector<uint8_t> &ref,
+                        std::vector<uint8_t> &qer)
+{
+    rec.assign((size_t)d.n * 5, 0);
+    if (d.n > 0) memcpy(rec.data(), b + d.rec_off, (size_t)d.n * 20);
+    auto planes = [&](int64_t off, int64_t nb, std::vector<uint8_t> &out) {
+        out.resize((size_t)nb);
+        for (int64_t k = 0; k < nb; ++k) out[(size_t)k] = (b[off + k / 4] >> (2 * (k & 3))) & 3;
+    };
+    planes(d.ref_off, d.ref_bytes, ref);
+    planes(d.qer_off, d.qer_bytes, qer);
+    const uint32_t *ex = (const uint32_t *)(b + d.exc_off);
+    for (int32_t k = 0; k < d.n_exc_ref + d.n_exc_qer; ++k) {
+        std::vector<uint8_t> &o = k < d.n_exc_ref ? ref : qer;
+        const uint32_t pos = ex[k] >> 2;
+        if (pos >= o.size()) return false;
+        o[pos] = (uint8_t)(o[pos] | (ex[k] & 3) << 2);
+    }
+    return true;
+}
+
+static void test_pack_batch()
+{
+    for (int it = 0; it < 60; ++it) {
+        const int32_t n = it < 3 ? it : (int32_t)(rnd() % 2000);
+        const bool permute = it % 4 == 3, nrich = it % 5 == 4;
+        std::vector<SeqPair> pairs((size_t)n);
+        std::vector<uint8_t> ref, qer;
+        for (int32_t i = 0; i < n; ++i) {
+            SeqPair &p = pairs[(size_t)i];
+            memset(&p, 0, sizeof(p));
+            p.len1 = rnd() % 9 == 0 ? 0 : (int32_t)(rnd() % 320);
+            p.len2 = rnd() % 11 == 0 ? 0 : (int32_t)(rnd() % 170);
+            p.h0 = (int32_t)(rnd() % 200);
+            p.idr = (int32_t)ref.size() + (int32_t)(rnd() % 3);       // small gaps between windows
+            p.idq = (int32_t)qer.size();
+            ref.resize((size_t)p.idr + (size_t)p.len1, 0);
+            qer.resize((size_t)p.idq + (size_t)p.len2, 0);
+        }
+        for (auto &c : ref) c = (uint8_t)(nrich && rnd() % 3 == 0 ? 4 + rnd() % 12 : rnd() % 64 ? rnd() % 4 : 4);
+        for (auto &c : qer) c = (uint8_t)(nrich && rnd() % 3 == 0 ? 4 + rnd() % 12 : rnd() % 64 ? rnd() % 4 : 4);
+        if (permute)
+            for (int32_t i = n - 1; i > 0; --i) std::swap(pairs[(size_t)i], pairs[rnd() % (uint32_t)(i + 1)]);
+        // exact-size heap copies: a read past either buffer is an ASan report
+        uint8_t *r = (uint8_t *)malloc(ref.size() + 1), *q = (uint8_t *)malloc(qer.size() + 1);
+        if (!ref.empty()) memcpy(r, ref.data(), ref.size());
+        if (!qer.empty()) memcpy(q, qer.data(), qer.size());
+        bsw_packed_t d;
+        int rc = bsw_pack_batch(n ? pairs.data() : nullptr, r, q, n, nullptr, 0, &d);
+        CHECK(rc == BSW_OK, "pack_batch size rc %d (n %d)", rc, n);
+        uint8_t *buf = (uint8_t *)malloc((size_t)d.total_bytes + 1);
+        if (d.total_bytes > 0) {
+            CHECK(bsw_pack_batch(pairs.data(), r, q, n, buf, d.total_bytes - 1, &d) == BSW_E_INVAL, "cap < total");
+        }
+        rc = bsw_pack_batch(n ? pairs.data() : nullptr, r, q, n, buf, d.total_bytes, &d);
+        CHECK(rc == BSW_OK, "pack_batch rc %d", rc);
+        std::vector<int32_t> rec;
+        std::vector<uint8_t> ur, uq;
+        CHECK(unpack_wire(buf, d, rec, ur, uq), "exception position outside its extent");
+        int64_t r_lo = INT64_MAX, q_lo = INT64_MAX;
+        for (const SeqPair &p : pairs) {
+            if (p.len1 > 0) r_lo = std::min<int64_t>(r_lo, p.idr);
+            if (p.len2 > 0) q_lo = std::min<int64_t>(q_lo, p.idq);
+        }
+        size_t bad = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            const SeqPair &p = pairs[(size_t)i];
+            const int32_t *o = &rec[(size_t)i * 5];
+            bad += o[2] != p.len1 || o[3] != p.len2 || o[4] != p.h0;
+            for (int32_t k = 0; k < p.len1; ++k) bad += ur[(size_t)o[0] + k] != (ref[(size_t)p.idr + k] & 15);
+            for (int32_t k = 0; k < p.len2; ++k) bad += uq[(size_t)o[1] + k] != (qer[(size_t)p.idq + k] & 15);
+            bad += p.len1 > 0 && (int64_t)o[0] != p.idr - r_lo;
+            bad += p.len2 > 0 && (int64_t)o[1] != p.idq - q_lo;
+        }
+        CHECK(bad == 0, "wire round trip: %zu mismatches (n %d, permute %d, nrich %d)", bad, n, permute, nrich);
+        if (n > 3) {                                      // a bad record anywhere: BSW_E_RANGE
+            std::vector<SeqPair> b2 = pairs;
+            b2[(size_t)(rnd() % (uint32_t)n)].len2 = -1;
+            CHECK(bsw_pack_batch(b2.data(), r, q, n, nullptr, 0, &d) == BSW_E_RANGE, "negative length accepted");
+        }
+        free(buf);
+        free(r);
+        free(q);
+    }
+    // extents one below and at the 2^30-byte bound (30-bit exception positions): the first packs and
+    // round-trips its N bases at the far end, the second is BSW_E_RANGE before any byte is read
+    const size_t lim = (size_t)1 << 30;
+    uint8_t *big = (uint8_t *)calloc(lim + 64, 1);
+    uint8_t qq[8] = {0, 1, 2, 3, 4, 0, 1, 2};
+    if (big) {
+        big[lim - 3] = 4;
+        big[lim - 2] = 7;
+        SeqPair two[2];
+        memset(two, 0, sizeof(two));
+        two[0].len1 = 10; two[0].idr = 0; two[0].len2 = 8; two[0].idq = 0;
+        two[1].len1 = 10; two[1].idr = (int32_t)(lim - 10); two[1].len2 = 8; two[1].idq = 0;
+        bsw_packed_t d;
+        CHECK(bsw_pack_batch(two, big, qq, 2, nullptr, 0, &d) == BSW_E_RANGE, "extent of exactly 2^30 accepted");
+        two[1].idr = (int32_t)(lim - 11);                // extent = 2^30 - 1: valid
+        CHECK(bsw_pack_batch(two, big, qq, 2, nullptr, 0, &d) == BSW_OK && d.ref_bytes == (int64_t)lim - 1,
+              "extent 2^30 - 1 rejected");
+        uint8_t *buf = (uint8_t *)malloc((size_t)d.total_bytes);
+        CHECK(buf && bsw_pack_batch(two, big, qq, 2, buf, d.total_bytes, &d) == BSW_OK, "pack at the bound");
+        std::vector<int32_t> rec;
+        std::vector<uint8_t> ur, uq;
+        CHECK(buf && unpack_wire(buf, d, rec, ur, uq) && ur[lim - 3] == 4 && ur[lim - 2] == 7 && uq[4] == 4 &&
+              d.n_exc_ref == 2 && d.n_exc_qer == 1, "exceptions at the far end of a 2^30 - 1 extent");
+        free(buf);
+        two[1].idr = (int32_t)(lim - 9);                 // extent = 2^30 + 1: past the bound
+        CHECK(bsw_pack_batch(two, big, qq, 2, nullptr, 0, &d) == BSW_E_RANGE, "extent past 2^30 accepted");
+        free(big);
+    }
 }
 
 static void test_batch_file()
@@ -315,6 +433,7 @@ static void test_extension_and_synth()
 int main()
 {
     test_pack();
+    test_pack_batch();
     test_batch_file();
     test_extension_and_synth();
     printf("asan_driver: %s (%d failed checks)\n", g_fail ? "FAIL" : "ok", g_fail);

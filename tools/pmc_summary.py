@@ -1,19 +1,35 @@
-"""Summarise rocprofv3 CSV output (kernel trace + PMC passes) for the lane kernel.
+"""Summarise rocprofv3 CSV output (kernel trace + PMC passes of tools/profile.sh).
 
-usage: python tools/pmc_summary.py gpurun_out/prof [profiles/<round>] [--only=kernel,...]
-(--only: merge just those kernels into pmc_latest.json -- e.g. a C4 profile's smem_kernel without
-its small extension launches replacing the C2 line's pc_kernel<160>)
-Writes <dest>/kernel_stats.csv (copied), <dest>/pmc_summary.json and profiles/pmc_latest.json
-(read by bench.py for roofline.traffic).
+usage: python tools/pmc_summary.py gpurun_out/prof [profiles/<round>/<name>]
+Writes <dest>/kernel_stats.csv (copied), <dest>/pmc_summary.json and, under the profiled run's
+workload key, profiles/pmc_latest.json (read by bench.py for roofline.traffic).  The key is taken
+from the profiled run's own JSON line (<src>/trace.log: roofline.pmc_key, bench.workload_key), so a
+bench line only ever finds the counters of a pass that ran its own workload.
 """
 import csv, glob, json, os, shutil, sys
 from collections import defaultdict
 
-args = [a for a in sys.argv[1:] if not a.startswith('--only=')]
-only = [a.split('=', 1)[1].split(',') for a in sys.argv[1:] if a.startswith('--only=')]
-only = only[0] if only else None   # --only=k1,k2: merge just these kernels into pmc_latest.json
+args = sys.argv[1:]
 src = args[0]
 dest = args[1] if len(args) > 1 else None
+
+
+def workload_key():
+    """roofline.pmc_key of the last JSON line the traced run printed (None if absent)"""
+    for log in ('trace.log', 'pmc_fetch.log'):
+        try:
+            with open(os.path.join(src, log)) as fh:
+                lines = [ln for ln in fh if ln.startswith('{')]
+        except OSError:
+            continue
+        for ln in reversed(lines):
+            try:
+                k = json.loads(ln).get('roofline', {}).get('pmc_key')
+            except ValueError:
+                continue
+            if k:
+                return k
+    return None
 
 def newest(pattern):
     """Per directory only the newest run's file: gpurun merges every call's output into the same
@@ -87,13 +103,19 @@ if dest:
         shutil.copy(f, os.path.join(dest, 'kernel_stats.csv'))
     with open(os.path.join(dest, 'pmc_summary.json'), 'w') as fh:
         json.dump(summary, fh, indent=1)
-    # profiles/pmc_latest.json: merged over workloads (bench.py reads each kernel's traffic)
-    latest = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'pmc_latest.json')
+    # profiles/pmc_latest.json: one entry per workload key (this pass replaces its own workload's)
+    key = workload_key()
+    if key is None:
+        print('no roofline.pmc_key in the traced run\'s output: profiles/pmc_latest.json not updated', file=sys.stderr)
+        sys.exit(0)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    latest = os.path.join(root, 'profiles', 'pmc_latest.json')
     merged = {}
     if os.path.exists(latest):
         with open(latest) as fh:
             merged = json.load(fh)
-    merged.update({k: v for k, v in summary.items()
-                   if (only is None and ('hbm_bytes_per_launch' in v or k not in merged)) or (only and k in only)})
+    merged[key] = {'source': os.path.relpath(os.path.join(dest, 'pmc_summary.json'), root),
+                   'kernels': {k: v for k, v in summary.items() if 'hbm_bytes_per_launch' in v}}
     with open(latest, 'w') as fh:
         json.dump(merged, fh, indent=1)
+    print(f'pmc_latest.json[{key}] <- {merged[key]["source"]}', file=sys.stderr)
