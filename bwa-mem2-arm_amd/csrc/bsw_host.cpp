@@ -1143,6 +1143,56 @@ static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, int mode)
     }
 }
 
+// The largest buffers any chunk of a host-buffer call needs (both staging forms, bulk or gathered
+// byte extents): reserve_slot grows a slot to them before its first chunk.
+struct SlotReserve {
+    int32_t m = 0;                      // pairs
+    size_t rb = 0, qb = 0, stage = 0;   // unpacked ref / qer bytes, pinned / device staging bytes
+    void add(int32_t mc, const BlkStat *b, int32_t nb)
+    {
+        int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
+        for (int32_t k = 0; k < nb; ++k) {
+            r_lo = std::min(r_lo, b[k].r_lo); r_hi = std::max(r_hi, b[k].r_hi); r_sum += b[k].r_sum;
+            q_lo = std::min(q_lo, b[k].q_lo); q_hi = std::max(q_hi, b[k].q_hi); q_sum += b[k].q_sum;
+        }
+        const size_t r = (size_t)std::max<int64_t>(r_lo == INT64_MAX ? 0 : r_hi - r_lo, r_sum);
+        const size_t q = (size_t)std::max<int64_t>(q_lo == INT64_MAX ? 0 : q_hi - q_lo, q_sum);
+        const size_t mm = (size_t)mc;
+        const size_t nib = align256(align256(mm * sizeof(SeqPair)) + (r + 1) / 2 + 4) + (q + 1) / 2 + 4;
+        const size_t two = align256(align256(align256(mm * sizeof(PairIn)) + (r + 3) / 4 + 4) + (q + 3) / 4 + 4) +
+                           ((r + q) / 32 + 1024) * 4;
+        const size_t gat = align256(align256(mm * sizeof(SeqPair)) + r + 4) + q + 4;   // gathered: bytes as is
+        m = std::max(m, mc);
+        rb = std::max(rb, r);
+        qb = std::max(qb, q);
+        stage = std::max({stage, nib, two, gat, mm * 24});
+    }
+};
+
+static int reserve_slot(Slot &s, const SlotReserve &r)
+{
+    if (r.m <= 0) return BSW_OK;
+    BSW_TRY(hipSetDevice(s.device));
+    if (r.stage > s.cap_stage) {
+        if (s.h_stage) (void)hipHostFree(s.h_stage);
+        s.h_stage = nullptr;
+        s.cap_stage = 0;
+        const size_t cap = r.stage + r.stage / 4;
+        BSW_TRY(hipHostMalloc(&s.h_stage, cap, 0));
+        s.cap_stage = cap;
+    }
+    BSW_TRY(grow(s.d_stage, s.cap_dstage, r.stage));
+    BSW_TRY(grow(s.d_ref, s.cap_ref, r.rb + 16));
+    BSW_TRY(grow(s.d_qer, s.cap_qer, r.qb + 16));
+    BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)r.m));
+    BSW_TRY(grow_sort(s, r.m));
+    size_t tmp_bytes = 0;
+    BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals, s.d_order, r.m, 0,
+                                               kKeyBits, (hipStream_t)0));
+    BSW_TRY(grow(s.d_tmp, s.cap_tmp, tmp_bytes));
+    return BSW_OK;
+}
+
 // One device's share of a host-buffer call: a pipeline of chunks over the device's slots (four by default).
 // Per chunk: stage into the slot's pinned buffer (records + nibble-packed sequences, host
 // pool) -> one H2D -> unpack -> plan / sort -> DP kernels -> D2H of the records.  The calling
@@ -1381,32 +1431,45 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         if (enqueuer.joinable()) enqueuer.join();
     };
     double stage_ms = 0;
-    rc = [&]() -> int {
-        BSW_TRY(hipSetDevice(dc.device));
-        int k = 0;
-        int32_t seq = 0;
+    // the chunk schedule (block ranges): `cur` blocks, doubling from first_blk up to `chunk` pairs,
+    // fewer when their sequence bytes pass ~512 MB (staged offsets stay int32).  (A small remainder
+    // stays its own chunk: folded into the last full chunk it added a third, nearly empty generation
+    // of waves to that launch -- 262144 pairs are exactly two generations at two waves per SIMD --
+    // and the call got ~1 ms slower; as its own launch it runs beside the last chunk on another
+    // queue.  Measured)  Calls of up to 128K pairs -- kt_for-sized batches -- run as
+    // one chunk on one slot.
+    std::vector<std::pair<int32_t, int32_t>> chs;
+    SlotReserve res{};
+    {
         const int32_t nblk = (int32_t)bs.size();
         const int32_t cap_blk = std::max<int32_t>(1, chunk / kStageBlk);
-        // (calls of up to 128K pairs -- kt_for-sized batches -- run as one chunk on one slot)
-        int32_t cur = first_blk;
-        for (int32_t b = 0, nb = 0; b < nblk; b += nb, k = (k + 1) % nslots, ++seq, cur = std::min(cap_blk, cur * 2)) {
-            // `cur` blocks, fewer when their sequence bytes pass ~512 MB (staged offsets stay int32)
+        for (int32_t b = 0, nb = 0, cur = first_blk; b < nblk; b += nb, cur = std::min(cap_blk, cur * 2)) {
             int64_t bytes = 0;
             for (nb = 0; nb < cur && b + nb < nblk; ++nb) {
                 const int64_t x = bs[b + nb].r_sum + bs[b + nb].q_sum;
                 if (nb > 0 && bytes + x > ((int64_t)1 << 29)) break;
                 bytes += x;
             }
-            // (a small remainder stays its own chunk: folded into the last full chunk it added a
-            // third, nearly empty generation of waves to that launch -- 262144 pairs are exactly
-            // two generations at two waves per SIMD -- and the call got ~1 ms slower; as its own
-            // launch it runs beside the last chunk on another queue.  Measured)
+            chs.emplace_back(b, nb);
+            res.add(std::min(n, (b + nb) * kStageBlk) - b * kStageBlk, bs.data() + b, nb);
+        }
+    }
+    rc = [&]() -> int {
+        BSW_TRY(hipSetDevice(dc.device));
+        int k = 0;
+        int32_t seq = 0;
+        for (const auto &ch : chs) {
+            const int32_t b = ch.first, nb = ch.second;
             const int32_t a = b * kStageBlk, m = std::min(n, (b + nb) * kStageBlk) - a;
             int r = finish(k);                          // slot k's last chunk
             if (r) return r;
             if (!slots[k]) {
                 slots[k] = dc.acquire(r);
                 if (r) return r;
+                // every buffer of the slot at the call's largest chunk at once: chunks rotate over
+                // the slots, so sizing by the chunk at hand regrew a slot (hipFree waits for the
+                // device) on the first calls of a context as its chunks got larger
+                if ((r = reserve_slot(*slots[k], res))) return r;
             }
             Slot &s = *slots[k];
             StagedChunk c;
@@ -1423,6 +1486,8 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
             } else if ((r = enqueue(k, seq, c, m))) {
                 return r;
             }
+            k = (k + 1) % nslots;
+            ++seq;
         }
         for (int j = 0; j < nslots; ++j) {
             const int r = finish(j);

@@ -10,6 +10,7 @@
 #   smoke           __graft_entry__.smoke()
 #   bench           the default bench line (driver form: python bench.py)
 #   bench:<args>    bench.py with extra arguments (commas for spaces: bench:--workload,c1)
+#   torchrun:<N>:<args>  bench.py --gpus N under torchrun (N ranks; --rehearse shares the box's GPU)
 #   prof            rocprofv3 kernel trace + PMC passes of a short C2 bench (tools/profile.sh)
 #   prof:<args>     the same over bench.py <args> (commas for spaces)
 #   segv            the round-3 traced 8-caller percall_bench (kernel + memory-copy trace) with the
@@ -54,6 +55,12 @@ for step in "$@"; do
         log=$O/bench${arg:+_$(echo "$arg" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-60)}_$n.log
         timeout -k 10 600 python bench.py $(sp "$arg") > "$log" 2>&1 || fail "$step" $? "$log"
         tail -1 "$log" | cut -c1-1500 ;;
+    torchrun)
+        nr=${arg%%:*}; targs=${arg#*:}
+        log=$O/torchrun_${nr}_$n.log
+        timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$nr" --master-addr 127.0.0.1 \
+            --master-port $((29000 + n)) bench.py --gpus "$nr" $(sp "$targs") > "$log" 2>&1 || fail "$step" $? "$log"
+        grep '^{' "$log" | tail -1 | cut -c1-1500 ;;
     prof)
         OUT=$O/prof${arg:+_$(echo "$arg" | tr -c 'A-Za-z0-9\n' '_' | cut -c1-40)} \
             ARGS="${arg:+$(sp "$arg") }--steps 5 --warmup 1 --no-cpu --no-host-path" \
