@@ -1143,29 +1143,39 @@ static void unstage_outputs(const Slot &s, SeqPair *pairs, int32_t n, int mode)
     }
 }
 
-// The largest buffers any chunk of a host-buffer call needs (both staging forms, bulk or gathered
-// byte extents): reserve_slot grows a slot to them before its first chunk.
+// The largest buffers any chunk of a host-buffer call needs, in the staging form stage_chunk will
+// pick for it (2-bit for bulk extents, gathered bytes otherwise; a chunk that falls back to nibbles
+// -- more than 1/32 non-ACGT bytes -- grows its slot as before): reserve_slot grows a slot to them
+// before its first chunk.
 struct SlotReserve {
     int32_t m = 0;                      // pairs
     size_t rb = 0, qb = 0, stage = 0;   // unpacked ref / qer bytes, pinned / device staging bytes
-    void add(int32_t mc, const BlkStat *b, int32_t nb)
+    void add(int32_t mc, const BlkStat *b, int32_t nb, bool two_bit)
     {
         int64_t r_lo = INT64_MAX, r_hi = 0, q_lo = INT64_MAX, q_hi = 0, r_sum = 0, q_sum = 0;
         for (int32_t k = 0; k < nb; ++k) {
             r_lo = std::min(r_lo, b[k].r_lo); r_hi = std::max(r_hi, b[k].r_hi); r_sum += b[k].r_sum;
             q_lo = std::min(q_lo, b[k].q_lo); q_hi = std::max(q_hi, b[k].q_hi); q_sum += b[k].q_sum;
         }
-        const size_t r = (size_t)std::max<int64_t>(r_lo == INT64_MAX ? 0 : r_hi - r_lo, r_sum);
-        const size_t q = (size_t)std::max<int64_t>(q_lo == INT64_MAX ? 0 : q_hi - q_lo, q_sum);
+        if (r_lo == INT64_MAX) r_lo = r_hi = 0;
+        if (q_lo == INT64_MAX) q_lo = q_hi = 0;
+        // stage_chunk's choice: bulk when the extents hold little besides the chunk's own bytes
+        const bool bulk = (r_hi - r_lo) <= r_sum + r_sum / 4 + 4096 && (q_hi - q_lo) <= q_sum + q_sum / 4 + 4096;
+        const size_t r = (size_t)(bulk ? r_hi - r_lo : r_sum), q = (size_t)(bulk ? q_hi - q_lo : q_sum);
         const size_t mm = (size_t)mc;
-        const size_t nib = align256(align256(mm * sizeof(SeqPair)) + (r + 1) / 2 + 4) + (q + 1) / 2 + 4;
-        const size_t two = align256(align256(align256(mm * sizeof(PairIn)) + (r + 3) / 4 + 4) + (q + 3) / 4 + 4) +
-                           ((r + q) / 32 + 1024) * 4;
-        const size_t gat = align256(align256(mm * sizeof(SeqPair)) + r + 4) + q + 4;   // gathered: bytes as is
+        size_t st;
+        if (bulk && two_bit && r < ((size_t)1 << 30) && q < ((size_t)1 << 30))
+            st = std::max(align256(align256(align256(mm * sizeof(PairIn)) + (r + 3) / 4 + 4) + (q + 3) / 4 + 4) +
+                              ((r + q) / 32 + 1024) * 4,
+                          mm * 24);
+        else if (bulk)
+            st = align256(align256(mm * sizeof(SeqPair)) + (r + 1) / 2 + 4) + (q + 1) / 2 + 4;
+        else
+            st = align256(align256(mm * sizeof(SeqPair)) + r + 4) + q + 4;
         m = std::max(m, mc);
         rb = std::max(rb, r);
         qb = std::max(qb, q);
-        stage = std::max({stage, nib, two, gat, mm * 24});
+        stage = std::max(stage, st);
     }
 };
 
@@ -1451,11 +1461,13 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
                 bytes += x;
             }
             chs.emplace_back(b, nb);
-            res.add(std::min(n, (b + nb) * kStageBlk) - b * kStageBlk, bs.data() + b, nb);
+            res.add(std::min(n, (b + nb) * kStageBlk) - b * kStageBlk, bs.data() + b, nb, two_bit);
         }
     }
+
     rc = [&]() -> int {
         BSW_TRY(hipSetDevice(dc.device));
+        if (int r = reserve_slot(*slots[0], res)) return r;     // (slot 0 was taken before the schedule)
         int k = 0;
         int32_t seq = 0;
         for (const auto &ch : chs) {
