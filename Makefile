@@ -87,8 +87,8 @@ $(PRODUCT): $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc.o $(LIBDIR)/bsw_wv.o $(LIBD
 $(SYNTH): $(CSRC)/bsw_synth.c include/bsw_seqpair.h | $(LIBDIR)
 	gcc $(CFLAGS) -shared -o $@ $<
 
-ORACLE_SRCS := oracle/ksw_ext_ref.c oracle/bsw_sse41.c oracle/ext_ref.c oracle/ksw_align_ref.c oracle/ksw_global_ref.c oracle/fmi_ref.c oracle/chain_ref.c
-$(ORACLE): $(ORACLE_SRCS) include/bsw_seqpair.h include/bsw_ext.h include/bsw_fmi.h
+ORACLE_SRCS := oracle/ksw_ext_ref.c oracle/bsw_sse41.c oracle/bsw_avx512.c oracle/ext_ref.c oracle/ksw_align_ref.c oracle/ksw_global_ref.c oracle/fmi_ref.c oracle/chain_ref.c
+$(ORACLE): $(ORACLE_SRCS) oracle/bsw_simd_batch.inc oracle/bsw_simd_common.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_fmi.h
 	gcc $(CFLAGS) -msse4.1 -shared -o $@ $(ORACLE_SRCS) -lpthread
 
 clean:
@@ -124,12 +124,12 @@ ASAN_DIR   := tools/asan
 ASAN_FLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined -g -O1 -Iinclude
 ASAN_BIN   := $(ASAN_DIR)/asan_driver
 ASAN_C     := $(CSRC)/bsw_batch.c $(CSRC)/bsw_synth.c oracle/ksw_ext_ref.c oracle/ext_ref.c oracle/ksw_align_ref.c oracle/ksw_global_ref.c oracle/fmi_ref.c oracle/chain_ref.c
-ASAN_SSE   := oracle/bsw_sse41.c
+ASAN_SSE   := oracle/bsw_sse41.c oracle/bsw_avx512.c
 ASAN_CXX   := $(ASAN_DIR)/asan_driver.cpp $(ASAN_DIR)/engine_stub.cpp $(CSRC)/bsw_ext.cpp $(CSRC)/bsw_pack.cpp
-$(ASAN_BIN): $(ASAN_C) $(ASAN_SSE) $(ASAN_CXX) $(CSRC)/bsw_internal.h include/bsw_ext.h include/bsw_fmi.h
+$(ASAN_BIN): $(ASAN_C) $(ASAN_SSE) oracle/bsw_simd_batch.inc oracle/bsw_simd_common.h $(ASAN_CXX) $(CSRC)/bsw_internal.h include/bsw_ext.h include/bsw_fmi.h
 	mkdir -p $(ASAN_DIR)/obj
 	for f in $(ASAN_C); do gcc $(ASAN_FLAGS) -std=gnu11 -c $$f -o $(ASAN_DIR)/obj/$$(basename $$f).o || exit 1; done
-	gcc $(ASAN_FLAGS) -std=gnu11 -msse4.1 -c $(ASAN_SSE) -o $(ASAN_DIR)/obj/bsw_sse41.c.o
+	for f in $(ASAN_SSE); do gcc $(ASAN_FLAGS) -std=gnu11 -msse4.1 -c $$f -o $(ASAN_DIR)/obj/$$(basename $$f).o || exit 1; done
 	g++ $(ASAN_FLAGS) -std=c++17 -o $@ $(ASAN_CXX) $(ASAN_DIR)/obj/*.o -lpthread
 asan: $(ASAN_BIN)
 	ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \

@@ -58,6 +58,11 @@ def lib():
         _lib.oracle_get_scores_mt.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
         _lib.sse41_get_scores16.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
         _lib.sse41_get_scores16.restype = ctypes.c_int
+        for f in ("avx2_get_scores16", "avx512_get_scores16"):
+            getattr(_lib, f).argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
+            getattr(_lib, f).restype = ctypes.c_int
+        _lib.avx2_supported.restype = ctypes.c_int
+        _lib.avx512bw_supported.restype = ctypes.c_int
     return _lib
 
 
@@ -105,6 +110,24 @@ def sse41_get_scores16(params: OracleParams, pairs: np.ndarray, ref: np.ndarray,
     assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
     return lib().sse41_get_scores16(ctypes.byref(params), _ptr(pairs), _ptr(ref), _ptr(qer),
                                     len(pairs), w, nthreads)
+
+
+def simd_get_scores16(isa: str, params: OracleParams, pairs: np.ndarray, ref: np.ndarray, qer: np.ndarray,
+                      w: int, nthreads: int = 1) -> int:
+    """The same batch restatement at upstream's wider dispatch widths (oracle/bsw_avx512.c): isa
+    "avx2" (16 x int16 lanes) or "avx512bw" (32); raises if the host CPU lacks the ISA"""
+    assert pairs.dtype == SEQPAIR_DTYPE and pairs.flags.c_contiguous
+    L = lib()
+    ok = L.avx2_supported() if isa == "avx2" else L.avx512bw_supported() if isa == "avx512bw" else 0
+    if not ok:
+        raise RuntimeError(f"host CPU lacks {isa}")
+    fn = L.avx2_get_scores16 if isa == "avx2" else L.avx512_get_scores16
+    return fn(ctypes.byref(params), _ptr(pairs), _ptr(ref), _ptr(qer), len(pairs), w, nthreads)
+
+
+def simd_supported(isa: str) -> bool:
+    L = lib()
+    return bool(L.avx2_supported() if isa == "avx2" else L.avx512bw_supported() if isa == "avx512bw" else 0)
 
 
 def chain2aln(params, opt, ref, reads, read_off, read_len, seeds, seed_read, seed_chain, nthreads=1):
