@@ -300,6 +300,7 @@ struct DeviceCtx {
     int agg_leaders_max = 4;            // BSW_OPT_COALESCE_LEADERS
     int agg_linger_us = 0;              // BSW_OPT_COALESCE_LINGER (off: a trade-off by caller count)
     std::atomic<int> ownq_n{0};         // slots whose stream got a hardware queue of its own (acquire)
+    std::atomic<bool> copies_warm{false};   // host_shard's copy-engine warm-up ran (prime_copies)
     std::mutex mu;
     std::vector<std::unique_ptr<Slot>> free_slots;
     uint8_t *d_refres = nullptr;        // resident reference (bsw_set_reference)
@@ -1183,6 +1184,10 @@ static int reserve_slot(Slot &s, const SlotReserve &r)
 {
     if (r.m <= 0) return BSW_OK;
     BSW_TRY(hipSetDevice(s.device));
+    // the helper stream now, on the calling thread: created lazily by the enqueuer thread it cost
+    // ~10 ms per slot (hipStreamCreateWithPriority) in the middle of a call's pipeline, stalling
+    // every chunk queued behind it (HIP API trace, profiles/r06/hostpath_first_calls_api.txt)
+    if (int e = ensure_pstream(s)) return e;
     if (r.stage > s.cap_stage) {
         if (s.h_stage) (void)hipHostFree(s.h_stage);
         s.h_stage = nullptr;
@@ -1200,6 +1205,31 @@ static int reserve_slot(Slot &s, const SlotReserve &r)
     BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals, s.d_order, r.m, 0,
                                                kKeyBits, (hipStream_t)0));
     BSW_TRY(grow(s.d_tmp, s.cap_tmp, tmp_bytes));
+    return BSW_OK;
+}
+
+// Copy-engine warm-up, once per device context, on its first multi-chunk host call: H2D and D2H
+// copies in flight at once on every slot's helper and DP streams, large and small, as the
+// pipeline issues them.  Without it one hipMemcpyAsync in each of a context's first two calls
+// blocked for 7.6-9.6 ms with the GPU idle (HIP API trace, profiles/r06/hostpath_first_calls_api.txt);
+// with SDMA disabled (HSA_ENABLE_SDMA=0, blit-kernel copies) the stall was gone, so the first
+// copies that land on a not yet used DMA engine pay its set-up.
+static int prime_copies(Slot *const *slots, int ns)
+{
+    for (size_t want : {(size_t)1 << 62, (size_t)4 << 20, (size_t)64 << 10}) {
+        for (int k = 0; k < ns; ++k) {
+            Slot &s = *slots[k];
+            const size_t half = std::min(s.cap_stage, s.cap_dstage) / 2, sz = std::min(want, half);
+            if (sz == 0) continue;
+            uint8_t *h = (uint8_t *)s.h_stage;
+            BSW_TRY(hipMemcpyAsync(s.d_stage, h, sz, hipMemcpyHostToDevice, s.pstream));
+            BSW_TRY(hipMemcpyAsync(h + half, s.d_stage + half, sz, hipMemcpyDeviceToHost, s.stream));
+        }
+        for (int k = 0; k < ns; ++k) {
+            BSW_TRY(hipStreamSynchronize(slots[k]->pstream));
+            BSW_TRY(hipStreamSynchronize(slots[k]->stream));
+        }
+    }
     return BSW_OK;
 }
 
@@ -1468,6 +1498,20 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     rc = [&]() -> int {
         BSW_TRY(hipSetDevice(dc.device));
         if (int r = reserve_slot(*slots[0], res)) return r;     // (slot 0 was taken before the schedule)
+        if (chs.size() > 1 && !dc.copies_warm.exchange(true)) {
+            // the context's first pipelined call: every slot it will use now, then the copy
+            // warm-up over all of them at once (prime_copies)
+            const int ns = std::min<int>(nslots, (int)chs.size());
+            Slot *sp[nslots] = {slots[0].get()};
+            for (int j = 1; j < ns; ++j) {
+                int r = BSW_OK;
+                slots[j] = dc.acquire(r);
+                if (r) return r;
+                if ((r = reserve_slot(*slots[j], res))) return r;
+                sp[j] = slots[j].get();
+            }
+            if (int r = prime_copies(sp, ns)) return r;
+        }
         int k = 0;
         int32_t seq = 0;
         for (const auto &ch : chs) {
