@@ -91,6 +91,19 @@ for step in "$@"; do
                 python3 -c "import json;d=json.loads(open('$O/ab_run.log').read().strip().splitlines()[-1]);print('$v', d['value'], d['roofline']['launch_ms'])" | tee -a "$log"
             done
         done ;;
+    abhp)
+        # same-box A/B of the drop-in host path: tools/host_path_once.py (1M-pair calls after a
+        # device warm-up) with lib/<arg> (base) vs the in-tree library (new), alternating x3;
+        # per run the median of calls 3..8
+        log=$O/abhp_$arg.log; : > "$log"
+        for k in 1 2 3; do
+            for v in base new; do
+                if [ $v = base ]; then L=$PWD/bwa-mem2-arm_amd/lib/$arg; else L=$PWD/bwa-mem2-arm_amd/lib/libbsw_hip.so; fi
+                BSW_HIP_LIB=$L timeout -k 10 200 python tools/host_path_once.py 262144 8 1 > "$O/abhp_run.log" 2>&1 \
+                    || fail "$step" $? "$O/abhp_run.log"
+                python3 -c "import statistics as S;v=[float(l.split()[1]) for l in open('$O/abhp_run.log') if l.startswith('call')][2:];print('$v', round(S.median(v),3), v)" | tee -a "$log"
+            done
+        done ;;
     hptrace)
         # the drop-in host path's timeline: per-chunk host times (BSW_DEBUG_HP) and a kernel +
         # copy trace of a few 1M-pair bsw_get_scores calls (tools/host_path_once.py [chunk] [calls])
