@@ -1644,6 +1644,11 @@ def main_mem(args, rank, local, world, c1: bool):
             "algorithmic": f"{alg_per_read:.0f} B per read ({n_blocks / S:.1f} occurrence-block loads x 64 B "
                            f"+ the read) x {n} reads per step", "launch_ms_per_step": round(smem_s * 1e3, 3),
             "backward_extensions_per_read": round(n_bext / S, 1)})
+    if "roofline" not in out_j and not c1:
+        # no CPU leg (--no-cpu, N > 1): the SMEM roofline from this workload's PMC pass alone
+        out_j["roofline"] = smem_roofline(args, None, {
+            "kernel": "smem_kernel", "launch_ms_per_step": round(fmi.last_kernel_ms(), 3),
+            "algorithmic": "logical occurrence-block loads: counted by the CPU leg only"})
     if not c1:
         # the reference's own published bwa-mem2 rate (another machine and another dataset, SAM output
         # included): beside the oracle leg, never as the baseline of a ratio
@@ -1832,10 +1837,13 @@ def smem_roofline(args, logical_gbps: float, extra: dict) -> dict:
     others -- beside it as logical_GBps.  Without one: the logical rate, labelled as such."""
     t = traffic_for(args, "smem_kernel")
     r = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", **t, "pmc_key": workload_key(args),
-         "logical_GBps": round(logical_gbps, 1), "logical_frac": round(logical_gbps / HBM_PEAK_GBS, 4)}
+         "logical_GBps": None if logical_gbps is None else round(logical_gbps, 1),
+         "logical_frac": None if logical_gbps is None else round(logical_gbps / HBM_PEAK_GBS, 4)}
     if t.get("counter_GBps"):
         r.update(achieved=t["counter_GBps"], frac=round(t["counter_GBps"] / HBM_PEAK_GBS, 4),
                  basis="PMC-counted HBM bytes per launch / traced launch time (this workload's pass)")
+    elif logical_gbps is None:          # (no CPU leg to count the logical loads, no PMC pass)
+        r.update(achieved=None, frac=None, basis="no PMC pass of this workload and no CPU leg: unmeasured")
     else:
         r.update(achieved=round(logical_gbps, 1), frac=round(logical_gbps / HBM_PEAK_GBS, 4),
                  basis="logical occurrence-block loads x 64 B (no PMC pass of this workload)")
