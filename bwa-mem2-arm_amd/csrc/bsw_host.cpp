@@ -209,6 +209,7 @@ struct Slot {
     // host-buffer pipeline: pinned staging of one chunk and its device copy
     void *h_stage = nullptr; size_t cap_stage = 0;
     uint8_t *d_stage = nullptr; size_t cap_dstage = 0;
+    int32_t *d_bkt = nullptr; size_t cap_bkt = 0;   // staged exceptions: first word per 4096 positions
     // mate rescue (bsw_mate.h)
     int32_t *d_mjobs = nullptr; size_t cap_mjobs = 0;
     uint16_t *d_mrows = nullptr; size_t cap_mrows = 0;
@@ -320,6 +321,7 @@ struct DeviceCtx {
         (void)hipFree(s->d_keys); (void)hipFree(s->d_keys2); (void)hipFree(s->d_vals); (void)hipFree(s->d_order);
         (void)hipFree(s->d_tmp); (void)hipFree(s->d_meta); (void)hipFree(s->d_scratch);
         (void)hipFree(s->d_stage);
+        (void)hipFree(s->d_bkt);
         if (s->h_stage) (void)hipHostFree(s->h_stage);
         (void)hipFree(s->d_mjobs); (void)hipFree(s->d_mrows); (void)hipFree(s->d_mmeta);
         (void)hipFree(s->d_mcells); (void)hipFree(s->d_mpairs); (void)hipFree(s->d_maln);
@@ -844,57 +846,139 @@ __global__ void expand_pairs_kernel(const PairIn *__restrict__ in, SeqPair *__re
 
 // The whole staged input of a coalesced batch in one launch (what unpack2 x2 + patch_codes +
 // expand_pairs + two pad memsets did in six): index space = ref 16-code units, qer units, pairs.
-// Exception words (pos << 2 | code bits 2-3, bsw_pack.cpp) are ascending per buffer, so a unit finds
-// its own by a binary search and patches them after unpacking (no second pass, no race).
-__device__ __forceinline__ void unpack_unit(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int64_t n,
-                                            int64_t t, const uint32_t *__restrict__ exc, int32_t ne)
+// Exception words (pos << 2 | code bits 2-3, bsw_pack.cpp) are ascending per buffer.  A lane
+// unpacks 64 codes (16 packed bytes in, 64 bytes out; see unpack_unit for the interleaving), a wave 4096 consecutive positions: the
+// wave reads the index of its first exception from exc_bucket_kernel's table (one entry per 4096
+// positions), loads the next 64 words (one per lane) and every lane patches the ones inside its
+// own codes from a uniform walk over those in the wave's range (~4 per wave at bwa's N rate).  A
+// binary search per lane per 16 codes -- ~20 dependent loads each at 900K exceptions per 3M-pair
+// piece -- made the staging kernel latency-bound: 1.8-3.0 ms per 3M pairs in the RCCL leg's trace,
+// ahead of every piece's DP; one search per wave still 1.2-2.4 ms (profiles/r06/rccl_leg_trace.txt).
+// Whole-wave function: every lane of the wave calls it (valid = the lane has codes to write).
+constexpr int kUnitCodes = 64;          // codes per lane
+__device__ __forceinline__ uint4 unpack16(uint32_t v)    // 16 codes from 4 packed bytes
 {
-    const int64_t o = t * 16;
-    uint32_t v = 0;
-    const int64_t ib = t * 4, nin = (n + 3) / 4;
-    if (ib + 4 <= nin) v = *(const uint32_t *)(in + ib);
-    else
-        for (int k = 0; k < 4 && ib + k < nin; ++k) v |= (uint32_t)in[ib + k] << (8 * k);
     const uint32_t p0 = v & 0x03030303u, p1 = (v >> 2) & 0x03030303u;
     const uint32_t p2 = (v >> 4) & 0x03030303u, p3 = (v >> 6) & 0x03030303u;
     const uint32_t a01 = __builtin_amdgcn_perm(p1, p0, 0x05010400u), b01 = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
     const uint32_t a23 = __builtin_amdgcn_perm(p3, p2, 0x05010400u), b23 = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
-    uint32_t w[4] = {__builtin_amdgcn_perm(a23, a01, 0x05040100u), __builtin_amdgcn_perm(a23, a01, 0x07060302u),
-                     __builtin_amdgcn_perm(b23, b01, 0x05040100u), __builtin_amdgcn_perm(b23, b01, 0x07060302u)};
+    return make_uint4(__builtin_amdgcn_perm(a23, a01, 0x05040100u), __builtin_amdgcn_perm(a23, a01, 0x07060302u),
+                      __builtin_amdgcn_perm(b23, b01, 0x05040100u), __builtin_amdgcn_perm(b23, b01, 0x07060302u));
+}
+__device__ __forceinline__ void unpack_unit(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int64_t n,
+                                            int64_t wave_t0, int64_t units,
+                                            const uint32_t *__restrict__ exc, int32_t ne,
+                                            const int32_t *__restrict__ bkt)
+{
+    // the wave's 4096 positions [W, W + 4096) as 4 sub-units per lane, interleaved so that every
+    // load / store instruction of the wave is contiguous: sub-unit u of lane L = the 16 codes at
+    // W + 1024 u + 16 L (4 packed bytes in, one 16-B store out)
+    if (wave_t0 >= units) return;                                // (the tail waves of a block: uniform)
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t W = wave_t0 * kUnitCodes, nin = (n + 3) / 4;
+    uint4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t pos = W + 1024 * u + 16 * lane, ib = pos / 4;
+        uint32_t v = 0;
+        if (ib + 4 <= nin) v = *(const uint32_t *)(in + ib);
+        else
+            for (int k = 0; k < 4 && ib + k < nin; ++k) v |= (uint32_t)in[ib + k] << (8 * k);
+        w[u] = unpack16(v);
+    }
     if (ne > 0) {
-        int32_t lo = 0, hi = ne;                       // first exception at or past o
-        while (lo < hi) {
-            const int32_t mid = (lo + hi) >> 1;
-            if ((int64_t)(exc[mid] >> 2) < o) lo = mid + 1; else hi = mid;
-        }
-        for (; lo < ne && (int64_t)(exc[lo] >> 2) < o + 16; ++lo) {
-            const int k = (int)((exc[lo] >> 2) - o);
-            w[k >> 2] |= (exc[lo] & 3u) << (8 * (k & 3) + 2);     // code bits 2-3 over the plane's 0-1
+        const int64_t whi = W + 64 * kUnitCodes;
+        const int32_t lo = min(max(bkt[wave_t0 / 64], 0), ne);  // first exception at or past W (uniform)
+        for (int32_t base = lo;; base += 64) {                   // uniform: 64 words per round
+            const int32_t j = base + lane;
+            const uint32_t e = j < ne ? exc[j] : 0u;
+            const bool in_w = j < ne && (int64_t)(e >> 2) < whi;
+            const int cnt = __popcll(__ballot(in_w));              // sorted: lanes 0 .. cnt - 1
+            for (int q = 0; q < cnt; ++q) {
+                const uint32_t eq = (uint32_t)__shfl((int)e, q);
+                const int64_t k = (int64_t)(eq >> 2) - W;         // 0 .. 4095 (in the wave's range)
+                if (k >= 0 && k < 4096 && (int)((k >> 4) & 63) == lane) {
+                    const int u = (int)(k >> 10), c = (int)(k & 15);
+                    const uint32_t bits = (eq & 3u) << (8 * (c & 3) + 2);   // code bits 2-3
+                    const int d = c >> 2;
+#pragma unroll
+                    for (int uu = 0; uu < 4; ++uu) {
+                        w[uu].x |= (u == uu && d == 0) ? bits : 0u;
+                        w[uu].y |= (u == uu && d == 1) ? bits : 0u;
+                        w[uu].z |= (u == uu && d == 2) ? bits : 0u;
+                        w[uu].w |= (u == uu && d == 3) ? bits : 0u;
+                    }
+                }
+            }
+            if (cnt < 64) break;
         }
     }
-    if (o + 16 <= n) {
-        *(uint4 *)(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-        for (int k = 0; o + k < n; ++k) out[o + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t pos = W + 1024 * u + 16 * lane;
+        if (pos + 16 <= n) {
+            *(uint4 *)(out + pos) = w[u];
+        } else {
+            const uint32_t word[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+            for (int k = 0; pos + k < n; ++k) out[pos + k] = (uint8_t)(word[k >> 2] >> (8 * (k & 3)));
+        }
     }
 }
 
-__global__ void stage_in_kernel(const uint8_t *__restrict__ ref2, int64_t r_tot, const uint8_t *__restrict__ qer2,
+// Blocks of 256 threads, each block inside one segment (so every wave is): [ref 64-code units |
+// qer units | records]; stage_in_grid() is the matching grid size
+__host__ __device__ inline int64_t stage_in_blocks(int64_t r_tot, int64_t q_tot, int64_t n, int64_t *br, int64_t *bq)
+{
+    *br = ((r_tot + kUnitCodes - 1) / kUnitCodes + 255) / 256;
+    *bq = ((q_tot + kUnitCodes - 1) / kUnitCodes + 255) / 256;
+    return *br + *bq + (n + 255) / 256;
+}
+
+// bkt[b] = the first exception word at or past position 4096 b: ref buckets [0, nbr), then qer
+// buckets [nbr, nbr + nbq) indexing the qer words (exc + n_r).  One lane per bucket, its own binary
+// search: ~nbr + nbq lanes instead of one search per staging wave
+__global__ void exc_bucket_kernel(const uint32_t *__restrict__ exc, int32_t n_r, int32_t ne, int64_t nbr, int64_t nbq,
+                                  int32_t *__restrict__ bkt)
+{
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nbr + nbq) return;
+    const bool q = b >= nbr;
+    const uint32_t *e = q ? exc + n_r : exc;
+    const int64_t pos = (q ? b - nbr : b) * 4096;
+    int32_t lo = 0, hi = q ? ne - n_r : n_r;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if ((int64_t)(e[mid] >> 2) < pos) lo = mid + 1; else hi = mid;
+    }
+    bkt[b] = lo;
+}
+
+__global__ __launch_bounds__(256) void stage_in_kernel(const uint8_t *__restrict__ ref2, int64_t r_tot,
+                                const uint8_t *__restrict__ qer2,
                                 int64_t q_tot, const uint32_t *__restrict__ exc, int32_t n_r, int32_t ne,
                                 const PairIn *__restrict__ pin, int32_t n, uint8_t *__restrict__ ref,
-                                uint8_t *__restrict__ qer, SeqPair *__restrict__ pairs, int32_t *__restrict__ zero2)
+                                uint8_t *__restrict__ qer, SeqPair *__restrict__ pairs, int32_t *__restrict__ zero2,
+                                const int32_t *__restrict__ bkt, int64_t nbr)
 {
-    const int64_t tr = (r_tot + 15) / 16, tq = (q_tot + 15) / 16;
-    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t == 0) {
+    const int64_t tr = (r_tot + kUnitCodes - 1) / kUnitCodes, tq = (q_tot + kUnitCodes - 1) / kUnitCodes;   // lanes
+    int64_t br, bq;
+    stage_in_blocks(r_tot, q_tot, n, &br, &bq);
+    const int64_t blk = blockIdx.x;
+    const int wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (blk == 0 && threadIdx.x == 0) {
         *(uint32_t *)(ref + r_tot) = 0u;          // 4 zero bytes past each buffer
         *(uint32_t *)(qer + q_tot) = 0u;
         if (zero2) { zero2[0] = 0; zero2[1] = 0; }
     }
-    if (t < tr) { unpack_unit(ref2, ref, r_tot, t, exc, n_r); return; }
-    t -= tr;
-    if (t < tq) { unpack_unit(qer2, qer, q_tot, t, exc + n_r, ne - n_r); return; }
-    t -= tq;
+    if (blk < br) {
+        unpack_unit(ref2, ref, r_tot, blk * 256 + 64 * wv, tr, exc, n_r, bkt);
+        return;
+    }
+    if (blk < br + bq) {
+        unpack_unit(qer2, qer, q_tot, (blk - br) * 256 + 64 * wv, tq, exc + n_r, ne - n_r, bkt + nbr);
+        return;
+    }
+    const int64_t t = (blk - br - bq) * 256 + threadIdx.x;
     if (t < n) {
         const PairIn p = pin[t];
         SeqPair sp;
@@ -902,6 +986,28 @@ __global__ void stage_in_kernel(const uint8_t *__restrict__ ref2, int64_t r_tot,
         sp.idr = p.idr; sp.idq = p.idq; sp.len1 = p.len1; sp.len2 = p.len2; sp.h0 = p.h0;
         pairs[t] = sp;
     }
+}
+
+static size_t exc_buckets(int64_t r_tot, int64_t q_tot) { return (size_t)((r_tot + 4095) / 4096 + (q_tot + 4095) / 4096 + 2); }
+
+// The whole staged input of one batch: the exceptions' bucket table (when there are exceptions),
+// then stage_in_kernel -- on `st`, the slot's d_bkt grown to the table
+static int launch_stage_in(Slot &s, hipStream_t st, const uint8_t *ref2, int64_t r_tot, const uint8_t *qer2,
+                           int64_t q_tot, const uint32_t *exc, int32_t n_r, int32_t ne, const PairIn *pin, int32_t n,
+                           uint8_t *ref, uint8_t *qer, SeqPair *pairs, int32_t *zero2)
+{
+    const int64_t nbr = (r_tot + 4095) / 4096 + 1, nbq = (q_tot + 4095) / 4096 + 1;
+    if (ne > 0) {
+        BSW_TRY(grow(s.d_bkt, s.cap_bkt, exc_buckets(r_tot, q_tot)));
+        hipLaunchKernelGGL(exc_bucket_kernel, dim3((unsigned)((nbr + nbq + 255) / 256)), dim3(256), 0, st, exc, n_r,
+                           ne, nbr, nbq, s.d_bkt);
+        BSW_TRY(hipGetLastError());
+    }
+    int64_t br, bq;
+    const unsigned grid = (unsigned)stage_in_blocks(r_tot, q_tot, n, &br, &bq);
+    hipLaunchKernelGGL(stage_in_kernel, dim3(grid), dim3(256), 0, st, ref2, r_tot, qer2, q_tot, exc, n_r, ne, pin, n,
+                       ref, qer, pairs, zero2, (const int32_t *)s.d_bkt, nbr);
+    return hip_rc(hipGetLastError());
 }
 
 // the six outputs of each pair (SeqPair bytes 32..55) -> 24 B per pair for the D2H
@@ -1200,6 +1306,7 @@ static int reserve_slot(Slot &s, const SlotReserve &r)
     BSW_TRY(grow(s.d_ref, s.cap_ref, r.rb + 16));
     BSW_TRY(grow(s.d_qer, s.cap_qer, r.qb + 16));
     BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)r.m));
+    BSW_TRY(grow(s.d_bkt, s.cap_bkt, exc_buckets((int64_t)r.rb, (int64_t)r.qb)));
     BSW_TRY(grow_sort(s, r.m));
     size_t tmp_bytes = 0;
     BSW_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s.d_keys, s.d_keys2, s.d_vals, s.d_order, r.m, 0,
@@ -1376,14 +1483,11 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
                 BSW_TRY(grow(s.d_ref, s.cap_ref, c.rb + 16));
                 BSW_TRY(grow(s.d_qer, s.cap_qer, c.qb + 16));
                 BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)m));
-                const int64_t tr = ((int64_t)c.rb + 15) / 16, tq = ((int64_t)c.qb + 15) / 16;
-                const int64_t nthr = tr + tq + m;
-                hipLaunchKernelGGL(stage_in_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, hs,
-                                   s.d_stage + c.ref_off, (int64_t)c.rb, s.d_stage + c.qer_off, (int64_t)c.qb,
-                                   (const uint32_t *)(s.d_stage + c.exc_off), c.n_exr, c.n_exr + c.n_exq,
-                                   (const PairIn *)(s.d_stage + c.pair_off), m, s.d_ref, s.d_qer, s.d_pairs,
-                                   (int32_t *)nullptr);
-                BSW_TRY(hipGetLastError());
+                if (int e = launch_stage_in(s, hs, s.d_stage + c.ref_off, (int64_t)c.rb, s.d_stage + c.qer_off,
+                                            (int64_t)c.qb, (const uint32_t *)(s.d_stage + c.exc_off), c.n_exr,
+                                            c.n_exr + c.n_exq, (const PairIn *)(s.d_stage + c.pair_off), m, s.d_ref,
+                                            s.d_qer, s.d_pairs, nullptr))
+                    return e;
                 d_r = s.d_ref;
                 d_q = s.d_qer;
                 d_p = s.d_pairs;
@@ -1682,15 +1786,12 @@ static int run_group_staged(const KParams &kp, DeviceCtx &dc, std::vector<AggSeg
         BSW_TRY(grow(s.d_ref, s.cap_ref, (size_t)r_tot + 4));
         BSW_TRY(grow(s.d_qer, s.cap_qer, (size_t)q_tot + 4));
         BSW_TRY(grow(s.d_pairs, s.cap_pairs, (size_t)N));
-        const int64_t tr = (r_tot + 15) / 16, tq = (q_tot + 15) / 16;
         const int32_t ne = (int32_t)(n_r + n_q);
-        const int64_t nthr = tr + tq + N;
-        hipLaunchKernelGGL(stage_in_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s.stream,
-                           s.d_stage + ref_off, r_tot, s.d_stage + qer_off, q_tot,
-                           (const uint32_t *)(s.d_stage + exc_off), (int32_t)n_r, ne,
-                           (const PairIn *)(s.d_stage + pair_off), N, s.d_ref, s.d_qer, s.d_pairs,
-                           s.d_meta + kMetaErr);
-        BSW_TRY(hipGetLastError());
+        if (int e = launch_stage_in(s, s.stream, s.d_stage + ref_off, r_tot, s.d_stage + qer_off, q_tot,
+                                    (const uint32_t *)(s.d_stage + exc_off), (int32_t)n_r, ne,
+                                    (const PairIn *)(s.d_stage + pair_off), N, s.d_ref, s.d_qer, s.d_pairs,
+                                    s.d_meta + kMetaErr))
+            return e;
         PlanCall pc;
         pc.d_pairs = s.d_pairs; pc.d_ref = s.d_ref; pc.d_qer = s.d_qer;
         pc.n = N; pc.w = w; pc.cell_bits = cell_bits; pc.stream = s.stream;
@@ -2460,13 +2561,21 @@ int bsw_get_scores_packed_device(bsw_ctx_t *ctx, const void *d_packed, const bsw
         BSW_TRY(bsw::grow(s.d_qer, s.cap_qer, (size_t)d.qer_bytes + 16));
         BSW_TRY(bsw::grow(s.d_pairs, s.cap_pairs, (size_t)d.n));
         const uint8_t *b = (const uint8_t *)d_packed;
-        const int64_t tr = (d.ref_bytes + 15) / 16, tq = (d.qer_bytes + 15) / 16;
-        const int64_t nthr = tr + tq + d.n;
-        hipLaunchKernelGGL(bsw::stage_in_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st,
-                           b + d.ref_off, d.ref_bytes, b + d.qer_off, d.qer_bytes, (const uint32_t *)(b + d.exc_off),
-                           d.n_exc_ref, d.n_exc_ref + d.n_exc_qer, (const bsw::PairIn *)(b + d.rec_off), d.n,
-                           s.d_ref, s.d_qer, s.d_pairs, (int32_t *)nullptr);
-        BSW_TRY(hipGetLastError());
+        // the staging kernels on the slot's high-priority stream (after the caller's stream: the
+        // piece may have been written there), as plan / sort already are: a piece's preparation is
+        // then dispatched ahead of another piece's queued DP workgroups instead of behind them (the
+        // RCCL leg's trace: the second piece's staging waited out the first piece's whole DP,
+        // profiles/r06/rccl_leg_trace.txt).  Its DP, on `st`, waits for the plan (run_dp).
+        if (int e = bsw::ensure_pstream(s)) return e;
+        BSW_TRY(hipEventRecord(s.evh, st));
+        BSW_TRY(hipStreamWaitEvent(s.pstream, s.evh, 0));
+        if (int e = bsw::launch_stage_in(s, s.pstream, b + d.ref_off, d.ref_bytes, b + d.qer_off, d.qer_bytes,
+                                         (const uint32_t *)(b + d.exc_off), d.n_exc_ref, d.n_exc_ref + d.n_exc_qer,
+                                         (const bsw::PairIn *)(b + d.rec_off), d.n, s.d_ref, s.d_qer, s.d_pairs, nullptr))
+            return e;
+        // everything after it on `st` (the small-batch route launches there without a plan)
+        BSW_TRY(hipEventRecord(s.evh, s.pstream));
+        BSW_TRY(hipStreamWaitEvent(st, s.evh, 0));
         int r = bsw::run_device(ctx->kp, s, s.d_pairs, s.d_ref, s.d_qer, d.n, w, cell_bits, st);
         if (r) return r;
         if ((r = bsw::finish_stats(s))) return r;
