@@ -409,8 +409,10 @@ def main():
                          "fixed batch of --total-pairs split over the ranks by band cells, host buffers "
                          "in, PCIe both ways inside the timed region (C5)")
     ap.add_argument("--total-pairs", type=int, default=10_000_000, help="strong: pairs in the whole batch")
-    ap.add_argument("--rccl-chunks", type=int, default=4,
-                    help="RCCL C2 leg: pieces per rank (chunk k + 1 scatters while chunk k is scored)")
+    ap.add_argument("--rccl-chunks", type=int, default=2,
+                    help="RCCL C2 leg: pieces per rank (chunk k + 1 scatters while chunk k is scored; one rank, "
+                         "same box: 2 pieces 0.968 of the single-GPU time, 4 pieces 0.941, "
+                         "profiles/r06/rccl_leg_trace.txt)")
     ap.add_argument("--rccl-pairs", type=int, default=6_000_000,
                     help="default C2 line at N > 1: pairs of the strong-scaling RCCL leg whose throughput is the "
                          "line's value (one batch on GPU 0, RCCL scatter -> score -> RCCL gather; the per-rank "
