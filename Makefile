@@ -139,7 +139,7 @@ asan: $(ASAN_BIN)
 # keeps its arenas).  Log: tools/asan/asan_suite.log
 ASAN_ORACLE := $(ASAN_DIR)/liboracle_asan.so
 ASAN_SYNTH  := $(ASAN_DIR)/libbsw_synth_asan.so
-$(ASAN_ORACLE): $(ORACLE_SRCS) include/bsw_seqpair.h include/bsw_ext.h include/bsw_fmi.h
+$(ASAN_ORACLE): $(ORACLE_SRCS) oracle/bsw_simd_batch.inc oracle/bsw_simd_common.h include/bsw_seqpair.h include/bsw_ext.h include/bsw_fmi.h
 	mkdir -p $(ASAN_DIR)
 	gcc $(ASAN_FLAGS) -fPIC -msse4.1 -shared -o $@ $(ORACLE_SRCS) -lpthread
 $(ASAN_SYNTH): $(CSRC)/bsw_synth.c include/bsw_seqpair.h
