@@ -41,6 +41,9 @@
 namespace bsw {
 
 constexpr int kPcChunkDw = 17;           // dwords per lane per 64-row target chunk (as lane kernel)
+#ifndef BSW_PC_EXP_HALFHEAD
+#define BSW_PC_EXP_HALFHEAD 0
+#endif
 #ifdef BSW_PC_STATS
 __device__ unsigned long long g_pc_stats[8];
 // per-wave schedule record (tools/pc_times.py): start / end (s_memrealtime, 100 MHz), XCC id and
@@ -704,6 +707,10 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
     uint32_t nrows = 0, nlast = 0, nue = 0;
 #endif
 
+#if BSW_PC_EXP_HALFHEAD
+    int emax = 0, emin = 0;                 // (experiment: the row head's state outlives its row)
+    PcRow r{0, 0, 0};
+#endif
     for (int i = 0;; ++i) {
         const bool act = alive && i < tlen;
         alive = act;
@@ -737,9 +744,17 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
         const int beg = max(0, i - wl);
         const int end = min(min(endc, i + wl + 1), qlen);
         endc = end;
+#if BSW_PC_EXP_HALFHEAD
+        // experiment build only (make ab AB_FLAGS=-DBSW_PC_EXP_HALFHEAD=1; WRONG outputs): the row
+        // head -- band-end reductions and the three group sets -- on even rows only, the odd rows
+        // reusing the previous row's: the time a two-rows-per-pass schedule could save on row heads
+        // (-1.3%)
+        if (i & 1) goto row_body;
+#else
         int emax, emin;
-        wave_maxmin_bc(act ? end : -1, act ? end : INT_MAX, emax, emin);
         PcRow r;
+#endif
+        wave_maxmin_bc(act ? end : -1, act ? end : INT_MAX, emax, emin);
         {
             const int ulo = __builtin_amdgcn_readfirstlane(max(0, i - wl_max));  // min beg
             const int uhi = __builtin_amdgcn_readfirstlane(emax);                // max end
@@ -756,6 +771,9 @@ __global__ __launch_bounds__(64 * WPB, BY ? 3 : 2) void pc_kernel(const KParams 
             r.fast = gbits(gfa, gfn);
             r.left = gbits(glo, gln + 1);
         }
+#if BSW_PC_EXP_HALFHEAD
+    row_body:
+#endif
         {   // every lane runs the row (dead lanes' registers take garbage); state updates are
             // gated by act below, so no exec-masked block wraps the row
             // h1 = H(i, j-1) entering each group, in the HIGH half (PC_FAST_CHAIN)
