@@ -604,8 +604,19 @@ def main():
         out["abi_inclusive"] = dict(hp, unit=UNIT, note="bsw_get_scores on pageable host buffers: staging "
                                     "(2-bit codes, 20-B input records) + H2D + plan/sort/DP + D2H of the outputs, "
                                     "chunked pipeline over four slots")
+        eng.set_option("host_pack", 4)                 # the nibble staging beside it (same box, same batch)
+        hp4 = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res, curve_sizes=())
+        eng.set_option("host_pack", 2)
+        out["abi_inclusive"]["nibble_staging"] = {"value": hp4["value"], "ms": hp4["ms"],
+                                                  "outputs_identical_to_resident": hp4["outputs_identical_to_resident"]}
         # the same curve from C++ kt_for-style threads through the C ABI (tools/percall_bench.cpp:
-        # no Python between calls), with and without cross-call coalescing
+        # no Python between calls), with and without cross-call coalescing -- in a process of its own,
+        # after this one has released its engine: the engine's slot streams each hold a hardware
+        # queue, and with both processes' queues on the GPU the 8 x 10K point read 37 M/s instead of
+        # the 41-42 the same binary measures alone (profiles/r06/percall_10k_quad_ab.txt)
+        eng.close()
+        for b in (d_pairs, d_ref, d_qer):
+            b.free()
         import subprocess
         exe = os.path.join(ROOT, "bwa-mem2-arm_amd", "lib", "percall_bench")
         if os.path.exists(exe):
@@ -616,11 +627,6 @@ def main():
                     out["abi_inclusive"]["per_call_curve_cpp_callers"] = json.loads(r.stdout.strip().splitlines()[-1])
             except (subprocess.SubprocessError, ValueError, IndexError):
                 pass
-        eng.set_option("host_pack", 4)                 # the nibble staging beside it (same box, same batch)
-        hp4 = host_path_rates(eng, pairs, ref, qer, args.w, args.cell_bits, res, curve_sizes=())
-        eng.set_option("host_pack", 2)
-        out["abi_inclusive"]["nibble_staging"] = {"value": hp4["value"], "ms": hp4["ms"],
-                                                  "outputs_identical_to_resident": hp4["outputs_identical_to_resident"]}
     if world == 1 and not args.no_cpu:
         cores = args.cpu_threads or len(os.sched_getaffinity(0))
         out["cpu_baseline"] = cpu_baseline(pairs, ref, qer, args.w, res, cores)

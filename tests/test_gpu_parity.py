@@ -535,6 +535,35 @@ def test_packed_device_equal_oracle(n):
     e.close()
 
 
+def test_packed_device_dense_exceptions():
+    """The staging kernel's exception walk past one 64-word round: runs of thousands of N in the
+    reference and the queries (every word of a wave's 4096 positions is an exception), N at a
+    segment's first and last positions, and exceptions in only one of the two buffers."""
+    pairs, ref, qer = bswgen.random_pairs(20_000, seed=777, qlen=(0, 160), tlen=(0, 300), h0=(0, 120))
+    for case in range(3):
+        r, q = ref.copy(), qer.copy()
+        if case != 2:
+            r[5000:17000] = 4                                 # 12K consecutive exception words
+            r[0] = 4
+            r[-1] = 4
+        if case != 1:
+            q[2000:9000] = 4
+            q[-1] = 4
+        want = pairs.copy()
+        oracle.get_scores(_oparams(), want, r, q, 100, nthreads=8)
+        buf, d = bsw.pack_batch(pairs, r, q)
+        db = hiprt.DeviceBuffer.from_array(buf)
+        out = np.full((len(pairs), 6), -7, dtype=np.int32)
+        dout = hiprt.DeviceBuffer.from_array(out)
+        e = bsw.Engine()
+        e.get_scores_packed_device(db.ptr, d, 100, 16, dout.ptr)
+        got = dout.download(np.empty_like(out))
+        for k, f in enumerate(bsw.OUT_FIELDS):
+            bad = int((got[:, k] != want[f]).sum())
+            assert bad == 0, f"dense exceptions case {case}: {f} differs in {bad} pairs"
+        e.close()
+
+
 def test_group_kernel_fallback_device():
     """Device entry point, small batch with a few pairs outside the row-group contract (query past
     160, int16-unsafe h0): the kernel flags them and the whole batch reruns on the planned path."""
