@@ -299,7 +299,8 @@ struct DeviceCtx {
     int agg_lingering = 0;              // leaders waiting for a deeper queue
     int agg_leaders = 0;
     int agg_leaders_max = 4;            // BSW_OPT_COALESCE_LEADERS
-    int agg_linger_us = 0;              // BSW_OPT_COALESCE_LINGER (off: a trade-off by caller count)
+    int agg_linger_us = 20;             // BSW_OPT_COALESCE_LINGER (20 us since round 6: 8 callers x 1K
+                                        //   +15-30%, 16 equal or better, <= 4 never linger)
     std::atomic<int> ownq_n{0};         // slots whose stream got a hardware queue of its own (acquire)
     std::atomic<bool> copies_warm{false};   // host_shard's copy-engine warm-up ran (prime_copies)
     std::mutex mu;

@@ -216,13 +216,14 @@ enum {
                                  BSW_OPT_GROUP_KERNEL is on -- an empty range at the defaults (the
                                  16-lane form measured faster up to 32K pairs; lower
                                  BSW_OPT_SMALL_BATCH to use it).  Outputs are identical either way */
-    BSW_OPT_COALESCE_LINGER = 16, /* microseconds (0..100000, default 0): with more concurrent
+    BSW_OPT_COALESCE_LINGER = 16, /* microseconds (0..100000, default 20): with more concurrent
                                  callers than BSW_OPT_COALESCE_LEADERS and two or more batches
                                  running, a new leader waits up to this long for 4096 queued pairs
                                  (or for fewer than two running batches) before taking the queue,
-                                 so batches fill up.  Measured at 150: 8 callers +16-25% at 1K-4K
-                                 pairs per call, 4 / 16 callers mixed, hence off by
-                                 default.  A lone caller never waits.  Outputs are identical     */
+                                 so batches fill up.  Measured at 20 (round 6): 8 callers +15-30%
+                                 at 1K-4K pairs per call, 16 callers equal or better (at 150,
+                                 round 4: 4 / 16 callers mixed).  0 = off.  A lone
+                                 caller never waits.  Outputs are identical                      */
     /* 15 and 17 (a busy-device routing knob and the persistent tile-queue kernel, ABI 7) were
        removed in ABI 8 after measuring slower than the defaults: BSW_E_INVAL */
     BSW_OPT_GQ32_MAX = 18,    /* batches of at most this many pairs (within BSW_OPT_SMALL_BATCH) run on
