@@ -409,10 +409,11 @@ def main():
                          "fixed batch of --total-pairs split over the ranks by band cells, host buffers "
                          "in, PCIe both ways inside the timed region (C5)")
     ap.add_argument("--total-pairs", type=int, default=10_000_000, help="strong: pairs in the whole batch")
-    ap.add_argument("--rccl-chunks", type=int, default=2,
-                    help="RCCL C2 leg: pieces per rank (chunk k + 1 scatters while chunk k is scored; one rank, "
-                         "same box: 2 pieces 0.968 of the single-GPU time, 4 pieces 0.941, "
-                         "profiles/r06/rccl_leg_trace.txt)")
+    ap.add_argument("--rccl-chunks", type=int, default=None,
+                    help="RCCL C2 leg: pieces per rank (chunk k + 1 scatters while chunk k is scored).  Default 2 "
+                         "at one rank (no scatter to hide: 2 pieces 0.946-0.968 of the single-GPU time, 4 pieces "
+                         "0.941-0.949, profiles/r06/rccl_leg_trace.txt), 4 at N > 1 (the first piece's scatter "
+                         "over xGMI is exposed: smaller pieces start each rank's DP sooner)")
     ap.add_argument("--rccl-pairs", type=int, default=6_000_000,
                     help="default C2 line at N > 1: pairs of the strong-scaling RCCL leg whose throughput is the "
                          "line's value (one batch on GPU 0, RCCL scatter -> score -> RCCL gather; the per-rank "
@@ -444,6 +445,8 @@ def main():
     rank, local, world = dist_init()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.rccl_chunks is None:
+        args.rccl_chunks = 2 if world == 1 else 4
     ndev = hiprt.device_count()
     if ndev < 1:
         raise SystemExit("bench.py: no HIP device visible")
