@@ -440,7 +440,9 @@ struct bsw_ctx {
     struct Pinned { std::mutex mu; void *p = nullptr; size_t cap = 0; } pin[2];
     int glob_band = 0;                  // BSW_OPT_GLOB_BAND
     int64_t ext_chunk = 0;              // BSW_OPT_EXT_CHUNK (0: the int32-offset bound)
-    int32_t host_chunk = 262144;        // BSW_OPT_HOST_CHUNK: pairs per host-buffer pipeline chunk
+    int32_t host_chunk = 196608;        // BSW_OPT_HOST_CHUNK: pairs per host-buffer pipeline chunk (round 6:
+                                        //   48 blocks beat 64 by 3-4% per 1M-pair call on two boxes,
+                                        //   profiles/r06/host_chunk_sweep.txt)
     int host_pack = 2;                  // BSW_OPT_HOST_PACK: 2-bit (2) or nibble (4) staging
     int64_t split_min = 131072;         // BSW_OPT_SPLIT_MIN: smaller calls go whole to one device
     int32_t coalesce = 8192;            // BSW_OPT_COALESCE: calls of <= this many pairs coalesce

@@ -179,7 +179,7 @@ enum {
                                  per alignment (bsw_wv.hip, default), 0 = the int32 wide kernel,
                                  2 = every pair the wave kernel can run goes there (tests)   */
     BSW_OPT_HOST_CHUNK = 6,   /* bsw_get_scores: largest pipeline chunk in pairs (default
-                                 262144, rounded down to whole 4096-pair blocks, at least one):
+                                 196608, rounded down to whole 4096-pair blocks, at least one):
                                  a host-buffer call is staged, copied and computed chunk by
                                  chunk over up to four slots so copies overlap the DP
                                  kernels; calls of <= 128K pairs run as one chunk            */
