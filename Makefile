@@ -109,13 +109,19 @@ ab:
 	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/bsw_pc.hip -o $(LIBDIR)/bsw_pc_ab.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(ABLIB) $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc_ab.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_devcache.o $(LIBDIR)/bsw_batch.o -lpthread
 
+# the same for bsw_host.cpp (host pipeline experiments): libbsw_hip_abhost.so
+ABHOSTLIB := $(LIBDIR)/libbsw_hip_abhost.so
+abhost:
+	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -x hip -c $(CSRC)/bsw_host.cpp -o $(LIBDIR)/bsw_host_ab.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(ABHOSTLIB) $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host_ab.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_devcache.o $(LIBDIR)/bsw_batch.o -lpthread
+
 # the same for bsw_fmi.hip (SMEM walk experiments): libbsw_hip_abfmi.so
 ABFMILIB := $(LIBDIR)/libbsw_hip_abfmi.so
 abfmi:
 	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/bsw_fmi.hip -o $(LIBDIR)/bsw_fmi_ab.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(ABFMILIB) $(LIBDIR)/bsw_kernels.o $(LIBDIR)/bsw_pc.o $(LIBDIR)/bsw_wv.o $(LIBDIR)/bsw_gq.o $(LIBDIR)/bsw_mate.o $(LIBDIR)/bsw_global.o $(LIBDIR)/bsw_ext_dev.o $(LIBDIR)/bsw_fmi_ab.o $(LIBDIR)/bsw_fmi_build.o $(LIBDIR)/bsw_memchain.o $(LIBDIR)/bsw_chain.o $(LIBDIR)/bsw_host.o $(LIBDIR)/bsw_ext.o $(LIBDIR)/bsw_pack.o $(LIBDIR)/bsw_devcache.o $(LIBDIR)/bsw_batch.o -lpthread
 
-.PHONY: all product synth oracle percall clean stats ab abfmi
+.PHONY: all product synth oracle percall clean stats ab abfmi abhost
 
 # host sanitizer build: AddressSanitizer + UBSan over the host C / C++ of the
 # product (bsw_pack.cpp, bsw_ext.cpp, bsw_batch.c, bsw_synth.c) and the oracle, driven by

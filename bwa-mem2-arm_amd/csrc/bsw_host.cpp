@@ -1543,8 +1543,11 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     const int32_t nblk0 = (int32_t)bs.size();
     // the first chunk: 16 blocks (64K pairs) or 1/32 of the call.  The same size decides whether
     // the call runs as several chunks (enqueuer thread) and cuts the chunks below
+#ifndef BSW_HP_FIRST_BLK               // experiment builds only (make abhost AB_FLAGS=-DBSW_HP_FIRST_BLK=8)
+#define BSW_HP_FIRST_BLK 16
+#endif
     const int32_t first_blk = std::min(std::max<int32_t>(1, chunk / kStageBlk),
-                                       nblk0 <= 32 ? nblk0 : std::max<int32_t>(16, nblk0 / 32));
+                                       nblk0 <= 32 ? nblk0 : std::max<int32_t>(BSW_HP_FIRST_BLK, nblk0 / 32));
     const bool async = nblk0 > first_blk;
     std::thread enqueuer;
     if (async)

@@ -99,7 +99,7 @@ for step in "$@"; do
         for k in 1 2 3; do
             for v in base new; do
                 if [ $v = base ]; then L=$PWD/bwa-mem2-arm_amd/lib/$arg; else L=$PWD/bwa-mem2-arm_amd/lib/libbsw_hip.so; fi
-                BSW_HIP_LIB=$L timeout -k 10 200 python tools/host_path_once.py 262144 8 1 > "$O/abhp_run.log" 2>&1 \
+                BSW_HIP_LIB=$L timeout -k 10 200 python tools/host_path_once.py 196608 8 1 > "$O/abhp_run.log" 2>&1 \
                     || fail "$step" $? "$O/abhp_run.log"
                 python3 -c "import statistics as S;v=[float(l.split()[1]) for l in open('$O/abhp_run.log') if l.startswith('call')][2:];print('$v', round(S.median(v),3), v)" | tee -a "$log"
             done
