@@ -1369,13 +1369,17 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
     // lets the next chunk stage a DP generation earlier (same box, alternating: 84.7 / 87.7 vs
     // 77.0 / 78.8 M/s per 1M-pair call; 5 slots pay more first-call allocation,
     // profiles/r04/hostpath_slots_r4w.txt)
-    constexpr int nslots = 4;
+#ifndef BSW_HP_SLOTS                   // experiment builds only (make abhost AB_FLAGS=-DBSW_HP_SLOTS=5)
+#define BSW_HP_SLOTS 4
+#endif
+    constexpr int nslots = BSW_HP_SLOTS;
     int rc = BSW_OK;
     std::unique_ptr<Slot> slots[nslots];
     slots[0] = dc.acquire(rc);
     if (rc) return rc;
     int32_t pend_at[nslots] = {}, pend_n[nslots] = {};  // chunk in flight per slot
-    int32_t pend_seq[nslots] = {-1, -1, -1, -1};
+    int32_t pend_seq[nslots];
+    std::fill(pend_seq, pend_seq + nslots, -1);
     int pend_mode[nslots] = {};
     bsw_stats_t agg{};
     // Everything but the DP kernels runs on the slot's high-priority stream: the next chunk's
@@ -1387,10 +1391,11 @@ static int host_shard(const KParams &kp, DeviceCtx &dc, SeqPair *pairs, const ui
         std::condition_variable cv;
         struct Job { int first; int32_t second; int mode; };
         std::deque<Job> q;                        // (slot, seq, staging mode)
-        int32_t launched[nslots] = {-1, -1, -1, -1};
+        int32_t launched[nslots];
         bool stop = false;
         int rc = BSW_OK;
     } L;
+    std::fill(L.launched, L.launched + nslots, -1);
     std::thread launcher([&] {
         const bool dev_ok = hipSetDevice(dc.device) == hipSuccess;
         for (;;) {
