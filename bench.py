@@ -1655,7 +1655,7 @@ def main_mem(args, rank, local, world, c1: bool):
             "algorithmic": f"{alg_per_read:.0f} B per read ({n_blocks / S:.1f} occurrence-block loads x 64 B "
                            f"+ the read) x {n} reads per step", "launch_ms_per_step": round(smem_s * 1e3, 3),
             "backward_extensions_per_read": round(n_bext / S, 1)})
-    if "roofline" not in out_j and not c1:
+    if "roofline" not in out_j:
         # no CPU leg (--no-cpu, N > 1): the SMEM roofline from this workload's PMC pass alone
         out_j["roofline"] = smem_roofline(args, None, {
             "kernel": "smem_kernel", "launch_ms_per_step": round(fmi.last_kernel_ms(), 3),
