@@ -110,7 +110,8 @@ def workload_key(args) -> str:
         return f"smem:n{args.reads}:ref{args.smem_ref_mb}{':blocks' if args.fmi_blocks_only else ''}"
     if w == "c1":
         return "c1"
-    return f"{w}:n{args.reads}:ref{args.ref_mb}:w{args.w}{':blocks' if args.fmi_blocks_only else ''}"
+    pipe = f":p{args.pipeline}" if w == "c4mem" and getattr(args, "pipeline", 1) > 1 else ""
+    return f"{w}:n{args.reads}:ref{args.ref_mb}:w{args.w}{':blocks' if args.fmi_blocks_only else ''}{pipe}"
 
 
 def traffic_for(args, kernel: str, prefix: bool = False) -> dict:
@@ -403,6 +404,11 @@ def main():
     ap.add_argument("--smem-ref-mb", type=int, default=16, help="smem: reference size (Mb) of the FM-index")
     ap.add_argument("--fmi-blocks-only", action="store_true",
                     help="smem / c1 / c4mem: index without the text-mode data (BSW_FMI_NO_TEXT; A/B)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="c4mem: split the step's reads into this many batches and run batch k's mem_chain2aln "
+                         "(VALU-bound extension kernels, the engine's streams) on a second host thread while "
+                         "batch k + 1 is seeded and chained (latency-bound SMEM walk, the index's stream); 1 = "
+                         "the three stages back to back over every read")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="weak (default): every rank scores its own resident 1M-pair shard; strong: one "
@@ -1527,16 +1533,92 @@ def main_mem(args, rank, local, world, c1: bool):
         bsw.chain2aln_resident(eng, d_reads.ptr, d_off.ptr, d_len.ptr, n, bufs["seeds"].ptr, bufs["sr"].ptr,
                                bufs["sc"].ptr, ns, bufs["out"].ptr, bufs["ext"].ptr, opt)
         td = time.perf_counter()
+        smem_ms[0] = fmi.last_kernel_ms()
         return ns, bsw.chain_last_stats(eng), (tb - ta, tc - tb, td - tc)
 
+    # --pipeline P: the reads in P batches; batch k's mem_chain2aln (engine streams) runs on a second
+    # host thread while batch k + 1 is seeded and chained (the index's stream, one call at a time per
+    # index).  Batch k's seeds go at seed offset soff_k of the shared buffers with batch-relative read
+    # numbers; read b of the batch is read a_k + b of the step (d_off / d_len / d_mems / d_cnt offset).
+    P = 1 if c1 else max(1, int(args.pipeline))
+    bounds = [n * k // P for k in range(P + 1)]
+    seg = []                                             # (a_k, soff_k, ns_k) of the last step
+    smem_ms = [0.0]
+
+    def step_pipe():
+        import queue
+        import threading
+        q, res = queue.Queue(), {"st": [], "err": None, "t": 0.0}
+        SZ, AZ, MZ = bsw.SEED_DTYPE.itemsize, bsw.ALNREG_DTYPE.itemsize, bsw.BWTINTV_DTYPE.itemsize
+
+        def extender():
+            while True:
+                it = q.get()
+                if it is None:
+                    return
+                a, b, so, nk = it
+                if res["err"] is not None or nk == 0:
+                    continue
+                try:
+                    t1 = time.perf_counter()
+                    bsw.chain2aln_resident(eng, d_reads.ptr, d_off.ptr + 8 * a, d_len.ptr + 4 * a, b - a,
+                                           bufs["seeds"].ptr + so * SZ, bufs["sr"].ptr + 4 * so,
+                                           bufs["sc"].ptr + 4 * so, nk, bufs["out"].ptr + so * AZ,
+                                           bufs["ext"].ptr + 4 * so, opt)
+                    res["t"] += time.perf_counter() - t1
+                    res["st"].append(bsw.chain_last_stats(eng))
+                except Exception as e:  # noqa: BLE001 -- re-raised on the caller's thread
+                    res["err"] = e
+
+        th = threading.Thread(target=extender, daemon=True)
+        th.start()
+        seg.clear()
+        so, t_smem, t_chain, kms = 0, 0.0, 0.0, 0.0
+        try:
+            for k in range(P):
+                a, b = bounds[k], bounds[k + 1]
+                t1 = time.perf_counter()
+                bsw._check(fmi.collect_intv_device(d_reads.ptr, d_off.ptr + 8 * a, d_len.ptr + 4 * a, b - a, 150,
+                                                   d_mems.ptr + a * cap * MZ, cap, d_cnt.ptr + 4 * a, mopt))
+                kms += fmi.last_kernel_ms()
+                t2 = time.perf_counter()
+                rc, nk = fmi.mem_chain_device(d_len.ptr + 4 * a, b - a, d_mems.ptr + a * cap * MZ, cap,
+                                              d_cnt.ptr + 4 * a, bufs["seeds"].ptr + so * SZ, bufs["sr"].ptr + 4 * so,
+                                              bufs["sc"].ptr + 4 * so, sc_cap[0] - so, copt)
+                if rc == -34:                            # sized by the sequential warm-up step: not expected
+                    raise RuntimeError(f"pipelined step: batch {k} needs {nk} seed slots past {so} of {sc_cap[0]}")
+                bsw._check(rc)
+                t_smem += t2 - t1
+                t_chain += time.perf_counter() - t2
+                seg.append((a, so, nk))
+                q.put((a, b, so, nk))
+                so += nk
+        finally:
+            q.put(None)
+            th.join()
+        if res["err"] is not None:
+            raise res["err"]
+        smem_ms[0] = kms
+        agg = bsw.ChainStats()
+        for s in res["st"]:
+            agg.rounds = max(agg.rounds, s.rounds)
+            agg.n_extended += s.n_extended
+            agg.n_skipped += s.n_skipped
+            for j in range(4):
+                agg.n_pairs[j] += s.n_pairs[j]
+        return so, agg, (t_smem, t_chain, res["t"])
+
+    if P > 1:
+        step()                                           # sizes the seed buffers (grown here if short)
+        log("sizing step done")
     for _ in range(args.warmup):
-        step()
+        step() if P == 1 else step_pipe()
         log("warm-up step done")
     barrier(world)
     t = time.perf_counter()
     n_ext, sts, parts = 0, [], []
     for _ in range(args.steps):
-        ns, st, pt = step()
+        ns, st, pt = step() if P == 1 else step_pipe()
         n_ext += sum(st.n_pairs)
         sts.append(st)
         parts.append(pt)
@@ -1549,6 +1631,8 @@ def main_mem(args, rank, local, world, c1: bool):
     sc = bufs["sc"].download(np.zeros(ns, dtype=np.int32))
     out = bufs["out"].download(np.zeros(ns, dtype=bsw.ALNREG_DTYPE))
     ext = bufs["ext"].download(np.zeros(ns, dtype=np.int32))
+    for a, so, nk in (seg if P > 1 else []):             # batch-relative read numbers -> the step's
+        sr[so:so + nk] += a
     if args.dump:                                    # every rank: its shard's seeds and regions (tests)
         np.savez(f"{args.dump}.rank{rank}.npz", seeds=seeds, sr=sr, sc=sc, out=out, ext=ext)
     if rank != 0:
@@ -1575,8 +1659,11 @@ def main_mem(args, rank, local, world, c1: bool):
         "reads_per_s_M": round(reads_s, 3),
         "extensions_per_s_M": round(n_ext_all / dt_max / 1e6, 3),
         "stage_ms": {"smem": round(float(pm[0]), 3), "chain": round(float(pm[1]), 3),
-                     "chain2aln": round(float(pm[2]), 3)},
-        "smem_kernel_ms": round(fmi.last_kernel_ms(), 3),
+                     "chain2aln": round(float(pm[2]), 3),
+                     **({"note": f"{P} batches: chain2aln of batch k on a second thread while batch k + 1 is "
+                                 "seeded and chained -- the three stage times overlap"} if P > 1 else {})},
+        "pipeline_batches": P,
+        "smem_kernel_ms": round(smem_ms[0], 3),
         "seeds_per_read": round(ns / n, 3), "chains_per_read": round(float(len(np.unique(sr.astype(np.int64) * 65536 + sc))) / n, 3),
         "extended_fraction": round(st.n_extended / max(1, ns), 4), "rounds": st.rounds,
         "extensions_per_step_rank0": list(st.n_pairs),
@@ -1648,7 +1735,7 @@ def main_mem(args, rank, local, world, c1: bool):
         # bytes; achieved = those bytes for every read of the step / the SMEM kernel time of the step
         # (the GPU's k-mer table and text mode skip part of these loads: achieved may pass traffic)
         alg_per_read = n_blocks * 64.0 / S + float(np.mean(lens))
-        smem_s = fmi.last_kernel_ms() * 1e-3
+        smem_s = smem_ms[0] * 1e-3
         ach = alg_per_read * n / smem_s / 1e9
         out_j["roofline"] = smem_roofline(args, ach, {
             "kernel": "smem_kernel",
@@ -1658,7 +1745,7 @@ def main_mem(args, rank, local, world, c1: bool):
     if "roofline" not in out_j:
         # no CPU leg (--no-cpu, N > 1): the SMEM roofline from this workload's PMC pass alone
         out_j["roofline"] = smem_roofline(args, None, {
-            "kernel": "smem_kernel", "launch_ms_per_step": round(fmi.last_kernel_ms(), 3),
+            "kernel": "smem_kernel", "launch_ms_per_step": round(smem_ms[0], 3),
             "algorithmic": "logical occurrence-block loads: counted by the CPU leg only"})
     if not c1:
         # the reference's own published bwa-mem2 rate (another machine and another dataset, SAM output
