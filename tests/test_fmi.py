@@ -421,6 +421,24 @@ def test_index_self_check():
         f.close()
 
 
+def test_sa_sample_sorted_checker():
+    """the host-side sampled suffix-array check of the genome-scale test: 0 on the oracle's suffix
+    array of a repetitive reference (long ties walked past the first window), every row sampled;
+    a swapped adjacent pair and a duplicated row are found"""
+    ref = repetitive_ref(20_000, 5)
+    T = np.concatenate([ref, (3 - ref[::-1])]).astype(np.uint8)
+    sa = oracle.FmiRef(ref).sa().astype(np.int64)
+    n = len(T)
+    assert len(sa) == n + 1
+    assert _sa_sample_sorted(T, lambda rows: sa[rows], n, 200_000, K=16) == 0
+    bad = sa.copy()
+    bad[[777, 778]] = bad[[778, 777]]
+    assert _sa_sample_sorted(T, lambda rows: bad[rows], n, 200_000, K=16) >= 1
+    dup = sa.copy()
+    dup[901] = dup[900]
+    assert _sa_sample_sorted(T, lambda rows: dup[rows], n, 200_000, K=16) >= 1
+
+
 @pytest.mark.parametrize("seed,n", [(3, 50_000), (4, 9_000)])
 def test_lean_oracle_equals_full(seed, n):
     """the oracle's lean (genome-scale) index -- occurrence checkpoints every 64 rows, SA sampled
@@ -467,6 +485,42 @@ def _text_check_intervals(T, reads, off, lens, mems, cnt, pos_of, n, max_rows=32
     return len(rows), bad
 
 
+def _sa_sample_sorted(T, pos_of, n, m, seed=11, K=64):
+    """Rows r, r + 1 for m random r < n: SA[r] and SA[r + 1] (pos_of) must start suffixes of T$ in
+    strictly increasing order, compared on the host from the text alone (K-byte windows, ties
+    resolved by walking further).  Returns the number of out-of-order pairs (plus bad positions)."""
+    r = np.unique(np.random.default_rng(seed).integers(0, n, m))
+    p = pos_of(np.concatenate([r, r + 1]))
+    pa, pb = p[:len(r)], p[len(r):]
+    bad = int(np.sum((pa < 0) | (pa > n) | (pb < 0) | (pb > n) | (pa == pb)))
+    L = len(T)
+
+    def win(q, o):
+        idx = q[:, None] + o + np.arange(K)[None, :]
+        v = T[np.minimum(idx, L - 1)].astype(np.int16)
+        v[idx >= L] = -1                                 # '$' and past it: below every base
+        return v
+    a, b = win(pa, 0), win(pb, 0)
+    ne = a != b
+    first = np.argmax(ne, axis=1)
+    diff = ne.any(axis=1)
+    rows = np.arange(len(r))
+    bad += int(np.sum(diff & (a[rows, first] > b[rows, first])))
+    for i in np.nonzero(~diff)[0]:                       # equal for K bytes: walk on
+        o = K
+        while True:
+            x, y = win(pa[i:i + 1], o)[0], win(pb[i:i + 1], o)[0]
+            if (x != y).any():
+                j = int(np.argmax(x != y))
+                bad += int(x[j] > y[j])
+                break
+            if pa[i] + o >= L or pb[i] + o >= L:         # both reached '$' together: equal suffixes
+                bad += 1
+                break
+            o += K
+    return bad
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_wide_index_at_genome_scale_text_and_oracle():
@@ -493,6 +547,9 @@ def test_wide_index_at_genome_scale_text_and_oracle():
         d_p = hiprt.DeviceBuffer(len(rows) * 8)
         f.sa_device(d_k.ptr, len(rows), d_p.ptr)
         return d_p.download(np.zeros(len(rows), dtype=np.int64))
+    # the suffix array checked on the host, independently of the product's own check: 100K random
+    # adjacent rows r, r + 1 hold suffixes of T$ in strictly increasing order ('$' below every base)
+    assert _sa_sample_sorted(T, pos_of, info.n, 100_000) == 0
     checked, bad = _text_check_intervals(T, reads, off, lens, mems, cnt, pos_of, info.n)
     assert bad == 0 and checked > 3 * len(lens)
     # chains + regions: the product's GPU pipeline vs the oracle on a compact copy of the SA rows
